@@ -1,0 +1,234 @@
+/*
+ * maxio_ec.h — C ABI of the MI355X erasure-coding backend for MaxIO's
+ * chunked-EC storage path (src/storage, reference v0.3.2).
+ *
+ * Plain C: pointers, sizes and int return codes; no C++ types, no torch types,
+ * no exceptions cross this boundary.  Every call is reentrant and thread-safe
+ * (tokio workers may call concurrently); each device has its own queues.
+ * Results are deterministic and independent of the device count.
+ *
+ * What each entry point replaces in the reference (file:line under the
+ * reference checkout; the crates are reed-solomon-erasure 6.0.0 and sha2 0.10.9,
+ * Cargo.lock:1462-1473 and :1778-1786):
+ *
+ *   mxec_rs_check            ReedSolomon::new(k, m) argument errors
+ *                            (called at filesystem.rs:1121, chunk_reader.rs:168)
+ *   mxec_rs_parity_matrix    the matrix ReedSolomon::new builds (build_matrix)
+ *   mxec_sha256_batch        Sha256::digest at filesystem.rs:1070 (write_chunk),
+ *                            :1131 (parity), chunk_reader.rs:108 and :184 (verify)
+ *   mxec_encode              FilesystemStorage::compute_and_write_parity,
+ *                            filesystem.rs:1084-1145 (guard :1095, pad :1108-1113,
+ *                            encode :1121-1124, parity digest :1131) plus the data
+ *                            digests of write_chunk :1062-1080 — minus the file I/O
+ *   mxec_reconstruct         try_reconstruct_data_chunk, chunk_reader.rs:157-226
+ *                            (verify :176-196, count :199-208, reconstruct :211,
+ *                            truncate :216-222) — minus the file I/O
+ *   mxec_*_device            the same two operations over device-resident
+ *                            batches (one launch per homogeneous group of objects)
+ *   mxec_write_chunk,
+ *   mxec_compute_and_write_parity,
+ *   mxec_try_reconstruct_data_chunk,
+ *   mxec_put_object_chunked  the file-level functions themselves, writing the
+ *                            same `{key}.ec/{index:06}` files and manifest.json
+ *                            (filesystem.rs:686-828, 1062-1145; chunk_reader.rs:87-226)
+ */
+#ifndef MAXIO_EC_H
+#define MAXIO_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes -------------------------------------------------------
+ * -1..-13 mirror reed_solomon_erasure::Error variants one for one; -14 is the
+ * crate's SingularMatrix (matrix.rs); the rest are MaxIO's own guards and this
+ * library's device / argument failures. */
+#define MXEC_OK 0
+#define MXEC_E_TOO_FEW_SHARDS (-1)
+#define MXEC_E_TOO_MANY_SHARDS (-2)
+#define MXEC_E_TOO_FEW_DATA_SHARDS (-3)
+#define MXEC_E_TOO_MANY_DATA_SHARDS (-4)
+#define MXEC_E_TOO_FEW_PARITY_SHARDS (-5)
+#define MXEC_E_TOO_MANY_PARITY_SHARDS (-6)
+#define MXEC_E_TOO_FEW_BUFFER_SHARDS (-7)
+#define MXEC_E_TOO_MANY_BUFFER_SHARDS (-8)
+#define MXEC_E_INCORRECT_SHARD_SIZE (-9)
+#define MXEC_E_TOO_FEW_SHARDS_PRESENT (-10)
+#define MXEC_E_EMPTY_SHARD (-11)
+#define MXEC_E_INVALID_SHARD_FLAGS (-12)
+#define MXEC_E_INVALID_INDEX (-13)
+#define MXEC_E_SINGULAR_MATRIX (-14)
+#define MXEC_E_TOO_MANY_SHARDS_255 (-20) /* filesystem.rs:1095-1102 k+m>255 */
+#define MXEC_E_INVALID_ARG (-21)
+#define MXEC_E_DEVICE (-30)
+#define MXEC_E_OOM (-31)
+#define MXEC_E_NO_DEVICE (-32)
+#define MXEC_E_IO (-40)              /* StorageError::Io / io::Error */
+#define MXEC_E_INTEGRITY (-41)       /* size or checksum mismatch (InvalidData) */
+#define MXEC_E_JSON (-42)            /* StorageError::Json */
+
+/* ---- flags ---------------------------------------------------------------- */
+#define MXEC_F_DATA_ONLY 0x1u /* reconstruct: rebuild missing data shards only
+                                 (crate reconstruct_data) */
+
+typedef struct mxec_ctx mxec_ctx;
+
+/* ---- library / context ---------------------------------------------------- */
+const char* mxec_version(void);
+const char* mxec_strerror(int code);
+/* Last error message of the calling thread (never NULL). */
+const char* mxec_last_error(void);
+/* Number of visible HIP devices (0 on a host without a GPU). */
+int mxec_device_count(void);
+/* device_mask: bit d selects HIP device d; 0 selects every visible device.
+ * streams_per_device: HIP streams (and staging rings) per device, >= 1.
+ * Returns NULL if no device can be opened (see mxec_last_error). */
+mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device);
+void mxec_close(mxec_ctx* ctx);
+int mxec_ctx_device_count(const mxec_ctx* ctx);
+/* HIP device id of the ctx's i-th device. */
+int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
+
+/* ---- ReedSolomon::new ----------------------------------------------------- */
+/* 0 if new(k, m) would succeed; otherwise the crate's error
+ * (TooFewDataShards / TooFewParityShards / TooManyShards). */
+int mxec_rs_check(int k, int m);
+/* Writes the m x k parity rows of the crate's encoding matrix, row-major. */
+int mxec_rs_parity_matrix(int k, int m, uint8_t* out);
+
+/* ---- host-pointer entry points (the drop-in for one request) -------------- */
+/* SHA-256 of n host buffers; out[i] = digest of bufs[i][0..lens[i]). */
+int mxec_sha256_batch(mxec_ctx* ctx, const uint8_t* const* bufs,
+                      const size_t* lens, size_t n, uint8_t (*out)[32]);
+
+/* Encode one object: k data chunks (data_len[j] <= shard_size bytes, zero
+ * padded to shard_size as filesystem.rs:1111 does), m parity outputs of
+ * shard_size bytes each.  sha256_out, if not NULL, receives k+m digests:
+ * data digests over the unpadded bytes (write_chunk :1070), parity digests over
+ * the full shard (:1131).  data_len NULL means every chunk is shard_size. */
+int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size,
+                const uint8_t* const* data, const size_t* data_len,
+                uint8_t* const* parity, uint8_t (*sha256_out)[32]);
+
+/* Reconstruct one object, try_reconstruct_data_chunk semantics.
+ * shards[i] (i < k+m) holds shard_len[i] bytes when present_inout[i] != 0;
+ * for a missing shard it is the output buffer (shard_len[i] bytes; parity
+ * shards use shard_size).  If expected_sha256 is not NULL every present shard
+ * is hashed and a mismatch turns it into an erasure (:176-196).  Missing
+ * shards are rebuilt (all of them, or data only with MXEC_F_DATA_ONLY);
+ * present_inout[i] is 1 on return for every verified or rebuilt shard.
+ * Fewer than k verified shards: MXEC_E_TOO_FEW_SHARDS_PRESENT, nothing is
+ * written, and *n_present (if not NULL) holds the verified count. */
+int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size,
+                     uint8_t* const* shards, const size_t* shard_len,
+                     const uint8_t (*expected_sha256)[32],
+                     uint8_t* present_inout, uint32_t flags, int* n_present);
+
+/* ---- device-resident batches ---------------------------------------------
+ * All data pointers below are HIP device pointers on ctx device `dev`
+ * (index into the ctx's devices).  `stream` is a hipStream_t of that device
+ * or NULL for the ctx's own stream.  Calls return after enqueueing, except
+ * mxec_reconstruct_strided_device which synchronises once to read the
+ * verification result (the erasure pattern picks the decode matrix). */
+
+/* Uniform batch of n_obj objects, each k data + m parity shards of
+ * shard_size bytes.  Object o, data shard j lives at
+ * data + o*data_obj_stride + j*data_shard_stride (likewise parity).
+ * data_len (host, k entries, NULL = shard_size) applies to every object.
+ * digests_dev (device, n_obj*(k+m)*32, NULL = skip) gets the data then
+ * parity digests of each object, object-major. */
+int mxec_encode_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
+                               int m, uint64_t shard_size, uint64_t n_obj,
+                               const uint8_t* data, uint64_t data_obj_stride,
+                               uint64_t data_shard_stride,
+                               const uint64_t* data_len, uint8_t* parity,
+                               uint64_t parity_obj_stride,
+                               uint64_t parity_shard_stride,
+                               uint8_t* digests_dev);
+
+/* General batch: object o has k[o] data and m[o] parity shards of
+ * shard_size[o] bytes; the pointer arrays are host arrays of device pointers,
+ * concatenated over objects (sum k, sum m entries); data_len likewise (NULL =
+ * full shards).  digests_dev: sum(k+m)*32 bytes, object-major, or NULL. */
+typedef struct mxec_object {
+    int32_t k;
+    int32_t m;
+    uint64_t shard_size;
+} mxec_object;
+int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream,
+                             const mxec_object* objs, uint64_t n_obj,
+                             const uint8_t* const* data,
+                             const uint64_t* data_len,
+                             uint8_t* const* parity, uint8_t* digests_dev);
+
+/* Uniform reconstruct batch.  Object o, shard i (0 <= i < k+m) lives at
+ * shards + o*obj_stride + i*shard_stride.  shard_len (host, k+m entries,
+ * NULL = shard_size) is the byte length of shard i in every object.
+ * present (host, n_obj*(k+m)) in/out as in mxec_reconstruct.
+ * expected_sha_dev (device, n_obj*(k+m)*32) or NULL to skip verification.
+ * status_out (host, n_obj, may be NULL): 0 or MXEC_E_TOO_FEW_SHARDS_PRESENT
+ * per object; the call returns the first non-zero status. */
+int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream,
+                                    int k, int m, uint64_t shard_size,
+                                    uint64_t n_obj, uint8_t* shards,
+                                    uint64_t obj_stride, uint64_t shard_stride,
+                                    const uint64_t* shard_len, uint8_t* present,
+                                    const uint8_t* expected_sha_dev,
+                                    uint32_t flags, int32_t* status_out);
+
+/* SHA-256 of n device buffers (host arrays of device pointers and lengths)
+ * into digests_dev (device, n*32). */
+int mxec_sha256_batch_device(mxec_ctx* ctx, int dev, void* stream,
+                             const uint8_t* const* bufs, const uint64_t* lens,
+                             uint64_t n, uint8_t* digests_dev);
+
+/* ---- file-level path (src/storage/filesystem.rs, chunk_reader.rs) -------- */
+/* ChunkInfo (mod.rs:182-189): kind 0 = data, 1 = parity. */
+typedef struct mxec_chunk_info {
+    uint32_t index;
+    uint64_t size;
+    char sha256[65]; /* lowercase hex + NUL, hex::encode(Sha256::digest) */
+    uint8_t kind;
+} mxec_chunk_info;
+
+/* write_chunk (filesystem.rs:1062-1080): writes ec_dir/{index:06}. */
+int mxec_write_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t index,
+                     const uint8_t* data, size_t len, mxec_chunk_info* out);
+
+/* compute_and_write_parity (filesystem.rs:1084-1145): re-reads the k data
+ * chunk files named by data_chunks, encodes, writes ec_dir/{k+i:06}. */
+int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir,
+                                  uint64_t chunk_size, uint32_t parity_shards,
+                                  const mxec_chunk_info* data_chunks, int k,
+                                  mxec_chunk_info* parity_out);
+
+/* put_object_chunked's chunking + manifest (filesystem.rs:686-773) for a
+ * fully buffered body: chunks of chunk_size, empty body -> one empty chunk and
+ * no parity, parity when parity_shards > 0 && len > 0, manifest.json written
+ * with serde_json::to_string_pretty's layout. */
+int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir,
+                            uint64_t chunk_size, uint32_t parity_shards,
+                            const uint8_t* body, size_t len);
+
+/* GET of a whole EC object (VerifiedChunkReader over manifest.json,
+ * chunk_reader.rs:35-152): verified chunks, RS recovery of bad ones.
+ * out must hold manifest total_size bytes; *out_len receives it.
+ * offset/length select a range as with_range (:52-82); length UINT64_MAX = to
+ * the end. */
+int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset,
+                            uint64_t length, uint8_t* out, uint64_t out_cap,
+                            uint64_t* out_len);
+
+/* try_reconstruct_data_chunk (chunk_reader.rs:157-226) over ec_dir's files and
+ * manifest.json: out receives chunks[target].size bytes. */
+int mxec_try_reconstruct_data_chunk(mxec_ctx* ctx, const char* ec_dir,
+                                    uint32_t target, uint8_t* out,
+                                    uint64_t out_cap, uint64_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAXIO_EC_H */

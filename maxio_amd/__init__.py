@@ -1,0 +1,31 @@
+"""maxio_amd — MI355X erasure-coding backend for MaxIO's chunked-EC path.
+
+Reed–Solomon GF(2^8) encode / reconstruct and per-chunk SHA-256 run as HIP
+kernels for gfx950 inside libmaxio_ec.so; include/maxio_ec.h is the C ABI a
+Rust ``extern "C"`` block binds.  This package is the
+Python mirror of that ABI used by the tests and bench.py.
+"""
+from .ec import (  # noqa: F401
+    DATA_ONLY,
+    Context,
+    ReedSolomon,
+    RSError,
+    device_count,
+    parity_matrix,
+    rs_check,
+)
+from ._native import LIB_PATH, NativeLibraryMissing, declared_symbols, lib  # noqa: F401
+
+__all__ = [
+    "Context",
+    "ReedSolomon",
+    "RSError",
+    "DATA_ONLY",
+    "device_count",
+    "parity_matrix",
+    "rs_check",
+    "lib",
+    "LIB_PATH",
+    "NativeLibraryMissing",
+    "declared_symbols",
+]

@@ -1,0 +1,105 @@
+"""ctypes binding of libmaxio_ec.so (include/maxio_ec.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
+maxio_amd/csrc``).  There is no fallback: if the shared object is missing or
+fails to load, every entry point raises ``NativeLibraryMissing``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmaxio_ec.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "maxio_ec.h")
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+class ChunkInfo(ctypes.Structure):
+    """mxec_chunk_info == the reference's ChunkInfo (storage/mod.rs:182-189)."""
+
+    _fields_ = [
+        ("index", ctypes.c_uint32),
+        ("size", ctypes.c_uint64),
+        ("sha256", ctypes.c_char * 65),
+        ("kind", ctypes.c_uint8),
+    ]
+
+
+class Object(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int32), ("m", ctypes.c_int32), ("shard_size", ctypes.c_uint64)]
+
+
+P = ctypes.c_void_p
+PP = ctypes.POINTER(ctypes.c_void_p)
+SZ = ctypes.c_size_t
+U64 = ctypes.c_uint64
+U64P = ctypes.POINTER(ctypes.c_uint64)
+SZP = ctypes.POINTER(ctypes.c_size_t)
+U8P = ctypes.POINTER(ctypes.c_uint8)
+I32P = ctypes.POINTER(ctypes.c_int32)
+INT = ctypes.c_int
+
+_SIGS = {
+    "mxec_version": (ctypes.c_char_p, []),
+    "mxec_strerror": (ctypes.c_char_p, [INT]),
+    "mxec_last_error": (ctypes.c_char_p, []),
+    "mxec_device_count": (INT, []),
+    "mxec_open": (P, [ctypes.c_uint32, INT]),
+    "mxec_close": (None, [P]),
+    "mxec_ctx_device_count": (INT, [P]),
+    "mxec_ctx_device_id": (INT, [P, INT]),
+    "mxec_rs_check": (INT, [INT, INT]),
+    "mxec_rs_parity_matrix": (INT, [INT, INT, U8P]),
+    "mxec_sha256_batch": (INT, [P, PP, SZP, SZ, U8P]),
+    "mxec_encode": (INT, [P, INT, INT, SZ, PP, SZP, PP, U8P]),
+    "mxec_reconstruct": (INT, [P, INT, INT, SZ, PP, SZP, U8P, U8P, ctypes.c_uint32, ctypes.POINTER(INT)]),
+    "mxec_encode_strided_device": (
+        INT, [P, INT, P, INT, INT, U64, U64, P, U64, U64, U64P, P, U64, U64, P]),
+    "mxec_encode_batch_device": (INT, [P, INT, P, ctypes.POINTER(Object), U64, PP, U64P, PP, P]),
+    "mxec_reconstruct_strided_device": (
+        INT, [P, INT, P, INT, INT, U64, U64, P, U64, U64, U64P, U8P, P, ctypes.c_uint32, I32P]),
+    "mxec_sha256_batch_device": (INT, [P, INT, P, PP, U64P, U64, P]),
+    "mxec_write_chunk": (INT, [P, ctypes.c_char_p, ctypes.c_uint32, P, SZ, ctypes.POINTER(ChunkInfo)]),
+    "mxec_compute_and_write_parity": (
+        INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, ctypes.POINTER(ChunkInfo), INT, ctypes.POINTER(ChunkInfo)]),
+    "mxec_put_object_chunked": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, SZ]),
+    "mxec_get_object_chunked": (INT, [P, ctypes.c_char_p, U64, U64, P, U64, U64P]),
+    "mxec_try_reconstruct_data_chunk": (INT, [P, ctypes.c_char_p, ctypes.c_uint32, P, U64, U64P]),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmaxio_ec.so once; raise loudly if it is not there."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not built: run __graft_entry__.build() or make -C maxio_amd/csrc")
+        try:
+            handle = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - environment specific
+            raise NativeLibraryMissing(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+        return _lib
+
+
+def declared_symbols() -> list[str]:
+    """Every function declared in include/maxio_ec.h."""
+    import re
+
+    text = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(mxec_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,553 @@
+// capi.cpp — extern "C" entry points of include/maxio_ec.h (context, host
+// pointer drop-ins, device-resident batches).  No exception crosses the ABI.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <tuple>
+
+#include "../../include/maxio_ec.h"
+#include "ops.hpp"
+
+using namespace mxec;
+
+struct mxec_ctx {
+    Ctx c;
+};
+
+namespace {
+
+constexpr uint64_t kSlotAlign = 256;
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return set_error(MXEC_E_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return set_error(MXEC_E_INVALID_ARG, e.what());
+    } catch (...) {
+        return set_error(MXEC_E_INVALID_ARG, "unknown exception");
+    }
+}
+
+struct DevScope {
+    Device* d = nullptr;
+    std::unique_lock<std::mutex> lk;
+    Slot* slot = nullptr;
+    int open(mxec_ctx* ctx, int dev_index) {
+        if (!ctx) return set_error(MXEC_E_INVALID_ARG, "null context");
+        d = pick_device(&ctx->c, dev_index);
+        if (!d) return set_error(MXEC_E_INVALID_ARG, "no such device in context");
+        MXEC_HIP(hipSetDevice(d->id));
+        slot = &lock_slot(*d, lk);
+        return MXEC_OK;
+    }
+};
+
+// Digest bytes for n shards of the host-staged image into out (host).
+int fetch_digests(Slot& slot, hipStream_t s, size_t n, uint8_t (*out)[32]) {
+    MXEC_TRY(slot.hdig.ensure(n * 32));
+    MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
+    MXEC_HIP(hipStreamSynchronize(s));
+    std::memcpy(out, slot.hdig.p, n * 32);
+    return MXEC_OK;
+}
+
+std::string too_few_msg(int present, int k, int total) {
+    return "too many missing/corrupt shards: only " + std::to_string(present) + " of " +
+           std::to_string(k) + " required shards available (" + std::to_string(total - present) +
+           " missing)";
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mxec_version(void) { return "maxio_ec 0.1.0 (gfx950)"; }
+
+const char* mxec_strerror(int code) {
+    switch (code) {
+        case MXEC_OK: return "ok";
+        case MXEC_E_TOO_FEW_SHARDS: return "The number of provided shards is smaller than the one in codec";
+        case MXEC_E_TOO_MANY_SHARDS: return "The number of provided shards is greater than the one in codec";
+        case MXEC_E_TOO_FEW_DATA_SHARDS: return "The number of provided data shards is smaller than the one in codec";
+        case MXEC_E_TOO_MANY_DATA_SHARDS: return "The number of provided data shards is greater than the one in codec";
+        case MXEC_E_TOO_FEW_PARITY_SHARDS: return "The number of provided parity shards is smaller than the one in codec";
+        case MXEC_E_TOO_MANY_PARITY_SHARDS: return "The number of provided parity shards is greater than the one in codec";
+        case MXEC_E_TOO_FEW_BUFFER_SHARDS: return "The number of provided buffer shards is smaller than the number of parity shards in codec";
+        case MXEC_E_TOO_MANY_BUFFER_SHARDS: return "The number of provided buffer shards is greater than the number of parity shards in codec";
+        case MXEC_E_INCORRECT_SHARD_SIZE: return "At least one of the provided shards is not of the correct size";
+        case MXEC_E_TOO_FEW_SHARDS_PRESENT: return "The number of shards present is smaller than number of parity shards, cannot reconstruct missing shards";
+        case MXEC_E_EMPTY_SHARD: return "The first shard provided is of zero length";
+        case MXEC_E_INVALID_SHARD_FLAGS: return "The number of flags does not match the total number of shards";
+        case MXEC_E_INVALID_INDEX: return "The data shard index provided is greater or equal to the number of data shards in codec";
+        case MXEC_E_SINGULAR_MATRIX: return "singular matrix";
+        case MXEC_E_TOO_MANY_SHARDS_255: return "too many shards (> 255, GF(2^8) limit)";
+        case MXEC_E_INVALID_ARG: return "invalid argument";
+        case MXEC_E_DEVICE: return "HIP device error";
+        case MXEC_E_OOM: return "out of memory";
+        case MXEC_E_NO_DEVICE: return "no HIP device";
+        case MXEC_E_IO: return "IO error";
+        case MXEC_E_INTEGRITY: return "integrity error";
+        case MXEC_E_JSON: return "JSON error";
+        default: return "unknown error";
+    }
+}
+
+const char* mxec_last_error(void) { return last_error(); }
+
+int mxec_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
+    try {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+            set_error(MXEC_E_NO_DEVICE, "no HIP device visible");
+            return nullptr;
+        }
+        if (streams_per_device < 1) streams_per_device = 1;
+        auto* ctx = new mxec_ctx();
+        for (int d = 0; d < n && d < 32; ++d) {
+            if (device_mask && !(device_mask & (1u << d))) continue;
+            auto dev = std::make_unique<Device>();
+            dev->id = d;
+            if (hipSetDevice(d) != hipSuccess) continue;
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && cus > 0)
+                dev->n_cus = cus;
+            bool ok = true;
+            for (int s = 0; s < streams_per_device; ++s) {
+                auto slot = std::make_unique<Slot>();
+                if (hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking) != hipSuccess) {
+                    ok = false;
+                    break;
+                }
+                dev->slots.push_back(std::move(slot));
+            }
+            if (ok) ctx->c.devs.push_back(std::move(dev));
+        }
+        if (ctx->c.devs.empty()) {
+            delete ctx;
+            set_error(MXEC_E_NO_DEVICE, "no selected HIP device could be opened");
+            return nullptr;
+        }
+        return ctx;
+    } catch (...) {
+        set_error(MXEC_E_OOM, "context allocation failed");
+        return nullptr;
+    }
+}
+
+void mxec_close(mxec_ctx* ctx) {
+    if (!ctx) return;
+    for (auto& d : ctx->c.devs) {
+        (void)hipSetDevice(d->id);
+        (void)hipDeviceSynchronize();
+        for (auto& s : d->slots) {
+            for (auto& rb : s->ring)
+                if (rb.done) (void)hipEventDestroy(rb.done);
+            if (s->stream) (void)hipStreamDestroy(s->stream);
+        }
+    }
+    delete ctx;
+}
+
+int mxec_ctx_device_count(const mxec_ctx* ctx) { return ctx ? int(ctx->c.devs.size()) : 0; }
+
+int mxec_ctx_device_id(const mxec_ctx* ctx, int i) {
+    if (!ctx || i < 0 || i >= int(ctx->c.devs.size())) return -1;
+    return ctx->c.devs[size_t(i)]->id;
+}
+
+int mxec_rs_check(int k, int m) { return rs_check(k, m); }
+
+int mxec_rs_parity_matrix(int k, int m, uint8_t* out) {
+    return guarded([&] {
+        int rc = rs_check(k, m);
+        if (rc) return rc;
+        if (!out) return set_error(MXEC_E_INVALID_ARG, "null output");
+        auto mat = rs_matrix(k, m);
+        if (!mat) return set_error(MXEC_E_SINGULAR_MATRIX, "matrix construction failed");
+        for (int i = 0; i < m; ++i)
+            for (int j = 0; j < k; ++j) out[size_t(i) * k + j] = mat->at(k + i, j);
+        return MXEC_OK;
+    });
+}
+
+int mxec_sha256_batch(mxec_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,
+                      uint8_t (*out)[32]) {
+    return guarded([&] {
+        if (n == 0) return MXEC_OK;
+        if (!bufs || !lens || !out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, -1));
+        Slot& slot = *ds.slot;
+        hipStream_t s = slot.stream;
+        uint64_t total = 0;
+        std::vector<uint64_t> off(n);
+        for (size_t i = 0; i < n; ++i) {
+            off[i] = total;
+            total += round_up(lens[i] ? lens[i] : 1, kSlotAlign);
+        }
+        MXEC_TRY(slot.shards.ensure(total));
+        MXEC_TRY(slot.digests.ensure(n * 32));
+        auto* base = static_cast<uint8_t*>(slot.shards.p);
+        std::vector<const uint8_t*> ptrs(n);
+        std::vector<uint64_t> l(n);
+        for (size_t i = 0; i < n; ++i) {
+            if (lens[i]) MXEC_HIP(hipMemcpyAsync(base + off[i], bufs[i], lens[i], hipMemcpyHostToDevice, s));
+            ptrs[i] = base + off[i];
+            l[i] = lens[i];
+        }
+        MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, l, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
+        return fetch_digests(slot, s, n, out);
+    });
+}
+
+int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* const* data,
+                const size_t* data_len, uint8_t* const* parity, uint8_t (*sha256_out)[32]) {
+    return guarded([&] {
+        MXEC_TRY(check_km(k, m));
+        if (shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+        if (!data || !parity) return set_error(MXEC_E_INVALID_ARG, "null shard array");
+        std::vector<uint64_t> len(static_cast<size_t>(k + m), shard_size);
+        for (int j = 0; j < k; ++j) {
+            len[size_t(j)] = data_len ? data_len[j] : shard_size;
+            if (len[size_t(j)] > shard_size)
+                return set_error(MXEC_E_INCORRECT_SHARD_SIZE, "data chunk longer than shard_size");
+            if (len[size_t(j)] && !data[j]) return set_error(MXEC_E_INVALID_ARG, "null data chunk");
+        }
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, -1));
+        Slot& slot = *ds.slot;
+        hipStream_t s = slot.stream;
+        const uint64_t sa = round_up(shard_size, kSlotAlign);
+        MXEC_TRY(slot.shards.ensure(sa * uint64_t(k + m)));
+        auto* base = static_cast<uint8_t*>(slot.shards.p);
+        std::vector<const uint8_t*> in(static_cast<size_t>(k));
+        std::vector<uint8_t*> out(static_cast<size_t>(m));
+        for (int j = 0; j < k; ++j) {
+            in[size_t(j)] = base + sa * uint64_t(j);
+            if (len[size_t(j)])
+                MXEC_HIP(hipMemcpyAsync(base + sa * uint64_t(j), data[j], len[size_t(j)], hipMemcpyHostToDevice, s));
+        }
+        for (int i = 0; i < m; ++i) out[size_t(i)] = base + sa * uint64_t(k + i);
+        uint32_t off = 0;
+        MXEC_TRY(encode_coef(*ds.d, k, m, &off));
+        RsObject ob{in.data(), len.data(), out.data(), len.data() + k, off};
+        MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, m, {ob}));
+        if (sha256_out) {
+            MXEC_TRY(slot.digests.ensure(size_t(k + m) * 32));
+            std::vector<const uint8_t*> ptrs(in.begin(), in.end());
+            for (auto* p : out) ptrs.push_back(p);
+            MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, len, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
+        }
+        for (int i = 0; i < m; ++i)
+            MXEC_HIP(hipMemcpyAsync(parity[i], out[size_t(i)], shard_size, hipMemcpyDeviceToHost, s));
+        if (sha256_out) return fetch_digests(slot, s, size_t(k + m), sha256_out);
+        MXEC_HIP(hipStreamSynchronize(s));
+        return MXEC_OK;
+    });
+}
+
+int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* const* shards,
+                     const size_t* shard_len, const uint8_t (*expected_sha256)[32],
+                     uint8_t* present_inout, uint32_t flags, int* n_present) {
+    return guarded([&] {
+        int rc = rs_check(k, m);
+        if (rc) return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
+        if (shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+        if (!shards || !present_inout) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        const int total = k + m;
+        std::vector<uint64_t> len(static_cast<size_t>(total));
+        for (int i = 0; i < total; ++i) {
+            len[size_t(i)] = shard_len ? std::min<uint64_t>(shard_len[i], shard_size) : shard_size;
+            if (!shards[i]) return set_error(MXEC_E_INVALID_ARG, "null shard buffer");
+        }
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, -1));
+        Slot& slot = *ds.slot;
+        hipStream_t s = slot.stream;
+        const uint64_t sa = round_up(shard_size, kSlotAlign);
+        MXEC_TRY(slot.shards.ensure(sa * uint64_t(total) + uint64_t(total) * 64));
+        auto* base = static_cast<uint8_t*>(slot.shards.p);
+        std::vector<uint8_t> present(present_inout, present_inout + total);
+        std::vector<const uint8_t*> sp;
+        std::vector<uint64_t> sl;
+        std::vector<int> si;
+        for (int i = 0; i < total; ++i) {
+            if (!present[size_t(i)]) continue;
+            if (len[size_t(i)])
+                MXEC_HIP(hipMemcpyAsync(base + sa * uint64_t(i), shards[i], len[size_t(i)], hipMemcpyHostToDevice, s));
+            sp.push_back(base + sa * uint64_t(i));
+            sl.push_back(len[size_t(i)]);
+            si.push_back(i);
+        }
+        if (expected_sha256 && !sp.empty()) {
+            // chunk_reader.rs:176-196: hash every present shard; mismatch -> erasure.
+            uint8_t* exp_dev = base + sa * uint64_t(total);
+            uint8_t* ok_dev = exp_dev + size_t(total) * 32;
+            std::vector<uint8_t> exp(sp.size() * 32);
+            for (size_t t = 0; t < si.size(); ++t) std::memcpy(&exp[t * 32], expected_sha256[si[t]], 32);
+            MXEC_HIP(hipMemcpyAsync(exp_dev, exp.data(), exp.size(), hipMemcpyHostToDevice, s));
+            MXEC_TRY(run_sha(*ds.d, slot, s, sp, sl, nullptr, exp_dev, ok_dev));
+            MXEC_TRY(slot.hdig.ensure(sp.size()));
+            MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok_dev, sp.size(), hipMemcpyDeviceToHost, s));
+            MXEC_HIP(hipStreamSynchronize(s));
+            const auto* okh = static_cast<const uint8_t*>(slot.hdig.p);
+            for (size_t t = 0; t < si.size(); ++t)
+                if (!okh[t]) present[size_t(si[t])] = 0;
+        }
+        int np = 0;
+        for (int i = 0; i < total; ++i) np += present[size_t(i)] ? 1 : 0;
+        if (n_present) *n_present = np;
+        if (np < k) return set_error(MXEC_E_TOO_FEW_SHARDS_PRESENT, too_few_msg(np, k, total));
+        const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
+        auto plan = decode_cache().get(k, m, present.data(), data_only);
+        if (!plan) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
+        if (!plan->missing.empty()) {
+            uint32_t off = 0;
+            MXEC_TRY(decode_coef(*ds.d, *plan, data_only, &off));
+            std::vector<const uint8_t*> in;
+            std::vector<uint64_t> in_len, out_len;
+            std::vector<uint8_t*> out;
+            for (int v : plan->valid) {
+                in.push_back(base + sa * uint64_t(v));
+                in_len.push_back(len[size_t(v)]);
+            }
+            for (int e : plan->missing) {
+                out.push_back(base + sa * uint64_t(e));
+                out_len.push_back(len[size_t(e)]);
+            }
+            RsObject ob{in.data(), in_len.data(), out.data(), out_len.data(), off};
+            MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, int(out.size()), {ob}));
+            for (size_t t = 0; t < out.size(); ++t)
+                if (out_len[t])
+                    MXEC_HIP(hipMemcpyAsync(shards[plan->missing[t]], out[t], out_len[t], hipMemcpyDeviceToHost, s));
+            MXEC_HIP(hipStreamSynchronize(s));
+            for (int e : plan->missing) present[size_t(e)] = 1;
+        }
+        std::memcpy(present_inout, present.data(), size_t(total));
+        return MXEC_OK;
+    });
+}
+
+int mxec_encode_strided_device(mxec_ctx* ctx, int dev, void* stream, int k, int m,
+                               uint64_t shard_size, uint64_t n_obj, const uint8_t* data,
+                               uint64_t data_obj_stride, uint64_t data_shard_stride,
+                               const uint64_t* data_len, uint8_t* parity,
+                               uint64_t parity_obj_stride, uint64_t parity_shard_stride,
+                               uint8_t* digests_dev) {
+    return guarded([&] {
+        MXEC_TRY(check_km(k, m));
+        if (shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+        if (n_obj == 0) return MXEC_OK;
+        if (!data || !parity) return set_error(MXEC_E_INVALID_ARG, "null base pointer");
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, dev));
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ds.slot->stream;
+        uint32_t off = 0;
+        MXEC_TRY(encode_coef(*ds.d, k, m, &off));
+        std::vector<uint64_t> len(static_cast<size_t>(k + m), shard_size);
+        for (int j = 0; j < k; ++j)
+            if (data_len) len[size_t(j)] = std::min<uint64_t>(data_len[j], shard_size);
+        std::vector<const uint8_t*> in(static_cast<size_t>(n_obj * k));
+        std::vector<uint8_t*> out(static_cast<size_t>(n_obj * m));
+        std::vector<RsObject> objs(static_cast<size_t>(n_obj));
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            for (int j = 0; j < k; ++j) in[o * k + j] = data + o * data_obj_stride + j * data_shard_stride;
+            for (int i = 0; i < m; ++i) out[o * m + i] = parity + o * parity_obj_stride + i * parity_shard_stride;
+            objs[o] = RsObject{&in[o * k], len.data(), &out[o * m], len.data() + k, off};
+        }
+        MXEC_TRY(run_rs(*ds.d, *ds.slot, s, shard_size, k, m, objs));
+        if (digests_dev) {
+            std::vector<const uint8_t*> ptrs;
+            std::vector<uint64_t> lens;
+            ptrs.reserve(size_t(n_obj * (k + m)));
+            lens.reserve(ptrs.capacity());
+            for (uint64_t o = 0; o < n_obj; ++o) {
+                for (int j = 0; j < k; ++j) { ptrs.push_back(in[o * k + j]); lens.push_back(len[size_t(j)]); }
+                for (int i = 0; i < m; ++i) { ptrs.push_back(out[o * m + i]); lens.push_back(shard_size); }
+            }
+            MXEC_TRY(run_sha(*ds.d, *ds.slot, s, ptrs, lens, digests_dev, nullptr, nullptr));
+        }
+        return MXEC_OK;
+    });
+}
+
+int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_object* objs,
+                             uint64_t n_obj, const uint8_t* const* data, const uint64_t* data_len,
+                             uint8_t* const* parity, uint8_t* digests_dev) {
+    return guarded([&] {
+        if (n_obj == 0) return MXEC_OK;
+        if (!objs || !data || !parity) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, dev));
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ds.slot->stream;
+        std::vector<uint64_t> dofs(static_cast<size_t>(n_obj)), pofs(static_cast<size_t>(n_obj));
+        uint64_t dsum = 0, psum = 0;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            MXEC_TRY(check_km(objs[o].k, objs[o].m));
+            if (objs[o].shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+            dofs[o] = dsum;
+            pofs[o] = psum;
+            dsum += uint64_t(objs[o].k);
+            psum += uint64_t(objs[o].m);
+        }
+        std::vector<uint64_t> dl(static_cast<size_t>(dsum)), pl(static_cast<size_t>(psum));
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            for (int j = 0; j < objs[o].k; ++j) {
+                const uint64_t idx = dofs[o] + uint64_t(j);
+                dl[idx] = data_len ? std::min<uint64_t>(data_len[idx], objs[o].shard_size) : objs[o].shard_size;
+            }
+            for (int i = 0; i < objs[o].m; ++i) pl[pofs[o] + uint64_t(i)] = objs[o].shard_size;
+        }
+        // One launch per homogeneous (k, m, shard_size) group.
+        std::map<std::tuple<int, int, uint64_t>, std::vector<uint64_t>> groups;
+        for (uint64_t o = 0; o < n_obj; ++o) groups[{objs[o].k, objs[o].m, objs[o].shard_size}].push_back(o);
+        for (auto& g : groups) {
+            const int k = std::get<0>(g.first), m = std::get<1>(g.first);
+            uint32_t off = 0;
+            MXEC_TRY(encode_coef(*ds.d, k, m, &off));
+            std::vector<RsObject> ro;
+            ro.reserve(g.second.size());
+            for (uint64_t o : g.second)
+                ro.push_back(RsObject{data + dofs[o], &dl[dofs[o]], parity + pofs[o], &pl[pofs[o]], off});
+            MXEC_TRY(run_rs(*ds.d, *ds.slot, s, std::get<2>(g.first), k, m, ro));
+        }
+        if (digests_dev) {
+            std::vector<const uint8_t*> ptrs;
+            std::vector<uint64_t> lens;
+            for (uint64_t o = 0; o < n_obj; ++o) {
+                for (int j = 0; j < objs[o].k; ++j) { ptrs.push_back(data[dofs[o] + j]); lens.push_back(dl[dofs[o] + j]); }
+                for (int i = 0; i < objs[o].m; ++i) { ptrs.push_back(parity[pofs[o] + i]); lens.push_back(objs[o].shard_size); }
+            }
+            MXEC_TRY(run_sha(*ds.d, *ds.slot, s, ptrs, lens, digests_dev, nullptr, nullptr));
+        }
+        return MXEC_OK;
+    });
+}
+
+int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k, int m,
+                                    uint64_t shard_size, uint64_t n_obj, uint8_t* shards,
+                                    uint64_t obj_stride, uint64_t shard_stride,
+                                    const uint64_t* shard_len, uint8_t* present,
+                                    const uint8_t* expected_sha_dev, uint32_t flags,
+                                    int32_t* status_out) {
+    return guarded([&] {
+        int rc = rs_check(k, m);
+        if (rc) return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
+        if (shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+        if (n_obj == 0) return MXEC_OK;
+        if (!shards || !present) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        const int total = k + m;
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, dev));
+        Slot& slot = *ds.slot;
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : slot.stream;
+        std::vector<uint64_t> len(static_cast<size_t>(total));
+        for (int i = 0; i < total; ++i)
+            len[size_t(i)] = shard_len ? std::min<uint64_t>(shard_len[i], shard_size) : shard_size;
+        auto shard_ptr = [&](uint64_t o, int i) { return shards + o * obj_stride + uint64_t(i) * shard_stride; };
+        if (expected_sha_dev) {
+            std::vector<const uint8_t*> ptrs;
+            std::vector<uint64_t> lens;
+            std::vector<uint64_t> idx;
+            for (uint64_t o = 0; o < n_obj; ++o)
+                for (int i = 0; i < total; ++i)
+                    if (present[o * total + i]) {
+                        ptrs.push_back(shard_ptr(o, i));
+                        lens.push_back(len[size_t(i)]);
+                        idx.push_back(o * total + i);
+                    }
+            if (!ptrs.empty()) {
+                // Expected digests are object-major over all k+m shards; the
+                // verify kernel compares message t against expected[idx[t]].
+                MXEC_TRY(slot.digests.ensure(ptrs.size()));
+                auto* ok = static_cast<uint8_t*>(slot.digests.p);
+                MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx));
+                MXEC_TRY(slot.hdig.ensure(ptrs.size()));
+                MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok, ptrs.size(), hipMemcpyDeviceToHost, s));
+                MXEC_HIP(hipStreamSynchronize(s));
+                const auto* okh = static_cast<const uint8_t*>(slot.hdig.p);
+                for (size_t t = 0; t < idx.size(); ++t)
+                    if (!okh[t]) present[idx[t]] = 0;
+            }
+        }
+        const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
+        int first_err = MXEC_OK;
+        // Group objects by (number of shards to rebuild); each object keeps
+        // its own decode table.
+        std::map<int, std::vector<uint64_t>> groups;
+        std::vector<std::shared_ptr<const DecodePlan>> plans(static_cast<size_t>(n_obj));
+        std::vector<uint32_t> offs(static_cast<size_t>(n_obj));
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            const uint8_t* pr = present + o * total;
+            int np = 0;
+            for (int i = 0; i < total; ++i) np += pr[i] ? 1 : 0;
+            int st = MXEC_OK;
+            if (np < k) {
+                st = MXEC_E_TOO_FEW_SHARDS_PRESENT;
+                if (first_err == MXEC_OK) {
+                    first_err = st;
+                    set_error(st, too_few_msg(np, k, total));
+                }
+            } else if (np < total) {
+                plans[o] = decode_cache().get(k, m, pr, data_only);
+                if (!plans[o]) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
+                if (!plans[o]->missing.empty()) {
+                    MXEC_TRY(decode_coef(*ds.d, *plans[o], data_only, &offs[o]));
+                    groups[int(plans[o]->missing.size())].push_back(o);
+                }
+            }
+            if (status_out) status_out[o] = st;
+        }
+        for (auto& g : groups) {
+            const int r = g.first;
+            const size_t n = g.second.size();
+            std::vector<const uint8_t*> in(n * k);
+            std::vector<uint64_t> il(n * k), ol(n * r);
+            std::vector<uint8_t*> out(n * r);
+            std::vector<RsObject> ro(n);
+            for (size_t t = 0; t < n; ++t) {
+                const uint64_t o = g.second[t];
+                const DecodePlan& p = *plans[o];
+                for (int v = 0; v < k; ++v) {
+                    in[t * k + v] = shard_ptr(o, p.valid[size_t(v)]);
+                    il[t * k + v] = len[size_t(p.valid[size_t(v)])];
+                }
+                for (int e = 0; e < r; ++e) {
+                    out[t * r + e] = shard_ptr(o, p.missing[size_t(e)]);
+                    ol[t * r + e] = len[size_t(p.missing[size_t(e)])];
+                }
+                ro[t] = RsObject{&in[t * k], &il[t * k], &out[t * r], &ol[t * r], offs[o]};
+            }
+            MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, r, ro));
+            for (uint64_t o : g.second)
+                for (int e : plans[o]->missing) present[o * total + e] = 1;
+        }
+        return first_err;
+    });
+}
+
+int mxec_sha256_batch_device(mxec_ctx* ctx, int dev, void* stream, const uint8_t* const* bufs,
+                             const uint64_t* lens, uint64_t n, uint8_t* digests_dev) {
+    return guarded([&] {
+        if (n == 0) return MXEC_OK;
+        if (!bufs || !lens || !digests_dev) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, dev));
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ds.slot->stream;
+        std::vector<const uint8_t*> p(bufs, bufs + n);
+        std::vector<uint64_t> l(lens, lens + n);
+        return run_sha(*ds.d, *ds.slot, s, p, l, digests_dev, nullptr, nullptr);
+    });
+}
+
+}  // extern "C"

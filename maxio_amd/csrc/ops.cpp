@@ -1,0 +1,133 @@
+// ops.cpp — descriptor planning and kernel launches over device pointers.
+#include "ops.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "kernels.hpp"
+
+namespace mxec {
+
+int check_km(int k, int m) {
+    if (k + m > 255)
+        return set_error(MXEC_E_TOO_MANY_SHARDS_255,
+                         "too many shards: " + std::to_string(k) + " data + " + std::to_string(m) +
+                             " parity = " + std::to_string(k + m) +
+                             " > 255 (GF(2^8) limit). Increase --chunk-size");
+    int rc = rs_check(k, m);
+    if (rc) return set_error(rc, std::string("Reed-Solomon init error: ") + mxec_strerror(rc));
+    return MXEC_OK;
+}
+
+int encode_coef(Device& dev, int k, int m, uint32_t* off) {
+    std::vector<uint8_t> key = {'E', uint8_t(k), uint8_t(m)};
+    {
+        std::lock_guard<std::mutex> g(dev.coef_mu);
+        auto it = dev.coef_index.find(key);
+        if (it != dev.coef_index.end()) {
+            *off = it->second;
+            return MXEC_OK;
+        }
+    }
+    auto mat = rs_matrix(k, m);
+    if (!mat) return set_error(MXEC_E_SINGULAR_MATRIX, "encoding matrix construction failed");
+    GfMatrix rows(m, k);
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < k; ++j) rows.at(i, j) = mat->at(k + i, j);
+    return coef_offset(dev, key, coef_tables(rows), off);
+}
+
+int decode_coef(Device& dev, const DecodePlan& plan, bool data_only, uint32_t* off) {
+    std::vector<uint8_t> key = {'D', uint8_t(plan.k), uint8_t(plan.m), uint8_t(data_only)};
+    for (int v : plan.valid) key.push_back(uint8_t(v));
+    key.push_back(0xFF);
+    for (int v : plan.missing) key.push_back(uint8_t(v));
+    return coef_offset(dev, key, plan.table, off);
+}
+
+int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
+           const std::vector<RsObject>& objs) {
+    if (objs.empty() || r == 0) return MXEC_OK;
+    const size_t n = objs.size();
+    DescWriter w(slot);
+    const size_t o_in = w.add(sizeof(void*) * n * k);
+    const size_t o_out = w.add(sizeof(void*) * n * r);
+    const size_t o_inlen = w.add(8 * n * k);
+    const size_t o_outlen = w.add(8 * n * r);
+    const size_t o_coef = w.add(4 * n);
+    char* hb = w.data();
+    auto** ip = reinterpret_cast<const uint8_t**>(hb + o_in);
+    auto** op = reinterpret_cast<uint8_t**>(hb + o_out);
+    auto* il = reinterpret_cast<uint64_t*>(hb + o_inlen);
+    auto* ol = reinterpret_cast<uint64_t*>(hb + o_outlen);
+    auto* co = reinterpret_cast<uint32_t*>(hb + o_coef);
+    uint64_t fast = shard_size;
+    bool aligned = true;
+    for (size_t o = 0; o < n; ++o) {
+        const RsObject& ob = objs[o];
+        for (int j = 0; j < k; ++j) {
+            ip[o * k + j] = ob.in[j];
+            il[o * k + j] = std::min<uint64_t>(ob.in_len[j], shard_size);
+            fast = std::min(fast, il[o * k + j]);
+            aligned &= (reinterpret_cast<uintptr_t>(ob.in[j]) & 15) == 0;
+        }
+        for (int i = 0; i < r; ++i) {
+            op[o * r + i] = ob.out[i];
+            ol[o * r + i] = std::min<uint64_t>(ob.out_len[i], shard_size);
+            fast = std::min(fast, ol[o * r + i]);
+            aligned &= (reinterpret_cast<uintptr_t>(ob.out[i]) & 15) == 0;
+        }
+        co[o] = ob.coef_off;
+    }
+    char* db = nullptr;
+    MXEC_TRY(w.commit(s, &db));
+    RsArgs a{};
+    a.in_ptrs = reinterpret_cast<const uint8_t* const*>(db + o_in);
+    a.out_ptrs = reinterpret_cast<uint8_t* const*>(db + o_out);
+    a.in_len = reinterpret_cast<const uint64_t*>(db + o_inlen);
+    a.out_len = reinterpret_cast<const uint64_t*>(db + o_outlen);
+    a.coef = static_cast<const uint32_t*>(dev.coef.p);
+    a.coef_off = reinterpret_cast<const uint32_t*>(db + o_coef);
+    a.shard_size = shard_size;
+    a.fast_cols = fast;
+    a.n_obj = uint32_t(n);
+    a.k = uint32_t(k);
+    a.r_total = uint32_t(r);
+    a.aligned = aligned ? 1u : 0u;
+    for (int row0 = 0; row0 < r; row0 += 8) {
+        a.row0 = uint32_t(row0);
+        a.r = uint32_t(std::min(8, r - row0));
+        MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
+    }
+    return w.finish(s);
+}
+
+int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
+            const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
+            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx) {
+    (void)dev;
+    const size_t n = ptrs.size();
+    if (!n) return MXEC_OK;
+    DescWriter w(slot);
+    const size_t o_p = w.add(sizeof(void*) * n);
+    const size_t o_l = w.add(8 * n);
+    const size_t o_e = exp_idx ? w.add(8 * n) : 0;
+    char* hb = w.data();
+    std::memcpy(hb + o_p, ptrs.data(), sizeof(void*) * n);
+    std::memcpy(hb + o_l, lens.data(), 8 * n);
+    if (exp_idx) std::memcpy(hb + o_e, exp_idx->data(), 8 * n);
+    char* db = nullptr;
+    MXEC_TRY(w.commit(s, &db));
+    ShaArgs a{};
+    a.ptrs = reinterpret_cast<const uint8_t* const*>(db + o_p);
+    a.lens = reinterpret_cast<const uint64_t*>(db + o_l);
+    a.digests = digests_dev;
+    a.expected = expected_dev;
+    a.exp_idx = exp_idx ? reinterpret_cast<const uint64_t*>(db + o_e) : nullptr;
+    a.ok = ok_dev;
+    a.n = uint32_t(n);
+    MXEC_HIP(launch_sha256(a, s));
+    return w.finish(s);
+}
+
+}  // namespace mxec

@@ -1,0 +1,39 @@
+// ops.hpp — device-pointer level operations shared by every C entry point.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "gf256.hpp"
+#include "runtime.hpp"
+
+namespace mxec {
+
+// One object of an RS launch: k inputs -> r outputs, device pointers.
+struct RsObject {
+    const uint8_t* const* in;  // k
+    const uint64_t* in_len;    // k
+    uint8_t* const* out;       // r
+    const uint64_t* out_len;   // r
+    uint32_t coef_off;         // dword offset of this object's [j][i][8] table
+};
+
+// Applies each object's matrix; all objects share (k, r, shard_size).
+int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
+           const std::vector<RsObject>& objs);
+
+// SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be
+// null (see ShaArgs).
+int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
+            const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
+            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx = nullptr);
+
+// Coefficient table of the (k, m) encoding matrix's parity rows.
+int encode_coef(Device& dev, int k, int m, uint32_t* off);
+// Coefficient table of a decode plan.
+int decode_coef(Device& dev, const DecodePlan& plan, bool data_only, uint32_t* off);
+
+// filesystem.rs:1095 guard, then the crate's ReedSolomon::new checks.
+int check_km(int k, int m);
+
+}  // namespace mxec

@@ -1,0 +1,265 @@
+// rs_kernel.hip — Reed-Solomon GF(2^8) encode / reconstruct for gfx950.
+//
+// Replaces the crate's pure-Rust code_some_slices (input-major MUL_TABLE
+// lookups, one byte at a time) behind filesystem.rs:1123 (encode) and
+// chunk_reader.rs:211 (reconstruct).  Both are the same operation: apply an
+// r x k coefficient matrix to k input shards, column by column:
+//     out[i][b] = XOR_j c[i][j] * in[j][b].
+//
+// Design (CDNA4):
+//  * HBM-bound streaming: each lane owns 16-byte columns, loads them with
+//    global_load_dwordx4 (1 KiB per wave-instruction, fully coalesced), so one
+//    workgroup tile covers 256 lanes x 16 B x V columns of every shard.
+//  * No LDS tables and no byte lookups: c*x for 4 packed bytes is three
+//    v_perm_b32 byte-selects from 8-entry tables (bits 0-2, 3-5, 6-7 of x)
+//    plus XORs.  The tables depend only on c, are wave-uniform, and arrive in
+//    SGPRs by scalar loads; one of each v_perm's two table dwords must be a
+//    VGPR (gfx950 constant-bus limit 1), the copy is hoisted per input column.
+//  * Input shards are loaded in blocks of 4 so each lane keeps 4*V 16-byte
+//    loads in flight; grid-stride over (object, tile) keeps 8 workgroups per
+//    CU busy without one launch per object.
+//  * Zero padding (the crate pads the short last chunk, filesystem.rs:1111)
+//    is never materialised: bytes at or past in_len read as zero in the
+//    edge-tile path.
+#include "kernels.hpp"
+
+namespace mxec {
+namespace {
+
+constexpr int kThreads = 256;
+
+struct Vec4 {
+    uint32_t w[4];
+};
+
+__device__ __forceinline__ Vec4 load16(const uint8_t* p) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    return Vec4{{v.x, v.y, v.z, v.w}};
+}
+
+__device__ __forceinline__ void store16(uint8_t* p, const uint32_t (&w)[4]) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Edge path: byte-granular load of up to 16 bytes, zero past `valid`.
+__device__ __forceinline__ Vec4 load_partial(const uint8_t* p, int64_t valid, bool aligned) {
+    if (aligned && valid >= 16) return load16(p);
+    Vec4 r{{0, 0, 0, 0}};
+    for (int b = 0; b < 16; ++b)
+        if (b < valid) r.w[b >> 2] |= uint32_t(p[b]) << (8 * (b & 3));
+    return r;
+}
+
+__device__ __forceinline__ void store_partial(uint8_t* p, const uint32_t (&w)[4], int64_t valid,
+                                              bool aligned) {
+    if (aligned && valid >= 16) {
+        store16(p, w);
+        return;
+    }
+    for (int b = 0; b < 16; ++b)
+        if (b < valid) p[b] = uint8_t(w[b >> 2] >> (8 * (b & 3)));
+}
+
+// acc[i] ^= c_i * x for R outputs, 4 packed bytes; t points at the [i][8]
+// coefficient tables of one input column (see gf256.hpp coef_entry).
+template <int R>
+__device__ __forceinline__ void mac_dword(uint32_t (&acc)[R], uint32_t x, const uint32_t* __restrict__ t,
+                                          const uint32_t (&hi)[R][2]) {
+    const uint32_t s0 = x & 0x07070707u;
+    const uint32_t s1 = (x >> 3) & 0x07070707u;
+    const uint32_t s2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const uint32_t p0 = __builtin_amdgcn_perm(hi[i][0], t[8 * i + 0], s0);
+        const uint32_t p1 = __builtin_amdgcn_perm(hi[i][1], t[8 * i + 2], s1);
+        const uint32_t p2 = __builtin_amdgcn_perm(s2, t[8 * i + 4], s2);
+        acc[i] ^= p0 ^ p1 ^ p2;
+    }
+}
+
+template <int R, int V>
+__device__ __forceinline__ void mac_column(uint32_t (&acc)[V][4][R], const Vec4 (&x)[V],
+                                           const uint32_t* __restrict__ t) {
+    // The high table dwords are made VGPR-resident once per input column and
+    // reused for all V*4 dwords of this lane.
+    uint32_t hi[R][2];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        hi[i][0] = __builtin_amdgcn_readfirstlane(t[8 * i + 1]);
+        hi[i][1] = __builtin_amdgcn_readfirstlane(t[8 * i + 3]);
+        asm volatile("" : "+v"(hi[i][0]), "+v"(hi[i][1]));
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) mac_dword<R>(acc[v][w], x[v].w[w], t, hi);
+}
+
+// Global-address-space views: pointers fetched from the descriptor tables are
+// generic in HIP; casting them lets the backend emit global_load/store
+// (vmcnt only) instead of flat_* (vmcnt + lgkmcnt).
+typedef const uint8_t __attribute__((address_space(1)))* gcptr;
+typedef uint8_t __attribute__((address_space(1)))* gptr;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ Vec4 gload16(gcptr p) {
+    const u32x4 v = *(const u32x4 __attribute__((address_space(1)))*)(p);
+    return Vec4{{v.x, v.y, v.z, v.w}};
+}
+__device__ __forceinline__ void gstore16(gptr p, const uint32_t (&w)[4]) {
+    u32x4 v = {w[0], w[1], w[2], w[3]};
+    *(u32x4 __attribute__((address_space(1)))*)(p) = v;
+}
+
+// Interior tiles: tile t < fast_tiles of every object, all columns in range,
+// all pointers 16-byte aligned.  No bounds checks in the loop.
+template <int R, int V>
+__global__ __launch_bounds__(kThreads) void rs_apply_fast(
+    const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
+    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint32_t k,
+    uint32_t r_total, uint32_t row0, uint32_t fast_tiles, uint64_t n_tiles) {
+    constexpr uint32_t kTile = kThreads * 16 * V;
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const uint32_t obj = uint32_t(tile / fast_tiles);
+        const uint64_t base = (tile - uint64_t(obj) * fast_tiles) * kTile;
+        const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
+        const uint8_t* const* __restrict__ ip = in_ptrs + uint64_t(obj) * k;
+        uint8_t* const* __restrict__ op = out_ptrs + uint64_t(obj) * r_total + row0;
+        const uint64_t lane = base + threadIdx.x * 16;
+
+        uint32_t acc[V][4][R];
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+#pragma unroll
+                for (int i = 0; i < R; ++i) acc[v][w][i] = 0;
+
+        uint32_t j = 0;
+        for (; j + 4 <= k; j += 4) {
+            Vec4 x[4][V];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                gcptr p = ((gcptr)(ip[j + jj])) + lane;
+#pragma unroll
+                for (int v = 0; v < V; ++v) x[jj][v] = gload16(p + v * kThreads * 16);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * r_total * 8);
+        }
+        for (; j < k; ++j) {
+            Vec4 x[V];
+            gcptr p = ((gcptr)(ip[j])) + lane;
+#pragma unroll
+            for (int v = 0; v < V; ++v) x[v] = gload16(p + v * kThreads * 16);
+            mac_column<R, V>(acc, x, tab + j * r_total * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            gptr o = ((gptr)(op[i])) + lane;
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                uint32_t ov[4] = {acc[v][0][i], acc[v][1][i], acc[v][2][i], acc[v][3][i]};
+                gstore16(o + v * kThreads * 16, ov);
+            }
+        }
+    }
+}
+
+// Edge tiles: tiles [first_tile, tiles_per_obj) of every object — the short
+// last chunk, the shard tail past a multiple of the tile, or everything when
+// a pointer is unaligned.  Byte-exact bounds on every input and output.
+template <int R>
+__global__ __launch_bounds__(kThreads) void rs_apply_edge(
+    const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
+    const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
+    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
+    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t first_tile, uint32_t tiles_per_obj,
+    uint32_t aligned, uint64_t n_tiles) {
+    constexpr uint32_t kTile = kThreads * 16;
+    const uint32_t per_obj = tiles_per_obj - first_tile;
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const uint32_t obj = uint32_t(tile / per_obj);
+        const uint64_t t = first_tile + (tile - uint64_t(obj) * per_obj);
+        const uint64_t col = t * kTile + threadIdx.x * 16;
+        const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
+        uint32_t acc[1][4][R];
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int i = 0; i < R; ++i) acc[0][w][i] = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint64_t len = in_len[uint64_t(obj) * k + j];
+            const int64_t valid = col < len ? int64_t(len - col) : 0;
+            Vec4 x[1] = {Vec4{{0, 0, 0, 0}}};
+            if (valid > 0) x[0] = load_partial(in_ptrs[uint64_t(obj) * k + j] + col, valid, aligned != 0);
+            mac_column<R, 1>(acc, x, tab + j * r_total * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            uint64_t olen = out_len[uint64_t(obj) * r_total + row0 + i];
+            if (olen > shard_size) olen = shard_size;
+            if (col < olen) {
+                uint32_t o[4] = {acc[0][0][i], acc[0][1][i], acc[0][2][i], acc[0][3][i]};
+                store_partial(out_ptrs[uint64_t(obj) * r_total + row0 + i] + col, o,
+                              int64_t(olen - col), aligned != 0);
+            }
+        }
+    }
+}
+
+constexpr int kV = 2;
+
+template <int R>
+hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s) {
+    const uint64_t fast_tile = uint64_t(kThreads) * 16 * kV;
+    const uint64_t edge_tile = uint64_t(kThreads) * 16;
+    // Interior: the first fast_tiles (of fast_tile bytes) of every object.
+    uint32_t fast_tiles = 0;
+    if (a.aligned) fast_tiles = uint32_t((a.fast_cols < a.shard_size ? a.fast_cols : a.shard_size) / fast_tile);
+    const uint64_t n_fast = uint64_t(fast_tiles) * a.n_obj;
+    if (n_fast) {
+        uint64_t blocks = uint64_t(n_cus) * 8;
+        if (blocks > n_fast) blocks = n_fast;
+        hipLaunchKernelGGL((rs_apply_fast<R, kV>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
+                           a.in_ptrs, a.out_ptrs, a.coef, a.coef_off, a.k, a.r_total, a.row0,
+                           fast_tiles, n_fast);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    // Edge: the rest of each shard, in tiles of edge_tile bytes.
+    const uint32_t first = uint32_t(uint64_t(fast_tiles) * fast_tile / edge_tile);
+    const uint32_t total = uint32_t((a.shard_size + edge_tile - 1) / edge_tile);
+    if (total > first) {
+        const uint64_t n_edge = uint64_t(total - first) * a.n_obj;
+        uint64_t blocks = uint64_t(n_cus) * 8;
+        if (blocks > n_edge) blocks = n_edge;
+        hipLaunchKernelGGL((rs_apply_edge<R>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
+                           a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off,
+                           a.shard_size, a.k, a.r_total, a.row0, first, total, a.aligned, n_edge);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+// Tile geometry exported to the host planner.
+uint64_t rs_tile_bytes() { return uint64_t(kThreads) * 16 * kV; }
+
+hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
+    switch (a.r) {
+        case 1: return launch_r<1>(a, n_cus, s);
+        case 2: return launch_r<2>(a, n_cus, s);
+        case 3: return launch_r<3>(a, n_cus, s);
+        case 4: return launch_r<4>(a, n_cus, s);
+        case 5: return launch_r<5>(a, n_cus, s);
+        case 6: return launch_r<6>(a, n_cus, s);
+        case 7: return launch_r<7>(a, n_cus, s);
+        case 8: return launch_r<8>(a, n_cus, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mxec

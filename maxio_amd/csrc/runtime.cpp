@@ -1,0 +1,134 @@
+// runtime.cpp — device buffers, descriptor rings, coefficient arena.
+#include "runtime.hpp"
+
+#include <cstring>
+
+namespace mxec {
+
+namespace {
+thread_local std::string t_last_error;
+}
+
+int set_error(int code, const std::string& msg) {
+    t_last_error = msg;
+    return code;
+}
+
+const char* last_error() { return t_last_error.c_str(); }
+
+int DevBuf::ensure(size_t n) {
+    if (n <= cap && p) return MXEC_OK;
+    release();
+    size_t want = n < 4096 ? 4096 : n;
+    MXEC_HIP(hipMalloc(&p, want));
+    cap = want;
+    return MXEC_OK;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+int PinnedBuf::ensure(size_t n) {
+    if (n <= cap && p) return MXEC_OK;
+    release();
+    size_t want = n < 4096 ? 4096 : n;
+    MXEC_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+    cap = want;
+    return MXEC_OK;
+}
+
+void PinnedBuf::release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+size_t DescWriter::add(size_t bytes) {
+    size_t off = (tmp_.size() + 15) & ~size_t(15);
+    tmp_.resize(off + ((bytes + 15) & ~size_t(15)), 0);
+    return off;
+}
+
+int DescWriter::commit(hipStream_t stream, char** dev_base) {
+    buf_ = &slot_.ring[slot_.ring_next];
+    slot_.ring_next = (slot_.ring_next + 1) % Slot::kRing;
+    if (!buf_->done) MXEC_HIP(hipEventCreateWithFlags(&buf_->done, hipEventDisableTiming));
+    if (buf_->pending) {
+        MXEC_HIP(hipEventSynchronize(buf_->done));
+        buf_->pending = false;
+    }
+    const size_t n = tmp_.empty() ? 16 : tmp_.size();
+    MXEC_TRY(buf_->host.ensure(n));
+    MXEC_TRY(buf_->dev.ensure(n));
+    std::memcpy(buf_->host.p, tmp_.data(), tmp_.size());
+    MXEC_HIP(hipMemcpyAsync(buf_->dev.p, buf_->host.p, n, hipMemcpyHostToDevice, stream));
+    *dev_base = static_cast<char*>(buf_->dev.p);
+    return MXEC_OK;
+}
+
+int DescWriter::finish(hipStream_t stream) {
+    if (!buf_) return MXEC_OK;
+    MXEC_HIP(hipEventRecord(buf_->done, stream));
+    buf_->pending = true;
+    return MXEC_OK;
+}
+
+int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<uint32_t>& table,
+                uint32_t* off) {
+    std::lock_guard<std::mutex> g(dev.coef_mu);
+    auto it = dev.coef_index.find(key);
+    if (it != dev.coef_index.end()) {
+        *off = it->second;
+        return MXEC_OK;
+    }
+    constexpr size_t kArenaDwords = size_t(16) << 20;  // 64 MiB of tables
+    if (!dev.coef.p) {
+        MXEC_TRY(dev.coef.ensure(kArenaDwords * 4));
+        dev.coef_used = 0;
+    }
+    if (table.size() > kArenaDwords)
+        return set_error(MXEC_E_INVALID_ARG, "coefficient table larger than the arena");
+    if (dev.coef_used + table.size() > kArenaDwords) {
+        // Arena full: every launch that could read it must have finished.
+        MXEC_HIP(hipDeviceSynchronize());
+        dev.coef_index.clear();
+        dev.coef_used = 0;
+    }
+    const uint32_t o = uint32_t(dev.coef_used);
+    // Synchronous copy: the table is on the device before any stream can see
+    // the key in the index.
+    MXEC_HIP(hipMemcpy(static_cast<uint32_t*>(dev.coef.p) + o, table.data(), table.size() * 4,
+                       hipMemcpyHostToDevice));
+    dev.coef_used += (table.size() + 3) & ~size_t(3);
+    dev.coef_index.emplace(key, o);
+    *off = o;
+    return MXEC_OK;
+}
+
+Device* pick_device(Ctx* ctx, int dev_index) {
+    if (!ctx || ctx->devs.empty()) return nullptr;
+    if (dev_index < 0) dev_index = int(ctx->rr.fetch_add(1) % ctx->devs.size());
+    if (dev_index >= int(ctx->devs.size())) return nullptr;
+    return ctx->devs[size_t(dev_index)].get();
+}
+
+Slot& lock_slot(Device& dev, std::unique_lock<std::mutex>& lk) {
+    const size_t n = dev.slots.size();
+    const unsigned start = dev.next_slot.fetch_add(1);
+    for (size_t t = 0; t < n; ++t) {
+        Slot& s = *dev.slots[(start + t) % n];
+        std::unique_lock<std::mutex> l(s.mu, std::try_to_lock);
+        if (l.owns_lock()) {
+            lk = std::move(l);
+            return s;
+        }
+    }
+    Slot& s = *dev.slots[start % n];
+    lk = std::unique_lock<std::mutex>(s.mu);
+    return s;
+}
+
+}  // namespace mxec

@@ -1,0 +1,117 @@
+// runtime.hpp — per-device state of the C ABI: streams, staging buffers,
+// descriptor rings and the coefficient-table arena.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/maxio_ec.h"
+
+namespace mxec {
+
+int set_error(int code, const std::string& msg);
+const char* last_error();
+
+#define MXEC_HIP(expr)                                                                  \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return ::mxec::set_error(_e == hipErrorOutOfMemory ? MXEC_E_OOM : MXEC_E_DEVICE, \
+                                     std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define MXEC_TRY(expr)              \
+    do {                            \
+        int _rc = (expr);           \
+        if (_rc != MXEC_OK) return _rc; \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n);
+    void release();
+    ~DevBuf() { release(); }
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n);
+    void release();
+    ~PinnedBuf() { release(); }
+};
+
+// One descriptor staging pair (pinned host + device) guarded by an event
+// recorded after the last launch that reads it.
+struct DescBuf {
+    PinnedBuf host;
+    DevBuf dev;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+};
+
+struct Slot {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    DevBuf shards;    // host-API staging: shard images on the device
+    DevBuf digests;   // host-API digests / ok flags
+    PinnedBuf hdig;   // pinned landing zone for digests / flags
+    static constexpr int kRing = 4;
+    DescBuf ring[kRing];
+    int ring_next = 0;
+};
+
+struct Device {
+    int id = 0;
+    int n_cus = 256;
+    std::vector<std::unique_ptr<Slot>> slots;
+    std::atomic<unsigned> next_slot{0};
+    // Coefficient tables (gf256.hpp coef_tables) for every matrix in use,
+    // keyed by matrix identity; uploaded once, read by every launch.
+    std::mutex coef_mu;
+    DevBuf coef;
+    size_t coef_used = 0;  // dwords
+    std::map<std::vector<uint8_t>, uint32_t> coef_index;
+};
+
+struct Ctx {
+    std::vector<std::unique_ptr<Device>> devs;
+    std::atomic<unsigned> rr{0};
+};
+
+// Builds one launch's descriptor tables in a pinned ring buffer, uploads
+// them on `stream`, and hands back device pointers.
+class DescWriter {
+public:
+    DescWriter(Slot& slot) : slot_(slot) {}
+    // Reserve `bytes` (16-byte aligned); returns its offset.  Host pointers
+    // into the tables are data() + offset, valid once every add() is done.
+    size_t add(size_t bytes);
+    char* data() { return tmp_.data(); }
+    // Upload; dev_base receives the device base to add offsets to.
+    int commit(hipStream_t stream, char** dev_base);
+    // Record completion after the launches that read the tables.
+    int finish(hipStream_t stream);
+
+private:
+    Slot& slot_;
+    DescBuf* buf_ = nullptr;
+    std::vector<char> tmp_;
+};
+
+// Device offset (in dwords) of a coefficient table, uploading it on first use.
+int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<uint32_t>& table,
+                uint32_t* off);
+
+Device* pick_device(Ctx* ctx, int dev_index);
+Slot& lock_slot(Device& dev, std::unique_lock<std::mutex>& lk);
+
+}  // namespace mxec

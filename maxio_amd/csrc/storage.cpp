@@ -1,0 +1,524 @@
+// storage.cpp — the file-level chunked-EC functions of MaxIO's
+// FilesystemStorage / VerifiedChunkReader, over the GPU encode / verify /
+// reconstruct entry points:
+//   write_chunk                  filesystem.rs:1062-1080
+//   compute_and_write_parity     filesystem.rs:1084-1145
+//   put_object_chunked (body)    filesystem.rs:686-773 (chunking + manifest)
+//   VerifiedChunkReader          chunk_reader.rs:35-152 (+ ranges :52-82)
+//   try_reconstruct_data_chunk   chunk_reader.rs:157-226
+// On-disk contract (mod.rs:145-189): `{key}.ec/{index:06}` chunk files and
+// manifest.json as serde_json::to_string_pretty writes ChunkManifest.
+//
+// Differences in *how*, not *what*: data digests of a whole body are computed
+// in one GPU batch instead of chunk by chunk, parity is encoded from the body
+// already in memory instead of re-reading the data chunk files (:1108-1113),
+// and a GET verifies every chunk of the range in one batch.
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/maxio_ec.h"
+#include "runtime.hpp"
+
+namespace fs = std::filesystem;
+using mxec::set_error;
+
+namespace {
+
+std::string hex32(const uint8_t* d) {
+    static const char* k = "0123456789abcdef";
+    std::string s(64, '0');
+    for (int i = 0; i < 32; ++i) {
+        s[size_t(2 * i)] = k[d[i] >> 4];
+        s[size_t(2 * i + 1)] = k[d[i] & 15];
+    }
+    return s;
+}
+
+bool unhex32(const std::string& s, uint8_t* out) {
+    if (s.size() != 64) return false;
+    auto v = [](char c) -> int {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        return -1;
+    };
+    for (int i = 0; i < 32; ++i) {
+        int hi = v(s[size_t(2 * i)]), lo = v(s[size_t(2 * i + 1)]);
+        if (hi < 0 || lo < 0) return false;
+        out[i] = uint8_t(hi << 4 | lo);
+    }
+    return true;
+}
+
+std::string chunk_name(uint32_t index) {
+    char b[32];
+    std::snprintf(b, sizeof b, "%06u", index);
+    return b;
+}
+
+int write_file(const fs::path& p, const uint8_t* data, size_t len) {
+    std::ofstream f(p, std::ios::binary | std::ios::trunc);
+    if (!f) return set_error(MXEC_E_IO, "IO error: cannot create " + p.string() + ": " + std::strerror(errno));
+    if (len) f.write(reinterpret_cast<const char*>(data), std::streamsize(len));
+    f.flush();
+    if (!f) return set_error(MXEC_E_IO, "IO error: write failed for " + p.string());
+    return MXEC_OK;
+}
+
+// std::fs::read: whole file or an io::Error.
+int read_file(const fs::path& p, std::vector<uint8_t>& out) {
+    std::ifstream f(p, std::ios::binary);
+    if (!f) return set_error(MXEC_E_IO, "IO error: " + p.string() + ": " + std::strerror(errno));
+    f.seekg(0, std::ios::end);
+    const std::streamoff n = f.tellg();
+    f.seekg(0, std::ios::beg);
+    out.resize(size_t(n < 0 ? 0 : n));
+    if (n > 0) f.read(reinterpret_cast<char*>(out.data()), n);
+    if (!f) return set_error(MXEC_E_IO, "IO error: read failed for " + p.string());
+    return MXEC_OK;
+}
+
+void fill_info(mxec_chunk_info* ci, uint32_t index, uint64_t size, const uint8_t* digest, uint8_t kind) {
+    ci->index = index;
+    ci->size = size;
+    std::string h = hex32(digest);
+    std::memcpy(ci->sha256, h.c_str(), 65);
+    ci->kind = kind;
+}
+
+// ---- ChunkManifest JSON --------------------------------------------------
+struct Manifest {
+    uint32_t version = 1;
+    uint64_t total_size = 0, chunk_size = 0;
+    uint32_t chunk_count = 0;
+    struct Chunk {
+        uint32_t index = 0;
+        uint64_t size = 0;
+        std::string sha256;
+        uint8_t kind = 0;
+    };
+    std::vector<Chunk> chunks;
+    bool has_parity = false, has_shard = false, has_plain = false;
+    uint32_t parity_shards = 0;
+    uint64_t shard_size = 0, plaintext_size = 0;
+};
+
+// serde_json::to_string_pretty layout (two-space indent, "key": value, no
+// trailing newline), fields in ChunkManifest declaration order; `kind` only
+// for parity (skip_serializing_if = is_data), Option fields only when Some.
+std::string manifest_json(const Manifest& m) {
+    std::ostringstream o;
+    o << "{\n  \"version\": " << m.version << ",\n  \"total_size\": " << m.total_size
+      << ",\n  \"chunk_size\": " << m.chunk_size << ",\n  \"chunk_count\": " << m.chunk_count
+      << ",\n  \"chunks\": [";
+    for (size_t i = 0; i < m.chunks.size(); ++i) {
+        const auto& c = m.chunks[i];
+        o << (i ? ",\n" : "\n") << "    {\n      \"index\": " << c.index << ",\n      \"size\": " << c.size
+          << ",\n      \"sha256\": \"" << c.sha256 << "\"";
+        if (c.kind == 1) o << ",\n      \"kind\": \"parity\"";
+        o << "\n    }";
+    }
+    o << (m.chunks.empty() ? "]" : "\n  ]");
+    if (m.has_parity) o << ",\n  \"parity_shards\": " << m.parity_shards;
+    if (m.has_shard) o << ",\n  \"shard_size\": " << m.shard_size;
+    if (m.has_plain) o << ",\n  \"plaintext_size\": " << m.plaintext_size;
+    o << "\n}";
+    return o.str();
+}
+
+// Minimal JSON reader for the manifest schema (serde accepts any field
+// order and whitespace, so this does too).
+class Json {
+public:
+    explicit Json(const std::string& s) : s_(s) {}
+    bool parse(Manifest& m) {
+        ws();
+        if (!eat('{')) return false;
+        ws();
+        if (eat('}')) return true;
+        for (;;) {
+            std::string key;
+            ws();
+            if (!str(key)) return false;
+            ws();
+            if (!eat(':')) return false;
+            ws();
+            if (key == "chunks") {
+                if (!chunks(m.chunks)) return false;
+            } else if (key == "version") {
+                uint64_t v; if (!num(v)) return false; m.version = uint32_t(v);
+            } else if (key == "total_size") {
+                if (!num(m.total_size)) return false;
+            } else if (key == "chunk_size") {
+                if (!num(m.chunk_size)) return false;
+            } else if (key == "chunk_count") {
+                uint64_t v; if (!num(v)) return false; m.chunk_count = uint32_t(v);
+            } else if (key == "parity_shards") {
+                if (null()) { m.has_parity = false; }
+                else { uint64_t v; if (!num(v)) return false; m.parity_shards = uint32_t(v); m.has_parity = true; }
+            } else if (key == "shard_size") {
+                if (null()) { m.has_shard = false; }
+                else { if (!num(m.shard_size)) return false; m.has_shard = true; }
+            } else if (key == "plaintext_size") {
+                if (null()) { m.has_plain = false; }
+                else { if (!num(m.plaintext_size)) return false; m.has_plain = true; }
+            } else if (!skip()) {
+                return false;
+            }
+            ws();
+            if (eat(',')) continue;
+            if (eat('}')) return true;
+            return false;
+        }
+    }
+
+private:
+    const std::string& s_;
+    size_t i_ = 0;
+    void ws() { while (i_ < s_.size() && std::isspace(static_cast<unsigned char>(s_[i_]))) ++i_; }
+    bool eat(char c) { if (i_ < s_.size() && s_[i_] == c) { ++i_; return true; } return false; }
+    bool null() { if (s_.compare(i_, 4, "null") == 0) { i_ += 4; return true; } return false; }
+    bool str(std::string& out) {
+        if (!eat('"')) return false;
+        while (i_ < s_.size() && s_[i_] != '"') {
+            if (s_[i_] == '\\' && i_ + 1 < s_.size()) ++i_;
+            out.push_back(s_[i_++]);
+        }
+        return eat('"');
+    }
+    bool num(uint64_t& v) {
+        size_t st = i_;
+        v = 0;
+        while (i_ < s_.size() && std::isdigit(static_cast<unsigned char>(s_[i_]))) v = v * 10 + uint64_t(s_[i_++] - '0');
+        return i_ > st;
+    }
+    bool skip() {
+        ws();
+        if (i_ >= s_.size()) return false;
+        char c = s_[i_];
+        if (c == '"') { std::string t; return str(t); }
+        if (c == '{' || c == '[') {
+            char close = c == '{' ? '}' : ']';
+            ++i_;
+            ws();
+            if (eat(close)) return true;
+            for (;;) {
+                if (c == '{') { std::string t; ws(); if (!str(t)) return false; ws(); if (!eat(':')) return false; }
+                if (!skip()) return false;
+                ws();
+                if (eat(',')) continue;
+                return eat(close);
+            }
+        }
+        while (i_ < s_.size() && (std::isalnum(static_cast<unsigned char>(s_[i_])) || s_[i_] == '-' || s_[i_] == '.' || s_[i_] == '+')) ++i_;
+        return true;
+    }
+    bool chunks(std::vector<Manifest::Chunk>& out) {
+        if (!eat('[')) return false;
+        ws();
+        if (eat(']')) return true;
+        for (;;) {
+            ws();
+            if (!eat('{')) return false;
+            Manifest::Chunk c;
+            ws();
+            if (!eat('}')) {
+                for (;;) {
+                    std::string key;
+                    ws();
+                    if (!str(key)) return false;
+                    ws();
+                    if (!eat(':')) return false;
+                    ws();
+                    if (key == "index") { uint64_t v; if (!num(v)) return false; c.index = uint32_t(v); }
+                    else if (key == "size") { if (!num(c.size)) return false; }
+                    else if (key == "sha256") { if (!str(c.sha256)) return false; }
+                    else if (key == "kind") { std::string k; if (!str(k)) return false; c.kind = k == "parity" ? 1 : 0; }
+                    else if (!skip()) return false;
+                    ws();
+                    if (eat(',')) continue;
+                    if (eat('}')) break;
+                    return false;
+                }
+            }
+            out.push_back(c);
+            ws();
+            if (eat(',')) continue;
+            return eat(']');
+        }
+    }
+};
+
+int read_manifest(const fs::path& ec_dir, Manifest& m) {
+    std::vector<uint8_t> raw;
+    MXEC_TRY(read_file(ec_dir / "manifest.json", raw));
+    std::string s(raw.begin(), raw.end());
+    Json j(s);
+    if (!j.parse(m)) return set_error(MXEC_E_JSON, "JSON error: malformed manifest.json");
+    if (m.chunks.size() < m.chunk_count) return set_error(MXEC_E_JSON, "JSON error: manifest lists fewer chunks than chunk_count");
+    return MXEC_OK;
+}
+
+// try_reconstruct_data_chunk over files: read every shard, verify against the
+// manifest digest, reconstruct on the GPU, return chunks[target].size bytes.
+int reconstruct_from_dir(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_t target,
+                         std::vector<uint8_t>& out) {
+    const int k = int(man.chunk_count);
+    const int m = man.has_parity ? int(man.parity_shards) : 0;
+    const uint64_t shard = man.has_shard ? man.shard_size : man.chunk_size;
+    int rc = mxec_rs_check(k, m);
+    if (rc) return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
+    const int total = k + m;
+    if (int(man.chunks.size()) < total) return set_error(MXEC_E_JSON, "JSON error: manifest lists fewer shards than k+m");
+    std::vector<std::vector<uint8_t>> bufs(static_cast<size_t>(total));
+    std::vector<uint8_t*> ptrs(static_cast<size_t>(total));
+    std::vector<size_t> lens(static_cast<size_t>(total));
+    std::vector<uint8_t> present(static_cast<size_t>(total), 0);
+    std::vector<uint8_t> expected(size_t(total) * 32, 0);
+    for (int i = 0; i < total; ++i) {
+        const auto& ci = man.chunks[size_t(i)];
+        std::vector<uint8_t> data;
+        bool ok = read_file(dir / chunk_name(uint32_t(i)), data) == MXEC_OK;
+        // A file longer than shard_size cannot carry the manifest digest (the
+        // reference hashes the whole file, :184): it is an erasure.
+        ok = ok && data.size() <= shard;
+        // A digest that does not parse can never match: the shard is an erasure.
+        ok = ok && unhex32(ci.sha256, &expected[size_t(i) * 32]);
+        // Vec::resize(shard_size) pads or truncates; the digest is checked first.
+        const size_t want = size_t(i < k ? std::min<uint64_t>(ci.size, shard) : shard);
+        bufs[size_t(i)].assign(std::max<size_t>(want, data.size()), 0);
+        if (ok) {
+            std::memcpy(bufs[size_t(i)].data(), data.data(), data.size());
+            lens[size_t(i)] = data.size();
+            present[size_t(i)] = 1;
+        } else {
+            lens[size_t(i)] = want;
+        }
+        ptrs[size_t(i)] = bufs[size_t(i)].data();
+    }
+    // Present shards are hashed over their on-disk bytes; a shard whose file
+    // is longer than shard_size fails its digest exactly as in the reference.
+    int np = 0;
+    rc = mxec_reconstruct(ctx, k, m, shard, ptrs.data(), lens.data(),
+                          reinterpret_cast<const uint8_t(*)[32]>(expected.data()), present.data(), 0, &np);
+    if (rc) return rc;
+    const uint64_t real = std::min<uint64_t>(man.chunks[target].size, shard);
+    out.assign(bufs[target].begin(), bufs[target].begin() + long(real));
+    return MXEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxec_write_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t index, const uint8_t* data, size_t len,
+                     mxec_chunk_info* out) {
+    if (!ec_dir || !out || (len && !data)) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    uint8_t dig[1][32];
+    const uint8_t* b = data ? data : reinterpret_cast<const uint8_t*>("");
+    MXEC_TRY(mxec_sha256_batch(ctx, &b, &len, 1, dig));
+    MXEC_TRY(write_file(fs::path(ec_dir) / chunk_name(index), data, len));
+    fill_info(out, index, len, dig[0], 0);
+    return MXEC_OK;
+}
+
+int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
+                                  uint32_t parity_shards, const mxec_chunk_info* data_chunks, int k,
+                                  mxec_chunk_info* parity_out) {
+    if (!ec_dir || (k > 0 && !data_chunks) || !parity_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    const int m = int(parity_shards);
+    MXEC_TRY([&] {
+        if (k + m > 255)
+            return set_error(MXEC_E_TOO_MANY_SHARDS_255,
+                             "too many shards: " + std::to_string(k) + " data + " + std::to_string(m) + " parity = " +
+                                 std::to_string(k + m) + " > 255 (GF(2^8) limit). Increase --chunk-size");
+        return MXEC_OK;
+    }());
+    const fs::path dir(ec_dir);
+    std::vector<std::vector<uint8_t>> data(static_cast<size_t>(k));
+    std::vector<const uint8_t*> dp(static_cast<size_t>(k));
+    std::vector<size_t> dl(static_cast<size_t>(k));
+    for (int j = 0; j < k; ++j) {
+        MXEC_TRY(read_file(dir / chunk_name(data_chunks[j].index), data[size_t(j)]));
+        if (data[size_t(j)].size() > chunk_size) data[size_t(j)].resize(chunk_size);  // Vec::resize
+        dp[size_t(j)] = data[size_t(j)].data();
+        dl[size_t(j)] = data[size_t(j)].size();
+    }
+    std::vector<std::vector<uint8_t>> parity(static_cast<size_t>(m > 0 ? m : 0), std::vector<uint8_t>(chunk_size));
+    std::vector<uint8_t*> pp(parity.size());
+    for (size_t i = 0; i < parity.size(); ++i) pp[i] = parity[i].data();
+    std::vector<uint8_t> dig(size_t(k + m) * 32);
+    int rc = mxec_encode(ctx, k, m, chunk_size, dp.data(), dl.data(), pp.data(),
+                         reinterpret_cast<uint8_t(*)[32]>(dig.data()));
+    if (rc) return rc;
+    for (int i = 0; i < m; ++i) {
+        MXEC_TRY(write_file(dir / chunk_name(uint32_t(k + i)), pp[size_t(i)], chunk_size));
+        fill_info(&parity_out[i], uint32_t(k + i), chunk_size, &dig[size_t(k + i) * 32], 1);
+    }
+    return MXEC_OK;
+}
+
+int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
+                            const uint8_t* body, size_t len) {
+    if (!ec_dir || (len && !body)) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    if (chunk_size == 0) return set_error(MXEC_E_INVALID_ARG, "chunk_size must be > 0");
+    const fs::path dir(ec_dir);
+    std::error_code ec;
+    fs::create_directories(dir, ec);
+    if (ec) return set_error(MXEC_E_IO, "IO error: " + ec.message());
+    // Chunking (:709-737): full chunk_size slices, final partial unpadded;
+    // empty body -> one empty chunk (:740-743).
+    std::vector<const uint8_t*> dp;
+    std::vector<size_t> dl;
+    for (size_t off = 0; off < len; off += chunk_size) {
+        dp.push_back(body + off);
+        dl.push_back(size_t(std::min<uint64_t>(chunk_size, len - off)));
+    }
+    static const uint8_t empty = 0;
+    if (dp.empty()) {
+        dp.push_back(&empty);
+        dl.push_back(0);
+    }
+    const int k = int(dp.size());
+    const bool has_parity = parity_shards > 0 && len > 0;  // :748
+    const int m = has_parity ? int(parity_shards) : 0;
+    Manifest man;
+    man.version = has_parity ? 2 : 1;
+    man.total_size = len;
+    man.chunk_size = chunk_size;
+    man.chunk_count = uint32_t(k);
+    std::vector<uint8_t> dig(size_t(k + m) * 32);
+    std::vector<std::vector<uint8_t>> parity;
+    if (has_parity) {
+        // The reference writes the data chunks first (write_chunk), then
+        // hits the k+m guard inside compute_and_write_parity.
+        for (int j = 0; j < k; ++j) MXEC_TRY(write_file(dir / chunk_name(uint32_t(j)), dp[size_t(j)], dl[size_t(j)]));
+        if (k + m > 255)
+            return set_error(MXEC_E_TOO_MANY_SHARDS_255,
+                             "too many shards: " + std::to_string(k) + " data + " + std::to_string(m) + " parity = " +
+                                 std::to_string(k + m) + " > 255 (GF(2^8) limit). Increase --chunk-size");
+        parity.assign(size_t(m), std::vector<uint8_t>(chunk_size));
+        std::vector<uint8_t*> pp(static_cast<size_t>(m));
+        for (int i = 0; i < m; ++i) pp[size_t(i)] = parity[size_t(i)].data();
+        MXEC_TRY(mxec_encode(ctx, k, m, chunk_size, dp.data(), dl.data(), pp.data(),
+                             reinterpret_cast<uint8_t(*)[32]>(dig.data())));
+        for (int i = 0; i < m; ++i)
+            MXEC_TRY(write_file(dir / chunk_name(uint32_t(k + i)), pp[size_t(i)], chunk_size));
+    } else {
+        MXEC_TRY(mxec_sha256_batch(ctx, dp.data(), dl.data(), size_t(k), reinterpret_cast<uint8_t(*)[32]>(dig.data())));
+        for (int j = 0; j < k; ++j) MXEC_TRY(write_file(dir / chunk_name(uint32_t(j)), dp[size_t(j)], dl[size_t(j)]));
+    }
+    for (int j = 0; j < k + m; ++j) {
+        Manifest::Chunk c;
+        c.index = uint32_t(j);
+        c.size = j < k ? dl[size_t(j)] : chunk_size;
+        c.sha256 = hex32(&dig[size_t(j) * 32]);
+        c.kind = j < k ? 0 : 1;
+        man.chunks.push_back(c);
+    }
+    if (has_parity) {
+        man.has_parity = true;
+        man.parity_shards = parity_shards;
+        man.has_shard = true;
+        man.shard_size = chunk_size;
+    }
+    const std::string js = manifest_json(man);
+    return write_file(dir / "manifest.json", reinterpret_cast<const uint8_t*>(js.data()), js.size());
+}
+
+int mxec_try_reconstruct_data_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t target, uint8_t* out,
+                                    uint64_t out_cap, uint64_t* out_len) {
+    if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    Manifest man;
+    MXEC_TRY(read_manifest(ec_dir, man));
+    if (target >= man.chunk_count) return set_error(MXEC_E_INVALID_INDEX, "target is not a data chunk");
+    std::vector<uint8_t> buf;
+    MXEC_TRY(reconstruct_from_dir(ctx, ec_dir, man, target, buf));
+    *out_len = buf.size();
+    if (buf.size() > out_cap || (buf.size() && !out)) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
+    if (!buf.empty()) std::memcpy(out, buf.data(), buf.size());
+    return MXEC_OK;
+}
+
+int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, uint64_t length, uint8_t* out,
+                            uint64_t out_cap, uint64_t* out_len) {
+    if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    Manifest man;
+    MXEC_TRY(read_manifest(ec_dir, man));
+    const fs::path dir(ec_dir);
+    *out_len = 0;
+    if (length == UINT64_MAX) length = offset < man.total_size ? man.total_size - offset : 0;
+    if (length == 0 || man.total_size == 0) return MXEC_OK;  // with_range :53-65 / new :40
+    if (man.chunk_size == 0) return set_error(MXEC_E_JSON, "JSON error: chunk_size is 0");
+    if (offset + length > man.total_size) length = man.total_size > offset ? man.total_size - offset : 0;
+    if (length == 0) return MXEC_OK;
+    if (length > out_cap || !out) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
+    const uint32_t start = uint32_t(offset / man.chunk_size);
+    const uint32_t end = uint32_t((offset + length - 1) / man.chunk_size);
+    uint64_t skip = offset % man.chunk_size;
+    if (end >= man.chunk_count || end >= man.chunks.size()) return set_error(MXEC_E_JSON, "JSON error: range past chunk_count");
+    // load_chunk_sync (:87-152) for every chunk of the range: read, size
+    // check, then one batched digest pass.
+    const uint32_t n = end - start + 1;
+    std::vector<std::vector<uint8_t>> data(n);
+    std::vector<int> state(n, 0);  // 0 ok so far, 1 read/size failure
+    std::vector<std::string> err(n);
+    std::vector<const uint8_t*> hp;
+    std::vector<size_t> hl;
+    std::vector<uint32_t> hidx;
+    for (uint32_t c = 0; c < n; ++c) {
+        const uint32_t idx = start + c;
+        if (read_file(dir / chunk_name(idx), data[c]) != MXEC_OK) {
+            state[c] = 1;
+            err[c] = "failed to read chunk " + std::to_string(idx);
+            continue;
+        }
+        if (data[c].size() != man.chunks[idx].size) {
+            state[c] = 1;
+            err[c] = "chunk " + std::to_string(idx) + " size mismatch: expected " + std::to_string(man.chunks[idx].size) +
+                     ", got " + std::to_string(data[c].size());
+            continue;
+        }
+        hp.push_back(data[c].empty() ? reinterpret_cast<const uint8_t*>("") : data[c].data());
+        hl.push_back(data[c].size());
+        hidx.push_back(c);
+    }
+    if (!hp.empty()) {
+        std::vector<uint8_t> dig(hp.size() * 32);
+        MXEC_TRY(mxec_sha256_batch(ctx, hp.data(), hl.data(), hp.size(), reinterpret_cast<uint8_t(*)[32]>(dig.data())));
+        for (size_t t = 0; t < hidx.size(); ++t) {
+            const uint32_t c = hidx[t];
+            const std::string got = hex32(&dig[t * 32]);
+            if (got != man.chunks[start + c].sha256) {
+                state[c] = 1;
+                err[c] = "checksum mismatch on chunk " + std::to_string(start + c) + ": expected " +
+                         man.chunks[start + c].sha256 + ", got " + got;
+            }
+        }
+    }
+    uint64_t remaining = length, pos = 0;
+    for (uint32_t c = 0; c < n && remaining; ++c) {
+        if (state[c]) {
+            if (!(man.has_parity && man.parity_shards > 0))
+                return set_error(MXEC_E_INTEGRITY, err[c]);
+            MXEC_TRY(reconstruct_from_dir(ctx, dir, man, start + c, data[c]));
+        }
+        const uint64_t avail = data[c].size() > skip ? data[c].size() - skip : 0;
+        const uint64_t take = std::min(avail, remaining);
+        if (take) std::memcpy(out + pos, data[c].data() + skip, take);
+        pos += take;
+        remaining -= take;
+        skip = 0;
+    }
+    *out_len = pos;
+    return MXEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,353 @@
+"""Python host mirror of the reference's chunked-EC interface, over the C ABI.
+
+Names follow the reference so the parity tests read like its own tests:
+
+* ``ReedSolomon(k, m)`` mirrors ``reed_solomon_erasure::galois_8::ReedSolomon``
+  (``new`` / ``encode`` / ``reconstruct`` / ``reconstruct_data`` / ``verify``)
+  as called at filesystem.rs:1121-1124 and chunk_reader.rs:168,211; errors are
+  ``RSError`` carrying the crate's variant name.
+* ``Context.write_chunk`` / ``compute_and_write_parity`` /
+  ``try_reconstruct_data_chunk`` / ``put_object_chunked`` /
+  ``get_object_chunked`` mirror ``FilesystemStorage`` (filesystem.rs:686-1145)
+  and ``VerifiedChunkReader`` (chunk_reader.rs:35-226).
+
+Every byte of RS / SHA-256 work runs in the HIP kernels of libmaxio_ec.so;
+this module only marshals buffers.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+ERROR_NAMES = {
+    -1: "TooFewShards",
+    -2: "TooManyShards",
+    -3: "TooFewDataShards",
+    -4: "TooManyDataShards",
+    -5: "TooFewParityShards",
+    -6: "TooManyParityShards",
+    -7: "TooFewBufferShards",
+    -8: "TooManyBufferShards",
+    -9: "IncorrectShardSize",
+    -10: "TooFewShardsPresent",
+    -11: "EmptyShard",
+    -12: "InvalidShardFlags",
+    -13: "InvalidIndex",
+    -14: "SingularMatrix",
+    -20: "TooManyShards255",
+    -21: "InvalidArgument",
+    -30: "Device",
+    -31: "OutOfMemory",
+    -32: "NoDevice",
+    -40: "Io",
+    -41: "Integrity",
+    -42: "Json",
+}
+DATA_ONLY = 0x1
+
+
+class RSError(Exception):
+    def __init__(self, code: int, message: str = ""):
+        self.code = code
+        self.name = ERROR_NAMES.get(code, f"E{code}")
+        super().__init__(f"{self.name} ({code}): {message}")
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RSError(rc, N.lib().mxec_last_error().decode(errors="replace"))
+
+
+def _u8(buf) -> np.ndarray:
+    """A C-contiguous uint8 view (no copy for bytes/bytearray/np arrays)."""
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf.reshape(-1).view(np.uint8))
+    return np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, np.uint8)[:0]
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else _ptr.zero.ctypes.data
+
+
+_ptr.zero = np.zeros(16, np.uint8)
+
+
+def _pp(ptrs: Sequence[int]):
+    return (ctypes.c_void_p * max(1, len(ptrs)))(*ptrs)
+
+
+def _szp(vals: Sequence[int]):
+    return (ctypes.c_size_t * max(1, len(vals)))(*vals)
+
+
+def _u64p(vals: Sequence[int]):
+    return (ctypes.c_uint64 * max(1, len(vals)))(*vals)
+
+
+def rs_check(k: int, m: int) -> None:
+    """ReedSolomon::new(k, m) argument checks (no GPU needed)."""
+    _check(N.lib().mxec_rs_check(k, m))
+
+
+def parity_matrix(k: int, m: int) -> np.ndarray:
+    """The m x k parity rows of the crate's encoding matrix (host-side)."""
+    out = np.zeros((m, k), np.uint8)
+    _check(N.lib().mxec_rs_parity_matrix(k, m, out.ctypes.data_as(N.U8P)))
+    return out
+
+
+def device_count() -> int:
+    return int(N.lib().mxec_device_count())
+
+
+class Context:
+    """An ``mxec_ctx``: every visible MI355X (or the ones in device_mask)."""
+
+    def __init__(self, device_mask: int = 0, streams_per_device: int = 2):
+        self._lib = N.lib()
+        self._h = self._lib.mxec_open(device_mask, streams_per_device)
+        if not self._h:
+            raise RSError(-32, self._lib.mxec_last_error().decode())
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.mxec_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def device_ids(self) -> list[int]:
+        n = self._lib.mxec_ctx_device_count(self._h)
+        return [self._lib.mxec_ctx_device_id(self._h, i) for i in range(n)]
+
+    # ---- host-pointer drop-ins --------------------------------------------
+    def sha256(self, bufs: Sequence) -> list[bytes]:
+        arrs = [_u8(b) for b in bufs]
+        out = np.zeros((max(1, len(arrs)), 32), np.uint8)
+        _check(self._lib.mxec_sha256_batch(
+            self._h, _pp([_ptr(a) for a in arrs]), _szp([a.size for a in arrs]), len(arrs),
+            out.ctypes.data_as(N.U8P)))
+        return [bytes(out[i]) for i in range(len(arrs))]
+
+    def encode(self, data: Sequence, m: int, shard_size: int, digests: bool = True):
+        """compute_and_write_parity minus the files: returns (parity shards,
+        k+m digests or None)."""
+        arrs = [_u8(d) for d in data]
+        k = len(arrs)
+        parity = [np.zeros(shard_size, np.uint8) for _ in range(max(m, 0))]
+        dig = np.zeros((max(1, k + m), 32), np.uint8)
+        _check(self._lib.mxec_encode(
+            self._h, k, m, shard_size, _pp([_ptr(a) for a in arrs]), _szp([a.size for a in arrs]),
+            _pp([p.ctypes.data for p in parity]),
+            dig.ctypes.data_as(N.U8P) if digests else None))
+        return parity, ([bytes(dig[i]) for i in range(k + m)] if digests else None)
+
+    def reconstruct(self, shards: Sequence[Optional[object]], k: int, m: int, shard_size: int,
+                    shard_len: Optional[Sequence[int]] = None,
+                    expected: Optional[Sequence[bytes]] = None, data_only: bool = False):
+        """try_reconstruct_data_chunk minus the files.  Returns (shards as
+        numpy arrays, present flags).  Missing shards are None."""
+        total = k + m
+        if shard_len is None:
+            shard_len = [shard_size] * total
+        bufs, present = [], np.zeros(total, np.uint8)
+        for i in range(total):
+            s = shards[i] if i < len(shards) else None
+            if s is None:
+                bufs.append(np.zeros(max(int(shard_len[i]), 1), np.uint8))
+            else:
+                a = np.array(_u8(s), dtype=np.uint8, copy=True)
+                bufs.append(a if a.size else np.zeros(1, np.uint8))
+                present[i] = 1
+        exp = None
+        if expected is not None:
+            exp = np.frombuffer(b"".join(bytes(e) for e in expected), np.uint8).copy()
+        npres = ctypes.c_int(0)
+        _check(self._lib.mxec_reconstruct(
+            self._h, k, m, shard_size, _pp([b.ctypes.data for b in bufs]), _szp(list(shard_len)),
+            exp.ctypes.data_as(N.U8P) if exp is not None else None,
+            present.ctypes.data_as(N.U8P), DATA_ONLY if data_only else 0, ctypes.byref(npres)))
+        out = [bufs[i][: int(shard_len[i])] if present[i] else None for i in range(total)]
+        return out, present
+
+    # ---- device-resident batches (integer device pointers) ------------------
+    def encode_strided_device(self, k, m, shard_size, n_obj, data_ptr, data_obj_stride,
+                              data_shard_stride, parity_ptr, parity_obj_stride, parity_shard_stride,
+                              data_len=None, digests_ptr=None, dev=0, stream=None):
+        _check(self._lib.mxec_encode_strided_device(
+            self._h, dev, stream, k, m, shard_size, n_obj, data_ptr, data_obj_stride,
+            data_shard_stride, _u64p(data_len) if data_len is not None else None, parity_ptr,
+            parity_obj_stride, parity_shard_stride, digests_ptr))
+
+    def encode_batch_device(self, objs: Sequence[tuple], data_ptrs, parity_ptrs, data_len=None,
+                            digests_ptr=None, dev=0, stream=None):
+        arr = (N.Object * len(objs))(*[N.Object(k, m, s) for (k, m, s) in objs])
+        _check(self._lib.mxec_encode_batch_device(
+            self._h, dev, stream, arr, len(objs), _pp(data_ptrs),
+            _u64p(data_len) if data_len is not None else None, _pp(parity_ptrs), digests_ptr))
+
+    def reconstruct_strided_device(self, k, m, shard_size, n_obj, shards_ptr, obj_stride,
+                                   shard_stride, present: np.ndarray, shard_len=None,
+                                   expected_ptr=None, data_only=False, dev=0, stream=None):
+        """present: uint8 array of n_obj*(k+m), updated in place.  Returns
+        (rc, per-object status array)."""
+        assert present.dtype == np.uint8 and present.size == n_obj * (k + m)
+        status = np.zeros(max(1, n_obj), np.int32)
+        rc = self._lib.mxec_reconstruct_strided_device(
+            self._h, dev, stream, k, m, shard_size, n_obj, shards_ptr, obj_stride, shard_stride,
+            _u64p(shard_len) if shard_len is not None else None, present.ctypes.data_as(N.U8P),
+            expected_ptr, DATA_ONLY if data_only else 0, status.ctypes.data_as(N.I32P))
+        return rc, status[:n_obj]
+
+    def sha256_batch_device(self, ptrs, lens, digests_ptr, dev=0, stream=None):
+        _check(self._lib.mxec_sha256_batch_device(
+            self._h, dev, stream, _pp(ptrs), _u64p(lens), len(ptrs), digests_ptr))
+
+    # ---- file-level path (FilesystemStorage / VerifiedChunkReader) ---------
+    @staticmethod
+    def _info(ci: N.ChunkInfo) -> dict:
+        d = {"index": int(ci.index), "size": int(ci.size), "sha256": ci.sha256.decode()}
+        if ci.kind == 1:
+            d["kind"] = "parity"
+        return d
+
+    def write_chunk(self, ec_dir: str, index: int, data) -> dict:
+        a = _u8(data)
+        ci = N.ChunkInfo()
+        _check(self._lib.mxec_write_chunk(self._h, ec_dir.encode(), index, _ptr(a), a.size,
+                                          ctypes.byref(ci)))
+        return self._info(ci)
+
+    def compute_and_write_parity(self, ec_dir: str, chunk_size: int, parity_shards: int,
+                                 data_chunks: Sequence[dict]) -> list[dict]:
+        k = len(data_chunks)
+        ins = (N.ChunkInfo * max(1, k))()
+        for i, c in enumerate(data_chunks):
+            ins[i].index, ins[i].size = c["index"], c["size"]
+            ins[i].sha256 = c["sha256"].encode()
+        outs = (N.ChunkInfo * max(1, parity_shards))()
+        _check(self._lib.mxec_compute_and_write_parity(self._h, ec_dir.encode(), chunk_size,
+                                                       parity_shards, ins, k, outs))
+        return [self._info(outs[i]) for i in range(parity_shards)]
+
+    def put_object_chunked(self, ec_dir: str, chunk_size: int, parity_shards: int, body) -> None:
+        a = _u8(body)
+        _check(self._lib.mxec_put_object_chunked(self._h, ec_dir.encode(), chunk_size,
+                                                 parity_shards, _ptr(a), a.size))
+
+    def get_object_chunked(self, ec_dir: str, offset: int = 0, length: Optional[int] = None,
+                           capacity: Optional[int] = None) -> bytes:
+        import json
+        import os
+
+        if capacity is None:
+            with open(os.path.join(ec_dir, "manifest.json")) as f:
+                capacity = int(json.load(f)["total_size"])
+        out = np.zeros(max(1, capacity), np.uint8)
+        n = ctypes.c_uint64(0)
+        _check(self._lib.mxec_get_object_chunked(
+            self._h, ec_dir.encode(), offset, (1 << 64) - 1 if length is None else length,
+            out.ctypes.data, capacity, ctypes.byref(n)))
+        return out[: n.value].tobytes()
+
+    def try_reconstruct_data_chunk(self, ec_dir: str, target: int, capacity: int = 1 << 26) -> bytes:
+        out = np.zeros(max(1, capacity), np.uint8)
+        n = ctypes.c_uint64(0)
+        _check(self._lib.mxec_try_reconstruct_data_chunk(self._h, ec_dir.encode(), target,
+                                                         out.ctypes.data, capacity, ctypes.byref(n)))
+        return out[: n.value].tobytes()
+
+
+class ReedSolomon:
+    """Mirror of reed_solomon_erasure::galois_8::ReedSolomon (crate 6.0.0)."""
+
+    def __init__(self, data_shards: int, parity_shards: int, ctx: Optional[Context] = None):
+        rs_check(data_shards, parity_shards)
+        self.k, self.m = data_shards, parity_shards
+        self.ctx = ctx or _default_ctx()
+
+    def data_shard_count(self) -> int:
+        return self.k
+
+    def parity_shard_count(self) -> int:
+        return self.m
+
+    def total_shard_count(self) -> int:
+        return self.k + self.m
+
+    def _check_shards(self, shards, allow_none=False):
+        if len(shards) < self.k + self.m:
+            raise RSError(-1, "too few shards")
+        if len(shards) > self.k + self.m:
+            raise RSError(-2, "too many shards")
+        sizes = {len(s) for s in shards if s is not None}
+        if not sizes:
+            raise RSError(-10, "no shard present")
+        if len(sizes) != 1:
+            raise RSError(-9, "shard sizes differ")
+        size = sizes.pop()
+        if size == 0:
+            raise RSError(-11, "empty shard")
+        return size
+
+    def encode(self, shards: list) -> None:
+        """Fill shards[k:] with parity (in place), like the crate's encode."""
+        size = self._check_shards(shards)
+        parity, _ = self.ctx.encode(shards[: self.k], self.m, size, digests=False)
+        for i in range(self.m):
+            target = shards[self.k + i]
+            if isinstance(target, np.ndarray):
+                target.reshape(-1).view(np.uint8)[:] = parity[i]
+            else:
+                target[:] = parity[i].tobytes()
+
+    def verify(self, shards: list) -> bool:
+        size = self._check_shards(shards)
+        parity, _ = self.ctx.encode(shards[: self.k], self.m, size, digests=False)
+        return all(bytes(_u8(shards[self.k + i])) == parity[i].tobytes() for i in range(self.m))
+
+    def _reconstruct(self, shards: list, data_only: bool) -> None:
+        size = self._check_shards(shards, allow_none=True)
+        present = sum(s is not None for s in shards)
+        if present == self.k + self.m:
+            return
+        if present < self.k:
+            raise RSError(-10, "too few shards present")
+        out, _ = self.ctx.reconstruct(shards, self.k, self.m, size, data_only=data_only)
+        for i in range(self.k + self.m):
+            if shards[i] is None and out[i] is not None:
+                shards[i] = bytearray(out[i].tobytes())
+
+    def reconstruct(self, shards: list) -> None:
+        self._reconstruct(shards, False)
+
+    def reconstruct_data(self, shards: list) -> None:
+        self._reconstruct(shards, True)
+
+
+_ctx_singleton: Optional[Context] = None
+
+
+def _default_ctx() -> Context:
+    global _ctx_singleton
+    if _ctx_singleton is None:
+        _ctx_singleton = Context()
+    return _ctx_singleton

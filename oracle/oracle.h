@@ -1,0 +1,113 @@
+/*
+ * oracle.h — CPU restatement of the MaxIO chunked-EC hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in maxio_amd/ links, loads or calls this
+ * code.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * use it, and only as the checker / the timed CPU baseline.
+ *
+ * What it restates (the reference is Rust; the arithmetic lives in two crates
+ * that are NOT vendored under /root/reference, so they are restated from their
+ * published algorithm at the pinned versions):
+ *   - reed-solomon-erasure 6.0.0, galois_8 pure-Rust path (Cargo.lock:1462-1473)
+ *       GF(2^8), polynomial 29 (x^8+x^4+x^3+x^2+1 = 0x11D), generator 2;
+ *       matrix = vandermonde(k+m, k) * inverse(top k x k);
+ *       encode = code_some_slices (input-major MUL_TABLE lookups);
+ *       reconstruct = first-k-present decode matrix, then parity re-encode.
+ *   - sha2 0.10.9 Sha256::digest (Cargo.lock:1778-1786) = FIPS 180-4 SHA-256.
+ *   - chunk rules of src/storage/filesystem.rs:1084-1145 (compute_and_write_parity)
+ *     and src/storage/chunk_reader.rs:157-226 (try_reconstruct_data_chunk),
+ *     without the file I/O.
+ *
+ * Pinning: tests/test_oracle.py checks this code against the crate's own
+ * published known-answer tests (galois_8 mul/div/exp values, the 5+5
+ * `test_one_encode` vector), FIPS 180-4 vectors and Python hashlib, and the
+ * committed fixtures under tests/golden/.
+ */
+#ifndef MAXIO_ORACLE_H
+#define MAXIO_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes mirror reed_solomon_erasure::Error (crate errors.rs) and the
+ * reference's own guards.  Same numbering as include/maxio_ec.h.            */
+#define ORC_OK 0
+#define ORC_E_TOO_FEW_SHARDS (-1)
+#define ORC_E_TOO_MANY_SHARDS (-2)
+#define ORC_E_TOO_FEW_DATA_SHARDS (-3)
+#define ORC_E_TOO_MANY_DATA_SHARDS (-4)
+#define ORC_E_TOO_FEW_PARITY_SHARDS (-5)
+#define ORC_E_TOO_MANY_PARITY_SHARDS (-6)
+#define ORC_E_TOO_FEW_BUFFER_SHARDS (-7)
+#define ORC_E_TOO_MANY_BUFFER_SHARDS (-8)
+#define ORC_E_INCORRECT_SHARD_SIZE (-9)
+#define ORC_E_TOO_FEW_SHARDS_PRESENT (-10)
+#define ORC_E_EMPTY_SHARD (-11)
+#define ORC_E_INVALID_SHARD_FLAGS (-12)
+#define ORC_E_INVALID_INDEX (-13)
+#define ORC_E_SINGULAR_MATRIX (-14)
+#define ORC_E_TOO_MANY_SHARDS_255 (-20)
+#define ORC_E_INVALID_ARG (-21)
+
+/* --- galois_8 --------------------------------------------------------- */
+uint8_t orc_gf_mul(uint8_t a, uint8_t b);
+uint8_t orc_gf_div(uint8_t a, uint8_t b); /* b != 0 */
+uint8_t orc_gf_exp(uint8_t a, size_t n);
+/* exp_out: 510 bytes (EXP_TABLE), log_out: 256 bytes (LOG_TABLE) */
+void orc_gf_tables(uint8_t* exp_out, uint8_t* log_out);
+
+/* --- ReedSolomon::new(k, m): validation + the (k+m) x k encoding matrix ---- */
+int orc_rs_check(int k, int m);
+int orc_rs_matrix(int k, int m, uint8_t* matrix_out /* (k+m)*k */);
+/* Gauss-Jordan inverse, crate Matrix::invert restated; n x n in/out. */
+int orc_matrix_invert(int n, const uint8_t* in, uint8_t* out);
+
+/* --- ReedSolomon::encode ------------------------------------------------ */
+/* shards[0..k) data, shards[k..k+m) parity outputs, each `size` bytes. */
+int orc_rs_encode(int k, int m, size_t size, uint8_t* const* shards);
+
+/* --- ReedSolomon::reconstruct / reconstruct_data ------------------------- */
+/* present[i] != 0 marks shards[i] as Some.  Missing shards are written in
+ * place (the buffers must exist, `size` bytes).  data_only != 0 restates
+ * reconstruct_data (parity left untouched).  present[] is set to 1 for every
+ * shard rebuilt.  */
+int orc_rs_reconstruct(int k, int m, size_t size, uint8_t* const* shards,
+                       uint8_t* present, int data_only);
+
+/* --- Sha256::digest ------------------------------------------------------ */
+void orc_sha256(const uint8_t* data, size_t len, uint8_t out[32]);
+/* Same digest via the x86 SHA extensions when the host has them (sha2 0.10
+ * auto-selects that backend through cpufeatures); returns 1 if SHA-NI was
+ * used, 0 if it fell back to the scalar code. */
+int orc_sha256_fast(const uint8_t* data, size_t len, uint8_t out[32]);
+int orc_have_sha_ni(void);
+
+/* --- filesystem.rs:1084-1145 compute_and_write_parity, minus file I/O ----- */
+/* data[j] has data_len[j] <= chunk_size bytes; zero-padded to chunk_size.
+ * parity[i] receives chunk_size bytes; sha_out (k+m)*32 gets the digest of
+ * every data chunk (its unpadded bytes, as write_chunk does at :1070) and of
+ * every full parity shard (:1131).  sha_out may be NULL. */
+int orc_compute_parity(int k, int m, size_t chunk_size,
+                       const uint8_t* const* data, const size_t* data_len,
+                       uint8_t* const* parity, uint8_t* sha_out);
+
+/* --- chunk_reader.rs:157-226 try_reconstruct_data_chunk, minus file I/O --- */
+/* shards[i] / shard_len[i]: bytes "read from disk" for shard i, or NULL when
+ * the file is missing.  expected_sha: (k+m)*32 manifest digests.  On success
+ * writes chunk_size[target] bytes to out and returns 0.  On too few verified
+ * shards returns ORC_E_TOO_FEW_SHARDS_PRESENT and sets *n_present. */
+int orc_try_reconstruct_data_chunk(int k, int m, size_t shard_size,
+                                   const uint8_t* const* shards,
+                                   const size_t* shard_len,
+                                   const uint8_t* expected_sha,
+                                   const uint64_t* chunk_sizes, int target,
+                                   uint8_t* out, int* n_present);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

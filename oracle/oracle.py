@@ -1,0 +1,158 @@
+"""ctypes wrapper of the CPU oracle (oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker or the timed CPU baseline.  The
+product (maxio_amd/) never imports, links or calls anything under oracle/.
+See oracle.h for what it restates and how it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.orc_gf_mul.restype = ctypes.c_uint8
+        L.orc_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+        L.orc_gf_div.restype = ctypes.c_uint8
+        L.orc_gf_div.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+        L.orc_gf_exp.restype = ctypes.c_uint8
+        L.orc_gf_exp.argtypes = [ctypes.c_uint8, ctypes.c_size_t]
+        L.orc_rs_check.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_rs_matrix.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.orc_rs_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_rs_reconstruct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.orc_sha256.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_sha256_fast.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_compute_parity.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]
+        L.orc_try_reconstruct_data_chunk.argtypes = [
+            ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _arr(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b.reshape(-1).view(np.uint8))
+    return np.frombuffer(bytes(b), np.uint8)
+
+
+def _pp(arrs) -> ctypes.Array:
+    return (ctypes.c_void_p * max(1, len(arrs)))(*[a.ctypes.data for a in arrs])
+
+
+def gf_mul(a: int, b: int) -> int:
+    return int(lib().orc_gf_mul(a, b))
+
+
+def gf_div(a: int, b: int) -> int:
+    return int(lib().orc_gf_div(a, b))
+
+
+def gf_exp(a: int, n: int) -> int:
+    return int(lib().orc_gf_exp(a, n))
+
+
+def rs_check(k: int, m: int) -> int:
+    return int(lib().orc_rs_check(k, m))
+
+
+def matrix(k: int, m: int) -> np.ndarray:
+    out = np.zeros((k + m, k), np.uint8)
+    rc = lib().orc_rs_matrix(k, m, out.ctypes.data)
+    if rc:
+        raise ValueError(rc)
+    return out
+
+
+def encode(data: Sequence, m: int, size: Optional[int] = None) -> list[np.ndarray]:
+    """ReedSolomon::new(k, m).encode over k equal-size (or zero-padded to
+    `size`) data shards; returns the m parity shards."""
+    k = len(data)
+    arrs = [_arr(d) for d in data]
+    size = size if size is not None else arrs[0].size
+    shards = [np.zeros(size, np.uint8) for _ in range(k + m)]
+    for j, a in enumerate(arrs):
+        shards[j][: a.size] = a
+    rc = lib().orc_rs_encode(k, m, size, _pp(shards))
+    if rc:
+        raise ValueError(rc)
+    return shards[k:]
+
+
+def reconstruct(shards: Sequence[Optional[object]], k: int, m: int, size: int,
+                data_only: bool = False) -> tuple[list[np.ndarray], np.ndarray, int]:
+    bufs, present = [], np.zeros(k + m, np.uint8)
+    for i in range(k + m):
+        b = np.zeros(size, np.uint8)
+        if shards[i] is not None:
+            a = _arr(shards[i])
+            b[: a.size] = a
+            present[i] = 1
+        bufs.append(b)
+    rc = lib().orc_rs_reconstruct(k, m, size, _pp(bufs), present.ctypes.data, int(data_only))
+    return bufs, present, int(rc)
+
+
+def sha256(data, fast: bool = False) -> bytes:
+    a = _arr(data)
+    out = np.zeros(32, np.uint8)
+    ptr = a.ctypes.data if a.size else np.zeros(1, np.uint8).ctypes.data
+    (lib().orc_sha256_fast if fast else lib().orc_sha256)(ptr, a.size, out.ctypes.data)
+    return out.tobytes()
+
+
+def compute_parity(data: Sequence, m: int, chunk_size: int):
+    """filesystem.rs:1084-1145 minus I/O: (parity shards, k+m digests, rc)."""
+    arrs = [_arr(d) for d in data]
+    k = len(arrs)
+    parity = [np.zeros(chunk_size, np.uint8) for _ in range(max(m, 0))]
+    lens = (ctypes.c_size_t * max(1, k))(*[a.size for a in arrs])
+    dig = np.zeros((k + max(m, 0)) * 32 or 32, np.uint8)
+    src = [a if a.size else np.zeros(1, np.uint8) for a in arrs]
+    rc = lib().orc_compute_parity(k, m, chunk_size, _pp(src), lens, _pp(parity), dig.ctypes.data)
+    digests = [dig[32 * i: 32 * i + 32].tobytes() for i in range(k + max(m, 0))]
+    return parity, digests, int(rc)
+
+
+def try_reconstruct_data_chunk(shards: Sequence[Optional[object]], k: int, m: int,
+                               shard_size: int, expected: Sequence[bytes],
+                               chunk_sizes: Sequence[int], target: int):
+    """chunk_reader.rs:157-226 minus I/O: (bytes or None, rc, n_present)."""
+    total = k + m
+    arrs = [None if s is None else _arr(s) for s in shards]
+    keep = [a if (a is not None and a.size) else np.zeros(1, np.uint8) for a in arrs]
+    ptrs = (ctypes.c_void_p * total)(*[None if arrs[i] is None else keep[i].ctypes.data
+                                       for i in range(total)])
+    lens = (ctypes.c_size_t * total)(*[0 if a is None else a.size for a in arrs])
+    exp = np.frombuffer(b"".join(expected), np.uint8).copy()
+    sizes = (ctypes.c_uint64 * total)(*chunk_sizes)
+    out = np.zeros(max(1, shard_size), np.uint8)
+    npres = ctypes.c_int(0)
+    rc = lib().orc_try_reconstruct_data_chunk(k, m, shard_size, ptrs, lens, exp.ctypes.data,
+                                              sizes, target, out.ctypes.data, ctypes.byref(npres))
+    if rc:
+        return None, int(rc), npres.value
+    return out[: chunk_sizes[target]].tobytes(), 0, npres.value

@@ -1,0 +1,316 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the oracle and the
+golden fixtures.  Integer/byte work, so every comparison is bit-exact."""
+from __future__ import annotations
+
+import hashlib
+import itertools
+
+import numpy as np
+import pytest
+
+import maxio_amd
+import oracle
+from helpers import data_for, sha_vector_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+# ---- encode ------------------------------------------------------------------
+
+
+def test_one_encode_crate_vector(ctx, golden):
+    kat = golden("rs_kat.json")["one_encode"]
+    rs = maxio_amd.ReedSolomon(kat["k"], kat["m"], ctx)
+    shards = [bytearray(d) for d in kat["data"]] + [bytearray(2) for _ in range(kat["m"])]
+    rs.encode(shards)
+    assert [list(s) for s in shards[kat["k"]:]] == kat["parity"]
+    assert rs.verify(shards)
+    shards[8][0] = (shards[8][0] + 1) % 256
+    assert not rs.verify(shards)
+
+
+def test_encode_golden_vectors(ctx, golden):
+    for case in golden("encode_vectors.json")["cases"]:
+        data = data_for(case["seed"], case["k"], case["shard_size"], case["last_len"])
+        parity, digests = ctx.encode(data, case["m"], case["shard_size"])
+        assert [hashlib.sha256(p.tobytes()).hexdigest() for p in parity] == case["parity_sha256"], case
+        assert [d.hex() for d in digests] == case["chunk_sha256"], case
+
+
+@pytest.mark.parametrize("k,m,size,last", [
+    (1, 2, 4096, None), (4, 2, 65536, 40000), (8, 4, 1 << 20, None), (10, 4, 100_003, 77),
+    (3, 9, 12288, 1), (16, 11, 8192 + 16, None), (64, 4, 8192, 5000), (200, 55, 256, 255),
+    (253, 2, 64, None), (2, 1, 1, None), (7, 3, 17, 3),
+])
+def test_encode_matches_oracle(ctx, k, m, size, last):
+    data = data_for(k * 1000 + m, k, size, last)
+    parity, digests = ctx.encode(data, m, size)
+    want, want_dig, rc = oracle.compute_parity(data, m, size)
+    assert rc == 0
+    for i in range(m):
+        assert np.array_equal(parity[i], want[i]), (k, m, i)
+    assert digests == want_dig
+
+
+def test_encode_errors(ctx):
+    d = [np.zeros(8, np.uint8)] * 250
+    with pytest.raises(maxio_amd.RSError) as e:
+        ctx.encode(d, 6, 8)
+    assert e.value.name == "TooManyShards255"
+    with pytest.raises(maxio_amd.RSError) as e:
+        ctx.encode([b"ab"], 0, 2)
+    assert e.value.name == "TooFewParityShards"
+    with pytest.raises(maxio_amd.RSError) as e:
+        ctx.encode([b"ab"], 2, 0)
+    assert e.value.name == "EmptyShard"
+
+
+# ---- reconstruct ---------------------------------------------------------------
+
+
+def test_reconstruct_golden_all_patterns(ctx, golden):
+    for case in golden("reconstruct_vectors.json")["cases"]:
+        k, m, s = case["k"], case["m"], case["shard_size"]
+        data = data_for(case["seed"], k, s)
+        shards = data + oracle.encode(data, m, s)
+        for pat in case["erasure_patterns"]:
+            inp = [None if i in pat else shards[i] for i in range(k + m)]
+            out, present = ctx.reconstruct(inp, k, m, s)
+            assert present.all()
+            for i in range(k + m):
+                assert np.array_equal(out[i], shards[i]), (k, m, pat, i)
+            out, present = ctx.reconstruct(inp, k, m, s, data_only=True)
+            for i in range(k):
+                assert np.array_equal(out[i], shards[i])
+            assert all(present[i] == 0 for i in pat if i >= k)
+
+
+@pytest.mark.parametrize("k,m,size", [(8, 4, 1 << 20), (10, 4, 65536 + 48), (32, 8, 4096), (5, 5, 333)])
+def test_reconstruct_matches_oracle(ctx, k, m, size):
+    rng = np.random.default_rng(k * 31 + m)
+    data = data_for(k + m, k, size)
+    shards = data + oracle.encode(data, m, size)
+    for _ in range(3):
+        e = int(rng.integers(1, m + 1))
+        pat = sorted(rng.choice(k + m, e, replace=False).tolist())
+        inp = [None if i in pat else shards[i] for i in range(k + m)]
+        want, _, rc = oracle.reconstruct(inp, k, m, size)
+        assert rc == 0
+        out, present = ctx.reconstruct(inp, k, m, size)
+        for i in range(k + m):
+            assert np.array_equal(out[i], want[i]), (pat, i)
+
+
+def test_reconstruct_verify_turns_corruption_into_erasure(ctx):
+    k, m, s = 4, 2, 100
+    body = bytes([0xEF]) * 350
+    data = [np.frombuffer(body[o:o + s], np.uint8) for o in range(0, 350, s)]
+    parity, dig = ctx.encode(data, m, s)
+    sizes = [100, 100, 100, 50, 100, 100]
+    shards = [d.tobytes() for d in data] + [p.tobytes() for p in parity]
+    bad = list(shards)
+    bad[1] = bytes(100)
+    out, present = ctx.reconstruct(bad, k, m, s, shard_len=sizes, expected=dig)
+    assert present.all()
+    assert out[1].tobytes() == shards[1] and out[3].tobytes() == shards[3]
+    want, rc, _ = oracle.try_reconstruct_data_chunk(bad, k, m, s, dig, sizes, 1)
+    assert rc == 0 and want == out[1].tobytes()
+
+
+def test_reconstruct_too_few(ctx):
+    data = data_for(5, 4, 64)
+    shards = data + oracle.encode(data, 2, 64)
+    for pat in itertools.combinations(range(6), 3):
+        inp = [None if i in pat else shards[i] for i in range(6)]
+        with pytest.raises(maxio_amd.RSError) as e:
+            ctx.reconstruct(inp, 4, 2, 64)
+        assert e.value.name == "TooFewShardsPresent"
+
+
+def test_reedsolomon_mirror(ctx):
+    rs = maxio_amd.ReedSolomon(10, 4, ctx)
+    data = data_for(99, 10, 1000)
+    shards = [bytearray(d.tobytes()) for d in data] + [bytearray(1000) for _ in range(4)]
+    rs.encode(shards)
+    orig = [bytes(s) for s in shards]
+    for i in (0, 5, 11, 13):
+        shards[i] = None
+    rs.reconstruct(shards)
+    assert [bytes(s) for s in shards] == orig
+    with pytest.raises(maxio_amd.RSError):
+        maxio_amd.ReedSolomon(0, 1, ctx)
+
+
+# ---- SHA-256 ---------------------------------------------------------------------
+
+
+def test_sha256_golden(ctx, golden):
+    sv = golden("sha256_vectors.json")
+    lens = [c["len"] for c in sv["cases"]]
+    got = ctx.sha256(sha_vector_inputs(sv["seed"], lens))
+    assert [g.hex() for g in got] == [c["sha256"] for c in sv["cases"]]
+    assert ctx.sha256([b""])[0].hex() == sv["empty"]
+
+
+def test_sha256_all_tail_lengths(ctx):
+    rng = np.random.default_rng(11)
+    bufs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in range(0, 300)]
+    got = ctx.sha256(bufs)
+    assert got == [hashlib.sha256(b).digest() for b in bufs]
+
+
+# ---- device-resident batches ----------------------------------------------------
+
+
+def _torch():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no torch GPU")
+    return torch
+
+
+def test_encode_strided_device_with_digests(ctx):
+    torch = _torch()
+    k, m, s, n = 4, 2, 65536 + 4096, 7
+    rng = np.random.default_rng(5)
+    host = rng.integers(0, 256, (n, k, s), dtype=np.uint8)
+    data = torch.from_numpy(host).cuda()
+    parity = torch.zeros((n, m, s), dtype=torch.uint8, device="cuda")
+    dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    ctx.encode_strided_device(k, m, s, n, data.data_ptr(), k * s, s, parity.data_ptr(), m * s, s,
+                              digests_ptr=dig.data_ptr())
+    torch.cuda.synchronize()
+    par = parity.cpu().numpy()
+    dg = dig.cpu().numpy()
+    for o in range(n):
+        want, want_dig, _ = oracle.compute_parity(list(host[o]), m, s)
+        for i in range(m):
+            assert np.array_equal(par[o, i], want[i])
+        assert [dg[o, i].tobytes() for i in range(k + m)] == want_dig
+
+
+def test_encode_batch_device_mixed(ctx):
+    torch = _torch()
+    specs = [(4, 2, 65536), (8, 4, 4096), (10, 4, 1 << 20), (4, 2, 65536), (3, 1, 1000)]
+    rng = np.random.default_rng(8)
+    data_t, par_t, dptr, pptr, dlen, host = [], [], [], [], [], []
+    for (k, m, s) in specs:
+        h = rng.integers(0, 256, (k, s), dtype=np.uint8)
+        host.append(h)
+        d = torch.from_numpy(h).cuda()
+        p = torch.zeros((m, s), dtype=torch.uint8, device="cuda")
+        data_t.append(d)
+        par_t.append(p)
+        dptr += [d[j].data_ptr() for j in range(k)]
+        pptr += [p[i].data_ptr() for i in range(m)]
+        dlen += [s] * (k - 1) + [s - 13]
+    total = sum(k + m for (k, m, _) in specs)
+    dig = torch.zeros((total, 32), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(specs, dptr, pptr, data_len=dlen, digests_ptr=dig.data_ptr())
+    torch.cuda.synchronize()
+    row = 0
+    dg = dig.cpu().numpy()
+    for (k, m, s), h, p in zip(specs, host, par_t):
+        chunks = [h[j] for j in range(k - 1)] + [h[k - 1][: s - 13]]
+        want, want_dig, _ = oracle.compute_parity(chunks, m, s)
+        got = p.cpu().numpy()
+        for i in range(m):
+            assert np.array_equal(got[i], want[i])
+        assert [dg[row + i].tobytes() for i in range(k + m)] == want_dig
+        row += k + m
+
+
+def test_reconstruct_strided_device_verify(ctx):
+    torch = _torch()
+    k, m, s, n = 8, 4, 1 << 16, 16
+    rng = np.random.default_rng(21)
+    host = rng.integers(0, 256, (n, k + m, s), dtype=np.uint8)
+    for o in range(n):
+        host[o, k:] = np.stack(oracle.encode(list(host[o, :k]), m, s))
+    digests = np.stack([[np.frombuffer(hashlib.sha256(host[o, i].tobytes()).digest(), np.uint8)
+                         for i in range(k + m)] for o in range(n)])
+    dev = torch.from_numpy(host.copy()).cuda()
+    dig = torch.from_numpy(digests).cuda()
+    present = np.ones(n * (k + m), np.uint8)
+    for o in range(n):
+        lost = rng.choice(k + m, 2, replace=False)
+        for i in lost:
+            present[o * (k + m) + i] = 0
+            dev[o, i].zero_()
+    # silent corruption on object 3, shard 5 (if still present): verify must catch it
+    if present[3 * (k + m) + 5]:
+        dev[3, 5, 100] ^= 0xFF
+    # object 9: three shards lost + one corrupt -> too few
+    for i in range(4):
+        present[9 * (k + m) + i] = 0
+    dev[9, 4, 7] ^= 1
+    torch.cuda.synchronize()
+    rc, status = ctx.reconstruct_strided_device(k, m, s, n, dev.data_ptr(), (k + m) * s, s,
+                                                present, expected_ptr=dig.data_ptr())
+    torch.cuda.synchronize()
+    assert rc == -10 and status[9] == -10
+    out = dev.cpu().numpy()
+    for o in range(n):
+        if o == 9:
+            continue
+        assert status[o] == 0
+        assert np.array_equal(out[o], host[o]), o
+
+
+# ---- full-size properties (BASELINE config sizes) ---------------------------------
+
+
+def test_config2_full_size_roundtrip(ctx):
+    """k=4 m=2, 10 MiB chunks: encode -> erase 2 -> reconstruct == original;
+    one object also checked byte-for-byte against the oracle."""
+    torch = _torch()
+    k, m, s, n = 4, 2, 10 << 20, 6
+    g = torch.Generator(device="cuda").manual_seed(2)
+    obj = torch.randint(0, 256, (n, k + m, s), dtype=torch.uint8, device="cuda", generator=g)
+    ctx.encode_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s,
+                              obj[:, k:].data_ptr(), (k + m) * s, s)
+    torch.cuda.synchronize()
+    ref = obj.clone()
+    h0 = ref[0].cpu().numpy()
+    want = oracle.encode(list(h0[:k]), m, s)
+    for i in range(m):
+        assert np.array_equal(h0[k + i], want[i])
+    present = np.ones(n * (k + m), np.uint8)
+    rng = np.random.default_rng(3)
+    for o in range(n):
+        for i in rng.choice(k + m, 2, replace=False):
+            present[o * (k + m) + i] = 0
+            obj[o, i].fill_(0x5A)
+    rc, status = ctx.reconstruct_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s, present)
+    torch.cuda.synchronize()
+    assert rc == 0 and present.all()
+    assert torch.equal(obj, ref)
+
+
+def test_config3_full_size_verify_reconstruct(ctx):
+    """k=8 m=4, 1 MiB chunks, 2 data erasures + SHA verify of the rest."""
+    torch = _torch()
+    k, m, s, n = 8, 4, 1 << 20, 64
+    g = torch.Generator(device="cuda").manual_seed(4)
+    obj = torch.randint(0, 256, (n, k + m, s), dtype=torch.uint8, device="cuda", generator=g)
+    dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+    ctx.encode_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s,
+                              obj[:, k:].data_ptr(), (k + m) * s, s, digests_ptr=dig.data_ptr())
+    torch.cuda.synchronize()
+    ref = obj.clone()
+    # digests against hashlib for a sample
+    for (o, i) in [(0, 0), (5, 11), (63, 7)]:
+        assert dig[o, i].cpu().numpy().tobytes() == hashlib.sha256(ref[o, i].cpu().numpy().tobytes()).digest()
+    present = np.ones(n * (k + m), np.uint8)
+    rng = np.random.default_rng(6)
+    for o in range(n):
+        for i in rng.choice(k, 2, replace=False):
+            present[o * (k + m) + i] = 0
+            obj[o, i].zero_()
+    rc, status = ctx.reconstruct_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s, present,
+                                                expected_ptr=dig.data_ptr())
+    torch.cuda.synchronize()
+    assert rc == 0
+    assert torch.equal(obj, ref)

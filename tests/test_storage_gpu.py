@@ -1,0 +1,142 @@
+"""GPU: the reference's EC integration scenarios (tests/integration.rs
+:2702-2898, :3155-3385, :5646-5700) replayed at the file level through the
+C ABI's write / parity / verify / reconstruct functions.  Fault injection is
+done the way the reference tests do it: by editing chunk files."""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+
+import pytest
+
+import maxio_amd
+from helpers import scenario_body
+
+pytestmark = pytest.mark.gpu
+
+
+def _put(ctx, tmp_path, golden, name):
+    sc = golden("reference_scenarios.json")[name]
+    body = scenario_body(sc["body"])
+    ec = str(tmp_path / f"{name}.bin.ec")
+    ctx.put_object_chunked(ec, sc["chunk_size"], sc["parity_shards"], body)
+    return sc, body, ec
+
+
+@pytest.mark.parametrize("name", [
+    "parity_write_0xAB_350", "parity_read_0xCD_350", "v1_no_parity_0xAA_2048", "empty_with_parity",
+    "ec_put_get_0x42_3072", "ec_plus_parity_k49", "parity_range_per_chunk_350",
+])
+def test_layout_and_manifest_bytes(ctx, tmp_path, golden, name):
+    sc, body, ec = _put(ctx, tmp_path, golden, name)
+    files = sorted(os.listdir(ec))
+    assert files == sorted(list(sc["files"]) + ["manifest.json"])
+    assert open(os.path.join(ec, "manifest.json")).read() == sc["manifest"]
+    for fname, meta in sc["files"].items():
+        raw = open(os.path.join(ec, fname), "rb").read()
+        assert len(raw) == meta["size"]
+        if "hex" in meta:
+            assert raw.hex() == meta["hex"], fname
+    # digest format pinned by integration.rs:5699-5700: hex(sha256(raw chunk))
+    man = json.loads(sc["manifest"])
+    for c in man["chunks"]:
+        raw = open(os.path.join(ec, f"{c['index']:06}"), "rb").read()
+        assert c["sha256"] == hashlib.sha256(raw).hexdigest()
+    assert ctx.get_object_chunked(ec) == body
+
+
+def test_parity_write_structure(ctx, tmp_path, golden):
+    """integration.rs:3155 — 4 data + 2 parity + manifest = 7 entries, v2."""
+    _, _, ec = _put(ctx, tmp_path, golden, "parity_write_0xAB_350")
+    assert len(os.listdir(ec)) == 7
+    man = json.load(open(os.path.join(ec, "manifest.json")))
+    assert man["version"] == 2 and man["chunk_count"] == 4 and man["parity_shards"] == 2
+    assert len(man["chunks"]) == 6
+    assert all("kind" not in man["chunks"][i] for i in range(4))
+    assert man["chunks"][4]["kind"] == "parity" and man["chunks"][5]["kind"] == "parity"
+
+
+def test_recovery_corrupted_chunk(ctx, tmp_path, golden):
+    """integration.rs:3214 — chunk 1 overwritten with 100 zero bytes."""
+    _, body, ec = _put(ctx, tmp_path, golden, "parity_corrupt_0xEF_350")
+    open(os.path.join(ec, "000001"), "wb").write(bytes(100))
+    assert ctx.get_object_chunked(ec) == body
+    assert ctx.try_reconstruct_data_chunk(ec, 1) == body[100:200]
+
+
+def test_recovery_missing_chunk(ctx, tmp_path, golden):
+    """integration.rs:3239 — chunk 0 deleted."""
+    _, body, ec = _put(ctx, tmp_path, golden, "parity_missing_0x42_350")
+    os.remove(os.path.join(ec, "000000"))
+    assert ctx.get_object_chunked(ec) == body
+
+
+def test_too_many_failures(ctx, tmp_path, golden):
+    """integration.rs:3263 — 3 chunks deleted with m=2: must fail."""
+    _, _, ec = _put(ctx, tmp_path, golden, "parity_too_many_0x77_350")
+    for i in range(3):
+        os.remove(os.path.join(ec, f"{i:06}"))
+    with pytest.raises(maxio_amd.RSError) as e:
+        ctx.get_object_chunked(ec)
+    assert e.value.name == "TooFewShardsPresent"
+    assert "only 3 of 4 required shards available" in str(e.value)
+
+
+def test_range_read_degraded(ctx, tmp_path, golden):
+    """integration.rs:3299 — per-chunk bytes, chunk 1 corrupted, bytes=50-149."""
+    _, body, ec = _put(ctx, tmp_path, golden, "parity_range_per_chunk_350")
+    open(os.path.join(ec, "000001"), "wb").write(bytes(100))
+    assert ctx.get_object_chunked(ec, 50, 100) == body[50:150]
+    assert ctx.get_object_chunked(ec, 340, 10) == body[340:350]
+
+
+def test_empty_object_is_v1(ctx, tmp_path, golden):
+    """integration.rs:3357 — empty object: version 1, no parity fields."""
+    _, _, ec = _put(ctx, tmp_path, golden, "empty_with_parity")
+    man = json.load(open(os.path.join(ec, "manifest.json")))
+    assert man["version"] == 1 and "parity_shards" not in man
+    assert ctx.get_object_chunked(ec) == b""
+
+
+def test_bitrot_without_parity_is_an_error(ctx, tmp_path, golden):
+    """integration.rs:2860 — no parity + corrupt chunk: never the original bytes."""
+    _, _, ec = _put(ctx, tmp_path, golden, "ec_put_get_0x42_3072")
+    raw = bytearray(open(os.path.join(ec, "000001"), "rb").read())
+    raw[10] ^= 0xFF
+    open(os.path.join(ec, "000001"), "wb").write(raw)
+    with pytest.raises(maxio_amd.RSError) as e:
+        ctx.get_object_chunked(ec)
+    assert e.value.name == "Integrity" and "checksum mismatch on chunk 1" in str(e.value)
+
+
+def test_ec_plus_parity_k49_recovery(ctx, tmp_path, golden):
+    """integration.rs:5646 shape — 50 000 B at 1 KiB chunks, m=2 (k=49)."""
+    _, body, ec = _put(ctx, tmp_path, golden, "ec_plus_parity_k49")
+    open(os.path.join(ec, "000001"), "wb").write(bytes(1024))
+    os.remove(os.path.join(ec, "000048"))
+    assert ctx.get_object_chunked(ec) == body
+
+
+def test_write_chunk_then_parity_path(ctx, tmp_path, golden):
+    """write_chunk per chunk + compute_and_write_parity (re-reads the files,
+    filesystem.rs:1108-1113) produce the same files as the batched path."""
+    sc = golden("reference_scenarios.json")["parity_range_per_chunk_350"]
+    body = scenario_body(sc["body"])
+    ec = tmp_path / "x.ec"
+    ec.mkdir()
+    infos = [ctx.write_chunk(str(ec), j, body[j * 100:(j + 1) * 100]) for j in range(4)]
+    pinfos = ctx.compute_and_write_parity(str(ec), 100, 2, infos)
+    man = json.loads(sc["manifest"])
+    assert infos + pinfos == man["chunks"]
+    for fname, meta in sc["files"].items():
+        if "hex" in meta:
+            assert (ec / fname).read_bytes().hex() == meta["hex"]
+
+
+def test_parity_guard_255(ctx, tmp_path):
+    ec = tmp_path / "big.ec"
+    with pytest.raises(maxio_amd.RSError) as e:
+        ctx.put_object_chunked(str(ec), 4, 10, bytes(4 * 250))
+    assert e.value.name == "TooManyShards255"
+    assert "Increase --chunk-size" in str(e.value)
