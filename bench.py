@@ -5,7 +5,7 @@ Step = one pass of the hot path over one batch: Reed–Solomon encode of 1024
 objects per GPU, k=4 data + m=2 parity shards of chunk_size = 10 MiB each
 (MaxIO `--chunk-size 10485760 --parity-shards 2`, 40 MiB objects), inputs
 resident in HBM, parity written to HBM, through the C ABI
-(mxec_encode_strided_device) on torch's current stream.
+(mxec_encode_strided_device) on a dedicated HIP stream.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -114,7 +114,10 @@ def main() -> int:
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--chunk-size", type=int, default=10 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-extra", action="store_true", help="skip the secondary paths")
+    ap.add_argument("--extra", action="store_true",
+                    help="also time the secondary paths (PUT path with SHA-256, config 3 "
+                         "reconstruct + verify, copy peak); off by default so a rocprofv3 "
+                         "run of the default command profiles only the headline kernel")
     args = ap.parse_args()
 
     import torch
@@ -144,8 +147,12 @@ def main() -> int:
     for o in range(n_local):  # per object keeps the randint temporary small
         data[o].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
     parity = torch.zeros((n_local, m, S), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream()
+    # A dedicated stream: the kernels and the HIP events that time them are
+    # on the same queue (a NULL stream would let the library spread calls
+    # over its own streams).
+    stream = torch.cuda.Stream(device=dev)
     sh = stream.cuda_stream
+    torch.cuda.synchronize()
 
     def step():
         ctx.encode_strided_device(k, m, S, n_local, data.data_ptr(), k * S, S, parity.data_ptr(),
@@ -185,8 +192,8 @@ def main() -> int:
     alg_bytes = float(n_local) * (k + m) * S  # per launch, per GPU
     achieved = alg_bytes / (ms_launch * 1e-3) / 1e9
 
-    extra = {}
-    if not args.no_extra and rank == 0:
+    extra = None
+    if args.extra and rank == 0:
         extra = secondary(ctx, torch, dev, sh, data, parity, k, m, S, n_local)
     # free HBM before the CPU leg
     del data, parity
@@ -221,7 +228,7 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": "rs_apply_fast<R=2,V=2>",
+                "kernel": "rs_apply_fast<R=2,V=4,NT=1>",
                 "bytes_per_launch": alg_bytes,
                 "ms_per_launch": round(ms_launch, 4),
                 "traffic_source": tsrc,
@@ -244,8 +251,6 @@ def secondary(ctx, torch, dev, sh, data, parity, k, m, S, n_local) -> dict:
     the same batch, config 3 (reconstruct 8+4, 2 erasures + verify, 1 MiB,
     8192 data chunks) and the device copy peak.  Reported, not the headline."""
     out = {}
-    stream = torch.cuda.current_stream()
-
     def timed(fn, reps):
         fn()
         torch.cuda.synchronize()

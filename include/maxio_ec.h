@@ -129,8 +129,10 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size,
 
 /* ---- device-resident batches ---------------------------------------------
  * All data pointers below are HIP device pointers on ctx device `dev`
- * (index into the ctx's devices).  `stream` is a hipStream_t of that device
- * or NULL for the ctx's own stream.  Calls return after enqueueing, except
+ * (index into the ctx's devices).  `stream` is a hipStream_t of that device;
+ * NULL is the HIP null (default) stream, as in other HIP libraries, so work
+ * the caller queued there is ordered before ours.  Calls return after
+ * enqueueing, except
  * mxec_reconstruct_strided_device which synchronises once to read the
  * verification result (the erasure pattern picks the decode matrix). */
 

@@ -351,7 +351,7 @@ int mxec_encode_strided_device(mxec_ctx* ctx, int dev, void* stream, int k, int 
         if (!data || !parity) return set_error(MXEC_E_INVALID_ARG, "null base pointer");
         DevScope ds;
         MXEC_TRY(ds.open(ctx, dev));
-        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ds.slot->stream;
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
         uint32_t off = 0;
         MXEC_TRY(encode_coef(*ds.d, k, m, &off));
         std::vector<uint64_t> len(static_cast<size_t>(k + m), shard_size);
@@ -389,7 +389,7 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_ob
         if (!objs || !data || !parity) return set_error(MXEC_E_INVALID_ARG, "null argument");
         DevScope ds;
         MXEC_TRY(ds.open(ctx, dev));
-        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ds.slot->stream;
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
         std::vector<uint64_t> dofs(static_cast<size_t>(n_obj)), pofs(static_cast<size_t>(n_obj));
         uint64_t dsum = 0, psum = 0;
         for (uint64_t o = 0; o < n_obj; ++o) {
@@ -450,7 +450,7 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
         DevScope ds;
         MXEC_TRY(ds.open(ctx, dev));
         Slot& slot = *ds.slot;
-        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : slot.stream;
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
         std::vector<uint64_t> len(static_cast<size_t>(total));
         for (int i = 0; i < total; ++i)
             len[size_t(i)] = shard_len ? std::min<uint64_t>(shard_len[i], shard_size) : shard_size;
@@ -543,7 +543,7 @@ int mxec_sha256_batch_device(mxec_ctx* ctx, int dev, void* stream, const uint8_t
         if (!bufs || !lens || !digests_dev) return set_error(MXEC_E_INVALID_ARG, "null argument");
         DevScope ds;
         MXEC_TRY(ds.open(ctx, dev));
-        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ds.slot->stream;
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
         std::vector<const uint8_t*> p(bufs, bufs + n);
         std::vector<uint64_t> l(lens, lens + n);
         return run_sha(*ds.d, *ds.slot, s, p, l, digests_dev, nullptr, nullptr);

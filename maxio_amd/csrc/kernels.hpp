@@ -28,8 +28,15 @@ struct RsArgs {
     uint32_t aligned;               // all pointers 16-byte aligned
 };
 
+// Tuning knobs of the interior kernel (tools/kernel_lab.cpp sweeps them).
+struct RsVariant {
+    int vecs = 2;           // 16-byte column vectors per lane per tile (1, 2, 4)
+    bool nt = false;        // nontemporal loads / stores
+    int blocks_per_cu = 8;  // grid = n_cus * blocks_per_cu (grid-stride)
+};
+
 hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s);
-uint64_t rs_tile_bytes();
+hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& v);
 
 // SHA-256 over n messages, one lane per message.  If `expected` is set the
 // kernel also writes ok[i] = (digest == expected[i]).
@@ -42,6 +49,7 @@ struct ShaArgs {
                                  //   (null: expected[i])
     uint8_t* ok;                 // [n] or null
     uint32_t n;
+    int force = 0;               // 0 auto, 1 one wave per 64 messages, 2 split
 };
 
 hipError_t launch_sha256(const ShaArgs& a, hipStream_t s);

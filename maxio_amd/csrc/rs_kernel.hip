@@ -16,8 +16,9 @@
 //    SGPRs by scalar loads; one of each v_perm's two table dwords must be a
 //    VGPR (gfx950 constant-bus limit 1), the copy is hoisted per input column.
 //  * Input shards are loaded in blocks of 4 so each lane keeps 4*V 16-byte
-//    loads in flight; grid-stride over (object, tile) keeps 8 workgroups per
-//    CU busy without one launch per object.
+//    loads in flight; grid-stride over (object, tile) keeps 16 workgroups per
+//    CU busy without one launch per object.  Loads and stores carry the
+//    nontemporal hint (every byte is touched once).
 //  * Zero padding (the crate pads the short last chunk, filesystem.rs:1111)
 //    is never materialised: bytes at or past in_len read as zero in the
 //    edge-tile path.
@@ -73,7 +74,8 @@ __device__ __forceinline__ void mac_dword(uint32_t (&acc)[R], uint32_t x, const 
         const uint32_t p0 = __builtin_amdgcn_perm(hi[i][0], t[8 * i + 0], s0);
         const uint32_t p1 = __builtin_amdgcn_perm(hi[i][1], t[8 * i + 2], s1);
         const uint32_t p2 = __builtin_amdgcn_perm(s2, t[8 * i + 4], s2);
-        acc[i] ^= p0 ^ p1 ^ p2;
+        // gfx950 v_bitop3_b32: three-input XOR in one instruction.
+        acc[i] = __builtin_amdgcn_bitop3_b32(acc[i], p0, p1, 0x96) ^ p2;
     }
 }
 
@@ -103,18 +105,25 @@ typedef uint8_t __attribute__((address_space(1)))* gptr;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// NT: nontemporal (streaming) hint on the loads and stores — every shard
+// byte is touched exactly once per launch.
+template <bool NT>
 __device__ __forceinline__ Vec4 gload16(gcptr p) {
-    const u32x4 v = *(const u32x4 __attribute__((address_space(1)))*)(p);
+    const auto* q = (const u32x4 __attribute__((address_space(1)))*)(p);
+    const u32x4 v = NT ? __builtin_nontemporal_load(q) : *q;
     return Vec4{{v.x, v.y, v.z, v.w}};
 }
+template <bool NT>
 __device__ __forceinline__ void gstore16(gptr p, const uint32_t (&w)[4]) {
     u32x4 v = {w[0], w[1], w[2], w[3]};
-    *(u32x4 __attribute__((address_space(1)))*)(p) = v;
+    auto* q = (u32x4 __attribute__((address_space(1)))*)(p);
+    if (NT) __builtin_nontemporal_store(v, q);
+    else *q = v;
 }
 
 // Interior tiles: tile t < fast_tiles of every object, all columns in range,
 // all pointers 16-byte aligned.  No bounds checks in the loop.
-template <int R, int V>
+template <int R, int V, bool NT>
 __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint32_t k,
@@ -143,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
             for (int jj = 0; jj < 4; ++jj) {
                 gcptr p = ((gcptr)(ip[j + jj])) + lane;
 #pragma unroll
-                for (int v = 0; v < V; ++v) x[jj][v] = gload16(p + v * kThreads * 16);
+                for (int v = 0; v < V; ++v) x[jj][v] = gload16<NT>(p + v * kThreads * 16);
             }
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * r_total * 8);
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
             Vec4 x[V];
             gcptr p = ((gcptr)(ip[j])) + lane;
 #pragma unroll
-            for (int v = 0; v < V; ++v) x[v] = gload16(p + v * kThreads * 16);
+            for (int v = 0; v < V; ++v) x[v] = gload16<NT>(p + v * kThreads * 16);
             mac_column<R, V>(acc, x, tab + j * r_total * 8);
         }
 #pragma unroll
@@ -161,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 uint32_t ov[4] = {acc[v][0][i], acc[v][1][i], acc[v][2][i], acc[v][3][i]};
-                gstore16(o + v * kThreads * 16, ov);
+                gstore16<NT>(o + v * kThreads * 16, ov);
             }
         }
     }
@@ -211,21 +220,34 @@ __global__ __launch_bounds__(kThreads) void rs_apply_edge(
 
 constexpr int kV = 2;
 
+// Interior kernel for one (R, V, NT) choice.
+template <int R, int V, bool NT>
+hipError_t launch_fast(const RsArgs& a, uint32_t fast_tiles, uint64_t n_fast, uint64_t blocks,
+                       hipStream_t s) {
+    hipLaunchKernelGGL((rs_apply_fast<R, V, NT>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
+                       a.in_ptrs, a.out_ptrs, a.coef, a.coef_off, a.k, a.r_total, a.row0,
+                       fast_tiles, n_fast);
+    return hipGetLastError();
+}
+
 template <int R>
-hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s) {
-    const uint64_t fast_tile = uint64_t(kThreads) * 16 * kV;
+hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& var) {
+    const uint64_t fast_tile = uint64_t(kThreads) * 16 * var.vecs;
     const uint64_t edge_tile = uint64_t(kThreads) * 16;
     // Interior: the first fast_tiles (of fast_tile bytes) of every object.
     uint32_t fast_tiles = 0;
     if (a.aligned) fast_tiles = uint32_t((a.fast_cols < a.shard_size ? a.fast_cols : a.shard_size) / fast_tile);
     const uint64_t n_fast = uint64_t(fast_tiles) * a.n_obj;
     if (n_fast) {
-        uint64_t blocks = uint64_t(n_cus) * 8;
+        uint64_t blocks = uint64_t(n_cus) * uint64_t(var.blocks_per_cu);
         if (blocks > n_fast) blocks = n_fast;
-        hipLaunchKernelGGL((rs_apply_fast<R, kV>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
-                           a.in_ptrs, a.out_ptrs, a.coef, a.coef_off, a.k, a.r_total, a.row0,
-                           fast_tiles, n_fast);
-        hipError_t e = hipGetLastError();
+        hipError_t e = hipErrorInvalidValue;
+        if (var.vecs == 1) e = var.nt ? launch_fast<R, 1, true>(a, fast_tiles, n_fast, blocks, s)
+                                      : launch_fast<R, 1, false>(a, fast_tiles, n_fast, blocks, s);
+        else if (var.vecs == 2) e = var.nt ? launch_fast<R, 2, true>(a, fast_tiles, n_fast, blocks, s)
+                                           : launch_fast<R, 2, false>(a, fast_tiles, n_fast, blocks, s);
+        else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, fast_tiles, n_fast, blocks, s)
+                                           : launch_fast<R, 4, false>(a, fast_tiles, n_fast, blocks, s);
         if (e != hipSuccess) return e;
     }
     // Edge: the rest of each shard, in tiles of edge_tile bytes.
@@ -245,21 +267,30 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s) {
 
 }  // namespace
 
-// Tile geometry exported to the host planner.
-uint64_t rs_tile_bytes() { return uint64_t(kThreads) * 16 * kV; }
-
-hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
+hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& v) {
     switch (a.r) {
-        case 1: return launch_r<1>(a, n_cus, s);
-        case 2: return launch_r<2>(a, n_cus, s);
-        case 3: return launch_r<3>(a, n_cus, s);
-        case 4: return launch_r<4>(a, n_cus, s);
-        case 5: return launch_r<5>(a, n_cus, s);
-        case 6: return launch_r<6>(a, n_cus, s);
-        case 7: return launch_r<7>(a, n_cus, s);
-        case 8: return launch_r<8>(a, n_cus, s);
+        case 1: return launch_r<1>(a, n_cus, s, v);
+        case 2: return launch_r<2>(a, n_cus, s, v);
+        case 3: return launch_r<3>(a, n_cus, s, v);
+        case 4: return launch_r<4>(a, n_cus, s, v);
+        case 5: return launch_r<5>(a, n_cus, s, v);
+        case 6: return launch_r<6>(a, n_cus, s, v);
+        case 7: return launch_r<7>(a, n_cus, s, v);
+        case 8: return launch_r<8>(a, n_cus, s, v);
         default: return hipErrorInvalidValue;
     }
+}
+
+// Default geometry, from tools/kernel_lab sweeps on MI355X (profiles/): four
+// 16-byte vectors per lane with nontemporal loads/stores while the
+// accumulators fit (R <= 4: <= 158 VGPRs), two beyond that; 16 workgroups per
+// CU of grid-stride (16 beat 8 and 4 on every shape swept).
+hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
+    RsVariant v;
+    v.vecs = a.r <= 4 ? 4 : 2;
+    v.nt = true;
+    v.blocks_per_cu = 16;
+    return launch_rs_apply_variant(a, n_cus, s, v);
 }
 
 }  // namespace mxec

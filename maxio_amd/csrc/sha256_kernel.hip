@@ -23,16 +23,23 @@ __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
     return (m & a) | (~m & b);  // v_bfi_b32
 }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+// gfx950 v_bitop3_b32: any 3-input bitwise function in one instruction.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
 
-#define SHA_S0(a) (rotr((a), 2) ^ rotr((a), 13) ^ rotr((a), 22))
-#define SHA_S1(e) (rotr((e), 6) ^ rotr((e), 11) ^ rotr((e), 25))
-#define SHA_s0(x) (rotr((x), 7) ^ rotr((x), 18) ^ ((x) >> 3))
-#define SHA_s1(x) (rotr((x), 17) ^ rotr((x), 19) ^ ((x) >> 10))
+#define SHA_S0(a) xor3(rotr((a), 2), rotr((a), 13), rotr((a), 22))
+#define SHA_S1(e) xor3(rotr((e), 6), rotr((e), 11), rotr((e), 25))
+#define SHA_s0(x) xor3(rotr((x), 7), rotr((x), 18), ((x) >> 3))
+#define SHA_s1(x) xor3(rotr((x), 17), rotr((x), 19), ((x) >> 10))
 
 #define SHA_RND(a, b, c, d, e, f, g, h, kt, wt)                          \
     do {                                                                 \
         const uint32_t t1 = h + SHA_S1(e) + bsel(e, f, g) + (kt) + (wt); \
-        const uint32_t t2 = SHA_S0(a) + bsel((a) ^ (b), c, b);           \
+        const uint32_t t2 = SHA_S0(a) + maj(a, b, c);                    \
         d += t1;                                                         \
         h = t1 + t2;                                                     \
     } while (0)
@@ -80,13 +87,18 @@ __device__ __forceinline__ void compress(uint32_t (&st)[8], uint32_t (&w)[16]) {
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-__device__ __forceinline__ void load_block(const uint8_t* p, uint4 (&blk)[4]) {
-    const uint4* q = reinterpret_cast<const uint4*>(p);
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const u32x4 __attribute__((address_space(1)))* gvec;
+
+// Global (not flat) loads: the message pointers come from a table, so HIP
+// sees generic pointers; the cast keeps the loads on the vmcnt queue only.
+__device__ __forceinline__ void load_block(const uint8_t* p, u32x4 (&blk)[4]) {
+    gvec q = (gvec)(p);
 #pragma unroll
     for (int i = 0; i < 4; ++i) blk[i] = q[i];
 }
 
-__device__ __forceinline__ void block_words(const uint4 (&blk)[4], uint32_t (&w)[16]) {
+__device__ __forceinline__ void block_words(const u32x4 (&blk)[4], uint32_t (&w)[16]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         w[4 * i + 0] = bswap(blk[i].x);
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(64) void sha256_kernel(const uint8_t* const* __rest
                       0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
     uint32_t w[16];
     if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-        uint4 cur[4], nxt[4];
+        u32x4 cur[4], nxt[4];
         if (nfull) load_block(p, cur);
         for (uint64_t b = 0; b < nfull; ++b) {
             if (b + 1 < nfull) load_block(p + 64 * (b + 1), nxt);
@@ -172,13 +184,178 @@ __global__ __launch_bounds__(64) void sha256_kernel(const uint8_t* const* __rest
     if (ok) ok[i] = match ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Split form for latency-bound batches (fewer messages than SIMD slots).
+//
+// One wave issues at most one VALU instruction every ~4 cycles, so a lone
+// message's time per block is its instruction count.  The message schedule
+// (W[16..63]) depends only on the message bytes, not on the state, so a
+// second wave of the same workgroup computes K[t] + W[t] for block b+1 into
+// LDS while the first wave runs the 64 rounds of block b: the serial wave's
+// stream drops from ~1500 to ~950 instructions per block.  LDS is
+// double-buffered, laid out [buf][t/4][lane] x 16 B so each ds_read_b128 /
+// ds_write_b128 is 64 consecutive 16-byte slots (conflict-free).
+// ---------------------------------------------------------------------------
+
+// Ch as one v_bitop3 (0xCA = e ? f : g); t1 = (h + kw + Ch) + S1.
+#define SHA_RNDKW(a, b, c, d, e, f, g, h, kw)                                       \
+    do {                                                                            \
+        const uint32_t hk = h + (kw) + __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);  \
+        const uint32_t t1 = hk + SHA_S1(e);                                         \
+        d += t1;                                                                    \
+        h = t1 + SHA_S0(a) + maj(a, b, c);                                          \
+    } while (0)
+
+#define SHA_4RKW(v)                                  \
+    SHA_RNDKW(a, b, c, d, e, f, g, h, (v).x);        \
+    SHA_RNDKW(h, a, b, c, d, e, f, g, (v).y);        \
+    SHA_RNDKW(g, h, a, b, c, d, e, f, (v).z);        \
+    SHA_RNDKW(f, g, h, a, b, c, d, e, (v).w)
+
+#define SHA_4RKW2(v)                                 \
+    SHA_RNDKW(e, f, g, h, a, b, c, d, (v).x);        \
+    SHA_RNDKW(d, e, f, g, h, a, b, c, (v).y);        \
+    SHA_RNDKW(c, d, e, f, g, h, a, b, (v).z);        \
+    SHA_RNDKW(b, c, d, e, f, g, h, a, (v).w)
+
+// 64 rounds with K[t] + W[t] precomputed in LDS (kwl[q * 64] = words 4q..4q+3).
+__device__ __forceinline__ void compress_kw(uint32_t (&st)[8], const u32x4* kwl) {
+    // All 16 reads issued up front so their latency overlaps the first rounds.
+    u32x4 v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = kwl[q * 64];
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+        SHA_4RKW(v[q]);
+        SHA_4RKW2(v[q + 1]);
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+__constant__ uint32_t kK256[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+// Producer: K + W of one block (w = its 16 big-endian words) into LDS.
+__device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], u32x4* dst) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        uint32_t o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = 4 * q + u;
+            if (t >= 16) SHA_W(t);
+            o[u] = w[t & 15] + kK256[t];
+        }
+        dst[q * 64] = u32x4{o[0], o[1], o[2], o[3]};
+    }
+}
+
+__device__ __forceinline__ void message_words(const uint8_t* p, bool aligned, uint32_t (&w)[16]) {
+    if (aligned) {
+        u32x4 blk[4];
+        load_block(p, blk);
+        block_words(blk, w);
+    } else {
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            w[t] = uint32_t(p[4 * t]) << 24 | uint32_t(p[4 * t + 1]) << 16 |
+                   uint32_t(p[4 * t + 2]) << 8 | uint32_t(p[4 * t + 3]);
+    }
+}
+
+__global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const* __restrict__ ptrs,
+                                                           const uint64_t* __restrict__ lens,
+                                                           uint8_t* __restrict__ digests,
+                                                           const uint8_t* __restrict__ expected,
+                                                           const uint64_t* __restrict__ exp_idx,
+                                                           uint8_t* __restrict__ ok, uint32_t n) {
+    __shared__ u32x4 kw[2][16][64];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * 64 + lane;
+    const bool live = i < n;
+    const uint8_t* p = live ? ptrs[i] : nullptr;
+    const uint64_t len = live ? lens[i] : 0;
+    const uint64_t nfull = len / 64;
+    const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+    // Both waves serve the same 64 messages, so this trip count is the same
+    // in both and every barrier below is reached by both.
+    uint64_t nmax = nfull;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint64_t o = __shfl_xor(nmax, s);
+        nmax = o > nmax ? o : nmax;
+    }
+    uint32_t w[16];
+    if (wave == 1 && nfull > 0) {
+        message_words(p, aligned, w);
+        schedule_kw(w, &kw[0][0][lane]);
+    }
+    __syncthreads();
+    uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                      0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    for (uint64_t b = 0; b < nmax; ++b) {
+        if (wave == 1) {
+            if (b + 1 < nfull) {
+                message_words(p + 64 * (b + 1), aligned, w);
+                schedule_kw(w, &kw[(b + 1) & 1][0][lane]);
+            }
+        } else if (b < nfull) {
+            compress_kw(st, &kw[b & 1][0][lane]);
+        }
+        __syncthreads();
+    }
+    if (wave == 1 || !live) return;
+    const uint32_t rem = uint32_t(len - nfull * 64);
+    const uint8_t* tp = p + nfull * 64;
+    const int nblk = (rem + 9 <= 64) ? 1 : 2;
+    const uint64_t bits = len * 8;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = tail_word(tp, rem, t, nblk, bits);
+    compress(st, w);
+    if (nblk == 2) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) w[t] = tail_word(tp, rem, 16 + t, nblk, bits);
+        compress(st, w);
+    }
+    bool match = true;
+    const uint64_t ei = exp_idx ? exp_idx[i] : i;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const uint32_t be = bswap(st[t]);
+        if (digests) reinterpret_cast<uint32_t*>(digests + 32 * uint64_t(i))[t] = be;
+        if (expected) match &= reinterpret_cast<const uint32_t*>(expected + 32 * ei)[t] == be;
+    }
+    if (ok) ok[i] = match ? 1 : 0;
+}
+
 }  // namespace
+
+// Messages at or below this count run the split (two waves per 64 messages)
+// form: with fewer messages than SIMD slots, a message's latency is the
+// kernel's time; above it, one wave per 64 messages keeps every slot doing
+// rounds (throughput form).
+constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 / 2;
 
 hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const uint32_t blocks = (a.n + 63) / 64;
-    hipLaunchKernelGGL(sha256_kernel, dim3(blocks), dim3(64), 0, s, a.ptrs, a.lens, a.digests,
-                       a.expected, a.exp_idx, a.ok, a.n);
+    const bool split = a.force == 2 || (a.force == 0 && a.n <= kSplitMaxMessages);
+    if (split)
+        hipLaunchKernelGGL(sha256_split_kernel, dim3(blocks), dim3(128), 0, s, a.ptrs, a.lens,
+                           a.digests, a.expected, a.exp_idx, a.ok, a.n);
+    else
+        hipLaunchKernelGGL(sha256_kernel, dim3(blocks), dim3(64), 0, s, a.ptrs, a.lens, a.digests,
+                           a.expected, a.exp_idx, a.ok, a.n);
     return hipGetLastError();
 }
 

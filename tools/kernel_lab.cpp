@@ -1,0 +1,223 @@
+// kernel_lab.cpp — measurement harness for the RS kernel on one MI355X.
+//
+// Calibrates the HBM ceiling with plain streaming kernels (copy, read-only,
+// write-only, and the RS access pattern with the GF math removed: read k
+// shards, write m shards) and sweeps the interior RS kernel's knobs
+// (RsVariant) on the BASELINE shapes.  Development tool, not product; prints
+// one JSON object per measurement.
+//
+//   make -C tools && tools/kernel_lab [n_obj_cfg2]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../maxio_amd/csrc/gf256.hpp"
+#include "../maxio_amd/csrc/kernels.hpp"
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(1);                                                              \
+        }                                                                              \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) d[i] = s[i];
+}
+__global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) acc ^= s[i];
+    if (acc.x == 0x12345678u) d[0] = acc;  // keep the loads alive
+}
+__global__ __launch_bounds__(256) void k_write(u32x4* __restrict__ d, uint64_t n) {
+    const u32x4 v = {1, 2, 3, 4};
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) d[i] = v;
+}
+// RS access pattern without the math: object o, 16-B column c: read k shards,
+// write m shards (XOR of inputs), same layout as the bench.
+__global__ __launch_bounds__(256) void k_pattern(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                 uint32_t k, uint32_t m, uint64_t S, uint64_t n_obj) {
+    const uint64_t vec_per_shard = S / 16;
+    const uint64_t total = n_obj * vec_per_shard;
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < total; t += uint64_t(gridDim.x) * 256) {
+        const uint64_t o = t / vec_per_shard, c = t - o * vec_per_shard;
+        u32x4 acc = {0, 0, 0, 0};
+        for (uint32_t j = 0; j < k; ++j) acc ^= reinterpret_cast<const u32x4*>(data + (o * k + j) * S)[c];
+        for (uint32_t i = 0; i < m; ++i) reinterpret_cast<u32x4*>(par + (o * m + i) * S)[c] = acc + i;
+    }
+}
+
+struct Timer {
+    hipEvent_t a, b;
+    Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+    template <class F>
+    double median_ms(F f, int reps = 7) {
+        f();
+        CK(hipDeviceSynchronize());
+        std::vector<double> t;
+        for (int r = 0; r < reps; ++r) {
+            CK(hipEventRecord(a, 0));
+            f();
+            CK(hipEventRecord(b, 0));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        return t[t.size() / 2];
+    }
+};
+
+struct Shape {
+    int k, r;
+    uint64_t S, n;
+};
+
+// Device descriptors for a strided batch: in = data shard j of object o,
+// out = parity i of object o.
+struct Batch {
+    mxec::RsArgs a{};
+    void* mem = nullptr;
+    Batch(const uint8_t* data, uint8_t* par, Shape sh, const std::vector<uint32_t>& table, uint32_t** coef_dev) {
+        std::vector<const uint8_t*> ip(sh.n * sh.k);
+        std::vector<uint8_t*> op(sh.n * sh.r);
+        std::vector<uint64_t> il(sh.n * sh.k, sh.S), ol(sh.n * sh.r, sh.S);
+        std::vector<uint32_t> co(sh.n, 0);
+        for (uint64_t o = 0; o < sh.n; ++o) {
+            for (int j = 0; j < sh.k; ++j) ip[o * sh.k + j] = data + (o * sh.k + j) * sh.S;
+            for (int i = 0; i < sh.r; ++i) op[o * sh.r + i] = par + (o * sh.r + i) * sh.S;
+        }
+        size_t bytes = ip.size() * 8 + op.size() * 8 + il.size() * 8 + ol.size() * 8 + co.size() * 4 + 64;
+        CK(hipMalloc(&mem, bytes));
+        char* p = static_cast<char*>(mem);
+        auto put = [&](const void* src, size_t n) { CK(hipMemcpy(p, src, n, hipMemcpyHostToDevice)); char* r = p; p += (n + 15) & ~size_t(15); return r; };
+        a.in_ptrs = reinterpret_cast<const uint8_t* const*>(put(ip.data(), ip.size() * 8));
+        a.out_ptrs = reinterpret_cast<uint8_t* const*>(put(op.data(), op.size() * 8));
+        a.in_len = reinterpret_cast<const uint64_t*>(put(il.data(), il.size() * 8));
+        a.out_len = reinterpret_cast<const uint64_t*>(put(ol.data(), ol.size() * 8));
+        a.coef_off = reinterpret_cast<const uint32_t*>(put(co.data(), co.size() * 4));
+        CK(hipMalloc(coef_dev, table.size() * 4));
+        CK(hipMemcpy(*coef_dev, table.data(), table.size() * 4, hipMemcpyHostToDevice));
+        a.coef = *coef_dev;
+        a.shard_size = sh.S;
+        a.fast_cols = sh.S;
+        a.n_obj = uint32_t(sh.n);
+        a.k = uint32_t(sh.k);
+        a.r = uint32_t(sh.r);
+        a.r_total = uint32_t(sh.r);
+        a.row0 = 0;
+        a.aligned = 1;
+    }
+    ~Batch() { (void)hipFree(mem); }
+};
+
+int main(int argc, char** argv) {
+    const uint64_t n2 = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1024;
+    int cus = 256;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    Timer tm;
+    // One pool for everything: config 2 at n2 objects = n2 * 60 MiB.
+    const uint64_t S2 = 10ull << 20;
+    const uint64_t pool = n2 * 6 * S2;
+    uint8_t* buf;
+    CK(hipMalloc(&buf, pool));
+    CK(hipMemset(buf, 0x5A, pool));
+    // random-ish data (the RS math does not branch on data; DVFS might)
+    hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, reinterpret_cast<u32x4*>(buf), pool / 16);
+    CK(hipDeviceSynchronize());
+
+    auto report = [](const char* what, const char* shape, double ms, double bytes) {
+        std::printf("{\"what\": \"%s\", \"shape\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", what, shape, ms,
+                    bytes / (ms * 1e-3) / 1e9);
+        std::fflush(stdout);
+    };
+
+    // ---- calibration ----
+    {
+        const uint64_t half = pool / 2 / 16;
+        auto* s = reinterpret_cast<const u32x4*>(buf);
+        auto* d = reinterpret_cast<u32x4*>(buf + pool / 2);
+        for (int bpc : {4, 8, 16}) {
+            char nm[64];
+            std::snprintf(nm, sizeof nm, "copy_bpc%d", bpc);
+            double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_copy, dim3(cus * bpc), dim3(256), 0, 0, s, d, half); });
+            report(nm, "2x half pool", ms, 2.0 * half * 16);
+        }
+        double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_read, dim3(cus * 8), dim3(256), 0, 0, s, d, half * 2); });
+        report("read", "pool", ms, 2.0 * half * 16);
+        ms = tm.median_ms([&] { hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, d, half); });
+        report("write", "half pool", ms, 1.0 * half * 16);
+        ms = tm.median_ms([&] { hipLaunchKernelGGL(k_pattern, dim3(cus * 8), dim3(256), 0, 0, buf, buf + n2 * 4 * S2, 4u, 2u, S2, n2); });
+        report("pattern_4r2w", "k4m2 S10MiB", ms, double(n2) * 6 * S2);
+    }
+
+    // ---- RS variants ----
+    auto sweep = [&](Shape sh, const char* name, bool full) {
+        auto mat = mxec::rs_matrix(sh.k, sh.r);
+        mxec::GfMatrix rows(sh.r, sh.k);
+        for (int i = 0; i < sh.r; ++i)
+            for (int j = 0; j < sh.k; ++j) rows.at(i, j) = mat->at(sh.k + i, j);
+        uint32_t* coef = nullptr;
+        Batch b(buf, buf + sh.n * sh.k * sh.S, sh, mxec::coef_tables(rows), &coef);
+        const double bytes = double(sh.n) * (sh.k + sh.r) * sh.S;
+        std::vector<mxec::RsVariant> vs;
+        if (full) {
+            for (int v : {1, 2, 4})
+                for (bool nt : {false, true})
+                    for (int bpc : {4, 8, 16}) vs.push_back(mxec::RsVariant{v, nt, bpc});
+        } else {
+            for (int v : {1, 2, 4})
+                for (bool nt : {false, true}) vs.push_back(mxec::RsVariant{v, nt, 8});
+        }
+        for (const auto& v : vs) {
+            double ms = tm.median_ms([&] { CK(mxec::launch_rs_apply_variant(b.a, cus, 0, v)); });
+            char nm[96];
+            std::snprintf(nm, sizeof nm, "rs_v%d_nt%d_bpc%d", v.vecs, int(v.nt), v.blocks_per_cu);
+            report(nm, name, ms, bytes);
+        }
+        (void)hipFree(coef);
+    };
+    // ---- SHA-256: one lane per message ----
+    auto sha = [&](uint64_t n, uint64_t L, const char* name, int force = 0) {
+        std::vector<const uint8_t*> ptrs(n);
+        std::vector<uint64_t> lens(n, L);
+        for (uint64_t i = 0; i < n; ++i) ptrs[i] = buf + i * L;
+        void* d;
+        CK(hipMalloc(&d, n * 8 * 2 + n * 32));
+        CK(hipMemcpy(d, ptrs.data(), n * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(static_cast<char*>(d) + n * 8, lens.data(), n * 8, hipMemcpyHostToDevice));
+        mxec::ShaArgs sa{};
+        sa.ptrs = static_cast<const uint8_t* const*>(d);
+        sa.lens = reinterpret_cast<const uint64_t*>(static_cast<char*>(d) + n * 8);
+        sa.digests = static_cast<uint8_t*>(d) + n * 16;
+        sa.n = uint32_t(n);
+        sa.force = force;
+        double ms = tm.median_ms([&] { CK(mxec::launch_sha256(sa, 0)); }, 3);
+        report("sha256", name, ms, double(n) * L);
+        std::printf("{\"what\": \"sha256_us_per_block\", \"shape\": \"%s\", \"us\": %.3f}\n", name,
+                    ms * 1e3 / (L / 64.0));
+        CK(hipFree(d));
+    };
+    sha(10240, 1ull << 20, "10240 x 1 MiB (cfg3 verify)");
+    sha(10240, 1ull << 20, "10240 x 1 MiB one-wave form", 1);
+    sha(6144, 10ull << 20, "6144 x 10 MiB (cfg2 put path)");
+    sha(1024, 1ull << 20, "1024 x 1 MiB");
+    sha(65536, 64ull << 10, "65536 x 64 KiB");
+    sha(262144, 16ull << 10, "262144 x 16 KiB");
+
+    sweep(Shape{4, 2, S2, n2}, "k4m2 S10MiB (cfg2)", true);
+    sweep(Shape{8, 4, 1ull << 20, n2 * 60 / 12}, "k8m4 S1MiB (north star)", false);
+    sweep(Shape{10, 4, 1ull << 20, n2 * 60 / 14}, "k10m4 S1MiB (cfg4)", false);
+    sweep(Shape{8, 2, 1ull << 20, n2 * 60 / 10}, "k8r2 S1MiB (cfg3 decode)", false);
+    CK(hipFree(buf));
+    return 0;
+}
