@@ -166,6 +166,19 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream,
                              const uint64_t* data_len,
                              uint8_t* const* parity, uint8_t* digests_dev);
 
+/* End-to-end PUT compute for many objects whose chunks are in HOST memory
+ * (request bodies) — the batched form of mxec_encode.  Same array layout as
+ * mxec_encode_batch_device but host pointers; digests (host, sum(k+m)) and
+ * status_out (host, n_obj) may be NULL.  Objects are dealt round-robin over
+ * the ctx's devices; per device, uploads (direct from pinned memory, else via
+ * a pinned ring), RS + SHA-256 kernels and downloads are pipelined on
+ * separate streams with the whole batch resident in HBM.  Blocks until every
+ * parity chunk and digest is in host memory. */
+int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs,
+                           uint64_t n_obj, const uint8_t* const* data,
+                           const uint64_t* data_len, uint8_t* const* parity,
+                           uint8_t (*digests)[32], int32_t* status_out);
+
 /* Uniform reconstruct batch.  Object o, shard i (0 <= i < k+m) lives at
  * shards + o*obj_stride + i*shard_stride.  shard_len (host, k+m entries,
  * NULL = shard_size) is the byte length of shard i in every object.

@@ -10,10 +10,6 @@
 
 using namespace mxec;
 
-struct mxec_ctx {
-    Ctx c;
-};
-
 namespace {
 
 constexpr uint64_t kSlotAlign = 256;

@@ -46,10 +46,10 @@ int decode_coef(Device& dev, const DecodePlan& plan, bool data_only, uint32_t* o
 }
 
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
-           const std::vector<RsObject>& objs) {
+           const std::vector<RsObject>& objs, DescArena* arena) {
     if (objs.empty() || r == 0) return MXEC_OK;
     const size_t n = objs.size();
-    DescWriter w(slot);
+    DescWriter w(slot, arena);
     const size_t o_in = w.add(sizeof(void*) * n * k);
     const size_t o_out = w.add(sizeof(void*) * n * r);
     const size_t o_inlen = w.add(8 * n * k);
@@ -104,11 +104,11 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
 
 int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
             const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
-            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx) {
+            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx, DescArena* arena) {
     (void)dev;
     const size_t n = ptrs.size();
     if (!n) return MXEC_OK;
-    DescWriter w(slot);
+    DescWriter w(slot, arena);
     const size_t o_p = w.add(sizeof(void*) * n);
     const size_t o_l = w.add(8 * n);
     const size_t o_e = exp_idx ? w.add(8 * n) : 0;

@@ -19,14 +19,17 @@ struct RsObject {
 };
 
 // Applies each object's matrix; all objects share (k, r, shard_size).
+// arena: take the descriptor tables from it instead of the slot's ring (many
+// launches in flight, see pipeline.cpp).
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
-           const std::vector<RsObject>& objs);
+           const std::vector<RsObject>& objs, DescArena* arena = nullptr);
 
 // SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be
 // null (see ShaArgs).
 int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
             const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
-            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx = nullptr);
+            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx = nullptr,
+            DescArena* arena = nullptr);
 
 // Coefficient table of the (k, m) encoding matrix's parity rows.
 int encode_coef(Device& dev, int k, int m, uint32_t* off);

@@ -1,0 +1,427 @@
+// pipeline.cpp — end-to-end host-memory batch encode (the PUT path as MaxIO
+// sees it: request bodies in host memory, parity chunks and digests back in
+// host memory), spread over every device of the context.
+//
+// Per device (one host thread each, objects dealt round-robin over devices):
+//   * an HBM object pool holds a whole wave of objects (k+m shard slots and
+//     k+m digests each, up to kPoolCap bytes), so the latency-bound SHA-256
+//     launches of many groups run concurrently instead of waiting on a small
+//     staging window (288 GB of HBM makes this the cheap resource);
+//   * uploads go on a dedicated H2D stream, straight from the caller's buffer
+//     when it is pinned (hipHostMalloc / hipHostRegister), else through a ring
+//     of pinned staging buffers filled by memcpy;
+//   * each group of objects gets its RS launch(es) on the RS stream right
+//     behind its upload; one SHA-256 launch then covers every chunk of the
+//     wave (a message's hash latency does not depend on the batch size, so
+//     one launch finishes as early as any split of it); descriptor tables
+//     come from a per-wave arena so nothing throttles the launches in flight;
+//   * parity returns group by group on a D2H stream as RS finishes, digests
+//     after the SHA launch, direct to pinned destinations or via a pinned ring.
+// Results are bit-identical to mxec_encode (same kernels, same planner).
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#include "../../include/maxio_ec.h"
+#include "ops.hpp"
+
+namespace mxec {
+namespace {
+
+constexpr uint64_t kAlign = 256;
+constexpr uint64_t kPoolCap = uint64_t(96) << 30;     // HBM per wave per device
+constexpr uint64_t kGroupBytes = uint64_t(256) << 20;  // input bytes per group
+constexpr uint64_t kRingBuf = uint64_t(64) << 20;      // pinned ring buffer size
+constexpr int kRing = 4;
+constexpr int kComputeStreams = 2;  // RS stream + SHA stream (4 HW queues per process)
+
+uint64_t rup(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+bool pinned_addr(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+bool is_pinned(const void* p, uint64_t len) {
+    return p && len && pinned_addr(p) && pinned_addr(static_cast<const uint8_t*>(p) + len - 1);
+}
+
+struct HostObj {
+    int k, m;
+    uint64_t S;
+    const uint8_t* const* data;
+    const uint64_t* dlen;
+    uint8_t* const* parity;
+    uint8_t (*dig)[32];
+    uint64_t pool_off = 0;  // device image: k+m shard slots of rup(S) bytes
+    uint64_t slot() const { return rup(S, kAlign); }
+    uint64_t bytes() const { return uint64_t(k + m) * slot(); }
+};
+
+class PinRing {
+public:
+    int init() {
+        for (int i = 0; i < kRing; ++i) {
+            MXEC_TRY(buf_[i].ensure(kRingBuf));
+            MXEC_HIP(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming));
+        }
+        return MXEC_OK;
+    }
+    ~PinRing() {
+        for (auto e : ev_)
+            if (e) (void)hipEventDestroy(e);
+    }
+    int next() const { return next_; }
+    void* ptr(int i) { return buf_[i].p; }
+    hipEvent_t event(int i) { return ev_[i]; }
+    // Claim the next buffer, waiting for the DMA that last used it.
+    int take(int* i) {
+        *i = next_;
+        next_ = (next_ + 1) % kRing;
+        if (busy_[*i]) MXEC_HIP(hipEventSynchronize(ev_[*i]));
+        busy_[*i] = false;
+        return MXEC_OK;
+    }
+    int mark(int i, hipStream_t s) {
+        MXEC_HIP(hipEventRecord(ev_[i], s));
+        busy_[i] = true;
+        return MXEC_OK;
+    }
+    void release_all() {
+        for (auto& b : busy_) b = false;
+    }
+
+private:
+    PinnedBuf buf_[kRing];
+    hipEvent_t ev_[kRing] = {};
+    bool busy_[kRing] = {};
+    int next_ = 0;
+};
+
+// Long-lived per-device resources of the pipeline.
+struct PipeRes {
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    hipStream_t cs[kComputeStreams] = {};
+    PinRing in, out;
+    DescArena arena;
+    DevBuf pool, digests;
+    Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
+    bool ready = false;
+    int init() {
+        if (ready) return MXEC_OK;
+        MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+        MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+        for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        MXEC_TRY(in.init());
+        MXEC_TRY(out.init());
+        ready = true;
+        return MXEC_OK;
+    }
+    ~PipeRes() {
+        for (auto s : cs)
+            if (s) (void)hipStreamDestroy(s);
+        if (h2d) (void)hipStreamDestroy(h2d);
+        if (d2h) (void)hipStreamDestroy(d2h);
+    }
+};
+
+class DevicePipeline {
+public:
+    DevicePipeline(Device& d, PipeRes& r)
+        : d_(d), h2d_(r.h2d), d2h_(r.d2h), cs_(r.cs), in_(r.in), out_(r.out), arena_(r.arena),
+          pool_(r.pool), scratch_(r.digests), slot_(r.desc_slot) {}
+    ~DevicePipeline() {
+        for (auto e : events_) (void)hipEventDestroy(e);
+    }
+
+    int run(std::vector<HostObj>& objs) {
+        size_t o = 0;
+        while (o < objs.size()) {  // waves that fit the pool
+            uint64_t need = 0, desc = 1 << 20;
+            size_t e = o;
+            while (e < objs.size() && (e == o || need + objs[e].bytes() <= kPoolCap)) {
+                objs[e].pool_off = need;
+                need += objs[e].bytes();
+                desc += uint64_t(objs[e].k + objs[e].m) * 48 + 256;
+                ++e;
+            }
+            MXEC_TRY(pool_.ensure(need));
+            MXEC_TRY(arena_.reserve(desc * 2));
+            MXEC_TRY(wave(objs, o, e));
+            o = e;
+        }
+        return MXEC_OK;
+    }
+
+private:
+    struct Pending {  // ring DMA to copy out into pageable memory
+        int ring;
+        uint8_t* dst;
+        uint64_t len;
+    };
+
+    Device& d_;
+    hipStream_t h2d_, d2h_;
+    hipStream_t* cs_;
+    PinRing& in_;
+    PinRing& out_;
+    DescArena& arena_;
+    DevBuf& pool_;
+    DevBuf& scratch_;  // the wave's digests, message order
+    Slot& slot_;
+    std::vector<Pending> pend_;
+    std::vector<hipEvent_t> events_;
+
+    int new_event(hipEvent_t* e) {
+        MXEC_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        events_.push_back(*e);
+        return MXEC_OK;
+    }
+
+    int upload(uint8_t* dst, const uint8_t* src, uint64_t len) {
+        if (!len) return MXEC_OK;
+        if (is_pinned(src, len)) {
+            MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, h2d_));
+            return MXEC_OK;
+        }
+        for (uint64_t off = 0; off < len; off += kRingBuf) {
+            const uint64_t n = std::min(kRingBuf, len - off);
+            int r;
+            MXEC_TRY(in_.take(&r));
+            std::memcpy(in_.ptr(r), src + off, n);
+            MXEC_HIP(hipMemcpyAsync(dst + off, in_.ptr(r), n, hipMemcpyHostToDevice, h2d_));
+            MXEC_TRY(in_.mark(r, h2d_));
+        }
+        return MXEC_OK;
+    }
+
+    // Copy out the pending ring buffer the next take() will reuse.
+    int drain_next() {
+        const int r = out_.next();
+        for (size_t i = 0; i < pend_.size(); ++i) {
+            if (pend_[i].ring != r) continue;
+            MXEC_HIP(hipEventSynchronize(out_.event(r)));
+            std::memcpy(pend_[i].dst, out_.ptr(r), pend_[i].len);
+            pend_.erase(pend_.begin() + long(i));
+            break;
+        }
+        return MXEC_OK;
+    }
+
+    int download(uint8_t* dst, const uint8_t* src, uint64_t len) {
+        if (!len) return MXEC_OK;
+        if (is_pinned(dst, len)) {
+            MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, d2h_));
+            return MXEC_OK;
+        }
+        for (uint64_t off = 0; off < len; off += kRingBuf) {
+            const uint64_t n = std::min(kRingBuf, len - off);
+            MXEC_TRY(drain_next());
+            int r;
+            MXEC_TRY(out_.take(&r));
+            MXEC_HIP(hipMemcpyAsync(out_.ptr(r), src + off, n, hipMemcpyDeviceToHost, d2h_));
+            MXEC_TRY(out_.mark(r, d2h_));
+            pend_.push_back(Pending{r, dst + off, n});
+        }
+        return MXEC_OK;
+    }
+
+    int flush() {
+        MXEC_HIP(hipStreamSynchronize(d2h_));
+        for (auto& p : pend_) std::memcpy(p.dst, out_.ptr(p.ring), p.len);
+        pend_.clear();
+        out_.release_all();
+        return MXEC_OK;
+    }
+
+    int wave(std::vector<HostObj>& objs, size_t o0, size_t o1) {
+        Slot& slot = slot_;
+        uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        uint64_t msgs = 0;
+        for (size_t o = o0; o < o1; ++o) msgs += uint64_t(objs[o].k + objs[o].m);
+        MXEC_TRY(scratch_.ensure(msgs * 32));
+        uint8_t* digests = static_cast<uint8_t*>(scratch_.p);
+        // Groups: consecutive objects up to kGroupBytes of input.
+        std::vector<std::pair<size_t, size_t>> groups;
+        for (size_t g0 = o0; g0 < o1;) {
+            size_t g1 = g0;
+            uint64_t in_bytes = 0;
+            while (g1 < o1 && (g1 == g0 || in_bytes + uint64_t(objs[g1].k) * objs[g1].S <= kGroupBytes)) {
+                in_bytes += uint64_t(objs[g1].k) * objs[g1].S;
+                ++g1;
+            }
+            groups.emplace_back(g0, g1);
+            g0 = g1;
+        }
+        // Phase 1: each group's upload and RS launch(es), in order.  The
+        // host only waits on the input ring (an H2D copy), so uploads stream
+        // at PCIe rate while RS runs behind them.
+        std::vector<hipEvent_t> done(groups.size());
+        hipStream_t rs_s = cs_[0], sha_s = cs_[1];
+        for (size_t g = 0; g < groups.size(); ++g) {
+            const size_t g0 = groups[g].first, g1 = groups[g].second;
+            for (size_t o = g0; o < g1; ++o) {
+                const HostObj& h = objs[o];
+                for (int j = 0; j < h.k; ++j)
+                    MXEC_TRY(upload(base + h.pool_off + uint64_t(j) * h.slot(), h.data[j], h.dlen[j]));
+            }
+            hipEvent_t up;
+            MXEC_TRY(new_event(&up));
+            MXEC_TRY(new_event(&done[g]));
+            MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_HIP(hipStreamWaitEvent(rs_s, up, 0));
+            std::map<std::tuple<int, int, uint64_t>, std::vector<size_t>> classes;
+            for (size_t o = g0; o < g1; ++o) classes[{objs[o].k, objs[o].m, objs[o].S}].push_back(o);
+            for (auto& c : classes) {
+                const int k = std::get<0>(c.first), m = std::get<1>(c.first);
+                const uint64_t S = std::get<2>(c.first);
+                uint32_t coff = 0;
+                MXEC_TRY(encode_coef(d_, k, m, &coff));
+                const size_t n = c.second.size();
+                std::vector<const uint8_t*> ins(n * size_t(k));
+                std::vector<uint8_t*> outs(n * size_t(m));
+                std::vector<uint64_t> lens(n * size_t(k + m), S);
+                std::vector<RsObject> ro(n);
+                for (size_t t = 0; t < n; ++t) {
+                    const HostObj& h = objs[c.second[t]];
+                    uint8_t* ob = base + h.pool_off;
+                    for (int j = 0; j < k; ++j) {
+                        ins[t * k + j] = ob + uint64_t(j) * h.slot();
+                        lens[t * (k + m) + j] = std::min<uint64_t>(h.dlen[j], S);
+                    }
+                    for (int i = 0; i < m; ++i) outs[t * m + i] = ob + uint64_t(k + i) * h.slot();
+                    ro[t] = RsObject{&ins[t * k], &lens[t * (k + m)], &outs[t * m], &lens[t * (k + m) + k], coff};
+                }
+                MXEC_TRY(run_rs(d_, slot, rs_s, S, k, m, ro, &arena_));
+            }
+            MXEC_HIP(hipEventRecord(done[g], rs_s));
+        }
+        // Phase 2: ONE SHA-256 launch over every chunk of the wave once all
+        // parity exists.  A message's hash time does not depend on how many
+        // messages share the launch (up to the split-form limit), so one
+        // launch ends as early as any split of it would, and it needs no
+        // more than one hardware queue.
+        std::vector<const uint8_t*> sp;
+        std::vector<uint64_t> sl;
+        for (size_t o = o0; o < o1; ++o) {
+            const HostObj& h = objs[o];
+            if (!h.dig) continue;  // caller asked for no digests
+            for (int j = 0; j < h.k + h.m; ++j) {
+                sp.push_back(base + h.pool_off + uint64_t(j) * h.slot());
+                sl.push_back(j < h.k ? std::min<uint64_t>(h.dlen[j], h.S) : h.S);
+            }
+        }
+        hipEvent_t sha_done = nullptr;
+        if (!sp.empty()) {
+            MXEC_TRY(new_event(&sha_done));
+            MXEC_HIP(hipStreamWaitEvent(sha_s, done.back(), 0));
+            MXEC_TRY(run_sha(d_, slot, sha_s, sp, sl, digests, nullptr, nullptr, nullptr, &arena_));
+            MXEC_HIP(hipEventRecord(sha_done, sha_s));
+        }
+        // Phase 3: parity back group by group as RS finishes, digests last.
+        for (size_t g = 0; g < groups.size(); ++g) {
+            MXEC_HIP(hipStreamWaitEvent(d2h_, done[g], 0));
+            for (size_t o = groups[g].first; o < groups[g].second; ++o) {
+                const HostObj& h = objs[o];
+                uint8_t* ob = base + h.pool_off;
+                for (int i = 0; i < h.m; ++i)
+                    MXEC_TRY(download(h.parity[i], ob + uint64_t(h.k + i) * h.slot(), h.S));
+            }
+        }
+        if (sha_done) {
+            MXEC_HIP(hipStreamWaitEvent(d2h_, sha_done, 0));
+            uint64_t msg0 = 0;
+            for (size_t o = o0; o < o1; ++o) {
+                const HostObj& h = objs[o];
+                if (!h.dig) continue;
+                MXEC_TRY(download(reinterpret_cast<uint8_t*>(h.dig), digests + msg0 * 32, uint64_t(h.k + h.m) * 32));
+                msg0 += uint64_t(h.k + h.m);
+            }
+        }
+        return flush();
+    }
+
+};
+
+}  // namespace
+}  // namespace mxec
+
+using namespace mxec;
+
+extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, uint64_t n_obj,
+                                      const uint8_t* const* data, const uint64_t* data_len,
+                                      uint8_t* const* parity, uint8_t (*digests)[32],
+                                      int32_t* status_out) {
+    try {
+        if (n_obj == 0) return MXEC_OK;
+        if (!ctx || !objs || !data || !parity) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        const size_t D = ctx->c.devs.size();
+        if (!D) return set_error(MXEC_E_NO_DEVICE, "context has no device");
+        uint64_t dsum = 0;
+        for (uint64_t o = 0; o < n_obj; ++o) dsum += uint64_t(std::max(objs[o].k, 0));
+        std::vector<uint64_t> dlen(size_t(dsum), 0);
+        std::vector<std::vector<HostObj>> per(D);
+        uint64_t doff = 0, poff = 0, goff = 0;
+        int first_err = MXEC_OK;
+        std::string first_msg;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            const int k = objs[o].k, m = objs[o].m;
+            const uint64_t S = objs[o].shard_size;
+            int st = check_km(k, m);
+            if (st == MXEC_OK && S == 0) st = set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+            for (int j = 0; st == MXEC_OK && j < k; ++j) {
+                const uint64_t l = data_len ? data_len[doff + uint64_t(j)] : S;
+                if (l > S) st = set_error(MXEC_E_INCORRECT_SHARD_SIZE, "data chunk longer than shard_size");
+                dlen[size_t(doff) + size_t(j)] = l;
+            }
+            if (status_out) status_out[o] = st;
+            if (st != MXEC_OK) {
+                if (first_err == MXEC_OK) {
+                    first_err = st;
+                    first_msg = last_error();
+                }
+            } else {
+                HostObj h{k, m, S, data + doff, &dlen[size_t(doff)], parity + poff, digests ? digests + goff : nullptr};
+                per[o % D].push_back(h);
+            }
+            doff += uint64_t(std::max(k, 0));
+            poff += uint64_t(std::max(m, 0));
+            goff += uint64_t(std::max(k, 0) + std::max(m, 0));
+        }
+        std::vector<int> rcs(D, MXEC_OK);
+        std::vector<std::string> errs(D);
+        std::vector<std::thread> th;
+        for (size_t d = 0; d < D; ++d) {
+            if (per[d].empty()) continue;
+            th.emplace_back([&, d] {
+                Device& dev = *ctx->c.devs[d];
+                rcs[d] = [&]() -> int {
+                    MXEC_HIP(hipSetDevice(dev.id));
+                    std::lock_guard<std::mutex> g(dev.pipe_mu);
+                    if (!dev.pipe) dev.pipe = std::make_shared<PipeRes>();
+                    PipeRes& r = *static_cast<PipeRes*>(dev.pipe.get());
+                    MXEC_TRY(r.init());
+                    DevicePipeline p(dev, r);
+                    return p.run(per[d]);
+                }();
+                if (rcs[d] != MXEC_OK) errs[d] = last_error();
+            });
+        }
+        for (auto& t : th) t.join();
+        for (size_t d = 0; d < D; ++d)
+            if (rcs[d] != MXEC_OK) return set_error(rcs[d], errs[d]);
+        if (first_err != MXEC_OK) return set_error(first_err, first_msg);
+        return MXEC_OK;
+    } catch (const std::bad_alloc&) {
+        return set_error(MXEC_E_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return set_error(MXEC_E_INVALID_ARG, e.what());
+    }
+}

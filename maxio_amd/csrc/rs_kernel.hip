@@ -218,7 +218,6 @@ __global__ __launch_bounds__(kThreads) void rs_apply_edge(
     }
 }
 
-constexpr int kV = 2;
 
 // Interior kernel for one (R, V, NT) choice.
 template <int R, int V, bool NT>

@@ -53,6 +53,18 @@ size_t DescWriter::add(size_t bytes) {
 }
 
 int DescWriter::commit(hipStream_t stream, char** dev_base) {
+    if (arena_) {
+        const size_t n = (tmp_.size() + 255) & ~size_t(255);
+        if (arena_->used + n > arena_->host.cap || arena_->used + n > arena_->dev.cap)
+            return set_error(MXEC_E_OOM, "descriptor arena exhausted");
+        char* h = static_cast<char*>(arena_->host.p) + arena_->used;
+        char* d = static_cast<char*>(arena_->dev.p) + arena_->used;
+        std::memcpy(h, tmp_.data(), tmp_.size());
+        if (n) MXEC_HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream));
+        arena_->used += n;
+        *dev_base = d;
+        return MXEC_OK;
+    }
     buf_ = &slot_.ring[slot_.ring_next];
     slot_.ring_next = (slot_.ring_next + 1) % Slot::kRing;
     if (!buf_->done) MXEC_HIP(hipEventCreateWithFlags(&buf_->done, hipEventDisableTiming));
@@ -70,7 +82,7 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
 }
 
 int DescWriter::finish(hipStream_t stream) {
-    if (!buf_) return MXEC_OK;
+    if (arena_ || !buf_) return MXEC_OK;
     MXEC_HIP(hipEventRecord(buf_->done, stream));
     buf_->pending = true;
     return MXEC_OK;

@@ -80,6 +80,10 @@ struct Device {
     DevBuf coef;
     size_t coef_used = 0;  // dwords
     std::map<std::vector<uint8_t>, uint32_t> coef_index;
+    // Host-batch pipeline state (pipeline.cpp): streams, pinned rings, pools;
+    // created on first use and kept, one batch at a time per device.
+    std::mutex pipe_mu;
+    std::shared_ptr<void> pipe;
 };
 
 struct Ctx {
@@ -87,11 +91,25 @@ struct Ctx {
     std::atomic<unsigned> rr{0};
 };
 
+// Descriptor tables of many launches in flight at once (host pipeline): one
+// pinned + device region, bump-allocated, never reused until reset().
+struct DescArena {
+    PinnedBuf host;
+    DevBuf dev;
+    size_t used = 0;
+    int reserve(size_t bytes) {
+        MXEC_TRY(host.ensure(bytes));
+        MXEC_TRY(dev.ensure(bytes));
+        used = 0;
+        return 0;
+    }
+};
+
 // Builds one launch's descriptor tables in a pinned ring buffer, uploads
 // them on `stream`, and hands back device pointers.
 class DescWriter {
 public:
-    DescWriter(Slot& slot) : slot_(slot) {}
+    explicit DescWriter(Slot& slot, DescArena* arena = nullptr) : slot_(slot), arena_(arena) {}
     // Reserve `bytes` (16-byte aligned); returns its offset.  Host pointers
     // into the tables are data() + offset, valid once every add() is done.
     size_t add(size_t bytes);
@@ -103,6 +121,7 @@ public:
 
 private:
     Slot& slot_;
+    DescArena* arena_;
     DescBuf* buf_ = nullptr;
     std::vector<char> tmp_;
 };
@@ -112,6 +131,15 @@ int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<
                 uint32_t* off);
 
 Device* pick_device(Ctx* ctx, int dev_index);
+
+}  // namespace mxec
+
+// The opaque handle of include/maxio_ec.h.
+struct mxec_ctx {
+    mxec::Ctx c;
+};
+
+namespace mxec {
 Slot& lock_slot(Device& dev, std::unique_lock<std::mutex>& lk);
 
 }  // namespace mxec

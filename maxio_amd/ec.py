@@ -204,6 +204,20 @@ class Context:
             self._h, dev, stream, arr, len(objs), _pp(data_ptrs),
             _u64p(data_len) if data_len is not None else None, _pp(parity_ptrs), digests_ptr))
 
+    def encode_batch_host(self, objs: Sequence[tuple], data_ptrs, parity_ptrs, data_len=None,
+                          digests: Optional[np.ndarray] = None):
+        """mxec_encode_batch_host: host pointers in and out (ints), pipelined
+        over every device.  digests: uint8 array of sum(k+m)*32 or None.
+        Returns the per-object status array."""
+        arr = (N.Object * len(objs))(*[N.Object(k, m, s) for (k, m, s) in objs])
+        status = np.zeros(max(1, len(objs)), np.int32)
+        _check(self._lib.mxec_encode_batch_host(
+            self._h, arr, len(objs), _pp(data_ptrs),
+            _u64p(data_len) if data_len is not None else None, _pp(parity_ptrs),
+            digests.ctypes.data_as(N.U8P) if digests is not None else None,
+            status.ctypes.data_as(N.I32P)))
+        return status[: len(objs)]
+
     def reconstruct_strided_device(self, k, m, shard_size, n_obj, shards_ptr, obj_stride,
                                    shard_stride, present: np.ndarray, shard_len=None,
                                    expected_ptr=None, data_only=False, dev=0, stream=None):
