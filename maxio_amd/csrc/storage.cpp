@@ -267,9 +267,12 @@ int read_manifest(const fs::path& ec_dir, Manifest& m) {
 }
 
 // try_reconstruct_data_chunk over files: read every shard, verify against the
-// manifest digest, reconstruct on the GPU, return chunks[target].size bytes.
-int reconstruct_from_dir(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_t target,
-                         std::vector<uint8_t>& out) {
+// manifest digest, reconstruct on the GPU, return chunks[t].size bytes for
+// every requested target.  The reference runs this once per bad chunk, each
+// time re-reading and re-verifying all k+m shards; one pass rebuilds every
+// missing shard, so several bad chunks of a GET cost one decode.
+int reconstruct_from_dir(mxec_ctx* ctx, const fs::path& dir, const Manifest& man,
+                         const std::vector<uint32_t>& targets, std::vector<std::vector<uint8_t>*> outs) {
     const int k = int(man.chunk_count);
     const int m = man.has_parity ? int(man.parity_shards) : 0;
     const uint64_t shard = man.has_shard ? man.shard_size : man.chunk_size;
@@ -309,8 +312,11 @@ int reconstruct_from_dir(mxec_ctx* ctx, const fs::path& dir, const Manifest& man
     rc = mxec_reconstruct(ctx, k, m, shard, ptrs.data(), lens.data(),
                           reinterpret_cast<const uint8_t(*)[32]>(expected.data()), present.data(), 0, &np);
     if (rc) return rc;
-    const uint64_t real = std::min<uint64_t>(man.chunks[target].size, shard);
-    out.assign(bufs[target].begin(), bufs[target].begin() + long(real));
+    for (size_t t = 0; t < targets.size(); ++t) {
+        const uint32_t target = targets[t];
+        const uint64_t real = std::min<uint64_t>(man.chunks[target].size, shard);
+        outs[t]->assign(bufs[target].begin(), bufs[target].begin() + long(real));
+    }
     return MXEC_OK;
 }
 
@@ -440,7 +446,7 @@ int mxec_try_reconstruct_data_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t 
     MXEC_TRY(read_manifest(ec_dir, man));
     if (target >= man.chunk_count) return set_error(MXEC_E_INVALID_INDEX, "target is not a data chunk");
     std::vector<uint8_t> buf;
-    MXEC_TRY(reconstruct_from_dir(ctx, ec_dir, man, target, buf));
+    MXEC_TRY(reconstruct_from_dir(ctx, ec_dir, man, {target}, {&buf}));
     *out_len = buf.size();
     if (buf.size() > out_cap || (buf.size() && !out)) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
     if (!buf.empty()) std::memcpy(out, buf.data(), buf.size());
@@ -503,13 +509,19 @@ int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, 
             }
         }
     }
+    // Recovery (:130-150): without parity the first bad chunk is the error;
+    // with parity every bad chunk of the range is rebuilt in one decode.
+    std::vector<uint32_t> bad;
+    std::vector<std::vector<uint8_t>*> bad_out;
+    for (uint32_t c = 0; c < n; ++c) {
+        if (!state[c]) continue;
+        if (!(man.has_parity && man.parity_shards > 0)) return set_error(MXEC_E_INTEGRITY, err[c]);
+        bad.push_back(start + c);
+        bad_out.push_back(&data[c]);
+    }
+    if (!bad.empty()) MXEC_TRY(reconstruct_from_dir(ctx, dir, man, bad, bad_out));
     uint64_t remaining = length, pos = 0;
     for (uint32_t c = 0; c < n && remaining; ++c) {
-        if (state[c]) {
-            if (!(man.has_parity && man.parity_shards > 0))
-                return set_error(MXEC_E_INTEGRITY, err[c]);
-            MXEC_TRY(reconstruct_from_dir(ctx, dir, man, start + c, data[c]));
-        }
         const uint64_t avail = data[c].size() > skip ? data[c].size() - skip : 0;
         const uint64_t take = std::min(avail, remaining);
         if (take) std::memcpy(out + pos, data[c].data() + skip, take);
