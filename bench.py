@@ -1,22 +1,30 @@
 #!/usr/bin/env python3
-"""bench.py — device-resident RS encode throughput on MI355X (BASELINE configs[1]).
+"""bench.py — device-resident RS encode / reconstruct throughput on MI355X.
 
-Step = one pass of the hot path over one batch: Reed–Solomon encode of 1024
-objects per GPU, k=4 data + m=2 parity shards of chunk_size = 10 MiB each
-(MaxIO `--chunk-size 10485760 --parity-shards 2`, 40 MiB objects), inputs
-resident in HBM, parity written to HBM, through the C ABI
+Default step (BASELINE configs[1], the metric's configuration): Reed–Solomon
+encode of 1024 objects per GPU, k=4 data + m=2 parity shards of chunk_size =
+10 MiB each (MaxIO `--chunk-size 10485760 --parity-shards 2`, 40 MiB objects),
+inputs resident in HBM, parity written to HBM, through the C ABI
 (mxec_encode_strided_device) on a dedicated HIP stream.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4a|4b|5] [--extra]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Other BASELINE configs (same JSON line, for DESIGN.md / profiles):
+  3   reconstruct k=8 m=4, 2 data erasures + SHA-256 verify of the 10 present
+      shards, 1 MiB chunks, 1024 objects (8192 data chunks) per GPU
+  4a  encode k=10 m=4, 1 MiB chunks (10 MiB objects), 4096 objects per GPU
+  4b  encode k=64 m=4, 1 MiB chunks (literal 64 MiB objects), 640 per GPU
+  5   mixed 4+2 / 8+4 / 10+4 at 64 KiB..10 MiB chunks with short last chunks:
+      encode the batch, then reconstruct it with seeded erasures, per step
+
 One process per GPU; objects are partitioned per GPU (weak scaling, no
-collective on the data path; only the timing barrier / max-reduce).
-Rank 0 prints ONE JSON line.  value = payload GiB/s (k * chunk_size bytes per
-object) over all GPUs; roofline = the RS kernel's algorithmic bytes
-((k+m) * chunk_size per object) / its HIP-event-timed duration vs 8 TB/s;
-cpu_baseline = oracle/ (C restatement of the crate's pure-Rust path) timed on
-one host core over a bounded sample.
+collective on the data path; only the timing barrier / max-reduce).  Rank 0
+prints ONE JSON line.  value = payload GiB/s (k * chunk_size bytes per object)
+over all GPUs; roofline = the dominant kernel's algorithmic bytes / its
+HIP-event-timed duration vs 8 TB/s; cpu_baseline = oracle/ (C restatement of
+the crate's pure-Rust path) on one host core over a bounded sample, plus the
+same on every host core as cpu_baseline_all_cores.
 """
 from __future__ import annotations
 
@@ -25,6 +33,7 @@ import glob
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +42,7 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident RS encode+reconstruct GiB/s (k+m, chunk_size); % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GIB = float(1 << 30)
+SEED = 0x6D6178696F  # "maxio"
 
 
 def shard_objects(n_total: int, rank: int, world: int) -> range:
@@ -61,47 +71,276 @@ def barrier():
         dist.barrier()
 
 
-def cpu_baseline(k: int, m: int, size: int, seconds: float) -> dict:
-    """The reference's CPU encode (crate input-major MUL_TABLE lookups,
-    restated in oracle/) on one core, over a bounded sample."""
-    import numpy as np
-
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/baseline infrastructure only
 
-    rng = np.random.default_rng(0x6D6178696F)
-    objs = [[rng.integers(0, 256, size, dtype=np.uint8) for _ in range(k)] for _ in range(2)]
-    oracle.encode(objs[0], m, size)  # warm tables / page in
-    n, t0 = 0, time.perf_counter()
-    while True:
-        oracle.encode(objs[n % 2], m, size)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {
-        "value": round(n * k * size / GIB / el, 4),
-        "unit": "GiB/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"{n} objects (2 distinct, reused) of k={k} m={m} chunk_size={size} encoded "
-                  f"serially in {el:.1f}s by oracle/rs_oracle.c (crate 6.0.0 pure-Rust "
-                  f"mul_slice restated: 64 KiB MUL_TABLE, input-major), 1 thread",
-    }
+    return oracle
 
 
-def pmc_traffic(config_tag: str):
+def cpu_leg(work, payload_per_call: int, seconds: float, threads: int):
+    """Run `work(i)` (an oracle call; ctypes drops the GIL) on `threads`
+    threads for about `seconds`; returns (GiB/s, calls, elapsed)."""
+    work(0)  # warm tables / page in
+    stop = time.perf_counter() + seconds
+    counts = [0] * threads
+
+    def run(t):
+        while time.perf_counter() < stop:
+            work(t)
+            counts[t] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    n = sum(counts)
+    return n * payload_per_call / GIB / el, n, el
+
+
+# ---- workloads ------------------------------------------------------------------
+
+
+class Encode:
+    """RS encode of n uniform objects (data [n][k][S] -> parity [n][m][S])."""
+
+    bound = "hbm"
+
+    def __init__(self, torch, ctx, dev, sh, k, m, S, n, label, seed):
+        self.torch, self.ctx, self.sh = torch, ctx, sh
+        self.k, self.m, self.S, self.n = k, m, S, n
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self.data = torch.empty((n, k, S), dtype=torch.uint8, device=dev)
+        for o in range(n):  # per object keeps the randint temporary small
+            self.data[o].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
+        self.parity = torch.zeros((n, m, S), dtype=torch.uint8, device=dev)
+        self.payload = n * k * S
+        self.alg_bytes = n * (k + m) * S
+        r = min(m, 8)
+        self.kernel = f"rs_apply_fast<R={r},V={4 if r <= 4 else 2},NT=1>"
+        self.name = label
+
+    def step(self):
+        k, m, S = self.k, self.m, self.S
+        self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), k * S, S,
+                                       self.parity.data_ptr(), m * S, S, stream=self.sh)
+
+    def spot_check(self):
+        import numpy as np
+
+        want = _oracle().encode(list(self.data[0].cpu().numpy()), self.m, self.S)
+        got = self.parity[0].cpu().numpy()
+        return all(np.array_equal(got[i], want[i]) for i in range(self.m))
+
+    def cpu_work(self):
+        import numpy as np
+
+        oracle = _oracle()
+        rng = np.random.default_rng(SEED)
+        objs = [[rng.integers(0, 256, self.S, dtype=np.uint8) for _ in range(self.k)] for _ in range(2)]
+        return (lambda i: oracle.encode(objs[i % 2], self.m, self.S)), self.k * self.S, (
+            f"encode k={self.k} m={self.m} chunk_size={self.S}: oracle/rs_oracle.c "
+            "(crate 6.0.0 pure-Rust mul_slice restated: 64 KiB MUL_TABLE, input-major)")
+
+    def drop(self):
+        del self.data, self.parity
+
+
+class Reconstruct:
+    """configs[2]: k=8 m=4, 2 seeded data erasures per object, SHA-256 verify
+    of the present shards (chunk_reader.rs:176-196), rebuild, 1 MiB chunks."""
+
+    bound = "valu"
+
+    def __init__(self, torch, ctx, dev, sh, n, seed):
+        import numpy as np
+
+        self.torch, self.ctx, self.sh = torch, ctx, sh
+        self.k, self.m, self.S, self.n = 8, 4, 1 << 20, n
+        k, m, S = self.k, self.m, self.S
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self.obj = torch.randint(0, 256, (n, k + m, S), dtype=torch.uint8, device=dev, generator=g)
+        self.dig = torch.empty((n, k + m, 32), dtype=torch.uint8, device=dev)
+        ctx.encode_strided_device(k, m, S, n, self.obj.data_ptr(), (k + m) * S, S,
+                                  self.obj[:, k:].data_ptr(), (k + m) * S, S,
+                                  digests_ptr=self.dig.data_ptr(), stream=sh)
+        torch.cuda.synchronize()
+        self.ref = self.obj[0].clone()
+        rng = np.random.default_rng(seed)
+        self.present0 = np.ones(n * (k + m), np.uint8)
+        for o in range(n):
+            for i in rng.choice(k, 2, replace=False):
+                self.present0[o * (k + m) + i] = 0
+        self.payload = n * k * S
+        self.alg_bytes = n * (k + m) * S  # hash 10 present + write 2 rebuilt
+        self.kernel = "sha256_split_kernel + rs_apply_fast<R=2>"
+        self.name = ("RS reconstruct k=8 m=4, 2 data erasures + SHA-256 verify of the 10 present "
+                     f"shards, chunk_size=1 MiB, {n} objects per GPU (BASELINE configs[2])")
+
+    def step(self):
+        pr = self.present0.copy()
+        rc, _ = self.ctx.reconstruct_strided_device(
+            self.k, self.m, self.S, self.n, self.obj.data_ptr(), (self.k + self.m) * self.S, self.S,
+            pr, expected_ptr=self.dig.data_ptr(), stream=self.sh)
+        assert rc == 0
+
+    def spot_check(self):
+        return bool(self.torch.equal(self.obj[0], self.ref))
+
+    def cpu_work(self):
+        import numpy as np
+
+        oracle = _oracle()
+        k, m, S = self.k, self.m, self.S
+        rng = np.random.default_rng(SEED)
+        data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+        parity, dig, _ = oracle.compute_parity(data, m, S)
+        shards = [d.tobytes() for d in data] + [p.tobytes() for p in parity]
+        shards[1] = shards[5] = None
+        sizes = [S] * (k + m)
+        return (lambda i: oracle.try_reconstruct_data_chunk(shards, k, m, S, dig, sizes, 1)), k * S, (
+            "try_reconstruct_data_chunk restated (oracle): SHA-256 (scalar) of the 10 present 1 MiB "
+            "shards + crate reconstruct of 2, per object")
+
+    def drop(self):
+        del self.obj, self.dig, self.ref
+
+
+class Mixed:
+    """configs[4]: mixed (k, m) and chunk sizes with short last chunks;
+    a step encodes the batch and reconstructs it with seeded erasures."""
+
+    bound = "hbm"
+
+    def __init__(self, torch, ctx, dev, sh, budget, seed):
+        import numpy as np
+
+        self.torch, self.ctx, self.sh = torch, ctx, sh
+        rng = np.random.default_rng(seed)
+        kms = [(4, 2), (8, 4), (10, 4)]
+        sizes = [64 << 10, 256 << 10, 1 << 20, 4 << 20, 10 << 20]
+        self.classes = []  # (k, m, S, n, tensor, data_len, present0)
+        per = budget // (len(kms) * len(sizes))
+        payload = alg = 0
+        for (k, m) in kms:
+            for S in sizes:
+                n = max(1, per // ((k + m) * S))
+                t = torch.randint(0, 256, (n, k + m, S), dtype=torch.uint8, device=dev)
+                last = int(rng.integers(1, S))  # short last chunk, zero padded
+                dl = [S] * (k - 1) + [last]
+                pres = np.ones(n * (k + m), np.uint8)
+                for o in range(n):
+                    for i in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False):
+                        pres[o * (k + m) + i] = 0
+                self.classes.append((k, m, S, n, t, dl, pres))
+                payload += n * ((k - 1) * S + last) * 2  # encoded + decoded
+                alg += n * (k + m) * S * 2
+        self.payload, self.alg_bytes = payload, alg
+        self.kernel = "rs_apply_fast (mixed R) + edge tiles"
+        self.name = ("mixed 4+2 / 8+4 / 10+4 at 64 KiB-10 MiB chunks, short last chunks: encode then "
+                     f"reconstruct (1..m erasures), {sum(c[3] for c in self.classes)} objects per GPU "
+                     "(BASELINE configs[4], per GPU)")
+
+    def step(self):
+        for (k, m, S, n, t, dl, pres) in self.classes:
+            self.ctx.encode_strided_device(k, m, S, n, t.data_ptr(), (k + m) * S, S, t[:, k:].data_ptr(),
+                                           (k + m) * S, S, data_len=dl, stream=self.sh)
+        for (k, m, S, n, t, dl, pres) in self.classes:
+            pr = pres.copy()
+            rc, _ = self.ctx.reconstruct_strided_device(k, m, S, n, t.data_ptr(), (k + m) * S, S, pr,
+                                                        shard_len=dl + [S] * m, stream=self.sh)
+            assert rc == 0
+
+    def spot_check(self):
+        return None
+
+    def cpu_work(self):
+        return None
+
+    def drop(self):
+        del self.classes
+
+
+def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
+    seed = SEED + rank
+    if cfg == "2":
+        n = n_objects or 1024
+        return Encode(torch, ctx, dev, sh, 4, 2, 10 << 20, n,
+                      f"RS encode k=4 m=2, chunk_size=10485760 B, {n} objects per GPU, device-resident "
+                      "(BASELINE configs[1])", seed)
+    if cfg == "3":
+        return Reconstruct(torch, ctx, dev, sh, n_objects or 1024, seed)
+    if cfg == "4a":
+        n = n_objects or 4096
+        return Encode(torch, ctx, dev, sh, 10, 4, 1 << 20, n,
+                      f"RS encode k=10 m=4, chunk_size=1 MiB (10 MiB objects), {n} objects per GPU "
+                      "(BASELINE configs[3], primary reading)", seed)
+    if cfg == "4b":
+        n = n_objects or 640
+        return Encode(torch, ctx, dev, sh, 64, 4, 1 << 20, n,
+                      f"RS encode k=64 m=4, chunk_size=1 MiB (literal 64 MiB objects), {n} objects per "
+                      "GPU (BASELINE configs[3], literal reading)", seed)
+    if cfg == "5":
+        return Mixed(torch, ctx, dev, sh, 24 << 30, seed)
+    raise SystemExit(f"unknown --config {cfg}")
+
+
+def pmc_traffic(tag: str):
     """Per-launch HBM bytes of the RS kernel from the committed rocprofv3 PMC
     summary (profiles/*pmc*<tag>*.json), FETCH_SIZE x2 per the gfx950
     correction + WRITE_SIZE, or None."""
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{config_tag}*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{tag}*.json"))):
         try:
             with open(p) as f:
-                d = json.load(f)
-            return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+                return json.load(f).get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
         except Exception:
             continue
     return None, None
+
+
+def secondary(ctx, torch, dev, sh, w) -> dict:
+    """Reference-equivalent PUT path (encode + SHA-256 of all k+m chunks) on
+    the same batch, config 3 reconstruct + verify and the device copy peak.
+    Reported, not the headline."""
+    out = {}
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(buf)
+    t = timed(lambda: dst.copy_(buf), 5)
+    out["copy_peak_GBps"] = round(2 * buf.numel() / t / 1e9, 1)
+    del buf, dst
+
+    k, m, S, n = w.k, w.m, w.S, w.n
+    dig = torch.empty((n, k + m, 32), dtype=torch.uint8, device=dev)
+
+    def put_path():
+        ctx.encode_strided_device(k, m, S, n, w.data.data_ptr(), k * S, S, w.parity.data_ptr(),
+                                  m * S, S, digests_ptr=dig.data_ptr(), stream=sh)
+
+    t = timed(put_path, 2)
+    out["put_path_encode_plus_sha256"] = {
+        "GiBps_payload": round(n * k * S / GIB / t, 3), "ms": round(t * 1e3, 2),
+        "what": "RS encode + SHA-256 of every data and parity chunk (write_chunk + "
+                "compute_and_write_parity compute)"}
+    del dig
+    r = Reconstruct(torch, ctx, dev, sh, 1024, SEED)
+    t = timed(r.step, 3)
+    out["config3_reconstruct_verify"] = {
+        "GiBps_payload": round(r.payload / GIB / t, 3), "ms": round(t * 1e3, 2), "what": r.name}
+    r.drop()
+    return out
 
 
 def main() -> int:
@@ -109,10 +348,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--objects", type=int, default=1024, help="objects per GPU")
-    ap.add_argument("--k", type=int, default=4)
-    ap.add_argument("--m", type=int, default=2)
-    ap.add_argument("--chunk-size", type=int, default=10 << 20)
+    ap.add_argument("--config", default="2", choices=["2", "3", "4a", "4b", "5"])
+    ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra", action="store_true",
                     help="also time the secondary paths (PUT path with SHA-256, config 3 "
@@ -136,42 +373,18 @@ def main() -> int:
     import maxio_amd
 
     ctx = maxio_amd.Context(device_mask=1 << (local if world > 1 else 0), streams_per_device=2)
-    k, m, S, n = args.k, args.m, args.chunk_size, args.objects
-    objs = shard_objects(n * world, rank, world)
-    n_local = len(objs)
     dev = torch.device("cuda", torch.cuda.current_device())
-
-    # Object-major layout in HBM: data [n][k][S], parity [n][m][S].
-    g = torch.Generator(device=dev).manual_seed(0x6D6178696F + rank)
-    data = torch.empty((n_local, k, S), dtype=torch.uint8, device=dev)
-    for o in range(n_local):  # per object keeps the randint temporary small
-        data[o].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
-    parity = torch.zeros((n_local, m, S), dtype=torch.uint8, device=dev)
     # A dedicated stream: the kernels and the HIP events that time them are
-    # on the same queue (a NULL stream would let the library spread calls
-    # over its own streams).
+    # on the same queue.
     stream = torch.cuda.Stream(device=dev)
     sh = stream.cuda_stream
+    w = make_workload(args.config, torch, ctx, dev, sh, args.objects, rank)
     torch.cuda.synchronize()
-
-    def step():
-        ctx.encode_strided_device(k, m, S, n_local, data.data_ptr(), k * S, S, parity.data_ptr(),
-                                  m * S, S, stream=sh)
 
     for _ in range(args.warmup):
-        step()
+        w.step()
     torch.cuda.synchronize()
-
-    # Spot check one object against the oracle (bit-exact) before timing.
-    spot_ok = None
-    if rank == 0 and S <= (16 << 20):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import numpy as np
-        import oracle
-
-        want = oracle.encode(list(data[0].cpu().numpy()), m, S)
-        got = parity[0].cpu().numpy()
-        spot_ok = all(np.array_equal(got[i], want[i]) for i in range(m))
+    spot_ok = w.spot_check() if rank == 0 else None
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -180,27 +393,40 @@ def main() -> int:
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        step()
+        w.step()
         ev[i][1].record(stream)
     torch.cuda.synchronize()
     barrier()
     elapsed = reduce_max(time.perf_counter() - t0)
     ms_launch = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
 
-    payload = float(n_local * world) * k * S * args.steps  # weak scaling: all ranks
-    value = payload / GIB / elapsed
-    alg_bytes = float(n_local) * (k + m) * S  # per launch, per GPU
-    achieved = alg_bytes / (ms_launch * 1e-3) / 1e9
+    value = float(w.payload) * world * args.steps / GIB / elapsed  # weak scaling: all ranks
+    achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
 
     extra = None
-    if args.extra and rank == 0:
-        extra = secondary(ctx, torch, dev, sh, data, parity, k, m, S, n_local)
-    # free HBM before the CPU leg
-    del data, parity
+    if args.extra and rank == 0 and args.config == "2":
+        extra = secondary(ctx, torch, dev, sh, w)
+    cpu = cpu_all = None
+    if rank == 0 and args.cpu_seconds > 0:
+        spec = w.cpu_work()
+        if spec is not None:
+            work, per_call, what = spec
+            v, n, el = cpu_leg(work, per_call, args.cpu_seconds, 1)
+            cpu = {"value": round(v, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                   "sample": f"{n} calls in {el:.1f}s, 1 thread: {what}"}
+            # The GPU box grants 16 host cores (OMP_NUM_THREADS) while
+            # os.cpu_count() shows the whole machine.
+            nc = os.cpu_count() or 1
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(nc, 64)
+            v, n, el = cpu_leg(work, per_call, max(2.0, args.cpu_seconds / 2), threads)
+            cpu_all = {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+                       "sample": f"{n} calls in {el:.1f}s on {threads} threads "
+                                 f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={nc})"}
+    w.drop()
     torch.cuda.empty_cache()
 
     if rank == 0:
-        traffic, tsrc = pmc_traffic(f"k{k}m{m}")
+        traffic, tsrc = pmc_traffic("k4m2") if args.config == "2" else (None, None)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -215,25 +441,25 @@ def main() -> int:
             "dtype": "u8",
             "data": "synthetic: uniform random bytes (torch.randint on device, seeded)",
             "config": {
-                "workload": f"RS encode k={k} m={m}, chunk_size={S} B, {n} objects per GPU, "
-                            "device-resident (BASELINE configs[1])",
-                "k": k, "m": m, "chunk_size": S, "objects_per_gpu": n,
-                "payload_bytes_per_step_per_gpu": n_local * k * S,
+                "workload": w.name,
+                "bench_config": args.config,
+                "payload_bytes_per_step_per_gpu": int(w.payload),
                 "parallelism": "objects partitioned per GPU, no collectives",
             },
             "roofline": {
-                "bound": "hbm",
+                "bound": w.bound,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": "rs_apply_fast<R=2,V=4,NT=1>",
-                "bytes_per_launch": alg_bytes,
+                "kernel": w.kernel,
+                "bytes_per_launch": float(w.alg_bytes),
                 "ms_per_launch": round(ms_launch, 4),
                 "traffic_source": tsrc,
             },
-            "cpu_baseline": cpu_baseline(k, m, S, args.cpu_seconds) if args.cpu_seconds > 0 else None,
+            "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
             "spot_check_vs_oracle": spot_ok,
             "extra": extra,
         }
@@ -244,74 +470,6 @@ def main() -> int:
 
         dist.destroy_process_group()
     return 0
-
-
-def secondary(ctx, torch, dev, sh, data, parity, k, m, S, n_local) -> dict:
-    """Reference-equivalent PUT path (encode + SHA-256 of all k+m chunks) on
-    the same batch, config 3 (reconstruct 8+4, 2 erasures + verify, 1 MiB,
-    8192 data chunks) and the device copy peak.  Reported, not the headline."""
-    out = {}
-    def timed(fn, reps):
-        fn()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            fn()
-        torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / reps
-
-    # device copy peak (read + write bytes / time)
-    buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
-    dst = torch.empty_like(buf)
-    t = timed(lambda: dst.copy_(buf), 5)
-    out["copy_peak_GBps"] = round(2 * buf.numel() / t / 1e9, 1)
-    del buf, dst
-
-    dig = torch.empty((n_local, k + m, 32), dtype=torch.uint8, device=dev)
-
-    def put_path():
-        ctx.encode_strided_device(k, m, S, n_local, data.data_ptr(), k * S, S, parity.data_ptr(),
-                                  m * S, S, digests_ptr=dig.data_ptr(), stream=sh)
-
-    t = timed(put_path, 2)
-    out["put_path_encode_plus_sha256"] = {
-        "GiBps_payload": round(n_local * k * S / GIB / t, 3), "ms": round(t * 1e3, 2),
-        "what": "RS encode + SHA-256 of every data and parity chunk (write_chunk + "
-                "compute_and_write_parity compute)"}
-
-    # config 3: k=8 m=4 S=1MiB, 1024 objects (8192 data chunks), 2 data erasures
-    import numpy as np
-
-    k3, m3, s3, n3 = 8, 4, 1 << 20, 1024
-    g = torch.Generator(device=dev).manual_seed(3)
-    obj = torch.randint(0, 256, (n3, k3 + m3, s3), dtype=torch.uint8, device=dev, generator=g)
-    dg3 = torch.empty((n3, k3 + m3, 32), dtype=torch.uint8, device=dev)
-    ctx.encode_strided_device(k3, m3, s3, n3, obj.data_ptr(), (k3 + m3) * s3, s3,
-                              obj[:, k3:].data_ptr(), (k3 + m3) * s3, s3, digests_ptr=dg3.data_ptr(),
-                              stream=sh)
-    torch.cuda.synchronize()
-    rng = np.random.default_rng(0x6D6178696F)
-    base_present = np.ones(n3 * (k3 + m3), np.uint8)
-    for o in range(n3):
-        for i in rng.choice(k3, 2, replace=False):
-            base_present[o * (k3 + m3) + i] = 0
-
-    def recon(verify=True):
-        pr = base_present.copy()
-        rc, _ = ctx.reconstruct_strided_device(k3, m3, s3, n3, obj.data_ptr(), (k3 + m3) * s3, s3, pr,
-                                               expected_ptr=dg3.data_ptr() if verify else None,
-                                               stream=sh)
-        assert rc == 0
-
-    t = timed(recon, 3)
-    t_nv = timed(lambda: recon(False), 5)
-    out["config3_reconstruct_verify"] = {
-        "GiBps_payload": round(n3 * k3 * s3 / GIB / t, 3), "ms": round(t * 1e3, 2),
-        "rs_only_ms": round(t_nv * 1e3, 3),
-        "rs_only_alg_GBps": round(n3 * (k3 + 2) * s3 / t_nv / 1e9, 1),
-        "what": "k=8 m=4 1 MiB: SHA-256 verify of the 10 present shards + rebuild 2, 1024 objects"}
-    del obj, dg3, dig
-    return out
 
 
 if __name__ == "__main__":

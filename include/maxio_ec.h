@@ -117,7 +117,8 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size,
  * shards[i] (i < k+m) holds shard_len[i] bytes when present_inout[i] != 0;
  * for a missing shard it is the output buffer (shard_len[i] bytes; parity
  * shards use shard_size).  If expected_sha256 is not NULL every present shard
- * is hashed and a mismatch turns it into an erasure (:176-196).  Missing
+ * is hashed and a mismatch turns it into an erasure (:176-196), rebuilt into
+ * the same buffer at shard_len[i] bytes.  Missing
  * shards are rebuilt (all of them, or data only with MXEC_F_DATA_ONLY);
  * present_inout[i] is 1 on return for every verified or rebuilt shard.
  * Fewer than k verified shards: MXEC_E_TOO_FEW_SHARDS_PRESENT, nothing is
@@ -236,6 +237,21 @@ int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir,
 int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset,
                             uint64_t length, uint8_t* out, uint64_t out_cap,
                             uint64_t* out_len);
+
+/* VerifiedChunkReader (chunk_reader.rs:12-276) as a pull stream.
+ * mxec_reader_open = new (:35-49) when offset == 0 and length == UINT64_MAX,
+ * with_range (:52-82) otherwise.  mxec_reader_read = poll_read (:228-276):
+ * returns bytes copied (> 0), 0 at the end, or a negative error code; chunks
+ * are verified against the manifest (size + SHA-256) in GPU batches of up to
+ * `batch_bytes` (0 = 64 MiB), bad chunks of a batch are rebuilt in one decode
+ * when the manifest has parity, and an unrecoverable chunk fails the read
+ * that reaches it — after every byte before it was served, as the reference
+ * aborts mid-stream. */
+typedef struct mxec_reader mxec_reader;
+int mxec_reader_open(mxec_ctx* ctx, const char* ec_dir, uint64_t offset,
+                     uint64_t length, uint64_t batch_bytes, mxec_reader** out);
+int64_t mxec_reader_read(mxec_reader* r, uint8_t* buf, uint64_t cap);
+void mxec_reader_close(mxec_reader* r);
 
 /* try_reconstruct_data_chunk (chunk_reader.rs:157-226) over ec_dir's files and
  * manifest.json: out receives chunks[target].size bytes. */

@@ -74,6 +74,9 @@ _SIGS = {
     "mxec_put_object_chunked": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, SZ]),
     "mxec_get_object_chunked": (INT, [P, ctypes.c_char_p, U64, U64, P, U64, U64P]),
     "mxec_try_reconstruct_data_chunk": (INT, [P, ctypes.c_char_p, ctypes.c_uint32, P, U64, U64P]),
+    "mxec_reader_open": (INT, [P, ctypes.c_char_p, U64, U64, U64, ctypes.POINTER(ctypes.c_void_p)]),
+    "mxec_reader_read": (ctypes.c_int64, [P, P, U64]),
+    "mxec_reader_close": (None, [P]),
 }
 
 

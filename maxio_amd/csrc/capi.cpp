@@ -1,8 +1,11 @@
 // capi.cpp — extern "C" entry points of include/maxio_ec.h (context, host
 // pointer drop-ins, device-resident batches).  No exception crosses the ABI.
 #include <algorithm>
+#include <array>
+#include <unordered_map>
 #include <cstring>
 #include <map>
+#include <string>
 #include <tuple>
 
 #include "../../include/maxio_ec.h"
@@ -305,11 +308,11 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
         if (n_present) *n_present = np;
         if (np < k) return set_error(MXEC_E_TOO_FEW_SHARDS_PRESENT, too_few_msg(np, k, total));
         const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
-        auto plan = decode_cache().get(k, m, present.data(), data_only);
+        std::shared_ptr<const DecodePlan> plan;
+        uint32_t off = 0;
+        MXEC_TRY(decode_plan(*ds.d, k, m, present.data(), data_only, &plan, &off));
         if (!plan) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
         if (!plan->missing.empty()) {
-            uint32_t off = 0;
-            MXEC_TRY(decode_coef(*ds.d, *plan, data_only, &off));
             std::vector<const uint8_t*> in;
             std::vector<uint64_t> in_len, out_len;
             std::vector<uint8_t*> out;
@@ -485,22 +488,18 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
         std::vector<uint32_t> offs(static_cast<size_t>(n_obj));
         for (uint64_t o = 0; o < n_obj; ++o) {
             const uint8_t* pr = present + o * total;
-            int np = 0;
-            for (int i = 0; i < total; ++i) np += pr[i] ? 1 : 0;
             int st = MXEC_OK;
-            if (np < k) {
+            MXEC_TRY(decode_plan(*ds.d, k, m, pr, data_only, &plans[o], &offs[o]));
+            if (!plans[o]) {
                 st = MXEC_E_TOO_FEW_SHARDS_PRESENT;
                 if (first_err == MXEC_OK) {
+                    int np = 0;
+                    for (int i = 0; i < total; ++i) np += pr[i] != 0;
                     first_err = st;
                     set_error(st, too_few_msg(np, k, total));
                 }
-            } else if (np < total) {
-                plans[o] = decode_cache().get(k, m, pr, data_only);
-                if (!plans[o]) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
-                if (!plans[o]->missing.empty()) {
-                    MXEC_TRY(decode_coef(*ds.d, *plans[o], data_only, &offs[o]));
-                    groups[int(plans[o]->missing.size())].push_back(o);
-                }
+            } else if (!plans[o]->missing.empty()) {
+                groups[int(plans[o]->missing.size())].push_back(o);
             }
             if (status_out) status_out[o] = st;
         }

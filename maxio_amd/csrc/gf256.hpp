@@ -73,7 +73,7 @@ struct DecodePlan {
 // like the crate's data_decode_matrix_cache (capacity 254) but process-wide.
 class DecodeCache {
 public:
-    explicit DecodeCache(size_t capacity = 1024) : cap_(capacity) {}
+    explicit DecodeCache(size_t capacity = 16384) : cap_(capacity) {}
     // present: k+m flags; returns nullptr if fewer than k are present.
     std::shared_ptr<const DecodePlan> get(int k, int m, const uint8_t* present, bool data_only);
 

@@ -22,10 +22,14 @@ struct RsArgs {
     const uint64_t* out_len;        // [n_obj][r_total]
     const uint32_t* coef;           // tables, [j][i][8] per matrix (gf256.hpp)
     const uint32_t* coef_off;       // [n_obj] dword offset of object's table
+    const uint64_t* edge_list;      // [n_edge] object << 32 | tile: tiles a
+                                    //   length boundary or the shard end cuts
+    uint64_t n_edge;
+    uint64_t edge_tile_bytes;       // tile size the list was built for
     uint64_t shard_size;
-    uint64_t fast_cols;             // every in_len/out_len of every object >= this
     uint32_t n_obj, k, r, r_total, row0;
-    uint32_t aligned;               // all pointers 16-byte aligned
+    uint32_t aligned;               // all pointers 16-byte aligned (else every
+                                    //   tile is in the edge list)
 };
 
 // Tuning knobs of the interior kernel (tools/kernel_lab.cpp sweeps them).
@@ -37,6 +41,9 @@ struct RsVariant {
 
 hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s);
 hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& v);
+// Geometry the default launch uses for a given total row count, and its tile.
+RsVariant rs_default_variant(uint32_t r_total);
+uint64_t rs_tile_bytes(const RsVariant& v);
 
 // SHA-256 over n messages, one lane per message.  If `expected` is set the
 // kernel also writes ok[i] = (digest == expected[i]).

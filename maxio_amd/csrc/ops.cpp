@@ -45,40 +45,105 @@ int decode_coef(Device& dev, const DecodePlan& plan, bool data_only, uint32_t* o
     return coef_offset(dev, key, plan.table, off);
 }
 
+int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_only,
+                std::shared_ptr<const DecodePlan>* plan, uint32_t* off) {
+    const int total = k + m;
+    Device::PatternKey key;
+    key.kmf = uint32_t(k) | uint32_t(m) << 8 | uint32_t(data_only) << 16;
+    int np = 0;
+    for (int i = 0; i < total; ++i) {
+        const bool p = present[i] != 0;
+        np += p;
+        key.mask[size_t(i >> 6)] |= uint64_t(p) << (i & 63);
+    }
+    plan->reset();
+    *off = 0;
+    if (np < k) return MXEC_OK;
+    uint64_t epoch;
+    {
+        std::lock_guard<std::mutex> g(dev.coef_mu);
+        auto it = dev.patterns.find(key);
+        if (it != dev.patterns.end()) {
+            *plan = std::static_pointer_cast<const DecodePlan>(it->second.first);
+            *off = it->second.second;
+            return MXEC_OK;
+        }
+        epoch = dev.coef_epoch;
+    }
+    auto p = decode_cache().get(k, m, present, data_only);
+    if (!p) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
+    uint32_t o = 0;
+    if (!p->missing.empty()) MXEC_TRY(decode_coef(dev, *p, data_only, &o));
+    {
+        std::lock_guard<std::mutex> g(dev.coef_mu);
+        // Only remember the offset if the arena was not recycled meanwhile.
+        if (dev.coef_epoch == epoch) dev.patterns.emplace(key, std::make_pair(p, o));
+    }
+    *plan = p;
+    *off = o;
+    return MXEC_OK;
+}
+
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
            const std::vector<RsObject>& objs, DescArena* arena) {
     if (objs.empty() || r == 0) return MXEC_OK;
     const size_t n = objs.size();
     DescWriter w(slot, arena);
+    // Tiles a length boundary or the shard end cuts (or all tiles when a
+    // pointer is unaligned) go to the byte-exact edge kernel.
+    const uint64_t tile = rs_tile_bytes(rs_default_variant(uint32_t(r)));
+    const uint64_t tiles_per_obj = (shard_size + tile - 1) / tile;
+    bool aligned = true;
+    for (size_t o = 0; o < n && aligned; ++o) {
+        for (int j = 0; j < k; ++j) aligned &= (reinterpret_cast<uintptr_t>(objs[o].in[j]) & 15) == 0;
+        for (int i = 0; i < r; ++i) aligned &= (reinterpret_cast<uintptr_t>(objs[o].out[i]) & 15) == 0;
+    }
+    std::vector<uint64_t> edges;
+    std::vector<uint64_t> cut;
+    for (size_t o = 0; o < n; ++o) {
+        if (!aligned) {
+            for (uint64_t t = 0; t < tiles_per_obj; ++t) edges.push_back(uint64_t(o) << 32 | t);
+            continue;
+        }
+        // Boundaries at a tile multiple (or at the shard end) cut nothing.
+        cut.clear();
+        auto mark = [&](uint64_t len) {
+            if (len < shard_size && len % tile) cut.push_back(len / tile);
+        };
+        if (shard_size % tile) cut.push_back(shard_size / tile);
+        for (int j = 0; j < k; ++j) mark(objs[o].in_len[j]);
+        for (int i = 0; i < r; ++i) mark(objs[o].out_len[i]);
+        if (cut.size() > 1) {
+            std::sort(cut.begin(), cut.end());
+            cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
+        }
+        for (uint64_t t : cut) edges.push_back(uint64_t(o) << 32 | t);
+    }
     const size_t o_in = w.add(sizeof(void*) * n * k);
     const size_t o_out = w.add(sizeof(void*) * n * r);
     const size_t o_inlen = w.add(8 * n * k);
     const size_t o_outlen = w.add(8 * n * r);
     const size_t o_coef = w.add(4 * n);
+    const size_t o_edge = w.add(8 * edges.size());
     char* hb = w.data();
     auto** ip = reinterpret_cast<const uint8_t**>(hb + o_in);
     auto** op = reinterpret_cast<uint8_t**>(hb + o_out);
     auto* il = reinterpret_cast<uint64_t*>(hb + o_inlen);
     auto* ol = reinterpret_cast<uint64_t*>(hb + o_outlen);
     auto* co = reinterpret_cast<uint32_t*>(hb + o_coef);
-    uint64_t fast = shard_size;
-    bool aligned = true;
     for (size_t o = 0; o < n; ++o) {
         const RsObject& ob = objs[o];
         for (int j = 0; j < k; ++j) {
             ip[o * k + j] = ob.in[j];
             il[o * k + j] = std::min<uint64_t>(ob.in_len[j], shard_size);
-            fast = std::min(fast, il[o * k + j]);
-            aligned &= (reinterpret_cast<uintptr_t>(ob.in[j]) & 15) == 0;
         }
         for (int i = 0; i < r; ++i) {
             op[o * r + i] = ob.out[i];
             ol[o * r + i] = std::min<uint64_t>(ob.out_len[i], shard_size);
-            fast = std::min(fast, ol[o * r + i]);
-            aligned &= (reinterpret_cast<uintptr_t>(ob.out[i]) & 15) == 0;
         }
         co[o] = ob.coef_off;
     }
+    if (!edges.empty()) std::memcpy(hb + o_edge, edges.data(), 8 * edges.size());
     char* db = nullptr;
     MXEC_TRY(w.commit(s, &db));
     RsArgs a{};
@@ -88,8 +153,10 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     a.out_len = reinterpret_cast<const uint64_t*>(db + o_outlen);
     a.coef = static_cast<const uint32_t*>(dev.coef.p);
     a.coef_off = reinterpret_cast<const uint32_t*>(db + o_coef);
+    a.edge_list = reinterpret_cast<const uint64_t*>(db + o_edge);
+    a.n_edge = edges.size();
+    a.edge_tile_bytes = tile;
     a.shard_size = shard_size;
-    a.fast_cols = fast;
     a.n_obj = uint32_t(n);
     a.k = uint32_t(k);
     a.r_total = uint32_t(r);

@@ -36,6 +36,12 @@ int encode_coef(Device& dev, int k, int m, uint32_t* off);
 // Coefficient table of a decode plan.
 int decode_coef(Device& dev, const DecodePlan& plan, bool data_only, uint32_t* off);
 
+// Decode plan + table offset for one erasure pattern (present: k+m flags),
+// memoised per device so a batch that repeats patterns pays one hash lookup
+// per object.  *plan is null when fewer than k shards are present.
+int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_only,
+                std::shared_ptr<const DecodePlan>* plan, uint32_t* off);
+
 // filesystem.rs:1095 guard, then the crate's ReedSolomon::new checks.
 int check_km(int k, int m);
 

@@ -12,22 +12,25 @@
 //    workgroup tile covers 256 lanes x 16 B x V columns of every shard.
 //  * No LDS tables and no byte lookups: c*x for 4 packed bytes is three
 //    v_perm_b32 byte-selects from 8-entry tables (bits 0-2, 3-5, 6-7 of x)
-//    plus XORs.  The tables depend only on c, are wave-uniform, and arrive in
-//    SGPRs by scalar loads; one of each v_perm's two table dwords must be a
-//    VGPR (gfx950 constant-bus limit 1), the copy is hoisted per input column.
+//    plus a v_bitop3 XOR3.  The tables depend only on c, are wave-uniform, and
+//    arrive in SGPRs by scalar loads; one of each v_perm's two table dwords must
+//    be a VGPR (gfx950 constant-bus limit 1), the copy is hoisted per column.
 //  * Input shards are loaded in blocks of 4 so each lane keeps 4*V 16-byte
 //    loads in flight; grid-stride over (object, tile) keeps 16 workgroups per
 //    CU busy without one launch per object.  Loads and stores carry the
 //    nontemporal hint (every byte is touched once).
 //  * Zero padding (the crate pads the short last chunk, filesystem.rs:1111)
-//    is never materialised: bytes at or past in_len read as zero in the
-//    edge-tile path.
+//    is never materialised: in the fast kernel an input whose length ends at
+//    or before a tile contributes zero and is not loaded; only the few tiles
+//    that a length boundary cuts through go to the byte-exact edge kernel,
+//    from a per-launch list built by the host (edge_tiles()).
 #include "kernels.hpp"
 
 namespace mxec {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr uint64_t kEdgeTile = kThreads * 16;  // bytes per edge-kernel step
 
 struct Vec4 {
     uint32_t w[4];
@@ -121,17 +124,30 @@ __device__ __forceinline__ void gstore16(gptr p, const uint32_t (&w)[4]) {
     else *q = v;
 }
 
-// Interior tiles: tile t < fast_tiles of every object, all columns in range,
-// all pointers 16-byte aligned.  No bounds checks in the loop.
+// Fast tiles: every tile of every object that no length boundary cuts
+// through (those are in the edge list and skipped here).  An input whose
+// length ends at or before the tile reads as zero without a load; an output
+// whose length ends there is not stored.  All pointers 16-byte aligned.
 template <int R, int V, bool NT>
 __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
-    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint32_t k,
-    uint32_t r_total, uint32_t row0, uint32_t fast_tiles, uint64_t n_tiles) {
+    const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
+    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
+    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles) {
     constexpr uint32_t kTile = kThreads * 16 * V;
     for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const uint32_t obj = uint32_t(tile / fast_tiles);
-        const uint64_t base = (tile - uint64_t(obj) * fast_tiles) * kTile;
+        const uint32_t obj = uint32_t(tile / tiles_per_obj);
+        const uint64_t base = (tile - uint64_t(obj) * tiles_per_obj) * kTile;
+        const uint64_t end = base + kTile;
+        const uint64_t* __restrict__ il = in_len + uint64_t(obj) * k;
+        const uint64_t* __restrict__ ol = out_len + uint64_t(obj) * r_total + row0;
+        // Wave-uniform: skip tiles cut by a boundary (edge kernel's job).
+        bool cut = end > shard_size;
+        for (uint32_t j = 0; j < k; ++j) cut |= il[j] > base && il[j] < end;
+#pragma unroll
+        for (int i = 0; i < R; ++i) cut |= ol[i] > base && ol[i] < end;
+        if (cut) continue;
+
         const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
         const uint8_t* const* __restrict__ ip = in_ptrs + uint64_t(obj) * k;
         uint8_t* const* __restrict__ op = out_ptrs + uint64_t(obj) * r_total + row0;
@@ -151,13 +167,16 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
                 gcptr p = ((gcptr)(ip[j + jj])) + lane;
+                const bool live = il[j + jj] >= end;  // else ends at/before base: zero
 #pragma unroll
-                for (int v = 0; v < V; ++v) x[jj][v] = gload16<NT>(p + v * kThreads * 16);
+                for (int v = 0; v < V; ++v)
+                    x[jj][v] = live ? gload16<NT>(p + v * kThreads * 16) : Vec4{{0, 0, 0, 0}};
             }
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * r_total * 8);
         }
         for (; j < k; ++j) {
+            if (il[j] < end) continue;  // zero column: contributes nothing
             Vec4 x[V];
             gcptr p = ((gcptr)(ip[j])) + lane;
 #pragma unroll
@@ -166,6 +185,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
         }
 #pragma unroll
         for (int i = 0; i < R; ++i) {
+            if (ol[i] < end) continue;  // output ends at/before base
             gptr o = ((gptr)(op[i])) + lane;
 #pragma unroll
             for (int v = 0; v < V; ++v) {
@@ -176,22 +196,23 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     }
 }
 
-// Edge tiles: tiles [first_tile, tiles_per_obj) of every object — the short
-// last chunk, the shard tail past a multiple of the tile, or everything when
-// a pointer is unaligned.  Byte-exact bounds on every input and output.
+// Edge tiles: the list entries (object << 32 | fast tile index) are the fast
+// tiles that a length boundary or the shard end cuts through, or every tile
+// when a pointer is unaligned.  Each is walked in kEdgeTile steps with
+// byte-exact bounds on every input and output.
 template <int R>
 __global__ __launch_bounds__(kThreads) void rs_apply_edge(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
     const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
-    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t first_tile, uint32_t tiles_per_obj,
-    uint32_t aligned, uint64_t n_tiles) {
-    constexpr uint32_t kTile = kThreads * 16;
-    const uint32_t per_obj = tiles_per_obj - first_tile;
-    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const uint32_t obj = uint32_t(tile / per_obj);
-        const uint64_t t = first_tile + (tile - uint64_t(obj) * per_obj);
-        const uint64_t col = t * kTile + threadIdx.x * 16;
+    uint32_t k, uint32_t r_total, uint32_t row0, const uint64_t* __restrict__ edge_list,
+    uint32_t steps_per_tile, uint64_t tile_bytes, uint32_t aligned, uint64_t n_steps) {
+    for (uint64_t step = blockIdx.x; step < n_steps; step += gridDim.x) {
+        const uint64_t e = edge_list[step / steps_per_tile];
+        const uint32_t obj = uint32_t(e >> 32);
+        const uint64_t col = uint64_t(uint32_t(e)) * tile_bytes + (step % steps_per_tile) * kEdgeTile +
+                             threadIdx.x * 16;
+        if (col >= shard_size) continue;
         const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
         uint32_t acc[1][4][R];
 #pragma unroll
@@ -218,53 +239,64 @@ __global__ __launch_bounds__(kThreads) void rs_apply_edge(
     }
 }
 
-
-// Interior kernel for one (R, V, NT) choice.
 template <int R, int V, bool NT>
-hipError_t launch_fast(const RsArgs& a, uint32_t fast_tiles, uint64_t n_fast, uint64_t blocks,
+hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
     hipLaunchKernelGGL((rs_apply_fast<R, V, NT>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
-                       a.in_ptrs, a.out_ptrs, a.coef, a.coef_off, a.k, a.r_total, a.row0,
-                       fast_tiles, n_fast);
+                       a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.shard_size,
+                       a.k, a.r_total, a.row0, tiles_per_obj, n_tiles);
     return hipGetLastError();
 }
 
 template <int R>
 hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& var) {
-    const uint64_t fast_tile = uint64_t(kThreads) * 16 * var.vecs;
-    const uint64_t edge_tile = uint64_t(kThreads) * 16;
-    // Interior: the first fast_tiles (of fast_tile bytes) of every object.
-    uint32_t fast_tiles = 0;
-    if (a.aligned) fast_tiles = uint32_t((a.fast_cols < a.shard_size ? a.fast_cols : a.shard_size) / fast_tile);
-    const uint64_t n_fast = uint64_t(fast_tiles) * a.n_obj;
-    if (n_fast) {
+    const uint64_t tile = rs_tile_bytes(var);
+    if (a.n_edge && a.edge_tile_bytes != tile) return hipErrorInvalidValue;  // list built for another tile
+    if (a.aligned) {
+        const uint32_t tiles_per_obj = uint32_t((a.shard_size + tile - 1) / tile);
+        const uint64_t n_tiles = uint64_t(tiles_per_obj) * a.n_obj;
         uint64_t blocks = uint64_t(n_cus) * uint64_t(var.blocks_per_cu);
-        if (blocks > n_fast) blocks = n_fast;
+        if (blocks > n_tiles) blocks = n_tiles;
         hipError_t e = hipErrorInvalidValue;
-        if (var.vecs == 1) e = var.nt ? launch_fast<R, 1, true>(a, fast_tiles, n_fast, blocks, s)
-                                      : launch_fast<R, 1, false>(a, fast_tiles, n_fast, blocks, s);
-        else if (var.vecs == 2) e = var.nt ? launch_fast<R, 2, true>(a, fast_tiles, n_fast, blocks, s)
-                                           : launch_fast<R, 2, false>(a, fast_tiles, n_fast, blocks, s);
-        else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, fast_tiles, n_fast, blocks, s)
-                                           : launch_fast<R, 4, false>(a, fast_tiles, n_fast, blocks, s);
+        if (var.vecs == 1) e = var.nt ? launch_fast<R, 1, true>(a, tiles_per_obj, n_tiles, blocks, s)
+                                      : launch_fast<R, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (var.vecs == 2) e = var.nt ? launch_fast<R, 2, true>(a, tiles_per_obj, n_tiles, blocks, s)
+                                           : launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s)
+                                           : launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
         if (e != hipSuccess) return e;
     }
-    // Edge: the rest of each shard, in tiles of edge_tile bytes.
-    const uint32_t first = uint32_t(uint64_t(fast_tiles) * fast_tile / edge_tile);
-    const uint32_t total = uint32_t((a.shard_size + edge_tile - 1) / edge_tile);
-    if (total > first) {
-        const uint64_t n_edge = uint64_t(total - first) * a.n_obj;
+    if (a.n_edge) {
+        const uint32_t steps = uint32_t(tile / kEdgeTile);
+        const uint64_t n_steps = a.n_edge * steps;
         uint64_t blocks = uint64_t(n_cus) * 8;
-        if (blocks > n_edge) blocks = n_edge;
+        if (blocks > n_steps) blocks = n_steps;
         hipLaunchKernelGGL((rs_apply_edge<R>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                            a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off,
-                           a.shard_size, a.k, a.r_total, a.row0, first, total, a.aligned, n_edge);
+                           a.shard_size, a.k, a.r_total, a.row0, a.edge_list, steps, tile, a.aligned,
+                           n_steps);
         return hipGetLastError();
     }
     return hipSuccess;
 }
 
 }  // namespace
+
+uint64_t rs_tile_bytes(const RsVariant& v) { return uint64_t(kThreads) * 16 * uint64_t(v.vecs); }
+
+// Default geometry, from tools/kernel_lab sweeps on MI355X (profiles/): four
+// 16-byte vectors per lane with nontemporal loads/stores while the
+// accumulators fit (R <= 4: <= 158 VGPRs), two beyond that; 16 workgroups per
+// CU of grid-stride (16 beat 8 and 4 on every shape swept).  Chosen by the
+// launch's total row count so every row group of a launch shares one tile
+// size (and one edge list).
+RsVariant rs_default_variant(uint32_t r_total) {
+    RsVariant v;
+    v.vecs = r_total <= 4 ? 4 : 2;
+    v.nt = true;
+    v.blocks_per_cu = 16;
+    return v;
+}
 
 hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& v) {
     switch (a.r) {
@@ -280,16 +312,8 @@ hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, co
     }
 }
 
-// Default geometry, from tools/kernel_lab sweeps on MI355X (profiles/): four
-// 16-byte vectors per lane with nontemporal loads/stores while the
-// accumulators fit (R <= 4: <= 158 VGPRs), two beyond that; 16 workgroups per
-// CU of grid-stride (16 beat 8 and 4 on every shape swept).
 hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
-    RsVariant v;
-    v.vecs = a.r <= 4 ? 4 : 2;
-    v.nt = true;
-    v.blocks_per_cu = 16;
-    return launch_rs_apply_variant(a, n_cus, s, v);
+    return launch_rs_apply_variant(a, n_cus, s, rs_default_variant(a.r_total));
 }
 
 }  // namespace mxec

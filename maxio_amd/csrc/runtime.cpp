@@ -107,7 +107,9 @@ int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<
         // Arena full: every launch that could read it must have finished.
         MXEC_HIP(hipDeviceSynchronize());
         dev.coef_index.clear();
+        dev.patterns.clear();
         dev.coef_used = 0;
+        ++dev.coef_epoch;
     }
     const uint32_t o = uint32_t(dev.coef_used);
     // Synchronous copy: the table is on the device before any stream can see

@@ -4,12 +4,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <atomic>
 #include <cstdint>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/maxio_ec.h"
@@ -79,7 +81,23 @@ struct Device {
     std::mutex coef_mu;
     DevBuf coef;
     size_t coef_used = 0;  // dwords
+    uint64_t coef_epoch = 0;  // bumped whenever the arena is recycled
     std::map<std::vector<uint8_t>, uint32_t> coef_index;
+    // Erasure pattern -> (decode plan, table offset), resolved once per device
+    // and dropped with the arena (ops.cpp decode_plan).  Key: presence bitmask
+    // over k+m <= 256 shards, plus (k, m, data_only).
+    struct PatternKey {
+        std::array<uint64_t, 4> mask{};
+        uint32_t kmf = 0;
+        bool operator==(const PatternKey& o) const { return kmf == o.kmf && mask == o.mask; }
+    };
+    struct PatternHash {
+        size_t operator()(const PatternKey& a) const {
+            return size_t(a.mask[0] * 0x9E3779B97F4A7C15ull ^ a.mask[1] * 0xC2B2AE3D27D4EB4Full ^
+                          a.mask[2] * 0x165667B19E3779F9ull ^ a.mask[3] ^ uint64_t(a.kmf) << 40);
+        }
+    };
+    std::unordered_map<PatternKey, std::pair<std::shared_ptr<const void>, uint32_t>, PatternHash> patterns;
     // Host-batch pipeline state (pipeline.cpp): streams, pinned rings, pools;
     // created on first use and kept, one batch at a time per device.
     std::mutex pipe_mu;

@@ -19,6 +19,7 @@
 #include <filesystem>
 #include <fstream>
 #include <map>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -289,14 +290,16 @@ int reconstruct_from_dir(mxec_ctx* ctx, const fs::path& dir, const Manifest& man
         const auto& ci = man.chunks[size_t(i)];
         std::vector<uint8_t> data;
         bool ok = read_file(dir / chunk_name(uint32_t(i)), data) == MXEC_OK;
-        // A file longer than shard_size cannot carry the manifest digest (the
-        // reference hashes the whole file, :184): it is an erasure.
-        ok = ok && data.size() <= shard;
+        // The digest covers the whole file as written (:184); a file whose size
+        // differs from the manifest's cannot match it, so it is an erasure up
+        // front and is rebuilt at its full manifest length.
+        const size_t want = size_t(i < k ? std::min<uint64_t>(ci.size, shard) : shard);
+        ok = ok && data.size() == want;
         // A digest that does not parse can never match: the shard is an erasure.
         ok = ok && unhex32(ci.sha256, &expected[size_t(i) * 32]);
-        // Vec::resize(shard_size) pads or truncates; the digest is checked first.
-        const size_t want = size_t(i < k ? std::min<uint64_t>(ci.size, shard) : shard);
-        bufs[size_t(i)].assign(std::max<size_t>(want, data.size()), 0);
+        // Vec::resize(shard_size) zero pads; the kernels read bytes past a
+        // shard's length as zero, so the buffer holds only the real bytes.
+        bufs[size_t(i)].assign(want, 0);
         if (ok) {
             std::memcpy(bufs[size_t(i)].data(), data.data(), data.size());
             lens[size_t(i)] = data.size();
@@ -453,47 +456,44 @@ int mxec_try_reconstruct_data_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t 
     return MXEC_OK;
 }
 
-int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, uint64_t length, uint8_t* out,
-                            uint64_t out_cap, uint64_t* out_len) {
-    if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    Manifest man;
-    MXEC_TRY(read_manifest(ec_dir, man));
-    const fs::path dir(ec_dir);
-    *out_len = 0;
-    if (length == UINT64_MAX) length = offset < man.total_size ? man.total_size - offset : 0;
-    if (length == 0 || man.total_size == 0) return MXEC_OK;  // with_range :53-65 / new :40
-    if (man.chunk_size == 0) return set_error(MXEC_E_JSON, "JSON error: chunk_size is 0");
-    if (offset + length > man.total_size) length = man.total_size > offset ? man.total_size - offset : 0;
-    if (length == 0) return MXEC_OK;
-    if (length > out_cap || !out) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
-    const uint32_t start = uint32_t(offset / man.chunk_size);
-    const uint32_t end = uint32_t((offset + length - 1) / man.chunk_size);
-    uint64_t skip = offset % man.chunk_size;
-    if (end >= man.chunk_count || end >= man.chunks.size()) return set_error(MXEC_E_JSON, "JSON error: range past chunk_count");
-    // load_chunk_sync (:87-152) for every chunk of the range: read, size
-    // check, then one batched digest pass.
-    const uint32_t n = end - start + 1;
-    std::vector<std::vector<uint8_t>> data(n);
-    std::vector<int> state(n, 0);  // 0 ok so far, 1 read/size failure
-    std::vector<std::string> err(n);
+}  // extern "C"
+
+// ---- VerifiedChunkReader (chunk_reader.rs:12-276) --------------------------
+
+namespace {
+
+struct LoadedChunk {
+    std::vector<uint8_t> data;
+    int err = MXEC_OK;  // non-zero: this chunk fails the read that reaches it
+    std::string msg;
+};
+
+// load_chunk_sync (:87-152) for chunks [first, last]: read, size check, one
+// batched digest pass; with parity every bad chunk is rebuilt in one decode
+// (:130-150), without parity a bad chunk carries its original error.
+int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_t first, uint32_t last,
+                std::vector<LoadedChunk>& out) {
+    const uint32_t n = last - first + 1;
+    out.assign(n, LoadedChunk{});
     std::vector<const uint8_t*> hp;
     std::vector<size_t> hl;
     std::vector<uint32_t> hidx;
     for (uint32_t c = 0; c < n; ++c) {
-        const uint32_t idx = start + c;
-        if (read_file(dir / chunk_name(idx), data[c]) != MXEC_OK) {
-            state[c] = 1;
-            err[c] = "failed to read chunk " + std::to_string(idx);
+        const uint32_t idx = first + c;
+        LoadedChunk& lc = out[c];
+        if (read_file(dir / chunk_name(idx), lc.data) != MXEC_OK) {
+            lc.err = MXEC_E_IO;
+            lc.msg = "failed to read chunk " + std::to_string(idx) + ": " + mxec::last_error();
             continue;
         }
-        if (data[c].size() != man.chunks[idx].size) {
-            state[c] = 1;
-            err[c] = "chunk " + std::to_string(idx) + " size mismatch: expected " + std::to_string(man.chunks[idx].size) +
-                     ", got " + std::to_string(data[c].size());
+        if (lc.data.size() != man.chunks[idx].size) {
+            lc.err = MXEC_E_INTEGRITY;
+            lc.msg = "chunk " + std::to_string(idx) + " size mismatch: expected " +
+                     std::to_string(man.chunks[idx].size) + ", got " + std::to_string(lc.data.size());
             continue;
         }
-        hp.push_back(data[c].empty() ? reinterpret_cast<const uint8_t*>("") : data[c].data());
-        hl.push_back(data[c].size());
+        hp.push_back(lc.data.empty() ? reinterpret_cast<const uint8_t*>("") : lc.data.data());
+        hl.push_back(lc.data.size());
         hidx.push_back(c);
     }
     if (!hp.empty()) {
@@ -502,34 +502,126 @@ int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, 
         for (size_t t = 0; t < hidx.size(); ++t) {
             const uint32_t c = hidx[t];
             const std::string got = hex32(&dig[t * 32]);
-            if (got != man.chunks[start + c].sha256) {
-                state[c] = 1;
-                err[c] = "checksum mismatch on chunk " + std::to_string(start + c) + ": expected " +
-                         man.chunks[start + c].sha256 + ", got " + got;
+            if (got != man.chunks[first + c].sha256) {
+                out[c].err = MXEC_E_INTEGRITY;
+                out[c].msg = "checksum mismatch on chunk " + std::to_string(first + c) + ": expected " +
+                             man.chunks[first + c].sha256 + ", got " + got;
             }
         }
     }
-    // Recovery (:130-150): without parity the first bad chunk is the error;
-    // with parity every bad chunk of the range is rebuilt in one decode.
+    if (!(man.has_parity && man.parity_shards > 0)) return MXEC_OK;
     std::vector<uint32_t> bad;
     std::vector<std::vector<uint8_t>*> bad_out;
-    for (uint32_t c = 0; c < n; ++c) {
-        if (!state[c]) continue;
-        if (!(man.has_parity && man.parity_shards > 0)) return set_error(MXEC_E_INTEGRITY, err[c]);
-        bad.push_back(start + c);
-        bad_out.push_back(&data[c]);
+    for (uint32_t c = 0; c < n; ++c)
+        if (out[c].err) {
+            bad.push_back(first + c);
+            bad_out.push_back(&out[c].data);
+        }
+    if (bad.empty()) return MXEC_OK;
+    const int rc = reconstruct_from_dir(ctx, dir, man, bad, bad_out);
+    const std::string msg = rc ? std::string(mxec::last_error()) : std::string();
+    for (uint32_t c = 0; c < n; ++c)
+        if (out[c].err) {
+            out[c].err = rc;
+            out[c].msg = msg;
+        }
+    return MXEC_OK;
+}
+
+}  // namespace
+
+struct mxec_reader {
+    mxec_ctx* ctx = nullptr;
+    fs::path dir;
+    Manifest man;
+    uint32_t next = 0, end = 0;  // next chunk to load, last chunk of the range
+    uint64_t skip = 0, remaining = 0, batch_bytes = 0;
+    std::vector<LoadedChunk> batch;
+    size_t bi = 0;
+    uint64_t pos = 0;
+};
+
+extern "C" {
+
+int mxec_reader_open(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, uint64_t length, uint64_t batch_bytes,
+                     mxec_reader** out) {
+    if (!ec_dir || !out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    auto r = std::make_unique<mxec_reader>();
+    MXEC_TRY(read_manifest(ec_dir, r->man));
+    r->ctx = ctx;
+    r->dir = ec_dir;
+    r->batch_bytes = batch_bytes ? batch_bytes : (uint64_t(64) << 20);
+    const Manifest& man = r->man;
+    if (length == UINT64_MAX) length = offset < man.total_size ? man.total_size - offset : 0;
+    if (offset + length > man.total_size) length = man.total_size > offset ? man.total_size - offset : 0;
+    if (length > 0 && man.total_size > 0) {  // else Done at once (:40, :53-65)
+        if (man.chunk_size == 0) return set_error(MXEC_E_JSON, "JSON error: chunk_size is 0");
+        r->next = uint32_t(offset / man.chunk_size);
+        r->end = uint32_t((offset + length - 1) / man.chunk_size);
+        r->skip = offset % man.chunk_size;
+        if (r->end >= man.chunk_count || r->end >= man.chunks.size())
+            return set_error(MXEC_E_JSON, "JSON error: range past chunk_count");
+        r->remaining = length;
     }
-    if (!bad.empty()) MXEC_TRY(reconstruct_from_dir(ctx, dir, man, bad, bad_out));
-    uint64_t remaining = length, pos = 0;
-    for (uint32_t c = 0; c < n && remaining; ++c) {
-        const uint64_t avail = data[c].size() > skip ? data[c].size() - skip : 0;
-        const uint64_t take = std::min(avail, remaining);
-        if (take) std::memcpy(out + pos, data[c].data() + skip, take);
-        pos += take;
-        remaining -= take;
-        skip = 0;
+    *out = r.release();
+    return MXEC_OK;
+}
+
+int64_t mxec_reader_read(mxec_reader* r, uint8_t* buf, uint64_t cap) {
+    if (!r || (cap && !buf)) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    uint64_t copied = 0;
+    while (copied < cap && r->remaining > 0) {
+        if (r->bi >= r->batch.size()) {
+            // NeedLoad: the next chunks up to batch_bytes (at least one)
+            uint32_t last = r->next;
+            uint64_t bytes = r->man.chunks[r->next].size;
+            while (last < r->end && bytes + r->man.chunks[last + 1].size <= r->batch_bytes)
+                bytes += r->man.chunks[++last].size;
+            const int rc = load_chunks(r->ctx, r->dir, r->man, r->next, last, r->batch);
+            if (rc) return copied ? int64_t(copied) : int64_t(rc);
+            r->next = last + 1;
+            r->bi = 0;
+            r->pos = r->skip;  // skip applies to the first chunk of the range only
+            r->skip = 0;
+        }
+        LoadedChunk& c = r->batch[r->bi];
+        if (c.err) {  // serve everything before it first, as the reference streams
+            if (copied) return int64_t(copied);
+            return set_error(c.err, c.msg);
+        }
+        const uint64_t avail = c.data.size() > r->pos ? c.data.size() - r->pos : 0;
+        const uint64_t take = std::min(std::min(avail, cap - copied), r->remaining);
+        if (take) std::memcpy(buf + copied, c.data.data() + r->pos, take);
+        copied += take;
+        r->pos += take;
+        r->remaining -= take;
+        if (r->pos >= c.data.size()) {
+            c.data = std::vector<uint8_t>();
+            ++r->bi;
+            r->pos = 0;
+        }
     }
-    *out_len = pos;
+    return int64_t(copied);
+}
+
+void mxec_reader_close(mxec_reader* r) { delete r; }
+
+int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, uint64_t length, uint8_t* out,
+                            uint64_t out_cap, uint64_t* out_len) {
+    if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    *out_len = 0;
+    mxec_reader* r = nullptr;
+    MXEC_TRY(mxec_reader_open(ctx, ec_dir, offset, length, uint64_t(1) << 40, &r));
+    std::unique_ptr<mxec_reader, void (*)(mxec_reader*)> guard(r, mxec_reader_close);
+    if (r->remaining > out_cap || (r->remaining && !out))
+        return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
+    while (r->remaining > 0) {
+        const int64_t n = mxec_reader_read(r, out + *out_len, out_cap - *out_len);
+        if (n < 0) return int(n);
+        if (n == 0) break;
+        *out_len += uint64_t(n);
+    }
     return MXEC_OK;
 }
 

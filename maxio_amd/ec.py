@@ -282,12 +282,54 @@ class Context:
             out.ctypes.data, capacity, ctypes.byref(n)))
         return out[: n.value].tobytes()
 
+    def open_reader(self, ec_dir: str, offset: int = 0, length: Optional[int] = None,
+                    batch_bytes: int = 0) -> "ChunkReader":
+        return ChunkReader(self, ec_dir, offset, length, batch_bytes)
+
     def try_reconstruct_data_chunk(self, ec_dir: str, target: int, capacity: int = 1 << 26) -> bytes:
         out = np.zeros(max(1, capacity), np.uint8)
         n = ctypes.c_uint64(0)
         _check(self._lib.mxec_try_reconstruct_data_chunk(self._h, ec_dir.encode(), target,
                                                          out.ctypes.data, capacity, ctypes.byref(n)))
         return out[: n.value].tobytes()
+
+
+class ChunkReader:
+    """Mirror of VerifiedChunkReader (chunk_reader.rs:12-276): ``read(n)``
+    returns up to n bytes, b"" at the end of the range, and raises RSError
+    when it reaches a chunk that is corrupt and cannot be rebuilt -- after the
+    bytes before that chunk have been returned by earlier reads."""
+
+    def __init__(self, ctx: "Context", ec_dir: str, offset: int = 0, length: Optional[int] = None,
+                 batch_bytes: int = 0):
+        self._lib = ctx._lib
+        self._ctx = ctx  # keeps the device context alive while the reader is open
+        h = ctypes.c_void_p()
+        _check(self._lib.mxec_reader_open(ctx._h, ec_dir.encode(), offset,
+                                          (1 << 64) - 1 if length is None else length,
+                                          batch_bytes, ctypes.byref(h)))
+        self._r = h
+
+    def read(self, n: int = 1 << 20) -> bytes:
+        buf = np.empty(max(1, n), np.uint8)
+        got = self._lib.mxec_reader_read(self._r, buf.ctypes.data, n)
+        if got < 0:
+            _check(int(got))
+        return buf[:got].tobytes()
+
+    def close(self) -> None:
+        if self._r:
+            self._lib.mxec_reader_close(self._r)
+            self._r = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        self.close()
 
 
 class ReedSolomon:

@@ -330,3 +330,44 @@ def test_sha256_many_messages_throughput_form(ctx):
         o += int(n)
     got = ctx.sha256(bufs)
     assert got == [hashlib.sha256(b).digest() for b in bufs]
+
+
+@pytest.mark.parametrize("last", [300000, 16384, 1, (1 << 20) - 16])
+def test_short_last_chunk_device_encode_and_rebuild(ctx, last):
+    """Realistic objects: the last data chunk is short (object size not a
+    multiple of chunk_size).  Tiles past its end read it as zero without a
+    load; the tile it ends in goes to the edge kernel; a rebuilt short chunk
+    is written to its length only (chunk_reader.rs:216-222)."""
+    torch = _torch()
+    k, m, s, n = 8, 4, 1 << 20, 5
+    rng = np.random.default_rng(last)
+    host = rng.integers(0, 256, (n, k + m, s), dtype=np.uint8)
+    host[:, k - 1, last:] = 0
+    dl = [s] * (k - 1) + [last]
+    for o in range(n):
+        chunks = [host[o, j] for j in range(k - 1)] + [host[o, k - 1, :last]]
+        want, _, _ = oracle.compute_parity(chunks, m, s)
+        host[o, k:] = np.stack(want)
+    dev = torch.from_numpy(host).cuda()
+    dev[:, k:].fill_(0x33)  # parity must be fully rewritten
+    torch.cuda.synchronize()
+    ctx.encode_strided_device(k, m, s, n, dev.data_ptr(), (k + m) * s, s, dev[:, k:].data_ptr(),
+                              (k + m) * s, s, data_len=dl)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), host)
+    # lose the short chunk and one more; rebuild must write exactly `last` bytes
+    present = np.ones(n * (k + m), np.uint8)
+    for o in range(n):
+        present[o * (k + m) + k - 1] = 0
+        present[o * (k + m) + 2] = 0
+    dev[:, k - 1].fill_(0x77)
+    dev[:, 2].fill_(0x77)
+    torch.cuda.synchronize()
+    rc, _ = ctx.reconstruct_strided_device(k, m, s, n, dev.data_ptr(), (k + m) * s, s, present,
+                                           shard_len=dl + [s] * m)
+    torch.cuda.synchronize()
+    assert rc == 0
+    got = dev.cpu().numpy()
+    assert np.array_equal(got[:, k - 1, :last], host[:, k - 1, :last])
+    assert (got[:, k - 1, last:] == 0x77).all()  # untouched past the chunk's end
+    assert np.array_equal(got[:, 2], host[:, 2])

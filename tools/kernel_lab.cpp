@@ -109,7 +109,7 @@ struct Batch {
         CK(hipMemcpy(*coef_dev, table.data(), table.size() * 4, hipMemcpyHostToDevice));
         a.coef = *coef_dev;
         a.shard_size = sh.S;
-        a.fast_cols = sh.S;
+        a.n_edge = 0;
         a.n_obj = uint32_t(sh.n);
         a.k = uint32_t(sh.k);
         a.r = uint32_t(sh.r);
