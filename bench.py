@@ -264,6 +264,83 @@ class Mixed:
         del self.classes
 
 
+class BodySums:
+    """the PUT body digests of a batch of device-resident
+    bodies — MD5 (the ETag, every PUT) + CRC32C (x-amz-checksum-crc32c) —
+    in one call (filesystem.rs:700-725, 775-777)."""
+
+    bound = "hbm"
+
+    def __init__(self, torch, ctx, dev, sh, n, size, seed):
+        self.torch, self.ctx, self.sh = torch, ctx, sh
+        self.n, self.size = n, size
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self.buf = torch.empty((n, size), dtype=torch.uint8, device=dev)
+        for o in range(n):
+            self.buf[o].copy_(torch.randint(0, 256, (size,), dtype=torch.uint8, device=dev, generator=g))
+        self.out = torch.zeros((n, 76), dtype=torch.uint8, device=dev)
+        self.ptrs = [self.buf[o].data_ptr() for o in range(n)]
+        self.lens = [size] * n
+        self.payload = n * size
+        self.alg_bytes = n * size  # the CRC pass reads every body byte once
+        self.which = 0x01 | 0x04
+        self.kernel = "crc_tiles_kernel (CRC32C) + body_hash_kernel (MD5, lane per body)"
+        self.name = (f"PUT body digests MD5 + CRC32C of {n} device-resident bodies x {size} B "
+                     "(SURVEY 8f rank 3)")
+
+    def step(self):
+        self.ctx.body_sums_device(self.ptrs, self.lens, self.out.data_ptr(), self.which, stream=self.sh)
+
+    def breakdown(self):
+        """Each half alone, HIP-event timed on the same stream."""
+        torch = self.torch
+        res = {}
+        for name, which in (("crc32c", 0x04), ("md5", 0x01), ("crc32", 0x02), ("sha1", 0x08)):
+            self.ctx.body_sums_device(self.ptrs, self.lens, self.out.data_ptr(), which, stream=self.sh)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st = torch.cuda.ExternalStream(self.sh)
+            a.record(st)
+            self.ctx.body_sums_device(self.ptrs, self.lens, self.out.data_ptr(), which, stream=self.sh)
+            b.record(st)
+            torch.cuda.synchronize()
+            ms = a.elapsed_time(b)
+            d = {"ms": round(ms, 3)}
+            if name.startswith("crc"):
+                d["GBps"] = round(self.payload / (ms * 1e-3) / 1e9, 1)
+                d["frac_of_8TBps"] = round(self.payload / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+            else:
+                d["us_per_block"] = round(ms * 1e3 / (self.size / 64), 4)
+            res[name] = d
+        return res
+
+    def spot_check(self):
+        import hashlib
+
+        oracle = _oracle()
+        body = self.buf[0].cpu().numpy().tobytes()
+        rec = self.out[0].cpu().numpy()
+        return (rec[0:16].tobytes() == hashlib.md5(body).digest()
+                and int.from_bytes(rec[20:24].tobytes(), "little") == oracle.crc32c(body, fast=True))
+
+    def cpu_work(self):
+        import hashlib
+
+        import numpy as np
+
+        oracle = _oracle()
+        body = np.random.default_rng(SEED).integers(0, 256, self.size, dtype=np.uint8).tobytes()
+
+        def work(i):
+            hashlib.md5(body).digest()
+            oracle.crc32c(body, fast=True)
+
+        return work, self.size, ("hashlib.md5 (OpenSSL, as the md-5 crate) + CRC32C with SSE4.2 "
+                                 "(the crc32c crate's hardware path) over one body per call")
+
+    def drop(self):
+        del self.buf, self.out
+
+
 def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
     seed = SEED + rank
     if cfg == "2":
@@ -285,6 +362,8 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
                       "GPU (BASELINE configs[3], literal reading)", seed)
     if cfg == "5":
         return Mixed(torch, ctx, dev, sh, 24 << 30, seed)
+    if cfg == "sums":
+        return BodySums(torch, ctx, dev, sh, n_objects or 1024, 40 << 20, seed)
     raise SystemExit(f"unknown --config {cfg}")
 
 
@@ -348,7 +427,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="2", choices=["2", "3", "4a", "4b", "5"])
+    ap.add_argument("--config", default="2", choices=["2", "3", "4a", "4b", "5", "sums"])
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra", action="store_true",
@@ -403,7 +482,29 @@ def main() -> int:
     value = float(w.payload) * world * args.steps / GIB / elapsed  # weak scaling: all ranks
     achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
 
+    # §8(d) second denominator: this box's device copy rate (read + write).
+    copy_peak = None
+    if rank == 0:
+        src = torch.empty(2 << 30, dtype=torch.uint8, device=dev)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(5):
+            dst.copy_(src)
+        torch.cuda.synchronize()
+        copy_peak = 2 * src.numel() * 5 / (time.perf_counter() - t) / 1e9
+        del src, dst
+
     extra = None
+    if rank == 0 and hasattr(w, "breakdown"):
+        extra = {"breakdown": w.breakdown()}
+        crc = extra["breakdown"]["crc32c"]
+        # The HBM-bound kernel of this workload is the CRC pass; MD5 is a
+        # serial chain per body (us_per_block in the breakdown).
+        ms_launch = crc["ms"]
+        achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
+        w.kernel = "crc_tiles_kernel + crc_finish_kernel (CRC32C alone)"
     if args.extra and rank == 0 and args.config == "2":
         extra = secondary(ctx, torch, dev, sh, w)
     cpu = cpu_all = None
@@ -457,6 +558,8 @@ def main() -> int:
                 "bytes_per_launch": float(w.alg_bytes),
                 "ms_per_launch": round(ms_launch, 4),
                 "traffic_source": tsrc,
+                "box_copy_GBps": round(copy_peak, 1) if copy_peak else None,
+                "frac_of_box_copy": round(achieved / copy_peak, 4) if copy_peak else None,
             },
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,

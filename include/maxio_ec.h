@@ -31,6 +31,9 @@
  *   mxec_put_object_chunked  the file-level functions themselves, writing the
  *                            same `{key}.ec/{index:06}` files and manifest.json
  *                            (filesystem.rs:686-828, 1062-1145; chunk_reader.rs:87-226)
+ *   mxec_reader_*            VerifiedChunkReader (chunk_reader.rs:35-85, 228-276)
+ *   mxec_body_sums*          the PUT body digests: Md5 ETag + ChecksumHasher
+ *                            (filesystem.rs:28-63, 700-725, 775-777)
  */
 #ifndef MAXIO_EC_H
 #define MAXIO_EC_H
@@ -228,6 +231,38 @@ int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir,
 int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir,
                             uint64_t chunk_size, uint32_t parity_shards,
                             const uint8_t* body, size_t len);
+
+/* ---- PUT body digests (filesystem.rs:28-63, 700-725, 775-777) -------------
+ * Every PUT hashes the whole body with MD5 (the ETag, hex-encoded and quoted
+ * by the caller) and, when the request names an algorithm, with the
+ * ChecksumHasher (x-amz-checksum-*, base64 of the bytes below).              */
+#define MXEC_SUM_MD5    0x01u
+#define MXEC_SUM_CRC32  0x02u /* crc32fast::Hasher::finalize               */
+#define MXEC_SUM_CRC32C 0x04u /* crc32c::crc32c_append(0, body)            */
+#define MXEC_SUM_SHA1   0x08u
+#define MXEC_SUM_SHA256 0x10u
+typedef struct mxec_body_sums {
+    uint8_t md5[16];
+    uint32_t crc32;  /* the u32 value; to_be_bytes() before base64 */
+    uint32_t crc32c;
+    uint8_t sha1[20];
+    uint8_t sha256[32];
+} mxec_body_sums;    /* 76 bytes; fields not requested are left untouched */
+
+/* Digests of n host bodies (one record each). */
+int mxec_body_sums_batch(mxec_ctx* ctx, const uint8_t* const* bodies, const uint64_t* lens,
+                         uint64_t n, uint32_t which, mxec_body_sums* out);
+/* Device-resident bodies (host array of device pointers); out_dev is a device
+ * array of n records, written asynchronously on `stream`. */
+int mxec_body_sums_batch_device(mxec_ctx* ctx, int dev, void* stream,
+                                const uint8_t* const* bodies_dev, const uint64_t* lens,
+                                uint64_t n, uint32_t which, mxec_body_sums* out_dev);
+/* put_object_chunked plus the body digests it computes on the way
+ * (PutResult etag / checksum_value, filesystem.rs:775-777). */
+int mxec_put_object_chunked_sums(mxec_ctx* ctx, const char* ec_dir,
+                                 uint64_t chunk_size, uint32_t parity_shards,
+                                 const uint8_t* body, size_t len, uint32_t which,
+                                 mxec_body_sums* sums_out);
 
 /* GET of a whole EC object (VerifiedChunkReader over manifest.json,
  * chunk_reader.rs:35-152): verified chunks, RS recovery of bad ones.

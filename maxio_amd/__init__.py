@@ -7,6 +7,13 @@ Python mirror of that ABI used by the tests and bench.py.
 """
 from .ec import (  # noqa: F401
     DATA_ONLY,
+    SUM_CRC32,
+    SUM_CRC32C,
+    SUM_MD5,
+    SUM_SHA1,
+    SUM_SHA256,
+    ChunkReader,
+    put_result,
     Context,
     ReedSolomon,
     RSError,
@@ -21,6 +28,13 @@ __all__ = [
     "ReedSolomon",
     "RSError",
     "DATA_ONLY",
+    "SUM_MD5",
+    "SUM_CRC32",
+    "SUM_CRC32C",
+    "SUM_SHA1",
+    "SUM_SHA256",
+    "ChunkReader",
+    "put_result",
     "device_count",
     "parity_matrix",
     "rs_check",

@@ -22,6 +22,18 @@ class NativeLibraryMissing(RuntimeError):
     pass
 
 
+class BodySums(ctypes.Structure):
+    """mxec_body_sums: Md5 ETag + ChecksumHasher values (filesystem.rs:28-63)."""
+
+    _fields_ = [
+        ("md5", ctypes.c_uint8 * 16),
+        ("crc32", ctypes.c_uint32),
+        ("crc32c", ctypes.c_uint32),
+        ("sha1", ctypes.c_uint8 * 20),
+        ("sha256", ctypes.c_uint8 * 32),
+    ]
+
+
 class ChunkInfo(ctypes.Structure):
     """mxec_chunk_info == the reference's ChunkInfo (storage/mod.rs:182-189)."""
 
@@ -72,6 +84,10 @@ _SIGS = {
     "mxec_compute_and_write_parity": (
         INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, ctypes.POINTER(ChunkInfo), INT, ctypes.POINTER(ChunkInfo)]),
     "mxec_put_object_chunked": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, SZ]),
+    "mxec_put_object_chunked_sums": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, SZ,
+                                           ctypes.c_uint32, P]),
+    "mxec_body_sums_batch": (INT, [P, PP, U64P, U64, ctypes.c_uint32, P]),
+    "mxec_body_sums_batch_device": (INT, [P, INT, P, PP, U64P, U64, ctypes.c_uint32, P]),
     "mxec_get_object_chunked": (INT, [P, ctypes.c_char_p, U64, U64, P, U64, U64P]),
     "mxec_try_reconstruct_data_chunk": (INT, [P, ctypes.c_char_p, ctypes.c_uint32, P, U64, U64P]),
     "mxec_reader_open": (INT, [P, ctypes.c_char_p, U64, U64, U64, ctypes.POINTER(ctypes.c_void_p)]),

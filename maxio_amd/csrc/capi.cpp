@@ -15,35 +15,6 @@ using namespace mxec;
 
 namespace {
 
-constexpr uint64_t kSlotAlign = 256;
-uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
-
-template <class F>
-int guarded(F&& f) {
-    try {
-        return f();
-    } catch (const std::bad_alloc&) {
-        return set_error(MXEC_E_OOM, "host allocation failed");
-    } catch (const std::exception& e) {
-        return set_error(MXEC_E_INVALID_ARG, e.what());
-    } catch (...) {
-        return set_error(MXEC_E_INVALID_ARG, "unknown exception");
-    }
-}
-
-struct DevScope {
-    Device* d = nullptr;
-    std::unique_lock<std::mutex> lk;
-    Slot* slot = nullptr;
-    int open(mxec_ctx* ctx, int dev_index) {
-        if (!ctx) return set_error(MXEC_E_INVALID_ARG, "null context");
-        d = pick_device(&ctx->c, dev_index);
-        if (!d) return set_error(MXEC_E_INVALID_ARG, "no such device in context");
-        MXEC_HIP(hipSetDevice(d->id));
-        slot = &lock_slot(*d, lk);
-        return MXEC_OK;
-    }
-};
 
 // Digest bytes for n shards of the host-staged image into out (host).
 int fetch_digests(Slot& slot, hipStream_t s, size_t n, uint8_t (*out)[32]) {

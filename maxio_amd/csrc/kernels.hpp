@@ -61,4 +61,51 @@ struct ShaArgs {
 
 hipError_t launch_sha256(const ShaArgs& a, hipStream_t s);
 
+// ---- PUT body digests (digest_kernel.hip) -----------------------------------
+enum : uint32_t { kBodyMd5 = 0, kBodySha1 = 1, kBodySha256 = 2 };
+struct BodyHashArgs {
+    const uint8_t* const* ptrs;  // [n] device pointers
+    const uint64_t* lens;        // [n]
+    const uint32_t* algs;        // [gridDim.y] kBody* per launch row
+    uint8_t* out;                // [n] records of out_stride bytes
+    uint64_t out_stride;
+    uint32_t off_md5, off_sha1, off_sha256;
+    uint32_t n;
+};
+hipError_t launch_body_hash(const BodyHashArgs& a, uint32_t n_algs, hipStream_t s);
+
+// Per-polynomial constants (reflected domain), built on the host.
+struct CrcTables {
+    uint32_t poly;
+    uint32_t slice[16][256];      // slice[k][b] = raw CRC of byte b followed by 15-k zero bytes
+    uint32_t shift4k[4][256];     // byte k of v -> (v's byte k) * x^(8*4096)
+    uint32_t shift_tile[4][256];  // same for x^(8*crc_tile_bytes())
+    uint32_t lane_shift[256];     // x^(8*16*(255-L))
+    uint32_t tile_pow[64];        // x^(8*TILE*2^j)
+    uint32_t byte_pow[64];        // x^(8*2^j)
+};
+struct CrcBody {
+    const uint8_t* base;   // floor16(p): 16-byte aligned
+    const uint8_t* tail;   // last partial unit (tail_len < 16 bytes)
+    uint64_t len;          // body length
+    uint64_t tile0;        // first tile in the launch's tile space
+    uint64_t n_tiles;
+    uint64_t pad_units;    // leading virtual zero units of the first tile
+    uint32_t head_skip;    // bytes of unit 0 before p
+    uint32_t tail_len;
+    uint32_t prev;         // running CRC to continue (crc32c_append); 0 = fresh
+    uint32_t _pad;
+};
+struct CrcArgs {
+    const CrcTables* tables;
+    const CrcBody* bodies;  // [n_bodies], tile0 ascending
+    uint32_t* tile_crc;     // [n_tiles] scratch
+    uint8_t* out;           // finished CRC of body b at out + b * out_stride
+    uint64_t out_stride;
+    uint64_t n_tiles;
+    uint32_t n_bodies;
+};
+uint64_t crc_tile_bytes();
+hipError_t launch_crc(const CrcArgs& a, int n_cus, hipStream_t s);
+
 }  // namespace mxec

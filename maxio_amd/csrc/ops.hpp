@@ -2,6 +2,9 @@
 #pragma once
 
 #include <cstdint>
+#include <exception>
+#include <mutex>
+#include <new>
 #include <vector>
 
 #include "gf256.hpp"
@@ -41,6 +44,46 @@ int decode_coef(Device& dev, const DecodePlan& plan, bool data_only, uint32_t* o
 // per object.  *plan is null when fewer than k shards are present.
 int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_only,
                 std::shared_ptr<const DecodePlan>* plan, uint32_t* off);
+
+// Host-API staging: shard slots are this many bytes apart on the device.
+constexpr uint64_t kSlotAlign = 256;
+inline uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// Runs an entry point body; no C++ exception crosses the C ABI.
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return set_error(MXEC_E_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return set_error(MXEC_E_INVALID_ARG, e.what());
+    } catch (...) {
+        return set_error(MXEC_E_INVALID_ARG, "unknown exception");
+    }
+}
+
+// A device of the context (dev_index < 0: round robin) with one of its slots
+// locked for the duration of a call.
+struct DevScope {
+    Device* d = nullptr;
+    std::unique_lock<std::mutex> lk;
+    Slot* slot = nullptr;
+    int open(mxec_ctx* ctx, int dev_index) {
+        if (!ctx) return set_error(MXEC_E_INVALID_ARG, "null context");
+        d = pick_device(&ctx->c, dev_index);
+        if (!d) return set_error(MXEC_E_INVALID_ARG, "no such device in context");
+        MXEC_HIP(hipSetDevice(d->id));
+        slot = &lock_slot(*d, lk);
+        return MXEC_OK;
+    }
+};
+
+
+// PUT body digests of device-resident bodies into mxec_body_sums records
+// (sums.cpp); enqueued on s.
+int run_body_sums(Device& d, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
+                  const std::vector<uint64_t>& lens, uint32_t which, uint8_t* out_dev, uint64_t stride);
 
 // filesystem.rs:1095 guard, then the crate's ReedSolomon::new checks.
 int check_km(int k, int m);

@@ -456,6 +456,18 @@ int mxec_try_reconstruct_data_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t 
     return MXEC_OK;
 }
 
+int mxec_put_object_chunked_sums(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
+                                 const uint8_t* body, size_t len, uint32_t which, mxec_body_sums* sums_out) {
+    if (which && !sums_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    MXEC_TRY(mxec_put_object_chunked(ctx, ec_dir, chunk_size, parity_shards, body, len));
+    if (!which) return MXEC_OK;
+    // The reference feeds the same bytes to Md5 / ChecksumHasher as it
+    // chunks them (:722-725); here one batched pass over the whole body.
+    const uint8_t* b = body ? body : reinterpret_cast<const uint8_t*>("");
+    const uint64_t l = len;
+    return mxec_body_sums_batch(ctx, &b, &l, 1, which, sums_out);
+}
+
 }  // extern "C"
 
 // ---- VerifiedChunkReader (chunk_reader.rs:12-276) --------------------------

@@ -48,6 +48,37 @@ ERROR_NAMES = {
     -42: "Json",
 }
 DATA_ONLY = 0x1
+# mxec_body_sums_batch flags (include/maxio_ec.h MXEC_SUM_*)
+SUM_MD5, SUM_CRC32, SUM_CRC32C, SUM_SHA1, SUM_SHA256 = 0x01, 0x02, 0x04, 0x08, 0x10
+_SUM_BY_ALGO = {"CRC32": SUM_CRC32, "CRC32C": SUM_CRC32C, "SHA1": SUM_SHA1, "SHA256": SUM_SHA256}
+
+
+def _sums_dict(r: "N.BodySums", which: int) -> dict:
+    d = {}
+    if which & SUM_MD5:
+        d["md5"] = bytes(r.md5)
+    if which & SUM_CRC32:
+        d["crc32"] = int(r.crc32)
+    if which & SUM_CRC32C:
+        d["crc32c"] = int(r.crc32c)
+    if which & SUM_SHA1:
+        d["sha1"] = bytes(r.sha1)
+    if which & SUM_SHA256:
+        d["sha256"] = bytes(r.sha256)
+    return d
+
+
+def put_result(sums: dict, algo: Optional[str]) -> dict:
+    """PutResult's etag / checksum_value strings (filesystem.rs:775-777)."""
+    import base64
+
+    out = {"etag": '"%s"' % sums["md5"].hex()}
+    if algo:
+        raw = {"CRC32": lambda: sums["crc32"].to_bytes(4, "big"),
+               "CRC32C": lambda: sums["crc32c"].to_bytes(4, "big"),
+               "SHA1": lambda: sums["sha1"], "SHA256": lambda: sums["sha256"]}[algo]()
+        out["checksum_value"] = base64.b64encode(raw).decode()
+    return out
 
 
 class RSError(Exception):
@@ -285,6 +316,32 @@ class Context:
     def open_reader(self, ec_dir: str, offset: int = 0, length: Optional[int] = None,
                     batch_bytes: int = 0) -> "ChunkReader":
         return ChunkReader(self, ec_dir, offset, length, batch_bytes)
+
+    def body_sums(self, bodies: Sequence, which: int = 0x1F) -> list[dict]:
+        """mxec_body_sums_batch: digests of host bodies (one dict each)."""
+        arrs = [_u8(b) for b in bodies]
+        n = len(arrs)
+        if n == 0:
+            return []
+        out = (N.BodySums * n)()
+        _check(self._lib.mxec_body_sums_batch(self._h, _pp([_ptr(a) for a in arrs]),
+                                              _u64p([a.size for a in arrs]), n, which, out))
+        return [_sums_dict(out[i], which) for i in range(n)]
+
+    def body_sums_device(self, ptrs, lens, out_ptr: int, which: int = 0x1F, dev: int = 0, stream=None):
+        """mxec_body_sums_batch_device: records (76 B each) written to out_ptr."""
+        _check(self._lib.mxec_body_sums_batch_device(self._h, dev, stream, _pp(ptrs), _u64p(lens),
+                                                     len(ptrs), which, out_ptr))
+
+    def put_object_chunked_sums(self, ec_dir: str, chunk_size: int, parity_shards: int, body,
+                                checksum_algo: Optional[str] = None) -> dict:
+        """put_object_chunked + PutResult etag / checksum_value."""
+        a = _u8(body)
+        which = SUM_MD5 | (_SUM_BY_ALGO[checksum_algo] if checksum_algo else 0)
+        r = N.BodySums()
+        _check(self._lib.mxec_put_object_chunked_sums(self._h, ec_dir.encode(), chunk_size, parity_shards,
+                                                      _ptr(a), a.size, which, ctypes.byref(r)))
+        return put_result(_sums_dict(r, which), checksum_algo)
 
     def try_reconstruct_data_chunk(self, ec_dir: str, target: int, capacity: int = 1 << 26) -> bytes:
         out = np.zeros(max(1, capacity), np.uint8)

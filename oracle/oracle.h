@@ -107,6 +107,13 @@ int orc_try_reconstruct_data_chunk(int k, int m, size_t shard_size,
                                    const uint64_t* chunk_sizes, int target,
                                    uint8_t* out, int* n_present);
 
+/* --- PUT body digests (body_oracle.c; filesystem.rs:28-63, 700-777) ------ */
+uint32_t orc_crc32(const uint8_t* p, size_t n);                      /* crc32fast::hash */
+uint32_t orc_crc32c_append(uint32_t crc, const uint8_t* p, size_t n); /* crc32c::crc32c_append */
+uint32_t orc_crc32c_append_fast(uint32_t crc, const uint8_t* p, size_t n); /* SSE4.2 form */
+void orc_md5(const uint8_t* p, size_t n, uint8_t out[16]);
+void orc_sha1(const uint8_t* p, size_t n, uint8_t out[20]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,14 @@ def lib() -> ctypes.CDLL:
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.orc_sha256.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_sha256_fast.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_crc32.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.orc_crc32.restype = ctypes.c_uint32
+        L.orc_crc32c_append.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        L.orc_crc32c_append.restype = ctypes.c_uint32
+        L.orc_crc32c_append_fast.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+        L.orc_crc32c_append_fast.restype = ctypes.c_uint32
+        L.orc_md5.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_sha1.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_compute_parity.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]
@@ -122,6 +130,54 @@ def sha256(data, fast: bool = False) -> bytes:
     ptr = a.ctypes.data if a.size else np.zeros(1, np.uint8).ctypes.data
     (lib().orc_sha256_fast if fast else lib().orc_sha256)(ptr, a.size, out.ctypes.data)
     return out.tobytes()
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else np.zeros(1, np.uint8).ctypes.data
+
+
+def crc32(data) -> int:
+    """crc32fast::hash (filesystem.rs:28-63 CRC32 arm)."""
+    a = _arr(data)
+    return int(lib().orc_crc32(_ptr(a), a.size))
+
+
+def crc32c(data, crc: int = 0, fast: bool = False) -> int:
+    """crc32c::crc32c_append(crc, data) (CRC32C arm); fast = SSE4.2 form."""
+    a = _arr(data)
+    f = lib().orc_crc32c_append_fast if fast else lib().orc_crc32c_append
+    return int(f(crc, _ptr(a), a.size))
+
+
+def md5(data) -> bytes:
+    a = _arr(data)
+    out = np.zeros(16, np.uint8)
+    lib().orc_md5(_ptr(a), a.size, out.ctypes.data)
+    return out.tobytes()
+
+
+def sha1(data) -> bytes:
+    a = _arr(data)
+    out = np.zeros(20, np.uint8)
+    lib().orc_sha1(_ptr(a), a.size, out.ctypes.data)
+    return out.tobytes()
+
+
+def put_checksum_b64(algo: str, data) -> str:
+    """ChecksumHasher::finalize_base64 (filesystem.rs:55-63)."""
+    import base64
+
+    if algo == "CRC32":
+        raw = crc32(data).to_bytes(4, "big")
+    elif algo == "CRC32C":
+        raw = crc32c(data).to_bytes(4, "big")
+    elif algo == "SHA1":
+        raw = sha1(data)
+    elif algo == "SHA256":
+        raw = sha256(data)
+    else:
+        raise ValueError(algo)
+    return base64.b64encode(raw).decode()
 
 
 def compute_parity(data: Sequence, m: int, chunk_size: int):

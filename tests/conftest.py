@@ -15,6 +15,15 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's): whichever
+# loads first serves the whole process.  Load torch's first so the tests that
+# use torch as a device allocator and libmaxio_ec share that runtime, as in
+# bench.py.
+try:
+    import torch  # noqa: F401
+except ImportError:  # CPU-only environments without torch still run the oracle tests
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libmaxio_ec.so")
