@@ -52,6 +52,8 @@ extern "C" {
 #define ORC_E_SINGULAR_MATRIX (-14)
 #define ORC_E_TOO_MANY_SHARDS_255 (-20)
 #define ORC_E_INVALID_ARG (-21)
+#define ORC_E_AUTH (-41)        /* "AES-GCM decryption failed: authentication error" */
+#define ORC_E_FRAME_INDEX (-44) /* "frame index mismatch" */
 
 /* --- galois_8 --------------------------------------------------------- */
 uint8_t orc_gf_mul(uint8_t a, uint8_t b);
@@ -113,6 +115,19 @@ uint32_t orc_crc32c_append(uint32_t crc, const uint8_t* p, size_t n); /* crc32c:
 uint32_t orc_crc32c_append_fast(uint32_t crc, const uint8_t* p, size_t n); /* SSE4.2 form */
 void orc_md5(const uint8_t* p, size_t n, uint8_t out[16]);
 void orc_sha1(const uint8_t* p, size_t n, uint8_t out[20]);
+
+/* --- encrypt-then-EC frames (gcm_oracle.c; storage/crypto.rs) ------------ */
+void orc_aes256_expand(const uint8_t key[32], uint8_t rk[240]);
+void orc_aes256_encrypt_block(const uint8_t rk[240], const uint8_t in[16], uint8_t out[16]);
+void orc_gf128_mul(const uint8_t x[16], const uint8_t y[16], uint8_t out[16]);
+int orc_gcm_encrypt(const uint8_t key[32], const uint8_t iv[12], const uint8_t* aad, size_t aad_len,
+                    const uint8_t* pt, size_t len, uint8_t* ct, uint8_t tag[16]);
+int orc_gcm_decrypt(const uint8_t key[32], const uint8_t iv[12], const uint8_t* aad, size_t aad_len,
+                    const uint8_t* ct, size_t len, const uint8_t tag[16], uint8_t* pt);
+int orc_frames_encrypt(const uint8_t key[32], const uint8_t prefix[4], uint64_t first_index, const uint8_t* aad,
+                       size_t aad_len, size_t frame_size, const uint8_t* pt, size_t len, uint8_t* out);
+int orc_frames_decrypt(const uint8_t key[32], uint64_t first_index, const uint8_t* aad, size_t aad_len,
+                       size_t frame_size, const uint8_t* frames, size_t plaintext_size, uint8_t* out);
 
 #ifdef __cplusplus
 }

@@ -49,6 +49,18 @@ def lib() -> ctypes.CDLL:
         L.orc_crc32c_append.restype = ctypes.c_uint32
         L.orc_crc32c_append_fast.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
         L.orc_crc32c_append_fast.restype = ctypes.c_uint32
+        L.orc_aes256_expand.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_aes256_encrypt_block.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_gf128_mul.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_gcm_encrypt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_gcm_decrypt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_frames_encrypt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                         ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p]
+        L.orc_frames_decrypt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_md5.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_sha1.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_compute_parity.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
@@ -161,6 +173,83 @@ def sha1(data) -> bytes:
     out = np.zeros(20, np.uint8)
     lib().orc_sha1(_ptr(a), a.size, out.ctypes.data)
     return out.tobytes()
+
+
+FRAME_CHUNK_SIZE = 65536  # crypto.rs:46
+
+
+def aes256_block(key: bytes, block: bytes) -> bytes:
+    rk = np.zeros(240, np.uint8)
+    k = _arr(key)
+    lib().orc_aes256_expand(k.ctypes.data, rk.ctypes.data)
+    b = _arr(block)
+    out = np.zeros(16, np.uint8)
+    lib().orc_aes256_encrypt_block(rk.ctypes.data, b.ctypes.data, out.ctypes.data)
+    return out.tobytes()
+
+
+def gf128_mul(x: bytes, y: bytes) -> bytes:
+    a, b = _arr(x), _arr(y)
+    out = np.zeros(16, np.uint8)
+    lib().orc_gf128_mul(a.ctypes.data, b.ctypes.data, out.ctypes.data)
+    return out.tobytes()
+
+
+def gcm_encrypt(key: bytes, iv: bytes, pt, aad=b"") -> tuple[bytes, bytes]:
+    k, v, p, a = _arr(key), _arr(iv), _arr(pt), _arr(aad)
+    ct = np.zeros(max(1, p.size), np.uint8)
+    tag = np.zeros(16, np.uint8)
+    lib().orc_gcm_encrypt(k.ctypes.data, v.ctypes.data, _ptr(a), a.size, _ptr(p), p.size, ct.ctypes.data,
+                          tag.ctypes.data)
+    return ct[:p.size].tobytes(), tag.tobytes()
+
+
+def gcm_decrypt(key: bytes, iv: bytes, ct, tag: bytes, aad=b"") -> Optional[bytes]:
+    k, v, c, a, t = _arr(key), _arr(iv), _arr(ct), _arr(aad), _arr(tag)
+    pt = np.zeros(max(1, c.size), np.uint8)
+    rc = lib().orc_gcm_decrypt(k.ctypes.data, v.ctypes.data, _ptr(a), a.size, _ptr(c), c.size, t.ctypes.data,
+                               pt.ctypes.data)
+    return None if rc else pt[:c.size].tobytes()
+
+
+def frames_len(n: int, frame_size: int = FRAME_CHUNK_SIZE) -> int:
+    return n + 28 * ((n + frame_size - 1) // frame_size)
+
+
+def frames_encrypt(key: bytes, prefix: bytes, pt, aads: Optional[Sequence[bytes]] = None,
+                   first_index: int = 0, frame_size: int = FRAME_CHUNK_SIZE) -> bytes:
+    """FrameEncryptor over a whole buffer; aads[i] = AAD of frame i (equal lengths)."""
+    p = _arr(pt)
+    out = np.zeros(max(1, frames_len(p.size, frame_size)), np.uint8)
+    a = _arr(b"".join(aads)) if aads else np.zeros(0, np.uint8)
+    alen = len(aads[0]) if aads else 0
+    lib().orc_frames_encrypt(_arr(key).ctypes.data, _arr(prefix).ctypes.data, first_index,
+                             a.ctypes.data if aads else None, alen, frame_size, _ptr(p), p.size, out.ctypes.data)
+    return out[:frames_len(p.size, frame_size)].tobytes()
+
+
+def frames_decrypt(key: bytes, frames, plaintext_size: int, aads: Optional[Sequence[bytes]] = None,
+                   first_index: int = 0, frame_size: int = FRAME_CHUNK_SIZE):
+    """FrameDecryptor over a whole buffer -> (rc, plaintext)."""
+    f = _arr(frames)
+    out = np.zeros(max(1, plaintext_size), np.uint8)
+    a = _arr(b"".join(aads)) if aads else np.zeros(0, np.uint8)
+    alen = len(aads[0]) if aads else 0
+    rc = lib().orc_frames_decrypt(_arr(key).ctypes.data, first_index, a.ctypes.data if aads else None, alen,
+                                  frame_size, _ptr(f), plaintext_size, out.ctypes.data)
+    return int(rc), out[:plaintext_size].tobytes()
+
+
+def frame_aad(prefix: bytes, index: int) -> bytes:
+    """build_frame_aad / build_part_aad (filesystem.rs:118-158): SHA-256 of the
+    identity prefix || chunk_index as u64 LE."""
+    import hashlib
+
+    return hashlib.sha256(prefix + index.to_bytes(8, "little")).digest()
+
+
+def object_aad_prefix(bucket: str, key: str, version_id: Optional[str] = None) -> bytes:
+    return bucket.encode() + b"\0" + key.encode() + b"\0" + (version_id or "").encode() + b"\0"
 
 
 def put_checksum_b64(algo: str, data) -> str:
