@@ -34,6 +34,8 @@
  *   mxec_reader_*            VerifiedChunkReader (chunk_reader.rs:35-85, 228-276)
  *   mxec_body_sums*          the PUT body digests: Md5 ETag + ChecksumHasher
  *                            (filesystem.rs:28-63, 700-725, 775-777)
+ *   mxec_frames_*            FrameEncryptor / FrameDecryptor (storage/crypto.rs)
+ *                            and the frame AAD builders (filesystem.rs:112-163)
  */
 #ifndef MAXIO_EC_H
 #define MAXIO_EC_H
@@ -231,6 +233,56 @@ int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir,
 int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir,
                             uint64_t chunk_size, uint32_t parity_shards,
                             const uint8_t* body, size_t len);
+
+/* ---- encrypt-then-EC frames (src/storage/crypto.rs, filesystem.rs:112-163) --
+ * The object body is cut into frame_size (FRAME_CHUNK_SIZE = 65536) plaintext
+ * frames; frame i is nonce(12) = prefix(4) || (first_index + i) as u64 LE,
+ * then the AES-256-GCM ciphertext, then the 16-byte tag (crypto.rs:1-20,
+ * 426-432).  The EC layer then chunks these bytes like any body.
+ * aad: NULL with aad_len 0 (no_aad), or n_frames * aad_len bytes with frame
+ * i's AAD at aad + i * aad_len (mxec_frame_aads builds the reference's
+ * SHA-256(identity || index LE) AADs).                                      */
+#define MXEC_FRAME_CHUNK_SIZE 65536u
+#define MXEC_FRAME_OVERHEAD 28u
+/* Bytes of the frame stream for plaintext_len bytes. */
+uint64_t mxec_frames_len(uint64_t plaintext_len, uint32_t frame_size);
+/* FrameEncryptor over a whole buffer; out receives mxec_frames_len bytes. */
+int mxec_frames_encrypt(mxec_ctx* ctx, const uint8_t key[32], const uint8_t nonce_prefix[4],
+                        uint64_t first_index, const uint8_t* aad, uint32_t aad_len,
+                        uint32_t frame_size, const uint8_t* pt, uint64_t len,
+                        uint8_t* out, uint64_t out_cap, uint64_t* out_len);
+/* FrameDecryptor over a whole buffer: every frame's stored index and tag are
+ * checked (MXEC_E_INTEGRITY with crypto.rs's messages: "frame index mismatch:
+ * expected E, got G", "AES-GCM decryption failed: authentication error",
+ * "truncated encrypted frame"); no plaintext is returned on failure. */
+int mxec_frames_decrypt(mxec_ctx* ctx, const uint8_t key[32], uint64_t first_index,
+                        const uint8_t* aad, uint32_t aad_len, uint32_t frame_size,
+                        const uint8_t* frames, uint64_t frames_len, uint64_t plaintext_size,
+                        uint8_t* out, uint64_t out_cap, uint64_t* out_len);
+/* Device-resident batches: one launch over every frame of every job. */
+typedef struct mxec_frames_job {
+    const uint8_t* key;       /* host, 32 bytes */
+    uint8_t nonce_prefix[4];  /* encrypt only */
+    uint32_t frame_size;
+    uint64_t first_index;
+    const uint8_t* aad_dev;   /* device, n_frames * aad_len bytes, or NULL */
+    uint32_t aad_len;
+    uint32_t reserved;
+    const uint8_t* in_dev;    /* encrypt: plaintext; decrypt: frame stream */
+    uint64_t len;             /* plaintext bytes */
+    uint8_t* out_dev;         /* encrypt: frame stream; decrypt: plaintext */
+} mxec_frames_job;
+int mxec_frames_encrypt_device(mxec_ctx* ctx, int dev, void* stream,
+                               const mxec_frames_job* jobs, uint64_t n_jobs);
+/* Synchronous; status_out[j] = 0 or MXEC_E_INTEGRITY per job. */
+int mxec_frames_decrypt_device(mxec_ctx* ctx, int dev, void* stream,
+                               const mxec_frames_job* jobs, uint64_t n_jobs,
+                               int32_t* status_out);
+/* build_frame_aad / build_part_aad (filesystem.rs:118-158): out[i] =
+ * SHA-256(prefix || (first_index + i) as u64 LE), prefix = the identity bytes
+ * (bucket 0 key 0 version 0, or "PART" 0 upload_id 0 part_le4 0). */
+int mxec_frame_aads(mxec_ctx* ctx, const uint8_t* prefix, uint32_t prefix_len,
+                    uint64_t first_index, uint64_t n_frames, uint8_t (*out)[32]);
 
 /* ---- PUT body digests (filesystem.rs:28-63, 700-725, 775-777) -------------
  * Every PUT hashes the whole body with MD5 (the ETag, hex-encoded and quoted

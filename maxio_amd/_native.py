@@ -34,6 +34,23 @@ class BodySums(ctypes.Structure):
     ]
 
 
+class FramesJob(ctypes.Structure):
+    """mxec_frames_job (encrypt-then-EC frames, storage/crypto.rs)."""
+
+    _fields_ = [
+        ("key", ctypes.c_void_p),
+        ("nonce_prefix", ctypes.c_uint8 * 4),
+        ("frame_size", ctypes.c_uint32),
+        ("first_index", ctypes.c_uint64),
+        ("aad_dev", ctypes.c_void_p),
+        ("aad_len", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("in_dev", ctypes.c_void_p),
+        ("len", ctypes.c_uint64),
+        ("out_dev", ctypes.c_void_p),
+    ]
+
+
 class ChunkInfo(ctypes.Structure):
     """mxec_chunk_info == the reference's ChunkInfo (storage/mod.rs:182-189)."""
 
@@ -87,6 +104,12 @@ _SIGS = {
     "mxec_put_object_chunked_sums": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, SZ,
                                            ctypes.c_uint32, P]),
     "mxec_body_sums_batch": (INT, [P, PP, U64P, U64, ctypes.c_uint32, P]),
+    "mxec_frames_len": (U64, [U64, ctypes.c_uint32]),
+    "mxec_frames_encrypt": (INT, [P, P, P, U64, P, ctypes.c_uint32, ctypes.c_uint32, P, U64, P, U64, U64P]),
+    "mxec_frames_decrypt": (INT, [P, P, U64, P, ctypes.c_uint32, ctypes.c_uint32, P, U64, U64, P, U64, U64P]),
+    "mxec_frames_encrypt_device": (INT, [P, INT, P, P, U64]),
+    "mxec_frames_decrypt_device": (INT, [P, INT, P, P, U64, ctypes.POINTER(ctypes.c_int32)]),
+    "mxec_frame_aads": (INT, [P, P, ctypes.c_uint32, U64, U64, P]),
     "mxec_body_sums_batch_device": (INT, [P, INT, P, PP, U64P, U64, ctypes.c_uint32, P]),
     "mxec_get_object_chunked": (INT, [P, ctypes.c_char_p, U64, U64, P, U64, U64P]),
     "mxec_try_reconstruct_data_chunk": (INT, [P, ctypes.c_char_p, ctypes.c_uint32, P, U64, U64P]),

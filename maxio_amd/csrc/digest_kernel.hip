@@ -299,6 +299,7 @@ __global__ __launch_bounds__(64) void body_hash_kernel(BodyHashArgs a) {
 // ((255 - L) * 16 bytes, a per-lane constant) and the 256 lanes are XORed.
 
 constexpr int kCrcRows = 32;
+constexpr int kCrcDepth = 4;  // rows in flight per lane
 
 // Reflected-domain a * b mod P (zlib multmodp), fixed 32 iterations.
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b, uint32_t poly) {
@@ -352,7 +353,9 @@ __global__ __launch_bounds__(256) void crc_tiles_kernel(CrcArgs a) {
         // real unit = virtual - pad (pad = leading virtual zero units).
         const int64_t first = int64_t(t_in) * kCrcRows * 256 - int64_t(bd.pad_units);
         const int r0 = first < 0 ? int((-first) / 256) : 0;  // rows entirely in the padding
-        auto load_unit = [&](int r) {
+        // Row r0 is the only row that can hold padding units or the masked
+        // head unit; every later row is entirely real data.
+        auto load_first = [&](int r) {
             const int64_t u = first + int64_t(r) * 256 + lane;
             u32x4 v = {0u, 0u, 0u, 0u};
             if (u >= 0) {
@@ -372,14 +375,11 @@ __global__ __launch_bounds__(256) void crc_tiles_kernel(CrcArgs a) {
             }
             return v;
         };
-        uint32_t acc = 0;
-        // One row ahead in flight while the current row is folded.
-        u32x4 nxt = load_unit(r0);
-        for (int r = r0; r < kCrcRows; ++r) {
-            const u32x4 v = nxt;
-            if (r + 1 < kCrcRows) nxt = load_unit(r + 1);
+        gvec row_base = (gvec)(bd.base) + (first + lane);  // unit of row 0 for this lane
+        auto load_row = [&](int r) { return row_base[int64_t(r) * 256]; };
+        auto fold = [&](uint32_t acc, const u32x4& v) {
             // slice[k] = T_(15-k): byte j of the unit is 15 - j bytes from its end.
-            // 20 lookups folded by v_bitop3 XOR3s (10 VALU instead of 19).
+            // 20 lookups folded by v_bitop3 XOR3s.
             uint32_t t[20];
             lut4v(lds.shift4k, acc, t);
             lut4v(&lds.slice[0], v.x, t + 4);
@@ -390,7 +390,41 @@ __global__ __launch_bounds__(256) void crc_tiles_kernel(CrcArgs a) {
 #pragma unroll
             for (int q = 0; q < 6; ++q) u[q] = xor3(t[3 * q], t[3 * q + 1], t[3 * q + 2]);
             u[6] = t[18] ^ t[19];
-            acc = xor3(xor3(u[0], u[1], u[2]), xor3(u[3], u[4], u[5]), u[6]);
+            return xor3(xor3(u[0], u[1], u[2]), xor3(u[3], u[4], u[5]), u[6]);
+        };
+        uint32_t acc = 0;
+        if (first >= 0) {
+            // Common case: every row real.  Fully unrolled so the ring slots
+            // stay in fixed registers; row r + kCrcDepth is issued before row
+            // r is folded, and the scheduler may not hoist row r's lookups
+            // above that load (it would wait for the whole ring).
+            u32x4 ring[kCrcDepth];
+#pragma unroll
+            for (int j = 0; j < kCrcDepth; ++j) ring[j] = load_row(j);
+#pragma unroll
+            for (int rr = 0; rr < kCrcRows; ++rr) {
+                u32x4 v = ring[rr % kCrcDepth];
+                if (rr + kCrcDepth < kCrcRows) ring[rr % kCrcDepth] = load_row(rr + kCrcDepth);
+                __builtin_amdgcn_sched_barrier(0);
+                if (rr == 0 && first == 0 && lane == 0 && bd.head_skip) {
+                    const uint32_t sk = bd.head_skip;  // bytes before the body's start
+                    uint32_t* ww = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t lo_b = 4 * q;
+                        const uint32_t keep = sk >= lo_b + 4 ? 0u
+                                              : sk <= lo_b   ? 0xFFFFFFFFu
+                                                             : (0xFFFFFFFFu << (8 * (sk - lo_b)));
+                        ww[q] &= keep;
+                    }
+                }
+                acc = fold(acc, v);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+            // First tile of a body with leading padding rows: row by row.
+            acc = fold(0u, load_first(r0));
+            for (int r = r0 + 1; r < kCrcRows; ++r) acc = fold(acc, load_row(r));
         }
         acc = multmodp(klane, acc, poly);
 #pragma unroll

@@ -1,0 +1,240 @@
+// gcm_kernel.hip — encrypt-then-EC frames: AES-256-GCM over 64 KiB frames
+// for gfx950 (src/storage/crypto.rs).
+//
+// Frame f = nonce(12) = prefix(4) || index (u64 LE) || ciphertext || tag(16)
+// (crypto.rs:94-117, 426-432); every frame is an independent GCM message, so
+// one workgroup (256 threads) owns one frame at a time (grid-stride).
+//
+// * AES-256 counter blocks: T-table rounds (Te0..Te3 in LDS, 4 KiB), round
+//   keys read uniformly (scalar loads); lane l encrypts blocks l, l+256, ...
+//   so loads and stores stay coalesced.
+// * GHASH is linear: Y = sum_i X_i * H^(m-i) over the m blocks
+//   (AAD, ciphertext, length).  Lane l folds its blocks by Horner with the
+//   fixed multiplier H^256 (a 4-bit position table in LDS, 32 lookups per
+//   block, no reduction step), then multiplies by its own H^(m - i_last)
+//   once, and the workgroup XOR-reduces.  Tag = E(J0) ^ Y.
+// GF(2^128) elements are 4 big-endian u32 words (word 0 = bytes 0..3), bit 0
+// of the field element = MSB of byte 0 (SP 800-38D).
+#include "kernels.hpp"
+
+namespace mxec {
+namespace {
+
+typedef gcm_u32x4 u32x4;
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+struct GcmLds {
+    uint32_t te[4][256];
+    u32x4 htab[32][16];  // object's H^256 table (GcmKey::htab)
+};
+
+// One AES-256 block: in/out as big-endian column words.
+__device__ __forceinline__ void aes_block(const uint32_t (*te)[256], const uint32_t* __restrict__ rk,
+                                          uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        const uint32_t t0 = xor3(te[0][s0 >> 24], te[1][(s1 >> 16) & 0xFF], te[2][(s2 >> 8) & 0xFF]) ^ te[3][s3 & 0xFF];
+        const uint32_t t1 = xor3(te[0][s1 >> 24], te[1][(s2 >> 16) & 0xFF], te[2][(s3 >> 8) & 0xFF]) ^ te[3][s0 & 0xFF];
+        const uint32_t t2 = xor3(te[0][s2 >> 24], te[1][(s3 >> 16) & 0xFF], te[2][(s0 >> 8) & 0xFF]) ^ te[3][s1 & 0xFF];
+        const uint32_t t3 = xor3(te[0][s3 >> 24], te[1][(s0 >> 16) & 0xFF], te[2][(s1 >> 8) & 0xFF]) ^ te[3][s2 & 0xFF];
+        s0 = t0 ^ rk[4 * r + 0];
+        s1 = t1 ^ rk[4 * r + 1];
+        s2 = t2 ^ rk[4 * r + 2];
+        s3 = t3 ^ rk[4 * r + 3];
+    }
+    // Last round: SubBytes + ShiftRows, the S-box byte taken from the table
+    // whose byte lane holds S[x] unmultiplied.
+    const uint32_t* k = rk + 56;
+    const uint32_t u0 = (te[2][s0 >> 24] & 0xFF000000u) ^ (te[3][(s1 >> 16) & 0xFF] & 0x00FF0000u) ^
+                        (te[0][(s2 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s3 & 0xFF] & 0x000000FFu) ^ k[0];
+    const uint32_t u1 = (te[2][s1 >> 24] & 0xFF000000u) ^ (te[3][(s2 >> 16) & 0xFF] & 0x00FF0000u) ^
+                        (te[0][(s3 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s0 & 0xFF] & 0x000000FFu) ^ k[1];
+    const uint32_t u2 = (te[2][s2 >> 24] & 0xFF000000u) ^ (te[3][(s3 >> 16) & 0xFF] & 0x00FF0000u) ^
+                        (te[0][(s0 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s1 & 0xFF] & 0x000000FFu) ^ k[2];
+    const uint32_t u3 = (te[2][s3 >> 24] & 0xFF000000u) ^ (te[3][(s0 >> 16) & 0xFF] & 0x00FF0000u) ^
+                        (te[0][(s1 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s2 & 0xFF] & 0x000000FFu) ^ k[3];
+    s0 = u0; s1 = u1; s2 = u2; s3 = u3;
+}
+
+// x * H^256 via the position table: sum over the 32 nibbles of x.
+__device__ __forceinline__ u32x4 mul_htab(const u32x4 (*ht)[16], u32x4 x) {
+    u32x4 z = {0u, 0u, 0u, 0u};
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int n = 0; n < 8; n += 2) {
+            const u32x4 a = ht[8 * q + n][(w[q] >> (28 - 4 * n)) & 0xF];
+            const u32x4 b = ht[8 * q + n + 1][(w[q] >> (24 - 4 * n)) & 0xF];
+            z.x = xor3(z.x, a.x, b.x);
+            z.y = xor3(z.y, a.y, b.y);
+            z.z = xor3(z.z, a.z, b.z);
+            z.w = xor3(z.w, a.w, b.w);
+        }
+    }
+    return z;
+}
+
+// Generic x * y (SP 800-38D Algorithm 1), 128 steps, branch free.
+__device__ __forceinline__ u32x4 mul_bitwise(u32x4 x, u32x4 y) {
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+    uint32_t v0 = y.x, v1 = y.y, v2 = y.z, v3 = y.w;
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t xw = w[q];
+#pragma unroll 8
+        for (int b = 0; b < 32; ++b) {
+            const uint32_t m = uint32_t(int32_t(xw) >> 31);  // bit set -> all ones
+            xw <<= 1;
+            z0 ^= v0 & m; z1 ^= v1 & m; z2 ^= v2 & m; z3 ^= v3 & m;
+            const uint32_t lsb = 0u - (v3 & 1u);
+            v3 = __builtin_amdgcn_alignbit(v2, v3, 1);
+            v2 = __builtin_amdgcn_alignbit(v1, v2, 1);
+            v1 = __builtin_amdgcn_alignbit(v0, v1, 1);
+            v0 = (v0 >> 1) ^ (0xE1000000u & lsb);
+        }
+    }
+    return u32x4{z0, z1, z2, z3};
+}
+
+// Up to 16 bytes at p (n <= 16) as big-endian words, zero padded.
+__device__ __forceinline__ u32x4 load_partial_be(const uint8_t* p, uint32_t n) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < n; ++i) w[i >> 2] |= uint32_t(p[i]) << (24 - 8 * (i & 3));
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ void store_partial_be(uint8_t* p, u32x4 v, uint32_t n) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t i = 0; i < n; ++i) p[i] = uint8_t(w[i >> 2] >> (24 - 8 * (i & 3)));
+}
+
+// Word q of a big-endian block keeps its first n - 4q bytes (n < 16).
+__device__ __forceinline__ uint32_t mask_be(uint32_t n, uint32_t q) {
+    const int c = int(n) - 4 * int(q);
+    return c >= 4 ? 0xFFFFFFFFu : c <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * c));
+}
+
+// 16 bytes at a 4-byte aligned address (frame payloads sit 12 bytes into a
+// frame) as big-endian words.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ u32x4 load16_be(const uint8_t* p) {
+    const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(p);
+    return u32x4{bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w)};
+}
+__device__ __forceinline__ void store16_be(uint8_t* p, u32x4 v) {
+    *reinterpret_cast<u32x4a4*>(p) = u32x4a4{bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w)};
+}
+
+template <bool kDecrypt>
+__global__ __launch_bounds__(256) void gcm_frames_kernel(GcmArgs a) {
+    __shared__ GcmLds lds;
+    __shared__ u32x4 red[4];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t t = lane; t < 4 * 256; t += 256) (&lds.te[0][0])[t] = a.te[t];
+    int64_t cur_key = -1;
+    for (uint64_t f = blockIdx.x; f < a.n_frames; f += gridDim.x) {
+        const GcmFrame fr = a.frames[f];
+        const uint32_t kidx = __builtin_amdgcn_readfirstlane(fr.key);
+        const GcmKey* key = a.keys + kidx;
+        if (int64_t(kidx) != cur_key) {  // uniform: a new object's H^256 table
+            __syncthreads();
+            for (uint32_t t = lane; t < 32 * 16; t += 256) (&lds.htab[0][0])[t] = key->htab[t / 16][t % 16];
+            cur_key = kidx;
+        }
+        __syncthreads();
+        const uint32_t* rk = key->rk;
+        const uint32_t nb = (fr.len + 15) / 16, na = (fr.aad_len + 15) / 16;
+        const uint32_t m = na + nb + 1;
+        // The 12-byte nonce: prefix || index (u64 LE).  Encrypt builds it and
+        // writes the frame header; decrypt reads the stored one (crypto.rs:323).
+        uint32_t n0, n1, n2;
+        if (kDecrypt) {
+            const u32x4 h = load_partial_be(fr.hdr, 12);
+            n0 = h.x; n1 = h.y; n2 = h.z;
+        } else {
+            n0 = fr.prefix_be;
+            n1 = bswap(uint32_t(fr.index));
+            n2 = bswap(uint32_t(fr.index >> 32));
+        }
+        // J0 = nonce || 0^31 || 1; block j of the payload uses counter 2 + j.
+        u32x4 acc = {0u, 0u, 0u, 0u};
+        uint32_t last = 0;
+        for (uint32_t i = lane; i < m; i += 256) {
+            u32x4 x;
+            if (i < na) {
+                const uint32_t off = 16 * i, n = min(16u, fr.aad_len - off);
+                x = load_partial_be(fr.aad + off, n);
+            } else if (i < na + nb) {
+                const uint32_t j = i - na, off = 16 * j, n = min(16u, fr.len - off);
+                uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = 2u + j;
+                aes_block(lds.te, rk, s0, s1, s2, s3);
+                const u32x4 ks = {s0, s1, s2, s3};
+                u32x4 in = n == 16 ? load16_be(fr.in + off) : load_partial_be(fr.in + off, n);
+                u32x4 out = {in.x ^ ks.x, in.y ^ ks.y, in.z ^ ks.z, in.w ^ ks.w};
+                if (n == 16) {
+                    store16_be(fr.out + off, out);
+                } else {
+                    store_partial_be(fr.out + off, out, n);
+                    // keystream bytes past n must not enter GHASH
+                    out.x &= mask_be(n, 0); out.y &= mask_be(n, 1);
+                    out.z &= mask_be(n, 2); out.w &= mask_be(n, 3);
+                }
+                x = kDecrypt ? in : out;  // GHASH runs over the ciphertext
+            } else {
+                const uint64_t abits = uint64_t(fr.aad_len) * 8, cbits = uint64_t(fr.len) * 8;
+                x = u32x4{uint32_t(abits >> 32), uint32_t(abits), uint32_t(cbits >> 32), uint32_t(cbits)};
+            }
+            const u32x4 h = mul_htab(lds.htab, acc);
+            acc = u32x4{h.x ^ x.x, h.y ^ x.y, h.z ^ x.z, h.w ^ x.w};
+            last = i;
+        }
+        if (lane < m) acc = mul_bitwise(acc, key->hpow[m - last - 1]);  // * H^(m - last)
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) {
+            acc.x ^= __shfl_xor(acc.x, s);
+            acc.y ^= __shfl_xor(acc.y, s);
+            acc.z ^= __shfl_xor(acc.z, s);
+            acc.w ^= __shfl_xor(acc.w, s);
+        }
+        if ((lane & 63) == 0) red[lane >> 6] = acc;
+        __syncthreads();
+        if (lane == 0) {
+            u32x4 y = red[0];
+            for (int q = 1; q < 4; ++q) y = u32x4{y.x ^ red[q].x, y.y ^ red[q].y, y.z ^ red[q].z, y.w ^ red[q].w};
+            uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = 1u;
+            aes_block(lds.te, rk, s0, s1, s2, s3);
+            const u32x4 tag = {s0 ^ y.x, s1 ^ y.y, s2 ^ y.z, s3 ^ y.w};
+            if (kDecrypt) {
+                // stored index (nonce bytes 4..11, LE) must be this frame's
+                const uint64_t stored = uint64_t(bswap(n1)) | uint64_t(bswap(n2)) << 32;
+                const u32x4 want = load_partial_be(fr.tag, 16);
+                const bool ok = want.x == tag.x && want.y == tag.y && want.z == tag.z && want.w == tag.w;
+                a.status[f] = stored != fr.index ? 2 : ok ? 0 : 1;
+            } else {
+                store_partial_be(fr.hdr, u32x4{n0, n1, n2, 0u}, 12);
+                store_partial_be(fr.tag, tag, 16);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_gcm_frames(const GcmArgs& a, bool decrypt, int n_cus, hipStream_t s) {
+    if (a.n_frames == 0) return hipSuccess;
+    const uint64_t grid = std::min<uint64_t>(a.n_frames, uint64_t(n_cus) * 6);
+    if (decrypt)
+        hipLaunchKernelGGL(gcm_frames_kernel<true>, dim3(uint32_t(grid)), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(gcm_frames_kernel<false>, dim3(uint32_t(grid)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace mxec

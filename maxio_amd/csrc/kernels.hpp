@@ -108,4 +108,34 @@ struct CrcArgs {
 uint64_t crc_tile_bytes();
 hipError_t launch_crc(const CrcArgs& a, int n_cus, hipStream_t s);
 
+// ---- encrypt-then-EC frames (gcm_kernel.hip) ----------------------------------
+// Per object (data key): AES-256 round keys as big-endian words, H^1..H^256
+// and the 4-bit position table of H^256 (htab[p][v] = (v at nibble p) * H^256).
+typedef uint32_t gcm_u32x4 __attribute__((ext_vector_type(4)));
+struct GcmKey {
+    uint32_t rk[60];
+    gcm_u32x4 hpow[256];     // hpow[e - 1] = H^e
+    gcm_u32x4 htab[32][16];
+};
+struct GcmFrame {
+    const uint8_t* in;       // payload in (plaintext / ciphertext)
+    uint8_t* out;            // payload out
+    uint8_t* hdr;            // encrypt: 12-byte nonce written here; decrypt: stored nonce
+    uint8_t* tag;            // encrypt: tag written here; decrypt: stored tag
+    const uint8_t* aad;      // aad_len bytes (may be null when aad_len == 0)
+    uint64_t index;          // chunk index of this frame
+    uint32_t len;            // payload bytes (<= frame size)
+    uint32_t aad_len;
+    uint32_t key;            // index into keys
+    uint32_t prefix_be;      // nonce prefix as a big-endian word (encrypt)
+};
+struct GcmArgs {
+    const uint32_t* te;      // Te0..Te3, 4 x 256 words
+    const GcmKey* keys;
+    const GcmFrame* frames;  // frames of one object are consecutive
+    int32_t* status;         // decrypt: 0 ok, 1 tag mismatch, 2 index mismatch
+    uint64_t n_frames;
+};
+hipError_t launch_gcm_frames(const GcmArgs& a, bool decrypt, int n_cus, hipStream_t s);
+
 }  // namespace mxec

@@ -83,6 +83,7 @@ struct Device {
     // CRC32 / CRC32C constant tables (sums.cpp), uploaded on first use.
     std::mutex sums_mu;
     DevBuf crc_tables;
+    DevBuf aes_te;  // AES T-tables (gcm.cpp)
     size_t coef_used = 0;  // dwords
     uint64_t coef_epoch = 0;  // bumped whenever the arena is recycled
     std::map<std::vector<uint8_t>, uint32_t> coef_index;

@@ -50,6 +50,7 @@ ERROR_NAMES = {
 DATA_ONLY = 0x1
 # mxec_body_sums_batch flags (include/maxio_ec.h MXEC_SUM_*)
 SUM_MD5, SUM_CRC32, SUM_CRC32C, SUM_SHA1, SUM_SHA256 = 0x01, 0x02, 0x04, 0x08, 0x10
+FRAME_CHUNK_SIZE = 65536  # crypto.rs:46
 _SUM_BY_ALGO = {"CRC32": SUM_CRC32, "CRC32C": SUM_CRC32C, "SHA1": SUM_SHA1, "SHA256": SUM_SHA256}
 
 
@@ -342,6 +343,71 @@ class Context:
         _check(self._lib.mxec_put_object_chunked_sums(self._h, ec_dir.encode(), chunk_size, parity_shards,
                                                       _ptr(a), a.size, which, ctypes.byref(r)))
         return put_result(_sums_dict(r, which), checksum_algo)
+
+    # ---- encrypt-then-EC frames (storage/crypto.rs) ----------------------------
+    def frames_encrypt(self, key: bytes, nonce_prefix: bytes, pt, aads: Optional[Sequence[bytes]] = None,
+                       first_index: int = 0, frame_size: int = FRAME_CHUNK_SIZE) -> bytes:
+        """FrameEncryptor over a whole buffer (aads[i] = frame i's AAD)."""
+        p = _u8(pt)
+        total = int(self._lib.mxec_frames_len(p.size, frame_size))
+        out = np.zeros(max(1, total), np.uint8)
+        a = _u8(b"".join(aads)) if aads else np.zeros(0, np.uint8)
+        alen = len(aads[0]) if aads else 0
+        n = ctypes.c_uint64(0)
+        k, pre = _u8(key), _u8(nonce_prefix)
+        _check(self._lib.mxec_frames_encrypt(self._h, _ptr(k), _ptr(pre), first_index, _ptr(a) if alen else None,
+                                             alen, frame_size, _ptr(p), p.size, out.ctypes.data, total,
+                                             ctypes.byref(n)))
+        return out[: n.value].tobytes()
+
+    def frames_decrypt(self, key: bytes, frames, plaintext_size: int, aads: Optional[Sequence[bytes]] = None,
+                       first_index: int = 0, frame_size: int = FRAME_CHUNK_SIZE) -> bytes:
+        """FrameDecryptor over a whole buffer; RSError(Integrity) on a bad frame."""
+        f = _u8(frames)
+        out = np.zeros(max(1, plaintext_size), np.uint8)
+        a = _u8(b"".join(aads)) if aads else np.zeros(0, np.uint8)
+        alen = len(aads[0]) if aads else 0
+        n = ctypes.c_uint64(0)
+        k = _u8(key)
+        _check(self._lib.mxec_frames_decrypt(self._h, _ptr(k), first_index, _ptr(a) if alen else None, alen,
+                                             frame_size, _ptr(f), f.size, plaintext_size, out.ctypes.data,
+                                             plaintext_size, ctypes.byref(n)))
+        return out[: n.value].tobytes()
+
+    def frames_device(self, jobs: Sequence[dict], decrypt: bool = False, dev: int = 0, stream=None):
+        """mxec_frames_{en,de}crypt_device; jobs: dicts with key, nonce_prefix,
+        frame_size, first_index, aad_dev, aad_len, in_dev, len, out_dev.
+        Decrypt returns the per-job status list."""
+        arr = (N.FramesJob * max(1, len(jobs)))()
+        keep = []
+        for i, j in enumerate(jobs):
+            k = _u8(j["key"])
+            keep.append(k)
+            arr[i].key = _ptr(k)
+            for b, v in enumerate(j.get("nonce_prefix", b"\0\0\0\0")):
+                arr[i].nonce_prefix[b] = v
+            arr[i].frame_size = j.get("frame_size", FRAME_CHUNK_SIZE)
+            arr[i].first_index = j.get("first_index", 0)
+            arr[i].aad_dev = j.get("aad_dev") or None
+            arr[i].aad_len = j.get("aad_len", 0)
+            arr[i].in_dev = j["in_dev"]
+            arr[i].len = j["len"]
+            arr[i].out_dev = j["out_dev"]
+        if not decrypt:
+            _check(self._lib.mxec_frames_encrypt_device(self._h, dev, stream, arr, len(jobs)))
+            return None
+        st = (ctypes.c_int32 * max(1, len(jobs)))()
+        self._lib.mxec_frames_decrypt_device(self._h, dev, stream, arr, len(jobs), st)
+        return [int(st[i]) for i in range(len(jobs))]
+
+    def frame_aads(self, prefix: bytes, first_index: int, n: int) -> list[bytes]:
+        """build_frame_aad for frames first_index .. first_index + n - 1."""
+        if n == 0:
+            return []
+        p = _u8(prefix)
+        out = np.zeros((n, 32), np.uint8)
+        _check(self._lib.mxec_frame_aads(self._h, _ptr(p), p.size, first_index, n, out.ctypes.data))
+        return [out[i].tobytes() for i in range(n)]
 
     def try_reconstruct_data_chunk(self, ec_dir: str, target: int, capacity: int = 1 << 26) -> bytes:
         out = np.zeros(max(1, capacity), np.uint8)
