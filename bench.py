@@ -341,6 +341,89 @@ class BodySums:
         del self.buf, self.out
 
 
+class Frames:
+    """encrypt-then-EC — AES-256-GCM frame encryption
+    (crypto.rs FrameEncryptor, 64 KiB frames, 32-byte per-frame AADs) of a
+    batch of device-resident object bodies, one launch per step."""
+
+    bound = "valu"
+
+    def __init__(self, torch, ctx, dev, sh, n, size, seed):
+        import numpy as np
+
+        self.torch, self.ctx, self.sh = torch, ctx, sh
+        self.n, self.size = n, size
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self.pt = torch.randint(0, 256, (n, size), dtype=torch.uint8, device=dev, generator=g)
+        fl = size + 28 * ((size + 65535) // 65536)
+        self.fr = torch.zeros((n, fl), dtype=torch.uint8, device=dev)
+        self.back = torch.zeros((n, size), dtype=torch.uint8, device=dev)
+        nfr = (size + 65535) // 65536
+        rng = np.random.default_rng(seed)
+        self.keys = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(n)]
+        aad = rng.integers(0, 256, (n, nfr, 32), dtype=np.uint8)
+        self.aad = torch.from_numpy(aad).to(dev)
+        self.jobs = [{"key": self.keys[o], "nonce_prefix": bytes([o & 255, 1, 2, 3]),
+                      "aad_dev": self.aad[o].data_ptr(), "aad_len": 32,
+                      "in_dev": self.pt[o].data_ptr(), "len": size, "out_dev": self.fr[o].data_ptr()}
+                     for o in range(n)]
+        self.djobs = [dict(j, in_dev=self.fr[o].data_ptr(), out_dev=self.back[o].data_ptr())
+                      for o, j in enumerate(self.jobs)]
+        self.payload = n * size
+        self.alg_bytes = n * (size + fl)  # read plaintext, write frames
+        self.kernel = "gcm_frames_kernel<encrypt> (T-table AES-256 + GHASH)"
+        self.name = (f"encrypt-then-EC: AES-256-GCM 64 KiB frames of {n} device-resident bodies x {size} B, "
+                     "32-byte AAD per frame (SURVEY 8f rank 4)")
+
+    def step(self):
+        self.ctx.frames_device(self.jobs, stream=self.sh)
+
+    def breakdown(self):
+        torch = self.torch
+        st = torch.cuda.ExternalStream(self.sh)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        status = self.ctx.frames_device(self.djobs, decrypt=True, stream=self.sh)
+        b.record(st)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b)
+        ok = all(s == 0 for s in status) and bool(torch.equal(self.back[0], self.pt[0]))
+        return {"decrypt": {"ms_incl_status_readback": round(ms, 3),
+                            "GiBps": round(self.payload / (ms * 1e-3) / GIB, 2), "round_trip_ok": ok}}
+
+    def spot_check(self):
+        oracle = _oracle()
+        o = 1 if self.n > 1 else 0
+        want = oracle.frames_encrypt(self.keys[o], self.jobs[o]["nonce_prefix"], self.pt[o].cpu().numpy(),
+                                     [bytes(x) for x in self.aad[o].cpu().numpy()])
+        return self.fr[o].cpu().numpy().tobytes() == want
+
+    def cpu_work(self):
+        import numpy as np
+
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import openssl_gcm  # baseline only: OpenSSL EVP (AES-NI + PCLMUL), as the aes-gcm crate
+
+        fn = openssl_gcm.frames_encrypt_fn()
+        if fn is None:
+            return None
+        body = np.random.default_rng(SEED).integers(0, 256, self.size, dtype=np.uint8)
+        key, pre, aad = np.zeros(32, np.uint8), np.frombuffer(b"abcd", np.uint8), np.full(32, 65, np.uint8)
+        fl = self.size + 28 * ((self.size + 65535) // 65536)
+        outs = {}
+
+        def work(i):
+            out = outs.setdefault(i, np.zeros(fl, np.uint8))  # one output buffer per thread
+            fn(key.ctypes.data, pre.ctypes.data, aad.ctypes.data, 32, 65536, body.ctypes.data, body.size,
+               out.ctypes.data)
+
+        return work, self.size, ("OpenSSL EVP_aes_256_gcm over 64 KiB frames with 32-byte AADs (AES-NI/PCLMUL, "
+                                 "as the aes-gcm crate), C loop, one body per call")
+
+    def drop(self):
+        del self.pt, self.fr, self.back, self.aad
+
+
 def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
     seed = SEED + rank
     if cfg == "2":
@@ -364,6 +447,8 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
         return Mixed(torch, ctx, dev, sh, 24 << 30, seed)
     if cfg == "sums":
         return BodySums(torch, ctx, dev, sh, n_objects or 1024, 40 << 20, seed)
+    if cfg == "frames":
+        return Frames(torch, ctx, dev, sh, n_objects or 256, 40 << 20, seed)
     raise SystemExit(f"unknown --config {cfg}")
 
 
@@ -427,7 +512,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="2", choices=["2", "3", "4a", "4b", "5", "sums"])
+    ap.add_argument("--config", default="2", choices=["2", "3", "4a", "4b", "5", "sums", "frames"])
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra", action="store_true",
@@ -499,6 +584,7 @@ def main() -> int:
     extra = None
     if rank == 0 and hasattr(w, "breakdown"):
         extra = {"breakdown": w.breakdown()}
+    if extra and "crc32c" in extra["breakdown"]:
         crc = extra["breakdown"]["crc32c"]
         # The HBM-bound kernel of this workload is the CRC pass; MD5 is a
         # serial chain per body (us_per_block in the breakdown).

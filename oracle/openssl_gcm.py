@@ -1,3 +1,4 @@
+# TEST / BASELINE INFRASTRUCTURE ONLY (see oracle.h): never imported by maxio_amd.
 """AES-256-GCM through the system OpenSSL (libcrypto.so.3, EVP API) via
 ctypes — an independent implementation used only to pin the oracle
 (tests/test_oracle_gcm.py).  None if libcrypto is not loadable."""
@@ -75,3 +76,26 @@ def decrypt(key: bytes, iv: bytes, ct: bytes, tag: bytes, aad: bytes = b"") -> O
         return out.raw[:total]
     finally:
         L.EVP_CIPHER_CTX_free(c)
+
+
+_ssl_frames = None
+
+
+def frames_encrypt_fn():
+    """orc_ssl_frames_encrypt from oracle/build/liboracle_ssl.so (CPU baseline),
+    or None."""
+    global _ssl_frames
+    if _ssl_frames is None:
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "liboracle_ssl.so")
+        try:
+            L = ctypes.CDLL(path)
+        except OSError:
+            return None
+        f = L.orc_ssl_frames_encrypt
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        f.restype = ctypes.c_int
+        _ssl_frames = f
+    return _ssl_frames
