@@ -229,132 +229,10 @@ __device__ __forceinline__ void words_le(const u32x4 (&blk)[4], uint32_t (&w)[16
 
 // blockIdx.y indexes a.algs: which digest this block computes for its 64
 // bodies.  Uniform per block, so there is no divergence between paths.
-// ---- MD5, split form ------------------------------------------------------------
-// MD5's message "schedule" is a fixed permutation of the block's words, so a
-// producer wave can hand the consumer K[t] + X[g(t)] through LDS (as the
-// SHA-256 split kernel does): the serial wave's step is then bitop3 + add3 +
-// alignbit + add.  The producer also owns the loads (4-deep ring).
-constexpr uint8_t kMd5G[64] = {0, 1, 2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
-                               1, 6, 11, 0,  5,  10, 15, 4,  9,  14, 3,  8,  13, 2,  7,  12,
-                               5, 8, 11, 14, 1,  4,  7,  10, 13, 0,  3,  6,  9,  12, 15, 2,
-                               0, 7, 14, 5,  12, 3,  10, 1,  8,  15, 6,  13, 4,  11, 2,  9};
-__constant__ uint32_t kMd5K[64] = {
-    0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u, 0xfd469501u,
-    0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u,
-    0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du, 0x02441453u, 0xd8a1e681u, 0xe7d3fbc8u,
-    0x21e1cde6u, 0xc33707d6u, 0xf4d50d87u, 0x455a14edu, 0xa9e3e905u, 0xfcefa3f8u, 0x676f02d9u, 0x8d2a4c8au,
-    0xfffa3942u, 0x8771f681u, 0x6d9d6122u, 0xfde5380cu, 0xa4beea44u, 0x4bdecfa9u, 0xf6bb4b60u, 0xbebfbc70u,
-    0x289b7ec6u, 0xeaa127fau, 0xd4ef3085u, 0x04881d05u, 0xd9d4d039u, 0xe6db99e5u, 0x1fa27cf8u, 0xc4ac5665u,
-    0xf4292244u, 0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
-    0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu, 0xeb86d391u};
-
-#define MD5_KSTEP(FN, a, b, c, d, kw, s) a = b + rotl(a + FN(b, c, d) + (kw), s)
-#define MD5_4K(FN, v, s0, s1, s2, s3)            \
-    MD5_KSTEP(FN, a, b, c, d, (v).x, s0);        \
-    MD5_KSTEP(FN, d, a, b, c, (v).y, s1);        \
-    MD5_KSTEP(FN, c, d, a, b, (v).z, s2);        \
-    MD5_KSTEP(FN, b, c, d, a, (v).w, s3)
-
-__device__ __forceinline__ void md5_compress_kw(uint32_t (&st)[4], const u32x4* kwl) {
-    u32x4 v[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = kwl[q * 64];
-    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { MD5_4K(MD5_F, v[q], 7, 12, 17, 22); }
-#pragma unroll
-    for (int q = 4; q < 8; ++q) { MD5_4K(MD5_G, v[q], 5, 9, 14, 20); }
-#pragma unroll
-    for (int q = 8; q < 12; ++q) { MD5_4K(MD5_H, v[q], 4, 11, 16, 23); }
-#pragma unroll
-    for (int q = 12; q < 16; ++q) { MD5_4K(MD5_I, v[q], 6, 10, 15, 21); }
-    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-}
-
-__device__ __forceinline__ void md5_schedule(const u32x4 (&blk)[4], u32x4* dst) {
-    uint32_t x[16];
-    words_le(blk, x);
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-        dst[q * 64] = u32x4{kMd5K[4 * q] + x[kMd5G[4 * q]], kMd5K[4 * q + 1] + x[kMd5G[4 * q + 1]],
-                            kMd5K[4 * q + 2] + x[kMd5G[4 * q + 2]], kMd5K[4 * q + 3] + x[kMd5G[4 * q + 3]]};
-}
-
-// Both waves of the block serve the same 64 bodies; wave 1 produces, wave 0
-// compresses.  Every barrier is reached by both waves (nmax is wave-uniform).
-__device__ void md5_split(const BodyHashArgs& a, u32x4 (*kw)[16][64], uint32_t wave, uint32_t lane) {
-    const uint32_t i = blockIdx.x * 64 + lane;
-    const bool live = i < a.n;
-    const uint8_t* p = live ? a.ptrs[i] : nullptr;
-    const uint64_t len = live ? a.lens[i] : 0;
-    const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-    // Unaligned bodies take the one-wave path (byte loads) on wave 0 alone.
-    const uint64_t nfull = aligned ? len / 64 : 0;
-    uint64_t nmax = nfull;
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        const uint64_t o = __shfl_xor(nmax, s);
-        nmax = o > nmax ? o : nmax;
-    }
-    u32x4 ring[kDepth][4];
-    const uint64_t lastb = nfull ? nfull - 1 : 0;
-    if (wave == 1 && nfull) {
-#pragma unroll
-        for (int j = 0; j < kDepth; ++j) load_block(p + 64 * min(uint64_t(j), lastb), ring[j]);
-        md5_schedule(ring[0], &kw[0][0][lane]);
-        load_block(p + 64 * min(uint64_t(kDepth), lastb), ring[0]);
-    }
-    __syncthreads();
-    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    for (uint64_t b0 = 0; b0 < nmax; b0 += kDepth) {
-#pragma unroll
-        for (int j = 0; j < kDepth; ++j) {
-            const uint64_t b = b0 + j;
-            if (b < nmax) {  // wave-uniform
-                if (wave == 1) {
-                    // block b+1 sits in ring slot (j+1) % kDepth
-                    if (b + 1 < nfull) {
-                        md5_schedule(ring[(j + 1) % kDepth], &kw[(b + 1) & 1][0][lane]);
-                        load_block(p + 64 * min(b + 1 + kDepth, lastb), ring[(j + 1) % kDepth]);
-                    }
-                } else if (b < nfull) {
-                    md5_compress_kw(st, &kw[b & 1][0][lane]);
-                }
-                __syncthreads();
-            }
-        }
-    }
-    if (wave == 1 || !live) return;
-    if (!aligned) {
-        hash_blocks(p, len / 64, [&](uint32_t (&x)[16]) { md5_compress(st, x); }, words_le);
-    }
-    const uint64_t nf = len / 64;
-    const uint32_t rem = uint32_t(len - nf * 64);
-    const uint8_t* tp = p + nf * 64;
-    const int nblk = (rem + 9 <= 64) ? 1 : 2;
-    const uint64_t bits = len * 8;
-    uint32_t w[16];
-    for (int blk = 0; blk < nblk; ++blk) {
-#pragma unroll
-        for (int t = 0; t < 16; ++t) w[t] = tail_word_le(tp, rem, 16 * blk + t, nblk, bits);
-        md5_compress(st, w);
-    }
-    uint32_t* o = reinterpret_cast<uint32_t*>(a.out + uint64_t(i) * a.out_stride + a.off_md5);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] = st[t];
-}
-
-__global__ __launch_bounds__(128) void body_hash_kernel(BodyHashArgs a) {
-    __shared__ u32x4 kw[2][16][64];  // MD5 split form only
-    const uint32_t alg = a.algs[blockIdx.y];
-    const uint32_t wave = threadIdx.x >> 6;
-    if (alg == kBodyMd5) {
-        md5_split(a, kw, wave, threadIdx.x & 63);
-        return;
-    }
-    if (wave == 1) return;
+__global__ __launch_bounds__(64) void body_hash_kernel(BodyHashArgs a) {
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
+    const uint32_t alg = a.algs[blockIdx.y];
     const uint8_t* p = a.ptrs[i];
     const uint64_t len = a.lens[i];
     const uint64_t nfull = len / 64;
@@ -364,7 +242,18 @@ __global__ __launch_bounds__(128) void body_hash_kernel(BodyHashArgs a) {
     const uint64_t bits = len * 8;
     uint8_t* out = a.out + uint64_t(i) * a.out_stride;
     uint32_t w[16];
-    if (alg == kBodySha1) {
+    if (alg == kBodyMd5) {
+        uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+        hash_blocks(p, nfull, [&](uint32_t (&x)[16]) { md5_compress(st, x); }, words_le);
+        for (int blk = 0; blk < nblk; ++blk) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) w[t] = tail_word_le(tp, rem, 16 * blk + t, nblk, bits);
+            md5_compress(st, w);
+        }
+        uint32_t* o = reinterpret_cast<uint32_t*>(out + a.off_md5);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[t] = st[t];
+    } else if (alg == kBodySha1) {
         uint32_t st[5] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u, 0xc3d2e1f0u};
         hash_blocks(p, nfull, [&](uint32_t (&x)[16]) { sha1_compress(st, x); },
                     [](const u32x4(&blk)[4], uint32_t(&x)[16]) { block_words(blk, x); });
@@ -591,7 +480,7 @@ __global__ __launch_bounds__(256) void crc_finish_kernel(CrcArgs a) {
 
 hipError_t launch_body_hash(const BodyHashArgs& a, uint32_t n_algs, hipStream_t s) {
     if (a.n == 0 || n_algs == 0) return hipSuccess;
-    hipLaunchKernelGGL(body_hash_kernel, dim3((a.n + 63) / 64, n_algs), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(body_hash_kernel, dim3((a.n + 63) / 64, n_algs), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
