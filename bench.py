@@ -529,8 +529,17 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # BENCH_GPU_OF_RANK=0 pins every rank to GPU 0 and BENCH_DIST_BACKEND=gloo
+        # carries the timing collectives on the host: a rehearsal of the
+        # multi-rank path on a one-GPU box.  Defaults: GPU = LOCAL_RANK, RCCL.
+        gpu = int(os.environ.get("BENCH_GPU_OF_RANK", local))
+        torch.cuda.set_device(gpu)
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+        local = gpu
     else:
         torch.cuda.set_device(0)
 

@@ -371,3 +371,21 @@ def test_short_last_chunk_device_encode_and_rebuild(ctx, last):
     assert np.array_equal(got[:, k - 1, :last], host[:, k - 1, :last])
     assert (got[:, k - 1, last:] == 0x77).all()  # untouched past the chunk's end
     assert np.array_equal(got[:, 2], host[:, 2])
+
+
+@pytest.mark.parametrize("form", ["split", "one"])
+def test_sha256_every_kernel_form(ctx, form, monkeypatch):
+    """MXEC_SHA_FORM pins the SHA-256 kernel (split: producer/consumer waves;
+    one: one wave per 64 messages).
+    Mixed lengths (multi-block, tails 0..63, unaligned starts) per form."""
+    monkeypatch.setenv("MXEC_SHA_FORM", form)
+    rng = np.random.default_rng(13)
+    lens = list(rng.integers(0, 5000, 300)) + [0, 55, 56, 64, 4096, 100_003]
+    blob = rng.integers(0, 256, int(sum(lens)) + 64, dtype=np.uint8).tobytes()
+    bufs, o = [], 0
+    for i, n in enumerate(lens):
+        o += i % 3  # some unaligned starts
+        bufs.append(blob[o:o + int(n)])
+        o += int(n)
+    got = ctx.sha256(bufs)
+    assert got == [hashlib.sha256(b).digest() for b in bufs]

@@ -141,8 +141,10 @@ int main(int argc, char** argv) {
         std::fflush(stdout);
     };
 
+    // `kernel_lab N sha` runs the SHA-256 section only.
+    const bool sha_only = argc > 2 && !std::strcmp(argv[2], "sha");
     // ---- calibration ----
-    {
+    if (!sha_only) {
         const uint64_t half = pool / 2 / 16;
         auto* s = reinterpret_cast<const u32x4*>(buf);
         auto* d = reinterpret_cast<u32x4*>(buf + pool / 2);
@@ -208,7 +210,13 @@ int main(int argc, char** argv) {
         CK(hipFree(d));
     };
     sha(10240, 1ull << 20, "10240 x 1 MiB (cfg3 verify)");
+    sha(10240, 1ull << 20, "10240 x 1 MiB split form", 2);
     sha(10240, 1ull << 20, "10240 x 1 MiB one-wave form", 1);
+    sha(1024, 10ull << 20, "1024 x 10 MiB split form", 2);
+    if (sha_only) {
+        CK(hipFree(buf));
+        return 0;
+    }
     sha(6144, 10ull << 20, "6144 x 10 MiB (cfg2 put path)");
     sha(1024, 1ull << 20, "1024 x 1 MiB");
     sha(65536, 64ull << 10, "65536 x 64 KiB");
