@@ -219,11 +219,45 @@ __global__ __launch_bounds__(kThreads) void rs_apply_edge(
         for (int w = 0; w < 4; ++w)
 #pragma unroll
             for (int i = 0; i < R; ++i) acc[0][w][i] = 0;
-        for (uint32_t j = 0; j < k; ++j) {
+        // Four inputs' loads in flight before their multiply-accumulates.
+        // Whole vectors load unconditionally from a global address (a safe
+        // dummy when the lane's vector is not whole) so the waits stay
+        // counted; the lane whose vector a length boundary cuts, and
+        // unaligned launches, take the byte path afterwards.
+        const uint8_t* safe = reinterpret_cast<const uint8_t*>(coef);
+        auto issue = [&](uint32_t j, Vec4& x, const uint8_t*& p, int64_t& valid) {
             const uint64_t len = in_len[uint64_t(obj) * k + j];
-            const int64_t valid = col < len ? int64_t(len - col) : 0;
-            Vec4 x[1] = {Vec4{{0, 0, 0, 0}}};
-            if (valid > 0) x[0] = load_partial(in_ptrs[uint64_t(obj) * k + j] + col, valid, aligned != 0);
+            valid = col < len ? int64_t(len - col) : 0;
+            p = in_ptrs[uint64_t(obj) * k + j] + col;
+            const bool full = aligned && valid >= 16;
+            x = gload16<false>(gcptr(full ? p : safe));
+        };
+        // After all four loads are issued: zero what was not a whole vector
+        // (selects, no branch), then the rare cut lane reads its bytes.
+        auto fixup = [&](Vec4& x, const uint8_t* p, int64_t valid) {
+            const bool full = aligned && valid >= 16;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) x.w[w] = full ? x.w[w] : 0u;
+            if (valid > 0 && !full) x = load_partial(p, valid, aligned != 0);
+        };
+        uint32_t j = 0;
+        for (; j + 4 <= k; j += 4) {
+            Vec4 x[4][1];
+            const uint8_t* p[4];
+            int64_t valid[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) issue(j + u, x[u][0], p[u], valid[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fixup(x[u][0], p[u], valid[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) mac_column<R, 1>(acc, x[u], tab + (j + u) * r_total * 8);
+        }
+        for (; j < k; ++j) {
+            Vec4 x[1];
+            const uint8_t* p;
+            int64_t valid;
+            issue(j, x[0], p, valid);
+            fixup(x[0], p, valid);
             mac_column<R, 1>(acc, x, tab + j * r_total * 8);
         }
 #pragma unroll
