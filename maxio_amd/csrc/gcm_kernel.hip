@@ -27,21 +27,17 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-struct GcmLds {
-    uint32_t te[4][256];
-    u32x4 htab[32][16];  // object's H^256 table (GcmKey::htab)
-};
-
-// One AES-256 block: in/out as big-endian column words.
-__device__ __forceinline__ void aes_block(const uint32_t (*te)[256], const uint32_t* __restrict__ rk,
-                                          uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3) {
+// One AES-256 block: in/out as big-endian column words; te(k, x) = Te_k[x].
+template <class TE>
+__device__ __forceinline__ void aes_block(TE te, const uint32_t* __restrict__ rk, uint32_t& s0, uint32_t& s1,
+                                          uint32_t& s2, uint32_t& s3) {
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        const uint32_t t0 = xor3(te[0][s0 >> 24], te[1][(s1 >> 16) & 0xFF], te[2][(s2 >> 8) & 0xFF]) ^ te[3][s3 & 0xFF];
-        const uint32_t t1 = xor3(te[0][s1 >> 24], te[1][(s2 >> 16) & 0xFF], te[2][(s3 >> 8) & 0xFF]) ^ te[3][s0 & 0xFF];
-        const uint32_t t2 = xor3(te[0][s2 >> 24], te[1][(s3 >> 16) & 0xFF], te[2][(s0 >> 8) & 0xFF]) ^ te[3][s1 & 0xFF];
-        const uint32_t t3 = xor3(te[0][s3 >> 24], te[1][(s0 >> 16) & 0xFF], te[2][(s1 >> 8) & 0xFF]) ^ te[3][s2 & 0xFF];
+        const uint32_t t0 = xor3(te(0, s0 >> 24), te(1, (s1 >> 16) & 0xFF), te(2, (s2 >> 8) & 0xFF)) ^ te(3, s3 & 0xFF);
+        const uint32_t t1 = xor3(te(0, s1 >> 24), te(1, (s2 >> 16) & 0xFF), te(2, (s3 >> 8) & 0xFF)) ^ te(3, s0 & 0xFF);
+        const uint32_t t2 = xor3(te(0, s2 >> 24), te(1, (s3 >> 16) & 0xFF), te(2, (s0 >> 8) & 0xFF)) ^ te(3, s1 & 0xFF);
+        const uint32_t t3 = xor3(te(0, s3 >> 24), te(1, (s0 >> 16) & 0xFF), te(2, (s1 >> 8) & 0xFF)) ^ te(3, s2 & 0xFF);
         s0 = t0 ^ rk[4 * r + 0];
         s1 = t1 ^ rk[4 * r + 1];
         s2 = t2 ^ rk[4 * r + 2];
@@ -50,15 +46,48 @@ __device__ __forceinline__ void aes_block(const uint32_t (*te)[256], const uint3
     // Last round: SubBytes + ShiftRows, the S-box byte taken from the table
     // whose byte lane holds S[x] unmultiplied.
     const uint32_t* k = rk + 56;
-    const uint32_t u0 = (te[2][s0 >> 24] & 0xFF000000u) ^ (te[3][(s1 >> 16) & 0xFF] & 0x00FF0000u) ^
-                        (te[0][(s2 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s3 & 0xFF] & 0x000000FFu) ^ k[0];
-    const uint32_t u1 = (te[2][s1 >> 24] & 0xFF000000u) ^ (te[3][(s2 >> 16) & 0xFF] & 0x00FF0000u) ^
-                        (te[0][(s3 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s0 & 0xFF] & 0x000000FFu) ^ k[1];
-    const uint32_t u2 = (te[2][s2 >> 24] & 0xFF000000u) ^ (te[3][(s3 >> 16) & 0xFF] & 0x00FF0000u) ^
-                        (te[0][(s0 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s1 & 0xFF] & 0x000000FFu) ^ k[2];
-    const uint32_t u3 = (te[2][s3 >> 24] & 0xFF000000u) ^ (te[3][(s0 >> 16) & 0xFF] & 0x00FF0000u) ^
-                        (te[0][(s1 >> 8) & 0xFF] & 0x0000FF00u) ^ (te[1][s2 & 0xFF] & 0x000000FFu) ^ k[3];
+    const uint32_t u0 = (te(2, s0 >> 24) & 0xFF000000u) ^ (te(3, (s1 >> 16) & 0xFF) & 0x00FF0000u) ^
+                        (te(0, (s2 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s3 & 0xFF) & 0x000000FFu) ^ k[0];
+    const uint32_t u1 = (te(2, s1 >> 24) & 0xFF000000u) ^ (te(3, (s2 >> 16) & 0xFF) & 0x00FF0000u) ^
+                        (te(0, (s3 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s0 & 0xFF) & 0x000000FFu) ^ k[1];
+    const uint32_t u2 = (te(2, s2 >> 24) & 0xFF000000u) ^ (te(3, (s3 >> 16) & 0xFF) & 0x00FF0000u) ^
+                        (te(0, (s0 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s1 & 0xFF) & 0x000000FFu) ^ k[2];
+    const uint32_t u3 = (te(2, s3 >> 24) & 0xFF000000u) ^ (te(3, (s0 >> 16) & 0xFF) & 0x00FF0000u) ^
+                        (te(0, (s1 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s2 & 0xFF) & 0x000000FFu) ^ k[3];
     s0 = u0; s1 = u1; s2 = u2; s3 = u3;
+}
+
+// Two independent blocks, round by round.
+template <class TE>
+__device__ __forceinline__ void aes_block2(TE te, const uint32_t* __restrict__ rk, uint32_t& s0, uint32_t& s1,
+                                           uint32_t& s2, uint32_t& s3, uint32_t& q0, uint32_t& q1, uint32_t& q2,
+                                           uint32_t& q3) {
+    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+    q0 ^= rk[0]; q1 ^= rk[1]; q2 ^= rk[2]; q3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        const uint32_t t0 = xor3(te(0, s0 >> 24), te(1, (s1 >> 16) & 0xFF), te(2, (s2 >> 8) & 0xFF)) ^ te(3, s3 & 0xFF);
+        const uint32_t t1 = xor3(te(0, s1 >> 24), te(1, (s2 >> 16) & 0xFF), te(2, (s3 >> 8) & 0xFF)) ^ te(3, s0 & 0xFF);
+        const uint32_t t2 = xor3(te(0, s2 >> 24), te(1, (s3 >> 16) & 0xFF), te(2, (s0 >> 8) & 0xFF)) ^ te(3, s1 & 0xFF);
+        const uint32_t t3 = xor3(te(0, s3 >> 24), te(1, (s0 >> 16) & 0xFF), te(2, (s1 >> 8) & 0xFF)) ^ te(3, s2 & 0xFF);
+        const uint32_t v0 = xor3(te(0, q0 >> 24), te(1, (q1 >> 16) & 0xFF), te(2, (q2 >> 8) & 0xFF)) ^ te(3, q3 & 0xFF);
+        const uint32_t v1 = xor3(te(0, q1 >> 24), te(1, (q2 >> 16) & 0xFF), te(2, (q3 >> 8) & 0xFF)) ^ te(3, q0 & 0xFF);
+        const uint32_t v2 = xor3(te(0, q2 >> 24), te(1, (q3 >> 16) & 0xFF), te(2, (q0 >> 8) & 0xFF)) ^ te(3, q1 & 0xFF);
+        const uint32_t v3 = xor3(te(0, q3 >> 24), te(1, (q0 >> 16) & 0xFF), te(2, (q1 >> 8) & 0xFF)) ^ te(3, q2 & 0xFF);
+        s0 = t0 ^ rk[4 * r + 0]; s1 = t1 ^ rk[4 * r + 1]; s2 = t2 ^ rk[4 * r + 2]; s3 = t3 ^ rk[4 * r + 3];
+        q0 = v0 ^ rk[4 * r + 0]; q1 = v1 ^ rk[4 * r + 1]; q2 = v2 ^ rk[4 * r + 2]; q3 = v3 ^ rk[4 * r + 3];
+    }
+    const uint32_t* k = rk + 56;
+    auto last = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t kw) {
+        return (te(2, x0 >> 24) & 0xFF000000u) ^ (te(3, (x1 >> 16) & 0xFF) & 0x00FF0000u) ^
+               (te(0, (x2 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, x3 & 0xFF) & 0x000000FFu) ^ kw;
+    };
+    const uint32_t u0 = last(s0, s1, s2, s3, k[0]), u1 = last(s1, s2, s3, s0, k[1]);
+    const uint32_t u2 = last(s2, s3, s0, s1, k[2]), u3 = last(s3, s0, s1, s2, k[3]);
+    const uint32_t w0 = last(q0, q1, q2, q3, k[0]), w1 = last(q1, q2, q3, q0, k[1]);
+    const uint32_t w2 = last(q2, q3, q0, q1, k[2]), w3 = last(q3, q0, q1, q2, k[3]);
+    s0 = u0; s1 = u1; s2 = u2; s3 = u3;
+    q0 = w0; q1 = w1; q2 = w2; q3 = w3;
 }
 
 // x * H^256 via the position table: sum over the 32 nibbles of x.
@@ -132,41 +161,68 @@ __device__ __forceinline__ void store16_be(uint8_t* p, u32x4 v) {
     *reinterpret_cast<u32x4a4*>(p) = u32x4a4{bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w)};
 }
 
+// LDS: the four T-tables replicated 32 times, Te_k[x] for lane l at
+// [k][x][l % 32], so the 32 lanes of a half-wave read 32 different banks
+// whatever bytes they look up (random T-table indices otherwise serialise on
+// bank conflicts); then one H^256 table and reduction slots per frame group.
+#ifndef GCM_TE_COPIES
+#define GCM_TE_COPIES 32
+#endif
+#ifndef GCM_GROUPS
+#define GCM_GROUPS 2
+#endif
+constexpr uint32_t kTeCopies = GCM_TE_COPIES;
+constexpr uint32_t kGcmGroups = GCM_GROUPS;  // frames in flight per workgroup, 256 threads each
+constexpr size_t kTeWords = 4 * 256 * kTeCopies;
+constexpr size_t kGcmLdsBytes = kTeWords * 4 + kGcmGroups * (32 * 16 + 4) * sizeof(u32x4);
+
 template <bool kDecrypt>
-__global__ __launch_bounds__(256) void gcm_frames_kernel(GcmArgs a) {
-    __shared__ GcmLds lds;
-    __shared__ u32x4 red[4];
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t t = lane; t < 4 * 256; t += 256) (&lds.te[0][0])[t] = a.te[t];
+__global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a) {
+    extern __shared__ uint32_t smem[];
+    uint32_t* te = smem;
+    u32x4* gbase = reinterpret_cast<u32x4*>(smem + kTeWords);
+    const uint32_t g = threadIdx.x >> 8, lane = threadIdx.x & 255;
+    u32x4 (*htab)[16] = reinterpret_cast<u32x4 (*)[16]>(gbase + g * (32 * 16 + 4));
+    u32x4* red = gbase + g * (32 * 16 + 4) + 32 * 16;
+    for (uint32_t t = threadIdx.x; t < kTeWords; t += blockDim.x) te[t] = a.te[t / kTeCopies];
+    const uint32_t* tep = te + (lane % kTeCopies);
+    auto lk = [tep](int k, uint32_t x) { return tep[((uint32_t(k) << 8) | x) * kTeCopies]; };
     int64_t cur_key = -1;
-    for (uint64_t f = blockIdx.x; f < a.n_frames; f += gridDim.x) {
-        const GcmFrame fr = a.frames[f];
-        const uint32_t kidx = __builtin_amdgcn_readfirstlane(fr.key);
-        const GcmKey* key = a.keys + kidx;
-        if (int64_t(kidx) != cur_key) {  // uniform: a new object's H^256 table
-            __syncthreads();
-            for (uint32_t t = lane; t < 32 * 16; t += 256) (&lds.htab[0][0])[t] = key->htab[t / 16][t % 16];
-            cur_key = kidx;
+    for (uint64_t f0 = uint64_t(blockIdx.x) * kGcmGroups; f0 < a.n_frames;
+         f0 += uint64_t(gridDim.x) * kGcmGroups) {
+        const uint64_t f = f0 + g;
+        const bool live = f < a.n_frames;  // uniform within a frame group
+        GcmFrame fr{};
+        if (live) fr = a.frames[f];
+        const GcmKey* key = a.keys + fr.key;
+        __syncthreads();  // every group is done with its htab / red slots
+        if (live && int64_t(fr.key) != cur_key) {  // a new object's H^256 table
+            for (uint32_t t = lane; t < 32 * 16; t += 256) (&htab[0][0])[t] = key->htab[t / 16][t % 16];
+            cur_key = fr.key;
         }
         __syncthreads();
         const uint32_t* rk = key->rk;
         const uint32_t nb = (fr.len + 15) / 16, na = (fr.aad_len + 15) / 16;
-        const uint32_t m = na + nb + 1;
+        const uint32_t m = live ? na + nb + 1 : 0;
         // The 12-byte nonce: prefix || index (u64 LE).  Encrypt builds it and
         // writes the frame header; decrypt reads the stored one (crypto.rs:323).
-        uint32_t n0, n1, n2;
-        if (kDecrypt) {
-            const u32x4 h = load_partial_be(fr.hdr, 12);
-            n0 = h.x; n1 = h.y; n2 = h.z;
-        } else {
-            n0 = fr.prefix_be;
-            n1 = bswap(uint32_t(fr.index));
-            n2 = bswap(uint32_t(fr.index >> 32));
+        uint32_t n0 = 0, n1 = 0, n2 = 0;
+        if (live) {
+            if (kDecrypt) {
+                const u32x4 h = load_partial_be(fr.hdr, 12);
+                n0 = h.x; n1 = h.y; n2 = h.z;
+            } else {
+                n0 = fr.prefix_be;
+                n1 = bswap(uint32_t(fr.index));
+                n2 = bswap(uint32_t(fr.index >> 32));
+            }
         }
         // J0 = nonce || 0^31 || 1; block j of the payload uses counter 2 + j.
         u32x4 acc = {0u, 0u, 0u, 0u};
         uint32_t last = 0;
-        for (uint32_t i = lane; i < m; i += 256) {
+        // One block of the GHASH sequence: AAD, payload (encrypted here) or
+        // the length block.
+        auto block = [&](uint32_t i) -> u32x4 {
             u32x4 x;
             if (i < na) {
                 const uint32_t off = 16 * i, n = min(16u, fr.aad_len - off);
@@ -174,7 +230,9 @@ __global__ __launch_bounds__(256) void gcm_frames_kernel(GcmArgs a) {
             } else if (i < na + nb) {
                 const uint32_t j = i - na, off = 16 * j, n = min(16u, fr.len - off);
                 uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = 2u + j;
-                aes_block(lds.te, rk, s0, s1, s2, s3);
+#ifndef GCM_LAB_NO_AES
+                aes_block(lk, rk, s0, s1, s2, s3);
+#endif
                 const u32x4 ks = {s0, s1, s2, s3};
                 u32x4 in = n == 16 ? load16_be(fr.in + off) : load_partial_be(fr.in + off, n);
                 u32x4 out = {in.x ^ ks.x, in.y ^ ks.y, in.z ^ ks.z, in.w ^ ks.w};
@@ -191,8 +249,44 @@ __global__ __launch_bounds__(256) void gcm_frames_kernel(GcmArgs a) {
                 const uint64_t abits = uint64_t(fr.aad_len) * 8, cbits = uint64_t(fr.len) * 8;
                 x = u32x4{uint32_t(abits >> 32), uint32_t(abits), uint32_t(cbits >> 32), uint32_t(cbits)};
             }
-            const u32x4 h = mul_htab(lds.htab, acc);
+            return x;
+        };
+        auto fold = [&](const u32x4& x) {
+#ifndef GCM_LAB_NO_GHASH
+            const u32x4 h = mul_htab(htab, acc);
+#else
+            const u32x4 h = acc;
+#endif
             acc = u32x4{h.x ^ x.x, h.y ^ x.y, h.z ^ x.z, h.w ^ x.w};
+        };
+        const uint32_t full_end = na + fr.len / 16;  // blocks [na, full_end) are whole payload blocks
+        uint32_t i = lane;
+        if (i < na) {  // an AAD block first (lanes 0..na-1), then payload pairs
+            fold(block(i));
+            last = i;
+            i += 256;
+        }
+        // Two whole payload blocks per step: their AES chains are independent,
+        // so the scheduler interleaves them and each hides the other's LDS
+        // latency; two loads / stores in flight.
+        for (; i + 256 < full_end && i >= na; i += 512) {
+            const uint32_t j0 = i - na, j1 = j0 + 256;
+            const u32x4 in0 = load16_be(fr.in + 16 * j0), in1 = load16_be(fr.in + 16 * j1);
+            uint32_t a0 = n0, a1 = n1, a2 = n2, a3 = 2u + j0;
+            uint32_t b0 = n0, b1 = n1, b2 = n2, b3 = 2u + j1;
+#ifndef GCM_LAB_NO_AES
+            aes_block2(lk, rk, a0, a1, a2, a3, b0, b1, b2, b3);
+#endif
+            const u32x4 o0 = {in0.x ^ a0, in0.y ^ a1, in0.z ^ a2, in0.w ^ a3};
+            const u32x4 o1 = {in1.x ^ b0, in1.y ^ b1, in1.z ^ b2, in1.w ^ b3};
+            store16_be(fr.out + 16 * j0, o0);
+            store16_be(fr.out + 16 * j1, o1);
+            fold(kDecrypt ? in0 : o0);
+            fold(kDecrypt ? in1 : o1);
+            last = i + 256;
+        }
+        for (; i < m; i += 256) {
+            fold(block(i));
             last = i;
         }
         if (lane < m) acc = mul_bitwise(acc, key->hpow[m - last - 1]);  // * H^(m - last)
@@ -205,11 +299,11 @@ __global__ __launch_bounds__(256) void gcm_frames_kernel(GcmArgs a) {
         }
         if ((lane & 63) == 0) red[lane >> 6] = acc;
         __syncthreads();
-        if (lane == 0) {
+        if (live && lane == 0) {
             u32x4 y = red[0];
             for (int q = 1; q < 4; ++q) y = u32x4{y.x ^ red[q].x, y.y ^ red[q].y, y.z ^ red[q].z, y.w ^ red[q].w};
             uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = 1u;
-            aes_block(lds.te, rk, s0, s1, s2, s3);
+            aes_block(lk, rk, s0, s1, s2, s3);
             const u32x4 tag = {s0 ^ y.x, s1 ^ y.y, s2 ^ y.z, s3 ^ y.w};
             if (kDecrypt) {
                 // stored index (nonce bytes 4..11, LE) must be this frame's
@@ -229,11 +323,22 @@ __global__ __launch_bounds__(256) void gcm_frames_kernel(GcmArgs a) {
 
 hipError_t launch_gcm_frames(const GcmArgs& a, bool decrypt, int n_cus, hipStream_t s) {
     if (a.n_frames == 0) return hipSuccess;
-    const uint64_t grid = std::min<uint64_t>(a.n_frames, uint64_t(n_cus) * 6);
+    // 144 KiB of LDS per workgroup: one workgroup (two frames) per CU.
+    static const hipError_t attr = [] {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gcm_frames_kernel<true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(kGcmLdsBytes));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gcm_frames_kernel<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(kGcmLdsBytes));
+        return e;
+    }();
+    if (attr != hipSuccess) return attr;
+    const uint64_t groups = (a.n_frames + kGcmGroups - 1) / kGcmGroups;
+    const uint64_t grid = std::min<uint64_t>(groups, uint64_t(n_cus));
     if (decrypt)
-        hipLaunchKernelGGL(gcm_frames_kernel<true>, dim3(uint32_t(grid)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(gcm_frames_kernel<true>, dim3(uint32_t(grid)), dim3(256 * kGcmGroups), kGcmLdsBytes, s, a);
     else
-        hipLaunchKernelGGL(gcm_frames_kernel<false>, dim3(uint32_t(grid)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(gcm_frames_kernel<false>, dim3(uint32_t(grid)), dim3(256 * kGcmGroups), kGcmLdsBytes, s, a);
     return hipGetLastError();
 }
 
