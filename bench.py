@@ -452,14 +452,18 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
     raise SystemExit(f"unknown --config {cfg}")
 
 
-def pmc_traffic(tag: str):
-    """Per-launch HBM bytes of the RS kernel from the committed rocprofv3 PMC
-    summary (profiles/*pmc*<tag>*.json), FETCH_SIZE x2 per the gfx950
-    correction + WRITE_SIZE, or None."""
+def pmc_traffic(tag: str, alg_bytes: float):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/*pmc*<tag>*.json, FETCH_SIZE x2 per the gfx950
+    correction + WRITE_SIZE; tools/pmc_summary.py): the measured
+    traffic / algorithmic ratio applied to this launch's algorithmic bytes
+    (the summary may come from a smaller batch of the same kernel)."""
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{tag}*.json"))):
         try:
             with open(p) as f:
-                return json.load(f).get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+                d = json.load(f)
+            ratio = d["hbm_bytes_per_launch"] / d["algorithmic_bytes_per_launch"]
+            return round(ratio * alg_bytes, 0), os.path.relpath(p, ROOT)
         except Exception:
             continue
     return None, None
@@ -622,7 +626,8 @@ def main() -> int:
     torch.cuda.empty_cache()
 
     if rank == 0:
-        traffic, tsrc = pmc_traffic("k4m2") if args.config == "2" else (None, None)
+        tag = {"2": "k4m2", "sums": "crc_tiles", "frames": "gcm_frames"}.get(args.config)
+        traffic, tsrc = pmc_traffic(tag, w.alg_bytes) if tag else (None, None)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
