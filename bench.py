@@ -13,6 +13,8 @@ inputs resident in HBM, parity written to HBM, through the C ABI
 Other BASELINE configs (same JSON line, for DESIGN.md / profiles):
   3   reconstruct k=8 m=4, 2 data erasures + SHA-256 verify of the 10 present
       shards, 1 MiB chunks, 1024 objects (8192 data chunks) per GPU
+  3c  the same batches as a continuous GET stream: --workers host threads
+      (default 8) each reconstructing its own batch on its own HIP stream
   4a  encode k=10 m=4, 1 MiB chunks (10 MiB objects), 4096 objects per GPU
   4b  encode k=64 m=4, 1 MiB chunks (literal 64 MiB objects), 640 per GPU
   5   mixed 4+2 / 8+4 / 10+4 at 64 KiB..10 MiB chunks with short last chunks:
@@ -164,6 +166,7 @@ class Reconstruct:
         g = torch.Generator(device=dev).manual_seed(seed)
         self.obj = torch.randint(0, 256, (n, k + m, S), dtype=torch.uint8, device=dev, generator=g)
         self.dig = torch.empty((n, k + m, 32), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()  # randint ran on the current stream; encode runs on sh
         ctx.encode_strided_device(k, m, S, n, self.obj.data_ptr(), (k + m) * S, S,
                                   self.obj[:, k:].data_ptr(), (k + m) * S, S,
                                   digests_ptr=self.dig.data_ptr(), stream=sh)
@@ -185,7 +188,7 @@ class Reconstruct:
         rc, _ = self.ctx.reconstruct_strided_device(
             self.k, self.m, self.S, self.n, self.obj.data_ptr(), (self.k + self.m) * self.S, self.S,
             pr, expected_ptr=self.dig.data_ptr(), stream=self.sh)
-        assert rc == 0
+        assert rc == 0, f"reconstruct rc={rc}: {self.ctx.last_error() if hasattr(self.ctx, 'last_error') else ''}"
 
     def spot_check(self):
         return bool(self.torch.equal(self.obj[0], self.ref))
@@ -207,6 +210,63 @@ class Reconstruct:
 
     def drop(self):
         del self.obj, self.dig, self.ref
+
+
+class ReconstructStream:
+    """configs[2] as a continuous GET stream: W workers (host threads, as
+    MaxIO's tokio workers) each own an 8192-chunk batch and a HIP stream and
+    call mxec_reconstruct_strided_device concurrently through the one
+    context; a step is one batch per worker.  The SHA-256 verify of a batch
+    is a per-message latency chain (~1.8 us per 64-byte block, one lane per
+    1 MiB shard: 29 ms) that occupies ~160 of the 1024 SIMDs, so batches in
+    flight side by side are what fills the chip."""
+
+    bound = "valu"
+    wall_timed = True
+
+    def __init__(self, torch, ctx, dev, sh, n, workers, seed):
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.torch = torch
+        self.streams = [torch.cuda.Stream(device=dev) for _ in range(workers)]
+        self.parts = [Reconstruct(torch, ctx, dev, st.cuda_stream, n, seed + 97 * i)
+                      for i, st in enumerate(self.streams)]
+        self.pool = ThreadPoolExecutor(workers)
+        self.k, self.m, self.S, self.n = 8, 4, 1 << 20, n * workers
+        self.payload = sum(p.payload for p in self.parts)
+        self.alg_bytes = sum(p.alg_bytes for p in self.parts)
+        self.kernel = "sha256_kernel / sha256_split_kernel + rs_apply_fast<R=2>, W streams"
+        self.lat = []
+        self.name = (f"RS reconstruct k=8 m=4, 2 data erasures + SHA-256 verify, chunk_size=1 MiB: "
+                     f"{workers} concurrent batches of {n} objects (8192-chunk batches, BASELINE "
+                     "configs[2]) per GPU, one host thread + HIP stream each")
+
+    def _one(self, part):
+        t = time.perf_counter()
+        part.step()
+        self.lat.append(time.perf_counter() - t)
+
+    def step(self):
+        for f in [self.pool.submit(self._one, p) for p in self.parts]:
+            f.result()
+
+    def breakdown(self):
+        lat = sorted(self.lat)
+        return {"workers": len(self.parts),
+                "batch_call_ms_median": round(1e3 * lat[len(lat) // 2], 2) if lat else None,
+                "what": "host-side duration of one worker's reconstruct call (verify kernel + "
+                        "readback + decode enqueue)"}
+
+    def spot_check(self):
+        return all(p.spot_check() for p in self.parts)
+
+    def cpu_work(self):
+        return self.parts[0].cpu_work()
+
+    def drop(self):
+        self.pool.shutdown()
+        for p in self.parts:
+            p.drop()
 
 
 class Mixed:
@@ -424,7 +484,7 @@ class Frames:
         del self.pt, self.fr, self.back, self.aad
 
 
-def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
+def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank, workers=8):
     seed = SEED + rank
     if cfg == "2":
         n = n_objects or 1024
@@ -433,6 +493,8 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank):
                       "(BASELINE configs[1])", seed)
     if cfg == "3":
         return Reconstruct(torch, ctx, dev, sh, n_objects or 1024, seed)
+    if cfg == "3c":
+        return ReconstructStream(torch, ctx, dev, sh, n_objects or 1024, workers, seed)
     if cfg == "4a":
         n = n_objects or 4096
         return Encode(torch, ctx, dev, sh, 10, 4, 1 << 20, n,
@@ -516,7 +578,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="2", choices=["2", "3", "4a", "4b", "5", "sums", "frames"])
+    ap.add_argument("--config", default="2", choices=["2", "3", "3c", "4a", "4b", "5", "sums", "frames"])
+    ap.add_argument("--workers", type=int, default=8, help="config 3c: concurrent batches")
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--extra", action="store_true",
@@ -549,13 +612,14 @@ def main() -> int:
 
     import maxio_amd
 
-    ctx = maxio_amd.Context(device_mask=1 << (local if world > 1 else 0), streams_per_device=2)
+    ctx = maxio_amd.Context(device_mask=1 << (local if world > 1 else 0),
+                            streams_per_device=max(2, args.workers if args.config == "3c" else 2))
     dev = torch.device("cuda", torch.cuda.current_device())
     # A dedicated stream: the kernels and the HIP events that time them are
     # on the same queue.
     stream = torch.cuda.Stream(device=dev)
     sh = stream.cuda_stream
-    w = make_workload(args.config, torch, ctx, dev, sh, args.objects, rank)
+    w = make_workload(args.config, torch, ctx, dev, sh, args.objects, rank, args.workers)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -576,6 +640,8 @@ def main() -> int:
     barrier()
     elapsed = reduce_max(time.perf_counter() - t0)
     ms_launch = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    if getattr(w, "wall_timed", False):  # work on the workers' streams, not `stream`
+        ms_launch = elapsed * 1e3 / args.steps
 
     value = float(w.payload) * world * args.steps / GIB / elapsed  # weak scaling: all ranks
     achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9

@@ -191,8 +191,14 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
         nmax = o > nmax ? o : nmax;
     }
     uint32_t w[16];
+    // Producer prefetch: the raw bytes of the block after the one being
+    // scheduled stay in flight across the barrier (plain loads survive it),
+    // so the producer's step is the schedule alone, not an HBM round trip
+    // plus the schedule.
+    u32x4 nxt[4];
     if (wave == 1 && nfull > 0) {
         message_words(p, aligned, w);
+        if (aligned && nfull > 1) load_block(p + 64, nxt);
         schedule_kw(w, &kw[0][0][lane]);
     }
     __syncthreads();
@@ -201,7 +207,12 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
     for (uint64_t b = 0; b < nmax; ++b) {
         if (wave == 1) {
             if (b + 1 < nfull) {
-                message_words(p + 64 * (b + 1), aligned, w);
+                if (aligned) {
+                    block_words(nxt, w);
+                    if (b + 2 < nfull) load_block(p + 64 * (b + 2), nxt);
+                } else {
+                    message_words(p + 64 * (b + 1), false, w);
+                }
                 schedule_kw(w, &kw[(b + 1) & 1][0][lane]);
             }
         } else if (b < nfull) {

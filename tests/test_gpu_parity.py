@@ -389,3 +389,48 @@ def test_sha256_every_kernel_form(ctx, form, monkeypatch):
         o += int(n)
     got = ctx.sha256(bufs)
     assert got == [hashlib.sha256(b).digest() for b in bufs]
+
+
+def test_concurrent_reconstruct_workers(ctx):
+    """Several host threads (tokio workers) reconstruct their own batches on
+    their own streams through one context at once (bench config 3c): every
+    batch comes back bit-exact, corruption caught per batch."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    torch = _torch()
+    k, m, s, n, workers = 8, 4, 1 << 16, 24, 4
+    c = maxio_amd.Context(streams_per_device=workers)
+    try:
+        jobs = []
+        for w in range(workers):
+            g = torch.Generator(device="cuda").manual_seed(100 + w)
+            obj = torch.randint(0, 256, (n, k + m, s), dtype=torch.uint8, device="cuda", generator=g)
+            dig = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+            c.encode_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s,
+                                    obj[:, k:].data_ptr(), (k + m) * s, s, digests_ptr=dig.data_ptr())
+            torch.cuda.synchronize()
+            jobs.append((obj, dig, obj.clone(), torch.cuda.Stream(), np.random.default_rng(w)))
+
+        def run(job):
+            obj, dig, ref, st, rng = job
+            for _ in range(3):
+                present = np.ones(n * (k + m), np.uint8)
+                with torch.cuda.stream(st):
+                    for o in range(n):
+                        lost = rng.choice(k + m, 2, replace=False)
+                        present[o * (k + m) + lost[0]] = 0
+                        obj[o, lost[0]].zero_()
+                        obj[o, lost[1], 17] ^= 0x80  # silent corruption: still flagged present
+                st.synchronize()
+                rc, status = c.reconstruct_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s,
+                                                          present, expected_ptr=dig.data_ptr(),
+                                                          stream=st.cuda_stream)
+                st.synchronize()
+                if rc != 0 or not present.all() or not torch.equal(obj, ref):
+                    return False
+            return True
+
+        with ThreadPoolExecutor(workers) as pool:
+            assert all(pool.map(run, jobs))
+    finally:
+        c.close()

@@ -41,6 +41,39 @@ __global__ __launch_bounds__(256) void k_write(u32x4* __restrict__ d, uint64_t n
     const u32x4 v = {1, 2, 3, 4};
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) d[i] = v;
 }
+// Read ceilings by load form: four independent nontemporal 16-byte loads per
+// lane per step, and LDS-DMA (global_load_lds_dwordx4, 16 KiB per wave in
+// flight; AUX 2 = nontemporal).
+__global__ __launch_bounds__(256) void k_read_nt4(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+    u32x4 acc = {0, 0, 0, 0};
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
+        const u32x4 a = __builtin_nontemporal_load(s + i), b = __builtin_nontemporal_load(s + i + stride);
+        const u32x4 c = __builtin_nontemporal_load(s + i + 2 * stride), e = __builtin_nontemporal_load(s + i + 3 * stride);
+        acc ^= a ^ b ^ c ^ e;
+    }
+    if (acc.x == 0x12345678u) d[0] = acc;
+}
+template <int AUX>
+__global__ __launch_bounds__(256) void k_read_glds(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+    __shared__ u32x4 buf[4][16][64];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t chunks = n / 1024, nw = uint64_t(gridDim.x) * 4;
+    for (uint64_t c = blockIdx.x * 4ull + wave; c < chunks; c += nw) {
+        const u32x4* src = s + c * 1024 + lane;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src + q * 64),
+                                             (void __attribute__((address_space(3)))*)&buf[wave][q][0], 16, 0, AUX);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (d && buf[wave][0][lane].x == 0x12345678u) d[0] = buf[wave][1][lane];
+}
+__global__ __launch_bounds__(256) void k_write_nt(u32x4* __restrict__ d, uint64_t n) {
+    const u32x4 v = {1, 2, 3, 4};
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+        __builtin_nontemporal_store(v, d + i);
+}
 // RS access pattern without the math: object o, 16-B column c: read k shards,
 // write m shards (XOR of inputs), same layout as the bench.
 __global__ __launch_bounds__(256) void k_pattern(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
@@ -53,6 +86,16 @@ __global__ __launch_bounds__(256) void k_pattern(const uint8_t* __restrict__ dat
         for (uint32_t j = 0; j < k; ++j) acc ^= reinterpret_cast<const u32x4*>(data + (o * k + j) * S)[c];
         for (uint32_t i = 0; i < m; ++i) reinterpret_cast<u32x4*>(par + (o * m + i) * S)[c] = acc + i;
     }
+}
+
+__global__ __launch_bounds__(256) void k_diff(const u32x4* __restrict__ a, const u32x4* __restrict__ b, uint64_t n,
+                                             unsigned long long* bad) {
+    unsigned long long c = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) {
+        const u32x4 x = a[i] ^ b[i];
+        c += (x.x | x.y | x.z | x.w) != 0;
+    }
+    if (c) atomicAdd(bad, c);
 }
 
 struct Timer {
@@ -141,10 +184,43 @@ int main(int argc, char** argv) {
         std::fflush(stdout);
     };
 
-    // `kernel_lab N sha` runs the SHA-256 section only.
+    // `kernel_lab N sha` runs the SHA-256 section only; `kernel_lab N hbm`
+    // the load-form ceilings, the tile-order sweep and the SHA split form.
     const bool sha_only = argc > 2 && !std::strcmp(argv[2], "sha");
+    const bool hbm_only = argc > 2 && !std::strcmp(argv[2], "hbm");
     // ---- calibration ----
-    if (!sha_only) {
+    if (hbm_only) {
+        const uint64_t nvec = pool / 16, half = pool / 2 / 16;
+        auto* s = reinterpret_cast<const u32x4*>(buf);
+        auto* d = reinterpret_cast<u32x4*>(buf + pool / 2);
+        for (int rep = 0; rep < 2; ++rep) {
+            for (int bpc : {8, 16}) {
+                char nm[64];
+                std::snprintf(nm, sizeof nm, "read_bpc%d", bpc);
+                double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_read, dim3(cus * bpc), dim3(256), 0, 0, s, d, nvec); });
+                report(nm, "pool", ms, 16.0 * nvec);
+                std::snprintf(nm, sizeof nm, "read_nt4_bpc%d", bpc);
+                ms = tm.median_ms([&] { hipLaunchKernelGGL(k_read_nt4, dim3(cus * bpc), dim3(256), 0, 0, s, d, nvec); });
+                report(nm, "pool", ms, 16.0 * nvec);
+            }
+            for (int bpc : {2, 4}) {
+                char nm[64];
+                std::snprintf(nm, sizeof nm, "read_glds_bpc%d", bpc);
+                double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_read_glds<0>, dim3(cus * bpc), dim3(256), 0, 0, s, d, nvec); });
+                report(nm, "pool", ms, 16.0 * nvec);
+                std::snprintf(nm, sizeof nm, "read_glds_nt_bpc%d", bpc);
+                ms = tm.median_ms([&] { hipLaunchKernelGGL(k_read_glds<2>, dim3(cus * bpc), dim3(256), 0, 0, s, d, nvec); });
+                report(nm, "pool", ms, 16.0 * nvec);
+            }
+            double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, d, half); });
+            report("write", "half pool", ms, 16.0 * half);
+            ms = tm.median_ms([&] { hipLaunchKernelGGL(k_write_nt, dim3(cus * 8), dim3(256), 0, 0, d, half); });
+            report("write_nt", "half pool", ms, 16.0 * half);
+            ms = tm.median_ms([&] { hipLaunchKernelGGL(k_copy, dim3(cus * 16), dim3(256), 0, 0, s, d, half); });
+            report("copy_bpc16", "2x half pool", ms, 32.0 * half);
+        }
+    }
+    if (!sha_only && !hbm_only) {
         const uint64_t half = pool / 2 / 16;
         auto* s = reinterpret_cast<const u32x4*>(buf);
         auto* d = reinterpret_cast<u32x4*>(buf + pool / 2);
@@ -172,7 +248,12 @@ int main(int argc, char** argv) {
         Batch b(buf, buf + sh.n * sh.k * sh.S, sh, mxec::coef_tables(rows), &coef);
         const double bytes = double(sh.n) * (sh.k + sh.r) * sh.S;
         std::vector<mxec::RsVariant> vs;
-        if (full) {
+        if (hbm_only) {
+            // (An LDS-DMA ring form of this kernel and a contiguous-run tile
+            // order were measured here and dropped: profiles/r1_lab_rs_glds_variants.jsonl,
+            // profiles/r1_lab_hbm_ceilings_tile_order.jsonl.)
+            for (int bpc : {8, 16, 32}) vs.push_back(mxec::RsVariant{4, true, bpc});
+        } else if (full) {
             for (int v : {1, 2, 4})
                 for (bool nt : {false, true})
                     for (int bpc : {4, 8, 16}) vs.push_back(mxec::RsVariant{v, nt, bpc});
@@ -180,13 +261,37 @@ int main(int argc, char** argv) {
             for (int v : {1, 2, 4})
                 for (bool nt : {false, true}) vs.push_back(mxec::RsVariant{v, nt, 8});
         }
+        // Reference output of the default register kernel, for a bit-exact
+        // check of every variant (hbm mode).
+        uint8_t* par = buf + sh.n * sh.k * sh.S;
+        const uint64_t par_bytes = sh.n * sh.r * sh.S;
+        uint8_t* ref = nullptr;
+        unsigned long long* bad = nullptr;
+        if (hbm_only) {
+            CK(hipMalloc(&ref, par_bytes));
+            CK(hipMalloc(&bad, 8));
+            CK(mxec::launch_rs_apply_variant(b.a, cus, 0, mxec::RsVariant{4, true, 16}));
+            CK(hipMemcpy(ref, par, par_bytes, hipMemcpyDeviceToDevice));
+        }
         for (const auto& v : vs) {
+            if (hbm_only) {
+                CK(hipMemset(par, 0, par_bytes));
+                CK(mxec::launch_rs_apply_variant(b.a, cus, 0, v));
+                CK(hipMemset(bad, 0, 8));
+                hipLaunchKernelGGL(k_diff, dim3(cus * 8), dim3(256), 0, 0, reinterpret_cast<const u32x4*>(par),
+                                   reinterpret_cast<const u32x4*>(ref), par_bytes / 16, bad);
+                unsigned long long nb = 0;
+                CK(hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost));
+                std::printf("{\"what\": \"check\", \"v\": %d, \"bpc\": %d, \"bad16\": %llu}\n", v.vecs, v.blocks_per_cu, nb);
+            }
             double ms = tm.median_ms([&] { CK(mxec::launch_rs_apply_variant(b.a, cus, 0, v)); });
             char nm[96];
             std::snprintf(nm, sizeof nm, "rs_v%d_nt%d_bpc%d", v.vecs, int(v.nt), v.blocks_per_cu);
             report(nm, name, ms, bytes);
         }
         (void)hipFree(coef);
+        if (ref) (void)hipFree(ref);
+        if (bad) (void)hipFree(bad);
     };
     // ---- SHA-256: one lane per message ----
     auto sha = [&](uint64_t n, uint64_t L, const char* name, int force = 0) {
@@ -209,6 +314,15 @@ int main(int argc, char** argv) {
                     ms * 1e3 / (L / 64.0));
         CK(hipFree(d));
     };
+    if (hbm_only) {
+        sweep(Shape{4, 2, S2, n2}, "k4m2 S10MiB (cfg2)", true);
+        sweep(Shape{8, 4, 1ull << 20, n2 * 60 / 12}, "k8m4 S1MiB (north star)", true);
+        sha(10240, 1ull << 20, "10240 x 1 MiB split form", 2);
+        // (32 and 16 messages per wave of the split form measured 2.70 / 2.76
+        // us per block against 1.82: profiles/r1_lab_sha_lanes_per_wave.jsonl.)
+        CK(hipFree(buf));
+        return 0;
+    }
     sha(10240, 1ull << 20, "10240 x 1 MiB (cfg3 verify)");
     sha(10240, 1ull << 20, "10240 x 1 MiB split form", 2);
     sha(10240, 1ull << 20, "10240 x 1 MiB one-wave form", 1);
