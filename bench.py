@@ -442,6 +442,7 @@ class Frames:
         torch = self.torch
         st = torch.cuda.ExternalStream(self.sh)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        self.ctx.frames_device(self.djobs, decrypt=True, stream=self.sh)  # warm (first-call setup)
         a.record(st)
         status = self.ctx.frames_device(self.djobs, decrypt=True, stream=self.sh)
         b.record(st)

@@ -5,9 +5,10 @@
 // (crypto.rs:94-117, 426-432); every frame is an independent GCM message, so
 // one workgroup (256 threads) owns one frame at a time (grid-stride).
 //
-// * AES-256 counter blocks: T-table rounds (Te0..Te3 in LDS, 4 KiB), round
-//   keys read uniformly (scalar loads); lane l encrypts blocks l, l+256, ...
-//   so loads and stores stay coalesced.
+// * AES-256 counter blocks: T-table rounds (Te0..Te3 in LDS, replicated per
+//   bank, one v_perm per lookup address), round keys read uniformly (scalar
+//   loads); lane l encrypts blocks l, l+256, ... so loads and stores stay
+//   coalesced.
 // * GHASH is linear: Y = sum_i X_i * H^(m-i) over the m blocks
 //   (AAD, ciphertext, length).  Lane l folds its blocks by Horner with the
 //   fixed multiplier H^256 (a 4-bit position table in LDS, 32 lookups per
@@ -27,60 +28,57 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// One AES-256 block: in/out as big-endian column words; te(k, x) = Te_k[x].
+// One AES-256 block: in/out as big-endian column words; te(k, w, j) =
+// Te_k[byte j of w] (byte 0 = least significant).
 template <class TE>
 __device__ __forceinline__ void aes_block(TE te, const uint32_t* __restrict__ rk, uint32_t& s0, uint32_t& s1,
                                           uint32_t& s2, uint32_t& s3) {
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        const uint32_t t0 = xor3(te(0, s0 >> 24), te(1, (s1 >> 16) & 0xFF), te(2, (s2 >> 8) & 0xFF)) ^ te(3, s3 & 0xFF);
-        const uint32_t t1 = xor3(te(0, s1 >> 24), te(1, (s2 >> 16) & 0xFF), te(2, (s3 >> 8) & 0xFF)) ^ te(3, s0 & 0xFF);
-        const uint32_t t2 = xor3(te(0, s2 >> 24), te(1, (s3 >> 16) & 0xFF), te(2, (s0 >> 8) & 0xFF)) ^ te(3, s1 & 0xFF);
-        const uint32_t t3 = xor3(te(0, s3 >> 24), te(1, (s0 >> 16) & 0xFF), te(2, (s1 >> 8) & 0xFF)) ^ te(3, s2 & 0xFF);
-        s0 = t0 ^ rk[4 * r + 0];
-        s1 = t1 ^ rk[4 * r + 1];
-        s2 = t2 ^ rk[4 * r + 2];
-        s3 = t3 ^ rk[4 * r + 3];
+        const uint32_t t0 = xor3(xor3(te(0, s0, 3), te(1, s1, 2), te(2, s2, 1)), te(3, s3, 0), rk[4 * r + 0]);
+        const uint32_t t1 = xor3(xor3(te(0, s1, 3), te(1, s2, 2), te(2, s3, 1)), te(3, s0, 0), rk[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(te(0, s2, 3), te(1, s3, 2), te(2, s0, 1)), te(3, s1, 0), rk[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(te(0, s3, 3), te(1, s0, 2), te(2, s1, 1)), te(3, s2, 0), rk[4 * r + 3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     // Last round: SubBytes + ShiftRows, the S-box byte taken from the table
     // whose byte lane holds S[x] unmultiplied.
     const uint32_t* k = rk + 56;
-    const uint32_t u0 = (te(2, s0 >> 24) & 0xFF000000u) ^ (te(3, (s1 >> 16) & 0xFF) & 0x00FF0000u) ^
-                        (te(0, (s2 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s3 & 0xFF) & 0x000000FFu) ^ k[0];
-    const uint32_t u1 = (te(2, s1 >> 24) & 0xFF000000u) ^ (te(3, (s2 >> 16) & 0xFF) & 0x00FF0000u) ^
-                        (te(0, (s3 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s0 & 0xFF) & 0x000000FFu) ^ k[1];
-    const uint32_t u2 = (te(2, s2 >> 24) & 0xFF000000u) ^ (te(3, (s3 >> 16) & 0xFF) & 0x00FF0000u) ^
-                        (te(0, (s0 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s1 & 0xFF) & 0x000000FFu) ^ k[2];
-    const uint32_t u3 = (te(2, s3 >> 24) & 0xFF000000u) ^ (te(3, (s0 >> 16) & 0xFF) & 0x00FF0000u) ^
-                        (te(0, (s1 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, s2 & 0xFF) & 0x000000FFu) ^ k[3];
+    const uint32_t u0 = (te(2, s0, 3) & 0xFF000000u) ^ (te(3, s1, 2) & 0x00FF0000u) ^
+                        (te(0, s2, 1) & 0x0000FF00u) ^ (te(1, s3, 0) & 0x000000FFu) ^ k[0];
+    const uint32_t u1 = (te(2, s1, 3) & 0xFF000000u) ^ (te(3, s2, 2) & 0x00FF0000u) ^
+                        (te(0, s3, 1) & 0x0000FF00u) ^ (te(1, s0, 0) & 0x000000FFu) ^ k[1];
+    const uint32_t u2 = (te(2, s2, 3) & 0xFF000000u) ^ (te(3, s3, 2) & 0x00FF0000u) ^
+                        (te(0, s0, 1) & 0x0000FF00u) ^ (te(1, s1, 0) & 0x000000FFu) ^ k[2];
+    const uint32_t u3 = (te(2, s3, 3) & 0xFF000000u) ^ (te(3, s0, 2) & 0x00FF0000u) ^
+                        (te(0, s1, 1) & 0x0000FF00u) ^ (te(1, s2, 0) & 0x000000FFu) ^ k[3];
     s0 = u0; s1 = u1; s2 = u2; s3 = u3;
 }
 
-// Two independent blocks, round by round.
-template <class TE>
-__device__ __forceinline__ void aes_block2(TE te, const uint32_t* __restrict__ rk, uint32_t& s0, uint32_t& s1,
-                                           uint32_t& s2, uint32_t& s3, uint32_t& q0, uint32_t& q1, uint32_t& q2,
-                                           uint32_t& q3) {
-    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
-    q0 ^= rk[0]; q1 ^= rk[1]; q2 ^= rk[2]; q3 ^= rk[3];
+// Rounds R0..13 and the last round of two independent blocks, round by
+// round (each chain hides the other's LDS latency).
+template <int R0, class TE>
+__device__ __forceinline__ void aes_rounds2(TE te, const uint32_t* __restrict__ rk, uint32_t& s0, uint32_t& s1,
+                                            uint32_t& s2, uint32_t& s3, uint32_t& q0, uint32_t& q1,
+                                            uint32_t& q2, uint32_t& q3) {
 #pragma unroll
-    for (int r = 1; r < 14; ++r) {
-        const uint32_t t0 = xor3(te(0, s0 >> 24), te(1, (s1 >> 16) & 0xFF), te(2, (s2 >> 8) & 0xFF)) ^ te(3, s3 & 0xFF);
-        const uint32_t t1 = xor3(te(0, s1 >> 24), te(1, (s2 >> 16) & 0xFF), te(2, (s3 >> 8) & 0xFF)) ^ te(3, s0 & 0xFF);
-        const uint32_t t2 = xor3(te(0, s2 >> 24), te(1, (s3 >> 16) & 0xFF), te(2, (s0 >> 8) & 0xFF)) ^ te(3, s1 & 0xFF);
-        const uint32_t t3 = xor3(te(0, s3 >> 24), te(1, (s0 >> 16) & 0xFF), te(2, (s1 >> 8) & 0xFF)) ^ te(3, s2 & 0xFF);
-        const uint32_t v0 = xor3(te(0, q0 >> 24), te(1, (q1 >> 16) & 0xFF), te(2, (q2 >> 8) & 0xFF)) ^ te(3, q3 & 0xFF);
-        const uint32_t v1 = xor3(te(0, q1 >> 24), te(1, (q2 >> 16) & 0xFF), te(2, (q3 >> 8) & 0xFF)) ^ te(3, q0 & 0xFF);
-        const uint32_t v2 = xor3(te(0, q2 >> 24), te(1, (q3 >> 16) & 0xFF), te(2, (q0 >> 8) & 0xFF)) ^ te(3, q1 & 0xFF);
-        const uint32_t v3 = xor3(te(0, q3 >> 24), te(1, (q0 >> 16) & 0xFF), te(2, (q1 >> 8) & 0xFF)) ^ te(3, q2 & 0xFF);
-        s0 = t0 ^ rk[4 * r + 0]; s1 = t1 ^ rk[4 * r + 1]; s2 = t2 ^ rk[4 * r + 2]; s3 = t3 ^ rk[4 * r + 3];
-        q0 = v0 ^ rk[4 * r + 0]; q1 = v1 ^ rk[4 * r + 1]; q2 = v2 ^ rk[4 * r + 2]; q3 = v3 ^ rk[4 * r + 3];
+    for (int r = R0; r < 14; ++r) {
+        const uint32_t t0 = xor3(xor3(te(0, s0, 3), te(1, s1, 2), te(2, s2, 1)), te(3, s3, 0), rk[4 * r + 0]);
+        const uint32_t t1 = xor3(xor3(te(0, s1, 3), te(1, s2, 2), te(2, s3, 1)), te(3, s0, 0), rk[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(te(0, s2, 3), te(1, s3, 2), te(2, s0, 1)), te(3, s1, 0), rk[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(te(0, s3, 3), te(1, s0, 2), te(2, s1, 1)), te(3, s2, 0), rk[4 * r + 3]);
+        const uint32_t v0 = xor3(xor3(te(0, q0, 3), te(1, q1, 2), te(2, q2, 1)), te(3, q3, 0), rk[4 * r + 0]);
+        const uint32_t v1 = xor3(xor3(te(0, q1, 3), te(1, q2, 2), te(2, q3, 1)), te(3, q0, 0), rk[4 * r + 1]);
+        const uint32_t v2 = xor3(xor3(te(0, q2, 3), te(1, q3, 2), te(2, q0, 1)), te(3, q1, 0), rk[4 * r + 2]);
+        const uint32_t v3 = xor3(xor3(te(0, q3, 3), te(1, q0, 2), te(2, q1, 1)), te(3, q2, 0), rk[4 * r + 3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        q0 = v0; q1 = v1; q2 = v2; q3 = v3;
     }
     const uint32_t* k = rk + 56;
     auto last = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3, uint32_t kw) {
-        return (te(2, x0 >> 24) & 0xFF000000u) ^ (te(3, (x1 >> 16) & 0xFF) & 0x00FF0000u) ^
-               (te(0, (x2 >> 8) & 0xFF) & 0x0000FF00u) ^ (te(1, x3 & 0xFF) & 0x000000FFu) ^ kw;
+        return (te(2, x0, 3) & 0xFF000000u) ^ (te(3, x1, 2) & 0x00FF0000u) ^
+               (te(0, x2, 1) & 0x0000FF00u) ^ (te(1, x3, 0) & 0x000000FFu) ^ kw;
     };
     const uint32_t u0 = last(s0, s1, s2, s3, k[0]), u1 = last(s1, s2, s3, s0, k[1]);
     const uint32_t u2 = last(s2, s3, s0, s1, k[2]), u3 = last(s3, s0, s1, s2, k[3]);
@@ -88,6 +86,62 @@ __device__ __forceinline__ void aes_block2(TE te, const uint32_t* __restrict__ r
     const uint32_t w2 = last(q2, q3, q0, q1, k[2]), w3 = last(q3, q0, q1, q2, k[3]);
     s0 = u0; s1 = u1; s2 = u2; s3 = u3;
     q0 = w0; q1 = w1; q2 = w2; q3 = w3;
+}
+
+// Two whole AES-256 blocks.
+template <class TE>
+__device__ __forceinline__ void aes_block2(TE te, const uint32_t* __restrict__ rk, uint32_t& s0, uint32_t& s1,
+                                           uint32_t& s2, uint32_t& s3, uint32_t& q0, uint32_t& q1, uint32_t& q2,
+                                           uint32_t& q3) {
+    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+    q0 ^= rk[0]; q1 ^= rk[1]; q2 ^= rk[2]; q3 ^= rk[3];
+    aes_rounds2<1>(te, rk, s0, s1, s2, s3, q0, q1, q2, q3);
+}
+
+// Counter blocks nonce(12) || ctr with ctr < 2^16 (frames of at most 65534
+// blocks): after the first AddRoundKey three state words and the high half
+// of the fourth are the same for every block of the frame, so round 1 has
+// two block-dependent lookups (counter bytes 0, 1) and round 2 eight; the
+// rest of those rounds is per-frame constants (14 + 8 of the 224 lookups of
+// a block saved).
+struct CtrConst {
+    uint32_t c0, c1, c2, c3;  // round-1 outputs without the counter terms
+    uint32_t d0, d1, d2, d3;  // round-2 outputs' constant halves
+};
+
+template <class TE>
+__device__ __forceinline__ CtrConst ctr_const(TE te, const uint32_t* __restrict__ rk, uint32_t n0, uint32_t n1,
+                                              uint32_t n2) {
+    const uint32_t a0 = n0 ^ rk[0], a1 = n1 ^ rk[1], a2 = n2 ^ rk[2], a3 = rk[3];  // a3: bytes 2, 3 only
+    CtrConst c;
+    c.c0 = xor3(xor3(te(0, a0, 3), te(1, a1, 2), te(2, a2, 1)), rk[4], 0u);
+    c.c1 = xor3(xor3(te(0, a1, 3), te(1, a2, 2), te(3, a0, 0)), rk[5], 0u);
+    c.c2 = xor3(xor3(te(0, a2, 3), te(1, a3, 2), te(2, a0, 1)), te(3, a1, 0), rk[6]);
+    c.c3 = xor3(xor3(te(0, a3, 3), te(1, a0, 2), te(2, a1, 1)), te(3, a2, 0), rk[7]);
+    c.d0 = xor3(te(2, c.c2, 1), te(3, c.c3, 0), rk[8]);
+    c.d1 = xor3(te(1, c.c2, 2), te(2, c.c3, 1), rk[9]);
+    c.d2 = xor3(te(0, c.c2, 3), te(1, c.c3, 2), rk[10]);
+    c.d3 = xor3(te(0, c.c3, 3), te(3, c.c2, 0), rk[11]);
+    return c;
+}
+
+// Keystream of counters x and y (< 2^16) into (s0..s3), (q0..q3).
+template <class TE>
+__device__ __forceinline__ void aes_ctr2(TE te, const uint32_t* __restrict__ rk, const CtrConst& c, uint32_t x,
+                                         uint32_t y, uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                         uint32_t& q0, uint32_t& q1, uint32_t& q2, uint32_t& q3) {
+    const uint32_t ax = x ^ rk[3], ay = y ^ rk[3];
+    const uint32_t u0 = c.c0 ^ te(3, ax, 0), u1 = c.c1 ^ te(2, ax, 1);
+    const uint32_t p0 = c.c0 ^ te(3, ay, 0), p1 = c.c1 ^ te(2, ay, 1);
+    s0 = xor3(c.d0, te(0, u0, 3), te(1, u1, 2));
+    s1 = xor3(c.d1, te(0, u1, 3), te(3, u0, 0));
+    s2 = xor3(c.d2, te(2, u0, 1), te(3, u1, 0));
+    s3 = xor3(c.d3, te(1, u0, 2), te(2, u1, 1));
+    q0 = xor3(c.d0, te(0, p0, 3), te(1, p1, 2));
+    q1 = xor3(c.d1, te(0, p1, 3), te(3, p0, 0));
+    q2 = xor3(c.d2, te(2, p0, 1), te(3, p1, 0));
+    q3 = xor3(c.d3, te(1, p0, 2), te(2, p1, 1));
+    aes_rounds2<3>(te, rk, s0, s1, s2, s3, q0, q1, q2, q3);
 }
 
 // x * H^256 via the position table: sum over the 32 nibbles of x.
@@ -161,32 +215,50 @@ __device__ __forceinline__ void store16_be(uint8_t* p, u32x4 v) {
     *reinterpret_cast<u32x4a4*>(p) = u32x4a4{bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w)};
 }
 
-// LDS: the four T-tables replicated 32 times, Te_k[x] for lane l at
-// [k][x][l % 32], so the 32 lanes of a half-wave read 32 different banks
-// whatever bytes they look up (random T-table indices otherwise serialise on
-// bank conflicts); then one H^256 table and reduction slots per frame group.
-#ifndef GCM_TE_COPIES
-#define GCM_TE_COPIES 32
-#endif
+// LDS: the four T-tables replicated 32 times, laid out so that a lookup's
+// address is ONE v_perm_b32 of the state word and a per-lane constant:
+//     byte offset = pair * 65536 + x * 256 + t * 128 + (lane % 32) * 4
+// for table k = 2 * pair + t.  v_perm places byte j of the state word in
+// bits 8..15 and copies bits 0..7 ((lane % 32) * 4) and 16..23 (pair) from
+// the lane constant; t * 128 is the ds_read_b32 immediate.  ds_read_b32
+// banks are (address / 4) mod 32 over lane groups {0-31}, {32-63}, so each
+// group hits its 32 banks once whatever bytes it looks up (random T-table
+// indices otherwise serialise on bank conflicts).  The extraction +
+// lane-bank address was two VALU per lookup before (byte extract, shift-add).
+// The tables occupy LDS bytes [0, 128 KiB) (the dynamic LDS block starts at
+// address 0: the kernel has no static __shared__); then one H^256 table and
+// reduction slots per frame group.
 #ifndef GCM_GROUPS
-#define GCM_GROUPS 2
+#define GCM_GROUPS 3
 #endif
-constexpr uint32_t kTeCopies = GCM_TE_COPIES;
+constexpr uint32_t kTeCopies = 32;
 constexpr uint32_t kGcmGroups = GCM_GROUPS;  // frames in flight per workgroup, 256 threads each
 constexpr size_t kTeWords = 4 * 256 * kTeCopies;
 constexpr size_t kGcmLdsBytes = kTeWords * 4 + kGcmGroups * (32 * 16 + 4) * sizeof(u32x4);
+
+typedef const uint32_t __attribute__((address_space(3)))* lds_u32p;
 
 template <bool kDecrypt>
 __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a) {
     extern __shared__ uint32_t smem[];
     uint32_t* te = smem;
+    // The lookup addresses assume the tables start at LDS address 0.
+    if (size_t((lds_u32p)(smem)) != 0) __builtin_trap();
     u32x4* gbase = reinterpret_cast<u32x4*>(smem + kTeWords);
     const uint32_t g = threadIdx.x >> 8, lane = threadIdx.x & 255;
     u32x4 (*htab)[16] = reinterpret_cast<u32x4 (*)[16]>(gbase + g * (32 * 16 + 4));
     u32x4* red = gbase + g * (32 * 16 + 4) + 32 * 16;
-    for (uint32_t t = threadIdx.x; t < kTeWords; t += blockDim.x) te[t] = a.te[t / kTeCopies];
-    const uint32_t* tep = te + (lane % kTeCopies);
-    auto lk = [tep](int k, uint32_t x) { return tep[((uint32_t(k) << 8) | x) * kTeCopies]; };
+    // word t = pair << 14 | x << 6 | tsel << 5 | copy  ->  Te_{2 pair + tsel}[x]
+    for (uint32_t t = threadIdx.x; t < kTeWords; t += blockDim.x)
+        te[t] = a.te[((t >> 14) * 2 + ((t >> 5) & 1)) * 256 + ((t >> 6) & 255)];
+    const uint32_t lb0 = (lane % kTeCopies) * 4, lb1 = lb0 | 0x10000u;
+    auto lk = [lb0, lb1](int k, uint32_t w, int j) {
+        // result bytes: [lb.b0, w.byte j, lb.b2, 0]; sel 4..7 = bytes of w,
+        // 0..3 = bytes of lb, 12 = 0x00.
+        const uint32_t addr =
+            __builtin_amdgcn_perm(w, k < 2 ? lb0 : lb1, 0x0C020000u | (uint32_t(4 + j) << 8));
+        return reinterpret_cast<lds_u32p>(size_t(addr))[(k & 1) * 32];
+    };
     int64_t cur_key = -1;
     for (uint64_t f0 = uint64_t(blockIdx.x) * kGcmGroups; f0 < a.n_frames;
          f0 += uint64_t(gridDim.x) * kGcmGroups) {
@@ -269,13 +341,19 @@ __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a)
         // Two whole payload blocks per step: their AES chains are independent,
         // so the scheduler interleaves them and each hides the other's LDS
         // latency; two loads / stores in flight.
+        const bool short_ctr = nb <= 65534;  // every payload counter 2 + j < 2^16
+        CtrConst cc{};
+#ifndef GCM_LAB_NO_AES
+        if (short_ctr) cc = ctr_const(lk, rk, n0, n1, n2);
+#endif
         for (; i + 256 < full_end && i >= na; i += 512) {
             const uint32_t j0 = i - na, j1 = j0 + 256;
             const u32x4 in0 = load16_be(fr.in + 16 * j0), in1 = load16_be(fr.in + 16 * j1);
             uint32_t a0 = n0, a1 = n1, a2 = n2, a3 = 2u + j0;
             uint32_t b0 = n0, b1 = n1, b2 = n2, b3 = 2u + j1;
 #ifndef GCM_LAB_NO_AES
-            aes_block2(lk, rk, a0, a1, a2, a3, b0, b1, b2, b3);
+            if (short_ctr) aes_ctr2(lk, rk, cc, 2u + j0, 2u + j1, a0, a1, a2, a3, b0, b1, b2, b3);
+            else aes_block2(lk, rk, a0, a1, a2, a3, b0, b1, b2, b3);
 #endif
             const u32x4 o0 = {in0.x ^ a0, in0.y ^ a1, in0.z ^ a2, in0.w ^ a3};
             const u32x4 o1 = {in1.x ^ b0, in1.y ^ b1, in1.z ^ b2, in1.w ^ b3};
@@ -323,7 +401,8 @@ __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a)
 
 hipError_t launch_gcm_frames(const GcmArgs& a, bool decrypt, int n_cus, hipStream_t s) {
     if (a.n_frames == 0) return hipSuccess;
-    // 144 KiB of LDS per workgroup: one workgroup (two frames) per CU.
+    // 128 KiB of T-tables + 8.06 KiB per frame group (155 KiB at three groups):
+    // one workgroup (three frames, 12 waves) per CU.
     static const hipError_t attr = [] {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gcm_frames_kernel<true>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kGcmLdsBytes));

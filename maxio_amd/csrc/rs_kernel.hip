@@ -320,15 +320,17 @@ uint64_t rs_tile_bytes(const RsVariant& v) { return uint64_t(kThreads) * 16 * ui
 
 // Default geometry, from tools/kernel_lab sweeps on MI355X (profiles/): four
 // 16-byte vectors per lane with nontemporal loads/stores while the
-// accumulators fit (R <= 4: <= 158 VGPRs), two beyond that; 16 workgroups per
-// CU of grid-stride (16 beat 8 and 4 on every shape swept).  Chosen by the
+// accumulators fit (R <= 4: <= 158 VGPRs), two beyond that; 32 workgroups per
+// CU of grid-stride (16 beat 8 and 4 on every shape swept; 32 gained another
+// 0.8-0.9 % on one box and was level on another,
+// profiles/r1_lab_copy_pattern_ceilings.jsonl).  Chosen by the
 // launch's total row count so every row group of a launch shares one tile
 // size (and one edge list).
 RsVariant rs_default_variant(uint32_t r_total) {
     RsVariant v;
     v.vecs = r_total <= 4 ? 4 : 2;
     v.nt = true;
-    v.blocks_per_cu = 16;
+    v.blocks_per_cu = 32;
     return v;
 }
 

@@ -51,6 +51,17 @@ def test_small_frames_and_first_index(ctx):
     assert ctx.frames_decrypt(key, got, len(pt), aads, first_index=5, frame_size=1024) == pt
 
 
+def test_large_frames_long_counters(ctx):
+    """Frames of more than 65534 blocks (counters past 2^16) take the generic
+    AES path instead of the per-frame counter constants; both must match."""
+    key, prefix = _rand(32, 9), b"LONG"
+    fs = 65535 * 16  # 65535 blocks: the last counter is 65536
+    pt = _rand(fs + 4096 + 5, 10)
+    got = ctx.frames_encrypt(key, prefix, pt, first_index=2, frame_size=fs)
+    assert got == oracle.frames_encrypt(key, prefix, pt, first_index=2, frame_size=fs)
+    assert ctx.frames_decrypt(key, got, len(pt), first_index=2, frame_size=fs) == pt
+
+
 def test_decrypt_errors(ctx):
     key, prefix = _rand(32, 3), b"abcd"
     pt = _rand(3 * 1000, 4)

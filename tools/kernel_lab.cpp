@@ -74,6 +74,42 @@ __global__ __launch_bounds__(256) void k_write_nt(u32x4* __restrict__ d, uint64_
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
         __builtin_nontemporal_store(v, d + i);
 }
+// Copy with four independent nontemporal 16-byte loads in flight per lane.
+__global__ __launch_bounds__(256) void k_copy_nt4(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
+        const u32x4 a = __builtin_nontemporal_load(s + i), b = __builtin_nontemporal_load(s + i + stride);
+        const u32x4 c = __builtin_nontemporal_load(s + i + 2 * stride), e = __builtin_nontemporal_load(s + i + 3 * stride);
+        __builtin_nontemporal_store(a, d + i);
+        __builtin_nontemporal_store(b, d + i + stride);
+        __builtin_nontemporal_store(c, d + i + 2 * stride);
+        __builtin_nontemporal_store(e, d + i + 3 * stride);
+    }
+}
+// The RS fast kernel's exact access pattern without the GF math: tile =
+// 256 lanes x 16 B x 4 vectors of every shard, 4 inputs x 4 vectors of
+// nontemporal loads in flight, XOR, then 2 outputs x 4 vectors of nt stores.
+__global__ __launch_bounds__(256) void k_pattern_tile(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                      uint64_t S, uint64_t n_obj) {
+    constexpr uint64_t kTile = 256 * 16 * 4;
+    const uint64_t tpo = S / kTile, n_tiles = tpo * n_obj;
+    for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint64_t o = t / tpo, base = (t - o * tpo) * kTile + threadIdx.x * 16;
+        u32x4 x[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                x[j][v] = __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x4*>(data + (o * 4 + j) * S + base + v * 4096));
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const u32x4 p = x[0][v] ^ x[1][v] ^ x[2][v] ^ x[3][v];
+            __builtin_nontemporal_store(p, reinterpret_cast<u32x4*>(par + (o * 2) * S + base + v * 4096));
+            __builtin_nontemporal_store(p + 1u, reinterpret_cast<u32x4*>(par + (o * 2 + 1) * S + base + v * 4096));
+        }
+    }
+}
 // RS access pattern without the math: object o, 16-B column c: read k shards,
 // write m shards (XOR of inputs), same layout as the bench.
 __global__ __launch_bounds__(256) void k_pattern(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
@@ -211,6 +247,15 @@ int main(int argc, char** argv) {
                 std::snprintf(nm, sizeof nm, "read_glds_nt_bpc%d", bpc);
                 ms = tm.median_ms([&] { hipLaunchKernelGGL(k_read_glds<2>, dim3(cus * bpc), dim3(256), 0, 0, s, d, nvec); });
                 report(nm, "pool", ms, 16.0 * nvec);
+            }
+            for (int bpc : {8, 16, 32}) {
+                char nm[64];
+                std::snprintf(nm, sizeof nm, "copy_nt4_bpc%d", bpc);
+                double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_copy_nt4, dim3(cus * bpc), dim3(256), 0, 0, s, d, half); });
+                report(nm, "2x half pool", ms, 32.0 * half);
+                std::snprintf(nm, sizeof nm, "pattern_tile_4r2w_bpc%d", bpc);
+                ms = tm.median_ms([&] { hipLaunchKernelGGL(k_pattern_tile, dim3(cus * bpc), dim3(256), 0, 0, buf, buf + n2 * 4 * S2, S2, n2); });
+                report(nm, "k4m2 S10MiB", ms, double(n2) * 6 * S2);
             }
             double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, d, half); });
             report("write", "half pool", ms, 16.0 * half);
