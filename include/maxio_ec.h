@@ -96,6 +96,10 @@ void mxec_close(mxec_ctx* ctx);
 int mxec_ctx_device_count(const mxec_ctx* ctx);
 /* HIP device id of the ctx's i-th device. */
 int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
+/* Runtime statistics of ctx device i: SHA-256 verification launches run by
+ * the device's combiner (concurrent small requests share one launch) and the
+ * messages they hashed. */
+int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages);
 
 /* ---- ReedSolomon::new ----------------------------------------------------- */
 /* 0 if new(k, m) would succeed; otherwise the crate's error

@@ -16,15 +16,6 @@ using namespace mxec;
 namespace {
 
 
-// Digest bytes for n shards of the host-staged image into out (host).
-int fetch_digests(Slot& slot, hipStream_t s, size_t n, uint8_t (*out)[32]) {
-    MXEC_TRY(slot.hdig.ensure(n * 32));
-    MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
-    MXEC_HIP(hipStreamSynchronize(s));
-    std::memcpy(out, slot.hdig.p, n * 32);
-    return MXEC_OK;
-}
-
 std::string too_few_msg(int present, int k, int total) {
     return "too many missing/corrupt shards: only " + std::to_string(present) + " of " +
            std::to_string(k) + " required shards available (" + std::to_string(total - present) +
@@ -135,6 +126,13 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i) {
     return ctx->c.devs[size_t(i)]->id;
 }
 
+int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages) {
+    if (!ctx || i < 0 || i >= int(ctx->c.devs.size()) || !launches || !messages)
+        return set_error(MXEC_E_INVALID_ARG, "invalid argument");
+    combiner_stats(*ctx->c.devs[size_t(i)], launches, messages);
+    return MXEC_OK;
+}
+
 int mxec_rs_check(int k, int m) { return rs_check(k, m); }
 
 int mxec_rs_parity_matrix(int k, int m, uint8_t* out) {
@@ -175,8 +173,8 @@ int mxec_sha256_batch(mxec_ctx* ctx, const uint8_t* const* bufs, const size_t* l
             ptrs[i] = base + off[i];
             l[i] = lens[i];
         }
-        MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, l, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
-        return fetch_digests(slot, s, n, out);
+        MXEC_HIP(hipStreamSynchronize(s));  // uploads done: the combiner hashes on its own stream
+        return sha256_combined(*ds.d, slot, s, ptrs, l, &out[0][0]);
     });
 }
 
@@ -212,16 +210,16 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* c
         MXEC_TRY(encode_coef(*ds.d, k, m, &off));
         RsObject ob{in.data(), len.data(), out.data(), len.data() + k, off};
         MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, m, {ob}));
-        if (sha256_out) {
-            MXEC_TRY(slot.digests.ensure(size_t(k + m) * 32));
-            std::vector<const uint8_t*> ptrs(in.begin(), in.end());
-            for (auto* p : out) ptrs.push_back(p);
-            MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, len, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
-        }
         for (int i = 0; i < m; ++i)
             MXEC_HIP(hipMemcpyAsync(parity[i], out[size_t(i)], shard_size, hipMemcpyDeviceToHost, s));
-        if (sha256_out) return fetch_digests(slot, s, size_t(k + m), sha256_out);
         MXEC_HIP(hipStreamSynchronize(s));
+        if (sha256_out) {
+            // write_chunk / compute_and_write_parity digests (filesystem.rs:1070,
+            // :1131), combined with every concurrent caller's verification work.
+            std::vector<const uint8_t*> ptrs(in.begin(), in.end());
+            for (auto* p : out) ptrs.push_back(p);
+            return sha256_combined(*ds.d, slot, s, ptrs, len, &sha256_out[0][0]);
+        }
         return MXEC_OK;
     });
 }
@@ -261,18 +259,11 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
         }
         if (expected_sha256 && !sp.empty()) {
             // chunk_reader.rs:176-196: hash every present shard; mismatch -> erasure.
-            uint8_t* exp_dev = base + sa * uint64_t(total);
-            uint8_t* ok_dev = exp_dev + size_t(total) * 32;
-            std::vector<uint8_t> exp(sp.size() * 32);
-            for (size_t t = 0; t < si.size(); ++t) std::memcpy(&exp[t * 32], expected_sha256[si[t]], 32);
-            MXEC_HIP(hipMemcpyAsync(exp_dev, exp.data(), exp.size(), hipMemcpyHostToDevice, s));
-            MXEC_TRY(run_sha(*ds.d, slot, s, sp, sl, nullptr, exp_dev, ok_dev));
-            MXEC_TRY(slot.hdig.ensure(sp.size()));
-            MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok_dev, sp.size(), hipMemcpyDeviceToHost, s));
             MXEC_HIP(hipStreamSynchronize(s));
-            const auto* okh = static_cast<const uint8_t*>(slot.hdig.p);
+            std::vector<uint8_t> dig(sp.size() * 32);
+            MXEC_TRY(sha256_combined(*ds.d, slot, s, sp, sl, dig.data()));
             for (size_t t = 0; t < si.size(); ++t)
-                if (!okh[t]) present[size_t(si[t])] = 0;
+                if (std::memcmp(&dig[t * 32], expected_sha256[si[t]], 32) != 0) present[size_t(si[t])] = 0;
         }
         int np = 0;
         for (int i = 0; i < total; ++i) np += present[size_t(i)] ? 1 : 0;
@@ -436,9 +427,10 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                         lens.push_back(len[size_t(i)]);
                         idx.push_back(o * total + i);
                     }
-            if (!ptrs.empty()) {
-                // Expected digests are object-major over all k+m shards; the
-                // verify kernel compares message t against expected[idx[t]].
+            if (!ptrs.empty() && !sha_combines(ptrs.size())) {
+                // A batch that fills the chip: its own launch on `stream`,
+                // digests compared on the device (the verify kernel compares
+                // message t against expected[idx[t]]), n flags read back.
                 MXEC_TRY(slot.digests.ensure(ptrs.size()));
                 auto* ok = static_cast<uint8_t*>(slot.digests.p);
                 MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx));
@@ -448,6 +440,21 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 const auto* okh = static_cast<const uint8_t*>(slot.hdig.p);
                 for (size_t t = 0; t < idx.size(); ++t)
                     if (!okh[t]) present[idx[t]] = 0;
+            } else if (!ptrs.empty()) {
+                // A small batch: hashed by the device's combiner together with
+                // every concurrent caller's verification (combiner.cpp), once
+                // the work queued on `stream` has produced the shards; digests
+                // compared on the host.
+                const size_t ne = size_t(n_obj) * size_t(total) * 32;
+                MXEC_TRY(slot.hdig.ensure(ne));
+                MXEC_HIP(hipMemcpyAsync(slot.hdig.p, expected_sha_dev, ne, hipMemcpyDeviceToHost, s));
+                MXEC_HIP(hipStreamSynchronize(s));
+                std::vector<uint8_t> exph(static_cast<const uint8_t*>(slot.hdig.p),
+                                          static_cast<const uint8_t*>(slot.hdig.p) + ne);
+                std::vector<uint8_t> dig(ptrs.size() * 32);
+                MXEC_TRY(sha256_combined(*ds.d, slot, s, ptrs, lens, dig.data()));
+                for (size_t t = 0; t < idx.size(); ++t)
+                    if (std::memcmp(&dig[t * 32], exph.data() + idx[t] * 32, 32) != 0) present[idx[t]] = 0;
             }
         }
         const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;

@@ -1,0 +1,155 @@
+// combiner.cpp — cross-request coalescing of SHA-256 verification.
+//
+// SHA-256 of one message is a serial chain (~1.8 us per 64-byte block on one
+// lane, sha256_kernel.hip), so a launch over 8 chunks of one GET takes as
+// long as a launch over thousands: per-request launches leave the GPU nearly
+// idle and, past GPU_MAX_HW_QUEUES streams, even queue behind each other.
+// Concurrent callers on one device (MaxIO's tokio workers serving GETs, chunk
+// verification in chunk_reader.rs:87-152 / :176-196) therefore hand their
+// device-resident messages to one combiner: the first caller that finds no
+// launch in flight becomes the leader, takes every pending request, and runs
+// ONE launch over all their messages on the combiner's private stream;
+// callers that arrive meanwhile wait and form the next batch (flat
+// combining, no service thread).  A request waits at most for the batch in
+// flight plus its own, and a batch of N requests costs about one request's
+// latency.
+#include <condition_variable>
+#include <cstring>
+
+#include "ops.hpp"
+
+namespace mxec {
+
+struct ShaCombiner {
+    struct Req {
+        const std::vector<const uint8_t*>* ptrs = nullptr;
+        const std::vector<uint64_t>* lens = nullptr;
+        uint8_t* out = nullptr;  // host, n * 32
+        int rc = MXEC_OK;
+        std::string msg;
+        bool done = false;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Req*> pending;
+    bool busy = false;
+    Slot slot;  // private stream, descriptor ring and digest buffers
+    uint64_t batches = 0, messages = 0;
+
+    ~ShaCombiner() {
+        if (slot.stream) (void)hipStreamSynchronize(slot.stream);
+        for (auto& rb : slot.ring)
+            if (rb.done) (void)hipEventDestroy(rb.done);
+        if (slot.stream) (void)hipStreamDestroy(slot.stream);
+    }
+
+    // One launch over every message of `batch`; digests land in each
+    // request's host buffer.  Called by the leader without the lock held.
+    int run(Device& d, const std::vector<Req*>& batch) {
+        std::vector<const uint8_t*> ptrs;
+        std::vector<uint64_t> lens;
+        for (const Req* r : batch) {
+            ptrs.insert(ptrs.end(), r->ptrs->begin(), r->ptrs->end());
+            lens.insert(lens.end(), r->lens->begin(), r->lens->end());
+        }
+        const size_t n = ptrs.size();
+        if (n == 0) return MXEC_OK;
+        hipStream_t s = slot.stream;
+        MXEC_TRY(slot.digests.ensure(n * 32));
+        MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
+        MXEC_TRY(slot.hdig.ensure(n * 32));
+        MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
+        MXEC_HIP(hipStreamSynchronize(s));
+        const auto* h = static_cast<const uint8_t*>(slot.hdig.p);
+        size_t o = 0;
+        for (Req* r : batch) {
+            const size_t k = r->ptrs->size();
+            std::memcpy(r->out, h + o * 32, k * 32);
+            o += k;
+        }
+        ++batches;
+        messages += n;
+        return MXEC_OK;
+    }
+};
+
+// Requests with at least this many messages are not combined.
+constexpr size_t kCombineBelow = 8192;
+bool sha_combines(size_t n) { return n < kCombineBelow; }
+
+namespace {
+
+ShaCombiner* combiner_of(Device& d) {
+    std::lock_guard<std::mutex> g(d.comb_mu);
+    if (!d.comb) {
+        auto c = std::make_shared<ShaCombiner>();
+        if (hipStreamCreateWithFlags(&c->slot.stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        d.comb = c;
+    }
+    return static_cast<ShaCombiner*>(d.comb.get());
+}
+
+}  // namespace
+
+int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
+                    const std::vector<uint64_t>& lens, uint8_t* out) {
+    if (ptrs.empty()) return MXEC_OK;
+    if (!sha_combines(ptrs.size())) {
+        // Enough messages to fill the chip's SIMDs on its own (bench config 3:
+        // 10 240): its own launch on the caller's stream.  Folded into other
+        // large requests it would only cross the one-wave-per-SIMD line and
+        // make every message of the batch wait for the SIMDs that got two.
+        const size_t n = ptrs.size();
+        MXEC_TRY(slot.digests.ensure(n * 32));
+        MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
+        MXEC_TRY(slot.hdig.ensure(n * 32));
+        MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
+        MXEC_HIP(hipStreamSynchronize(s));
+        std::memcpy(out, slot.hdig.p, n * 32);
+        return MXEC_OK;
+    }
+    ShaCombiner* c = combiner_of(d);
+    if (!c) return set_error(MXEC_E_DEVICE, "combiner stream creation failed");
+    ShaCombiner::Req me;
+    me.ptrs = &ptrs;
+    me.lens = &lens;
+    me.out = out;
+    std::unique_lock<std::mutex> lk(c->mu);
+    c->pending.push_back(&me);
+    while (!me.done) {
+        if (c->busy) {
+            c->cv.wait(lk);
+            continue;
+        }
+        c->busy = true;
+        std::vector<ShaCombiner::Req*> batch;
+        batch.swap(c->pending);
+        lk.unlock();
+        int rc = MXEC_OK;
+        try {
+            rc = c->run(d, batch);
+        } catch (...) {
+            rc = set_error(MXEC_E_OOM, "host allocation failed");
+        }
+        const std::string msg = rc ? std::string(last_error()) : std::string();
+        lk.lock();
+        for (auto* r : batch) {
+            r->rc = rc;
+            r->msg = msg;
+            r->done = true;
+        }
+        c->busy = false;
+        c->cv.notify_all();
+    }
+    if (me.rc) return set_error(me.rc, me.msg);
+    return MXEC_OK;
+}
+
+void combiner_stats(Device& d, uint64_t* batches, uint64_t* messages) {
+    std::lock_guard<std::mutex> g(d.comb_mu);
+    auto* c = static_cast<ShaCombiner*>(d.comb.get());
+    *batches = c ? c->batches : 0;
+    *messages = c ? c->messages : 0;
+}
+
+}  // namespace mxec

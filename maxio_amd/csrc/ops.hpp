@@ -34,6 +34,17 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
             uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx = nullptr,
             DescArena* arena = nullptr);
 
+// SHA-256 digests (host out, n * 32 bytes) of n device-resident messages on
+// `dev`, blocking; the caller's work on `s` must have produced them (the
+// caller synchronises `s` first).  Concurrent small requests on one device
+// share one launch on the combiner's stream (combiner.cpp); large ones run on
+// the caller's slot and stream.
+int sha256_combined(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
+                    const std::vector<uint64_t>& lens, uint8_t* out);
+void combiner_stats(Device& dev, uint64_t* batches, uint64_t* messages);
+// Whether a request of n messages goes through the combiner.
+bool sha_combines(size_t n);
+
 // Coefficient table of the (k, m) encoding matrix's parity rows.
 int encode_coef(Device& dev, int k, int m, uint32_t* off);
 // Coefficient table of a decode plan.

@@ -106,6 +106,10 @@ struct Device {
     // created on first use and kept, one batch at a time per device.
     std::mutex pipe_mu;
     std::shared_ptr<void> pipe;
+    // SHA-256 combiner (combiner.cpp): one launch for the verification work
+    // of every concurrent caller on this device.
+    std::mutex comb_mu;
+    std::shared_ptr<void> comb;
 };
 
 struct Ctx {

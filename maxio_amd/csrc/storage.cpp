@@ -483,60 +483,153 @@ struct LoadedChunk {
 // load_chunk_sync (:87-152) for chunks [first, last]: read, size check, one
 // batched digest pass; with parity every bad chunk is rebuilt in one decode
 // (:130-150), without parity a bad chunk carries its original error.
+//
+// The reference rebuilds a bad chunk with try_reconstruct_data_chunk, which
+// re-reads and re-hashes every shard (:157-226), once per bad chunk.  Here:
+// when a chunk of the range is already known bad before hashing (its file is
+// missing or has the wrong size), every other shard is read up front and
+// hashed in the SAME pass as the range; a chunk that only fails its digest
+// costs one more pass over the shards not yet hashed.  Either way each shard
+// is hashed once and every bad chunk of the range comes out of one decode.
 int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_t first, uint32_t last,
                 std::vector<LoadedChunk>& out) {
     const uint32_t n = last - first + 1;
     out.assign(n, LoadedChunk{});
-    std::vector<const uint8_t*> hp;
-    std::vector<size_t> hl;
-    std::vector<uint32_t> hidx;
+    const bool parity = man.has_parity && man.parity_shards > 0;
+    const int k = int(man.chunk_count);
+    const int m = parity ? int(man.parity_shards) : 0;
+    const int total = k + m;
+    const uint64_t shard = man.has_shard ? man.shard_size : man.chunk_size;
+    bool known_bad = false;
     for (uint32_t c = 0; c < n; ++c) {
         const uint32_t idx = first + c;
         LoadedChunk& lc = out[c];
         if (read_file(dir / chunk_name(idx), lc.data) != MXEC_OK) {
             lc.err = MXEC_E_IO;
             lc.msg = "failed to read chunk " + std::to_string(idx) + ": " + mxec::last_error();
+            known_bad = true;
             continue;
         }
         if (lc.data.size() != man.chunks[idx].size) {
             lc.err = MXEC_E_INTEGRITY;
             lc.msg = "chunk " + std::to_string(idx) + " size mismatch: expected " +
                      std::to_string(man.chunks[idx].size) + ", got " + std::to_string(lc.data.size());
-            continue;
+            known_bad = true;
         }
-        hp.push_back(lc.data.empty() ? reinterpret_cast<const uint8_t*>("") : lc.data.data());
-        hl.push_back(lc.data.size());
-        hidx.push_back(c);
     }
-    if (!hp.empty()) {
+    if (parity && int(man.chunks.size()) < total)
+        return set_error(MXEC_E_JSON, "JSON error: manifest lists fewer shards than k+m");
+    // Shards outside the range, for a rebuild: bytes, loaded with the length
+    // the digest covers (:184), digest verified.
+    auto want_len = [&](int i) {
+        return size_t(i < k ? std::min<uint64_t>(man.chunks[size_t(i)].size, shard) : shard);
+    };
+    std::vector<std::vector<uint8_t>> extra(parity ? size_t(total) : 0);
+    std::vector<uint8_t> extra_loaded(extra.size(), 0), verified(extra.size(), 0);
+    bool extra_read = false;
+    auto read_extra = [&] {
+        extra_read = true;
+        for (int i = 0; i < total; ++i) {
+            if (i >= int(first) && i <= int(last)) continue;
+            std::vector<uint8_t>& d = extra[size_t(i)];
+            extra_loaded[size_t(i)] =
+                read_file(dir / chunk_name(uint32_t(i)), d) == MXEC_OK && d.size() == want_len(i);
+        }
+    };
+    if (parity && known_bad) read_extra();
+    // One digest pass over everything loaded and not yet hashed.
+    auto hash_pass = [&](bool range) -> int {
+        std::vector<const uint8_t*> hp;
+        std::vector<size_t> hl;
+        std::vector<int> who;  // >= 0: range chunk c; < 0: extra shard -(i+1)
+        if (range)
+            for (uint32_t c = 0; c < n; ++c)
+                if (!out[c].err) {
+                    hp.push_back(out[c].data.empty() ? reinterpret_cast<const uint8_t*>("") : out[c].data.data());
+                    hl.push_back(out[c].data.size());
+                    who.push_back(int(c));
+                }
+        for (size_t i = 0; i < extra.size(); ++i)
+            if (extra_loaded[i] && !verified[i]) {
+                hp.push_back(extra[i].empty() ? reinterpret_cast<const uint8_t*>("") : extra[i].data());
+                hl.push_back(extra[i].size());
+                who.push_back(-int(i) - 1);
+            }
+        if (hp.empty()) return MXEC_OK;
         std::vector<uint8_t> dig(hp.size() * 32);
         MXEC_TRY(mxec_sha256_batch(ctx, hp.data(), hl.data(), hp.size(), reinterpret_cast<uint8_t(*)[32]>(dig.data())));
-        for (size_t t = 0; t < hidx.size(); ++t) {
-            const uint32_t c = hidx[t];
+        for (size_t t = 0; t < who.size(); ++t) {
             const std::string got = hex32(&dig[t * 32]);
-            if (got != man.chunks[first + c].sha256) {
-                out[c].err = MXEC_E_INTEGRITY;
-                out[c].msg = "checksum mismatch on chunk " + std::to_string(first + c) + ": expected " +
-                             man.chunks[first + c].sha256 + ", got " + got;
+            if (who[t] >= 0) {
+                const uint32_t c = uint32_t(who[t]);
+                if (got != man.chunks[first + c].sha256) {
+                    out[c].err = MXEC_E_INTEGRITY;
+                    out[c].msg = "checksum mismatch on chunk " + std::to_string(first + c) + ": expected " +
+                                 man.chunks[first + c].sha256 + ", got " + got;
+                }
+            } else {
+                const size_t i = size_t(-who[t] - 1);
+                verified[i] = got == man.chunks[i].sha256;
+                extra_loaded[i] = verified[i];  // a failed shard is an erasure, not hashed again
             }
         }
-    }
-    if (!(man.has_parity && man.parity_shards > 0)) return MXEC_OK;
+        return MXEC_OK;
+    };
+    MXEC_TRY(hash_pass(true));
+    if (!parity) return MXEC_OK;
     std::vector<uint32_t> bad;
-    std::vector<std::vector<uint8_t>*> bad_out;
     for (uint32_t c = 0; c < n; ++c)
-        if (out[c].err) {
-            bad.push_back(first + c);
-            bad_out.push_back(&out[c].data);
-        }
+        if (out[c].err) bad.push_back(c);
     if (bad.empty()) return MXEC_OK;
-    const int rc = reconstruct_from_dir(ctx, dir, man, bad, bad_out);
-    const std::string msg = rc ? std::string(mxec::last_error()) : std::string();
-    for (uint32_t c = 0; c < n; ++c)
-        if (out[c].err) {
-            out[c].err = rc;
-            out[c].msg = msg;
+    if (!extra_read) {
+        read_extra();
+        MXEC_TRY(hash_pass(false));
+    }
+    // try_reconstruct_data_chunk (:157-226) from the verified shards: the
+    // buffers hold each shard's real bytes (the kernels read past a shard's
+    // length as zero = Vec::resize(shard_size)); no digest is recomputed.
+    std::vector<std::vector<uint8_t>> bufs(static_cast<size_t>(total));
+    std::vector<uint8_t*> ptrs(static_cast<size_t>(total));
+    std::vector<size_t> lens(static_cast<size_t>(total));
+    std::vector<uint8_t> present(static_cast<size_t>(total), 0);
+    for (int i = 0; i < total; ++i) {
+        const size_t w = want_len(i);
+        std::vector<uint8_t>& b = bufs[size_t(i)];
+        if (i >= int(first) && i <= int(last)) {
+            LoadedChunk& lc = out[size_t(i) - first];
+            if (!lc.err) {
+                b = lc.data;  // size == chunks[i].size == want_len(i)
+                present[size_t(i)] = 1;
+            }
+        } else if (verified[size_t(i)]) {
+            b.swap(extra[size_t(i)]);
+            present[size_t(i)] = 1;
         }
+        if (!present[size_t(i)]) b.assign(w, 0);
+        lens[size_t(i)] = w;
+        ptrs[size_t(i)] = b.empty() ? nullptr : b.data();
+    }
+    // Zero-length shards still need a non-null pointer for the C API.
+    uint8_t dummy = 0;
+    for (auto& p : ptrs)
+        if (!p) p = &dummy;
+    int np = 0;
+    const int rc = mxec_reconstruct(ctx, k, m, shard, ptrs.data(), lens.data(), nullptr, present.data(),
+                                    MXEC_F_DATA_ONLY, &np);
+    const std::string msg = rc ? std::string(mxec::last_error()) : std::string();
+    for (uint32_t c : bad) {
+        LoadedChunk& lc = out[c];
+        if (rc) {
+            lc.err = rc;
+            lc.msg = msg;
+            continue;
+        }
+        const uint32_t idx = first + c;
+        const size_t real = size_t(std::min<uint64_t>(man.chunks[idx].size, shard));
+        lc.data.assign(bufs[idx].begin(), bufs[idx].begin() + long(real));
+        lc.err = MXEC_OK;
+        lc.msg.clear();
+    }
     return MXEC_OK;
 }
 

@@ -166,6 +166,12 @@ class Context:
     def handle(self):
         return self._h
 
+    def combiner_stats(self, dev: int = 0) -> dict:
+        """SHA-256 launches of device `dev`'s combiner and the messages they hashed."""
+        b, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(self._lib.mxec_ctx_combiner_stats(self._h, dev, ctypes.byref(b), ctypes.byref(m)))
+        return {"batches": b.value, "messages": m.value}
+
     def device_ids(self) -> list[int]:
         n = self._lib.mxec_ctx_device_count(self._h)
         return [self._lib.mxec_ctx_device_id(self._h, i) for i in range(n)]

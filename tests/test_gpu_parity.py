@@ -434,3 +434,29 @@ def test_concurrent_reconstruct_workers(ctx):
             assert all(pool.map(run, jobs))
     finally:
         c.close()
+
+
+def test_concurrent_small_sha_requests_are_combined(ctx):
+    """Many threads hashing a few chunks each (GET verification of small
+    objects) share launches through the device's combiner; every digest must
+    still land with its own caller."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    c = maxio_amd.Context(streams_per_device=12)
+    try:
+        def job(t):
+            rng = np.random.default_rng(1000 + t)
+            bufs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()
+                    for n in np.random.default_rng(t).integers(0, 70000, 1 + t % 7)]
+            for _ in range(4):
+                if c.sha256(bufs) != [hashlib.sha256(b).digest() for b in bufs]:
+                    return False
+            return True
+
+        with ThreadPoolExecutor(12) as pool:
+            assert all(pool.map(job, range(48)))
+        stats = c.combiner_stats()
+        assert stats["messages"] >= 4 * sum(1 + t % 7 for t in range(48))
+        assert stats["batches"] <= 4 * 48  # some requests rode in another's launch
+    finally:
+        c.close()
