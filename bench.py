@@ -15,6 +15,8 @@ Other BASELINE configs (same JSON line, for DESIGN.md / profiles):
       shards, 1 MiB chunks, 1024 objects (8192 data chunks) per GPU
   3c  the same batches as a continuous GET stream: --workers host threads
       (default 8) each reconstructing its own batch on its own HIP stream
+  ns  encode k=8 m=4, 1 MiB chunks, 4096 objects per GPU (north_star's
+      target shape)
   4a  encode k=10 m=4, 1 MiB chunks (10 MiB objects), 4096 objects per GPU
   4b  encode k=64 m=4, 1 MiB chunks (literal 64 MiB objects), 640 per GPU
   5   mixed 4+2 / 8+4 / 10+4 at 64 KiB..10 MiB chunks with short last chunks:
@@ -496,6 +498,11 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank, workers=8):
         return Reconstruct(torch, ctx, dev, sh, n_objects or 1024, seed)
     if cfg == "3c":
         return ReconstructStream(torch, ctx, dev, sh, n_objects or 1024, workers, seed)
+    if cfg == "ns":
+        n = n_objects or 4096
+        return Encode(torch, ctx, dev, sh, 8, 4, 1 << 20, n,
+                      f"RS encode k=8 m=4, chunk_size=1 MiB (8 MiB objects), {n} objects per GPU "
+                      "(north_star target shape)", seed)
     if cfg == "4a":
         n = n_objects or 4096
         return Encode(torch, ctx, dev, sh, 10, 4, 1 << 20, n,
@@ -579,7 +586,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="2", choices=["2", "3", "3c", "4a", "4b", "5", "sums", "frames"])
+    ap.add_argument("--config", default="2", choices=["2", "3", "3c", "ns", "4a", "4b", "5", "sums", "frames"])
     ap.add_argument("--workers", type=int, default=8, help="config 3c: concurrent batches")
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""End-to-end GET-path rate from shard files (DESIGN.md §5 "GET end to end").
+"""End-to-end PUT and GET rates through the file layer.
 
 The GET path starts at the shard files `{key}.ec/{i:06}` + manifest.json and
 ends in a host buffer (VerifiedChunkReader, chunk_reader.rs:35-276): read each
@@ -92,11 +92,52 @@ def main() -> int:
         ctx = maxio_amd.Context(streams_per_device=args.threads)
         rng = np.random.default_rng(7)
         block = rng.integers(0, 256, size + 4096, dtype=np.uint8)
-        dirs = []
-        for o in range(n):
-            d = os.path.join(base, f"obj{o}.ec")
-            ctx.put_object_chunked(d, S, m, block[o % 4096: o % 4096 + size])
-            dirs.append(d)
+        dirs = [os.path.join(base, f"obj{o}.ec") for o in range(n)]
+        lib0 = maxio_amd.lib()
+
+        def gpu_put(o):
+            body = block[o % 4096: o % 4096 + size]
+            rc = lib0.mxec_put_object_chunked(ctx.handle, dirs[o].encode(), S, m, body.ctypes.data, size)
+            assert rc == 0, rc
+            return size
+
+        # PUT (put_object_chunked: chunk files + parity + manifest.json, SHA-256
+        # of every chunk), W threads; the first pass writes, the timed pass
+        # overwrites the same files.
+        with ThreadPoolExecutor(args.threads) as pool:
+            list(pool.map(gpu_put, range(n)))
+            t = time.perf_counter()
+            total = sum(pool.map(gpu_put, range(n)))
+            el = time.perf_counter() - t
+        out["gpu_put"] = {"GiBps": round(total / GIB / el, 3), "s": round(el, 4)}
+
+        def ref_put(o):
+            """filesystem.rs:686-828 with the crate algorithm (oracle/) and
+            hashlib: write the data chunks, encode, write parity, manifest."""
+            d = os.path.join(base, f"ref{o}.ec")
+            os.makedirs(d, exist_ok=True)
+            body = block[o % 4096: o % 4096 + size]
+            chunks = [body[i * S:(i + 1) * S] for i in range(k)]
+            dig = []
+            for i, c in enumerate(chunks):  # write_chunk: file + Sha256 (SHA-NI via OpenSSL)
+                with open(os.path.join(d, f"{i:06}"), "wb") as f:
+                    f.write(c.tobytes())
+                dig.append(hashlib.sha256(c).hexdigest())
+            for i, p in enumerate(oracle.encode(chunks, m, S)):  # compute_and_write_parity
+                with open(os.path.join(d, f"{k + i:06}"), "wb") as f:
+                    f.write(p.tobytes())
+                dig.append(hashlib.sha256(p).hexdigest())
+            with open(os.path.join(d, "manifest.json"), "w") as f:
+                json.dump({"chunks": dig}, f)
+            return size
+
+        for threads in (1, args.threads):
+            t = time.perf_counter()
+            with ThreadPoolExecutor(threads) as pool:
+                total = sum(pool.map(ref_put, range(args.cpu_objects)))
+            el = time.perf_counter() - t
+            out[f"cpu_reference_put_{threads}t"] = {"GiBps": round(total / GIB / el, 3),
+                                                   "objects": args.cpu_objects}
         lib = maxio_amd.lib()
         bufs = [np.zeros(size, np.uint8) for _ in range(args.threads)]
 
