@@ -320,6 +320,52 @@ int mxec_put_object_chunked_sums(mxec_ctx* ctx, const char* ec_dir,
                                  const uint8_t* body, size_t len, uint32_t which,
                                  mxec_body_sums* sums_out);
 
+/* put_object_chunked_encrypted (filesystem.rs:835-1060) for a buffered body:
+ * the plaintext becomes AES-256-GCM 64 KiB frames (first index 0, frame i's
+ * AAD = SHA-256(aad_prefix || i LE) with aad_prefix = bucket 0 key 0
+ * version 0, build_frame_aad :118-128), the frame stream is chunked, parity
+ * added, and manifest.json records total_size = frame-stream bytes and
+ * plaintext_size.  `which` / sums_out: the plaintext body digests as in
+ * mxec_put_object_chunked_sums (0 / NULL to skip). */
+int mxec_put_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir,
+                                      uint64_t chunk_size, uint32_t parity_shards,
+                                      const uint8_t key[32], const uint8_t nonce_prefix[4],
+                                      const uint8_t* aad_prefix, uint32_t aad_prefix_len,
+                                      const uint8_t* body, size_t len, uint32_t which,
+                                      mxec_body_sums* sums_out);
+
+/* One part of a CompleteMultipartUpload (PartMeta, multipart.rs). */
+typedef struct mxec_multipart_part {
+    const char* path;      /* part file (upload_part wrote it flat)          */
+    uint64_t size;         /* plaintext bytes of the part                    */
+    uint8_t md5[16];       /* the part ETag as raw bytes                     */
+    uint32_t part_number;
+    uint8_t encrypted;     /* frames under the upload key (SSE multipart)    */
+} mxec_multipart_part;
+
+/* complete_multipart_chunked (filesystem.rs:1147-1310): parts concatenated,
+ * re-chunked, parity, manifest.json; etag_out receives "<hex md5 of the
+ * parts' raw MD5s>-<n_parts>" (unquoted, :1240-1244).  The composite
+ * x-amz-checksum is mxec_body_sums_batch over the parts' raw checksums. */
+int mxec_complete_multipart_chunked(mxec_ctx* ctx, const char* ec_dir,
+                                    uint64_t chunk_size, uint32_t parity_shards,
+                                    const mxec_multipart_part* parts, uint32_t n_parts,
+                                    char etag_out[48]);
+
+/* complete_multipart_chunked_encrypted (filesystem.rs:1315-1560): encrypted
+ * parts are decrypted with upload_key (AADs of "PART" 0 upload_id 0
+ * part_number_le4 0, :147-163), the recombined plaintext re-encrypted under
+ * the object key as in mxec_put_object_chunked_encrypted, chunked, parity,
+ * manifest with plaintext_size; the same ETag. */
+int mxec_complete_multipart_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir,
+                                              uint64_t chunk_size, uint32_t parity_shards,
+                                              const mxec_multipart_part* parts, uint32_t n_parts,
+                                              const uint8_t upload_key[32], const char* upload_id,
+                                              const uint8_t key[32], const uint8_t nonce_prefix[4],
+                                              const uint8_t* aad_prefix, uint32_t aad_prefix_len,
+                                              char etag_out[48]);
+
+
 /* GET of a whole EC object (VerifiedChunkReader over manifest.json,
  * chunk_reader.rs:35-152): verified chunks, RS recovery of bad ones.
  * out must hold manifest total_size bytes; *out_len receives it.

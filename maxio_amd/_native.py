@@ -62,6 +62,18 @@ class ChunkInfo(ctypes.Structure):
     ]
 
 
+class MultipartPart(ctypes.Structure):
+    """mxec_multipart_part (PartMeta of a CompleteMultipartUpload)."""
+
+    _fields_ = [
+        ("path", ctypes.c_char_p),
+        ("size", ctypes.c_uint64),
+        ("md5", ctypes.c_uint8 * 16),
+        ("part_number", ctypes.c_uint32),
+        ("encrypted", ctypes.c_uint8),
+    ]
+
+
 class Object(ctypes.Structure):
     _fields_ = [("k", ctypes.c_int32), ("m", ctypes.c_int32), ("shard_size", ctypes.c_uint64)]
 
@@ -105,6 +117,13 @@ _SIGS = {
     "mxec_put_object_chunked_sums": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, SZ,
                                            ctypes.c_uint32, P]),
     "mxec_body_sums_batch": (INT, [P, PP, U64P, U64, ctypes.c_uint32, P]),
+    "mxec_put_object_chunked_encrypted": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, P, P,
+                                                ctypes.c_uint32, P, SZ, ctypes.c_uint32, P]),
+    "mxec_complete_multipart_chunked": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32,
+                                              ctypes.POINTER(MultipartPart), ctypes.c_uint32, ctypes.c_char_p]),
+    "mxec_complete_multipart_chunked_encrypted": (
+        INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, ctypes.POINTER(MultipartPart), ctypes.c_uint32, P,
+              ctypes.c_char_p, P, P, P, ctypes.c_uint32, ctypes.c_char_p]),
     "mxec_frames_len": (U64, [U64, ctypes.c_uint32]),
     "mxec_frames_encrypt": (INT, [P, P, P, U64, P, ctypes.c_uint32, ctypes.c_uint32, P, U64, P, U64, U64P]),
     "mxec_frames_decrypt": (INT, [P, P, U64, P, ctypes.c_uint32, ctypes.c_uint32, P, U64, U64, P, U64, U64P]),

@@ -374,8 +374,16 @@ int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir, uint64_t ch
     return MXEC_OK;
 }
 
-int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
-                            const uint8_t* body, size_t len) {
+}  // extern "C"
+
+namespace {
+
+// put_object_chunked's chunking, chunk files, parity and manifest for a
+// buffered body (filesystem.rs:686-828).  plain_size >= 0 records
+// manifest.plaintext_size: the encrypt-then-EC drivers chunk the frame
+// stream and keep the plaintext length (:973-990, :1472-1486).
+int put_chunked_buffer(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
+                       const uint8_t* body, size_t len, int64_t plain_size) {
     if (!ec_dir || (len && !body)) return set_error(MXEC_E_INVALID_ARG, "null argument");
     if (chunk_size == 0) return set_error(MXEC_E_INVALID_ARG, "chunk_size must be > 0");
     const fs::path dir(ec_dir);
@@ -438,9 +446,135 @@ int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_si
         man.has_shard = true;
         man.shard_size = chunk_size;
     }
+    if (plain_size >= 0) {
+        man.has_plain = true;
+        man.plaintext_size = uint64_t(plain_size);
+    }
     const std::string js = manifest_json(man);
     return write_file(dir / "manifest.json", reinterpret_cast<const uint8_t*>(js.data()), js.size());
 }
+
+// AES-256-GCM frame stream of `pt` under `key` (crypto.rs FrameEncryptor,
+// 64 KiB frames, first index 0), frame i's AAD = SHA-256(aad_prefix || i LE)
+// (build_frame_aad, filesystem.rs:118-128).
+int encrypt_frames(mxec_ctx* ctx, const uint8_t* key, const uint8_t* nonce_prefix, const uint8_t* aad_prefix,
+                   uint32_t aad_prefix_len, const uint8_t* pt, uint64_t len, std::vector<uint8_t>& ct) {
+    const uint64_t nf = (len + MXEC_FRAME_CHUNK_SIZE - 1) / MXEC_FRAME_CHUNK_SIZE;
+    ct.assign(size_t(mxec_frames_len(len, MXEC_FRAME_CHUNK_SIZE)), 0);
+    if (nf == 0) return MXEC_OK;
+    std::vector<uint8_t> aads(size_t(nf) * 32);
+    MXEC_TRY(mxec_frame_aads(ctx, aad_prefix, aad_prefix_len, 0, nf, reinterpret_cast<uint8_t(*)[32]>(aads.data())));
+    uint64_t n = 0;
+    MXEC_TRY(mxec_frames_encrypt(ctx, key, nonce_prefix, 0, aads.data(), 32, MXEC_FRAME_CHUNK_SIZE, pt, len,
+                                 ct.data(), ct.size(), &n));
+    ct.resize(size_t(n));
+    return MXEC_OK;
+}
+
+// The parts of a multipart upload concatenated in order (plaintext).  An
+// encrypted part is a frame stream under the upload key with AADs
+// SHA-256("PART" 0 upload_id 0 part_number_le4 0 || i LE) (part_aad_builder,
+// filesystem.rs:147-163), decrypted by FrameDecryptor (:1378-1388).
+int read_parts(mxec_ctx* ctx, const mxec_multipart_part* parts, uint32_t n_parts, const uint8_t* upload_key,
+               const char* upload_id, std::vector<uint8_t>& out) {
+    out.clear();
+    for (uint32_t p = 0; p < n_parts; ++p) {
+        const mxec_multipart_part& part = parts[p];
+        if (!part.path) return set_error(MXEC_E_INVALID_ARG, "null part path");
+        std::vector<uint8_t> raw;
+        MXEC_TRY(read_file(part.path, raw));
+        if (!part.encrypted) {
+            out.insert(out.end(), raw.begin(), raw.end());
+            continue;
+        }
+        if (!upload_key || !upload_id) return set_error(MXEC_E_INVALID_ARG, "encrypted part without upload key");
+        std::string prefix = std::string("PART") + '\0' + upload_id + '\0';
+        for (int b = 0; b < 4; ++b) prefix.push_back(char((part.part_number >> (8 * b)) & 0xFF));
+        prefix.push_back('\0');
+        const uint64_t nf = (part.size + MXEC_FRAME_CHUNK_SIZE - 1) / MXEC_FRAME_CHUNK_SIZE;
+        std::vector<uint8_t> aads(size_t(nf) * 32 + 32);
+        if (nf)
+            MXEC_TRY(mxec_frame_aads(ctx, reinterpret_cast<const uint8_t*>(prefix.data()), uint32_t(prefix.size()), 0,
+                                     nf, reinterpret_cast<uint8_t(*)[32]>(aads.data())));
+        const size_t at = out.size();
+        out.resize(at + size_t(part.size));
+        uint64_t n = 0;
+        MXEC_TRY(mxec_frames_decrypt(ctx, upload_key, 0, aads.data(), 32, MXEC_FRAME_CHUNK_SIZE, raw.data(),
+                                     raw.size(), part.size, out.data() + at, part.size, &n));
+        if (n != part.size) return set_error(MXEC_E_INTEGRITY, "part plaintext size mismatch");
+    }
+    return MXEC_OK;
+}
+
+// The multipart ETag (:1240-1244): MD5 over the parts' raw MD5s, "-N".
+int multipart_etag(mxec_ctx* ctx, const mxec_multipart_part* parts, uint32_t n_parts, char* etag_out) {
+    std::vector<uint8_t> md5s(size_t(n_parts) * 16 + 1);
+    for (uint32_t p = 0; p < n_parts; ++p) std::memcpy(&md5s[size_t(p) * 16], parts[p].md5, 16);
+    const uint8_t* b = md5s.data();
+    const uint64_t l = uint64_t(n_parts) * 16;
+    mxec_body_sums sums;
+    MXEC_TRY(mxec_body_sums_batch(ctx, &b, &l, 1, MXEC_SUM_MD5, &sums));
+    static const char* hx = "0123456789abcdef";
+    for (int i = 0; i < 16; ++i) {
+        etag_out[2 * i] = hx[sums.md5[i] >> 4];
+        etag_out[2 * i + 1] = hx[sums.md5[i] & 15];
+    }
+    std::snprintf(etag_out + 32, 16, "-%u", n_parts);
+    return MXEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
+                            const uint8_t* body, size_t len) {
+    return put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, body, len, -1);
+}
+
+int mxec_put_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
+                                      uint32_t parity_shards, const uint8_t key[32], const uint8_t nonce_prefix[4],
+                                      const uint8_t* aad_prefix, uint32_t aad_prefix_len, const uint8_t* body,
+                                      size_t len, uint32_t which, mxec_body_sums* sums_out) {
+    if (!key || !nonce_prefix || (len && !body) || (aad_prefix_len && !aad_prefix) || (which && !sums_out))
+        return set_error(MXEC_E_INVALID_ARG, "null argument");
+    std::vector<uint8_t> ct;
+    MXEC_TRY(encrypt_frames(ctx, key, nonce_prefix, aad_prefix, aad_prefix_len, body, len, ct));
+    MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, ct.data(), ct.size(), int64_t(len)));
+    if (!which) return MXEC_OK;
+    // Md5 / ChecksumHasher over the plaintext as it arrives (:878-884).
+    const uint8_t* b = body ? body : reinterpret_cast<const uint8_t*>("");
+    const uint64_t l = len;
+    return mxec_body_sums_batch(ctx, &b, &l, 1, which, sums_out);
+}
+
+int mxec_complete_multipart_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
+                                    uint32_t parity_shards, const mxec_multipart_part* parts, uint32_t n_parts,
+                                    char etag_out[48]) {
+    if ((n_parts && !parts) || !etag_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+    std::vector<uint8_t> body;
+    for (uint32_t p = 0; p < n_parts; ++p)
+        if (parts[p].encrypted) return set_error(MXEC_E_INVALID_ARG, "encrypted part: use the _encrypted driver");
+    MXEC_TRY(read_parts(ctx, parts, n_parts, nullptr, nullptr, body));
+    MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, body.data(), body.size(), -1));
+    return multipart_etag(ctx, parts, n_parts, etag_out);
+}
+
+int mxec_complete_multipart_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
+                                              uint32_t parity_shards, const mxec_multipart_part* parts,
+                                              uint32_t n_parts, const uint8_t upload_key[32], const char* upload_id,
+                                              const uint8_t key[32], const uint8_t nonce_prefix[4],
+                                              const uint8_t* aad_prefix, uint32_t aad_prefix_len,
+                                              char etag_out[48]) {
+    if ((n_parts && !parts) || !etag_out || !key || !nonce_prefix || (aad_prefix_len && !aad_prefix))
+        return set_error(MXEC_E_INVALID_ARG, "null argument");
+    std::vector<uint8_t> plain, ct;
+    MXEC_TRY(read_parts(ctx, parts, n_parts, upload_key, upload_id, plain));
+    MXEC_TRY(encrypt_frames(ctx, key, nonce_prefix, aad_prefix, aad_prefix_len, plain.data(), plain.size(), ct));
+    MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, ct.data(), ct.size(), int64_t(plain.size())));
+    return multipart_etag(ctx, parts, n_parts, etag_out);
+}
+
 
 int mxec_try_reconstruct_data_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t target, uint8_t* out,
                                     uint64_t out_cap, uint64_t* out_len) {

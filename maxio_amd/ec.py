@@ -350,6 +350,50 @@ class Context:
                                                       _ptr(a), a.size, which, ctypes.byref(r)))
         return put_result(_sums_dict(r, which), checksum_algo)
 
+    def put_object_chunked_encrypted(self, ec_dir: str, chunk_size: int, parity_shards: int, key: bytes,
+                                     nonce_prefix: bytes, aad_prefix: bytes, body,
+                                     checksum_algo: Optional[str] = None) -> dict:
+        """put_object_chunked_encrypted (filesystem.rs:835-1060): frames, chunks,
+        parity, manifest with plaintext_size; returns the PutResult digests."""
+        a, k, pre, ap = _u8(body), _u8(key), _u8(nonce_prefix), _u8(aad_prefix)
+        which = SUM_MD5 | (_SUM_BY_ALGO[checksum_algo] if checksum_algo else 0)
+        r = N.BodySums()
+        _check(self._lib.mxec_put_object_chunked_encrypted(
+            self._h, ec_dir.encode(), chunk_size, parity_shards, _ptr(k), _ptr(pre),
+            _ptr(ap) if ap.size else None, ap.size, _ptr(a), a.size, which, ctypes.byref(r)))
+        return put_result(_sums_dict(r, which), checksum_algo)
+
+    @staticmethod
+    def _parts(parts: Sequence[dict]):
+        arr = (N.MultipartPart * max(1, len(parts)))()
+        for i, p in enumerate(parts):
+            arr[i].path = p["path"].encode()
+            arr[i].size = p["size"]
+            arr[i].md5[:] = list(bytes.fromhex(p["etag"].strip('"')))
+            arr[i].part_number = p["part_number"]
+            arr[i].encrypted = 1 if p.get("encrypted") else 0
+        return arr
+
+    def complete_multipart_chunked(self, ec_dir: str, chunk_size: int, parity_shards: int,
+                                   parts: Sequence[dict]) -> str:
+        """complete_multipart_chunked (filesystem.rs:1147-1310); parts: dicts of
+        path, size, etag (hex), part_number.  Returns the quoted ETag."""
+        etag = ctypes.create_string_buffer(48)
+        _check(self._lib.mxec_complete_multipart_chunked(self._h, ec_dir.encode(), chunk_size, parity_shards,
+                                                         self._parts(parts), len(parts), etag))
+        return '"' + etag.value.decode() + '"'
+
+    def complete_multipart_chunked_encrypted(self, ec_dir: str, chunk_size: int, parity_shards: int,
+                                             parts: Sequence[dict], upload_key: bytes, upload_id: str,
+                                             key: bytes, nonce_prefix: bytes, aad_prefix: bytes) -> str:
+        """complete_multipart_chunked_encrypted (filesystem.rs:1315-1560)."""
+        etag = ctypes.create_string_buffer(48)
+        uk, k, pre, ap = _u8(upload_key), _u8(key), _u8(nonce_prefix), _u8(aad_prefix)
+        _check(self._lib.mxec_complete_multipart_chunked_encrypted(
+            self._h, ec_dir.encode(), chunk_size, parity_shards, self._parts(parts), len(parts), _ptr(uk),
+            upload_id.encode(), _ptr(k), _ptr(pre), _ptr(ap) if ap.size else None, ap.size, etag))
+        return '"' + etag.value.decode() + '"'
+
     # ---- encrypt-then-EC frames (storage/crypto.rs) ----------------------------
     def frames_encrypt(self, key: bytes, nonce_prefix: bytes, pt, aads: Optional[Sequence[bytes]] = None,
                        first_index: int = 0, frame_size: int = FRAME_CHUNK_SIZE) -> bytes:
