@@ -375,6 +375,19 @@ int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset,
                             uint64_t length, uint8_t* out, uint64_t out_cap,
                             uint64_t* out_len);
 
+/* GET / ranged GET of an encrypt-then-EC object (filesystem.rs:1618-1630,
+ * :1700-1725): the frames covering [offset, offset + length) of the
+ * plaintext (FrameDecryptor::ciphertext_offset / for_range) are read through
+ * the verified chunk reader, decrypted (AADs SHA-256(aad_prefix || i LE)) and
+ * the range copied to out.  frame_size = the object's encryption chunk_size;
+ * plaintext_size = ObjectMeta.size, or UINT64_MAX for the manifest's
+ * plaintext_size; length UINT64_MAX = to the end. */
+int mxec_get_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, const uint8_t key[32],
+                                      const uint8_t* aad_prefix, uint32_t aad_prefix_len,
+                                      uint32_t frame_size, uint64_t plaintext_size,
+                                      uint64_t offset, uint64_t length, uint8_t* out,
+                                      uint64_t out_cap, uint64_t* out_len);
+
 /* VerifiedChunkReader (chunk_reader.rs:12-276) as a pull stream.
  * mxec_reader_open = new (:35-49) when offset == 0 and length == UINT64_MAX,
  * with_range (:52-82) otherwise.  mxec_reader_read = poll_read (:228-276):

@@ -132,6 +132,8 @@ _SIGS = {
     "mxec_frame_aads": (INT, [P, P, ctypes.c_uint32, U64, U64, P]),
     "mxec_body_sums_batch_device": (INT, [P, INT, P, PP, U64P, U64, ctypes.c_uint32, P]),
     "mxec_get_object_chunked": (INT, [P, ctypes.c_char_p, U64, U64, P, U64, U64P]),
+    "mxec_get_object_chunked_encrypted": (INT, [P, ctypes.c_char_p, P, P, ctypes.c_uint32, ctypes.c_uint32, U64,
+                                                U64, U64, P, U64, U64P]),
     "mxec_try_reconstruct_data_chunk": (INT, [P, ctypes.c_char_p, ctypes.c_uint32, P, U64, U64P]),
     "mxec_reader_open": (INT, [P, ctypes.c_char_p, U64, U64, U64, ctypes.POINTER(ctypes.c_void_p)]),
     "mxec_reader_read": (ctypes.c_int64, [P, P, U64]),

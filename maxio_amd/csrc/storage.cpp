@@ -864,4 +864,44 @@ int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, 
     return MXEC_OK;
 }
 
+
+int mxec_get_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, const uint8_t key[32],
+                                      const uint8_t* aad_prefix, uint32_t aad_prefix_len, uint32_t frame_size,
+                                      uint64_t plaintext_size, uint64_t offset, uint64_t length, uint8_t* out,
+                                      uint64_t out_cap, uint64_t* out_len) {
+    if (!ec_dir || !key || !out_len || (aad_prefix_len && !aad_prefix))
+        return set_error(MXEC_E_INVALID_ARG, "null argument");
+    if (frame_size == 0 || frame_size % 16) return set_error(MXEC_E_INVALID_ARG, "frame_size must be a positive multiple of 16");
+    *out_len = 0;
+    Manifest man;
+    MXEC_TRY(read_manifest(ec_dir, man));
+    if (plaintext_size == UINT64_MAX) {
+        if (!man.has_plain) return set_error(MXEC_E_JSON, "JSON error: manifest has no plaintext_size");
+        plaintext_size = man.plaintext_size;
+    }
+    if (offset >= plaintext_size || length == 0) return MXEC_OK;
+    const uint64_t end = length == UINT64_MAX || length > plaintext_size - offset ? plaintext_size : offset + length;
+    // FrameDecryptor::ciphertext_offset / for_range: the frames that cover
+    // [offset, end), read through the verified chunk reader (with_range).
+    const uint64_t fl = uint64_t(frame_size) + MXEC_FRAME_OVERHEAD;
+    const uint64_t f0 = offset / frame_size, f1 = (end - 1) / frame_size;
+    const uint64_t ct_off = f0 * fl;
+    const uint64_t ct_len = std::min<uint64_t>(man.total_size - std::min(man.total_size, ct_off), (f1 - f0 + 1) * fl);
+    if (end - offset > out_cap || !out) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
+    std::vector<uint8_t> ct(size_t(ct_len) + 1);
+    uint64_t got = 0;
+    MXEC_TRY(mxec_get_object_chunked(ctx, ec_dir, ct_off, ct_len, ct.data(), ct_len, &got));
+    const uint64_t nf = f1 - f0 + 1;
+    const uint64_t pt_lo = f0 * frame_size, pt_hi = std::min<uint64_t>(plaintext_size, (f1 + 1) * uint64_t(frame_size));
+    std::vector<uint8_t> aads(size_t(nf) * 32);
+    MXEC_TRY(mxec_frame_aads(ctx, aad_prefix, aad_prefix_len, f0, nf, reinterpret_cast<uint8_t(*)[32]>(aads.data())));
+    std::vector<uint8_t> pt(size_t(pt_hi - pt_lo) + 1);
+    uint64_t n = 0;
+    MXEC_TRY(mxec_frames_decrypt(ctx, key, f0, aads.data(), 32, frame_size, ct.data(), got, pt_hi - pt_lo, pt.data(),
+                                 pt.size(), &n));
+    std::memcpy(out, pt.data() + (offset - pt_lo), size_t(end - offset));
+    *out_len = end - offset;
+    return MXEC_OK;
+}
+
 }  // extern "C"

@@ -320,6 +320,28 @@ class Context:
             out.ctypes.data, capacity, ctypes.byref(n)))
         return out[: n.value].tobytes()
 
+    def get_object_chunked_encrypted(self, ec_dir: str, key: bytes, aad_prefix: bytes, offset: int = 0,
+                                     length: Optional[int] = None, plaintext_size: Optional[int] = None,
+                                     frame_size: int = 65536) -> bytes:
+        """GET / ranged GET of an encrypt-then-EC object (FrameDecryptor over
+        VerifiedChunkReader, filesystem.rs:1618-1630, 1700-1725)."""
+        import json
+        import os
+
+        if plaintext_size is None:
+            with open(os.path.join(ec_dir, "manifest.json")) as f:
+                cap = int(json.load(f).get("plaintext_size", 0))
+        else:
+            cap = plaintext_size
+        out = np.zeros(max(1, cap), np.uint8)
+        n = ctypes.c_uint64(0)
+        k, ap = _u8(key), _u8(aad_prefix)
+        _check(self._lib.mxec_get_object_chunked_encrypted(
+            self._h, ec_dir.encode(), _ptr(k), _ptr(ap) if ap.size else None, ap.size, frame_size,
+            (1 << 64) - 1 if plaintext_size is None else plaintext_size, offset,
+            (1 << 64) - 1 if length is None else length, out.ctypes.data, cap, ctypes.byref(n)))
+        return out[: n.value].tobytes()
+
     def open_reader(self, ec_dir: str, offset: int = 0, length: Optional[int] = None,
                     batch_bytes: int = 0) -> "ChunkReader":
         return ChunkReader(self, ec_dir, offset, length, batch_bytes)
