@@ -700,7 +700,7 @@ def main() -> int:
     torch.cuda.empty_cache()
 
     if rank == 0:
-        tag = {"2": "k4m2", "sums": "crc_tiles", "frames": "gcm_frames"}.get(args.config)
+        tag = {"2": "k4m2", "ns": "k8m4", "sums": "crc_tiles", "frames": "gcm_frames"}.get(args.config)
         traffic, tsrc = pmc_traffic(tag, w.alg_bytes) if tag else (None, None)
         line = {
             "metric": METRIC,

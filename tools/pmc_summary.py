@@ -4,7 +4,7 @@
 FETCH_SIZE counts half the bytes of a wide coalesced streaming read, so read
 bytes = 2 x FETCH_SIZE KiB x 1024; WRITE_SIZE is exact.
 
-  python tools/pmc_summary.py <fetch_dir> <write_dir> <kernel-substring> <alg_bytes_per_launch> [--out f.json]
+  python tools/pmc_summary.py <fetch_dir|csv> <write_dir|csv> <kernel-substring> <alg_bytes_per_launch> [--out f.json]
 """
 from __future__ import annotations
 
@@ -17,7 +17,8 @@ import os
 
 def per_launch(d: str, counter: str, kernel: str) -> tuple[float, int]:
     vals = []
-    for path in glob.glob(os.path.join(d, "*counter_collection.csv")):
+    paths = [d] if os.path.isfile(d) else glob.glob(os.path.join(d, "*counter_collection.csv"))
+    for path in paths:
         with open(path) as f:
             for r in csv.DictReader(f):
                 if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
