@@ -210,3 +210,22 @@ def test_k1_parity_is_copy():
     d = data_for(3, 1, 4096)
     parity = oracle.encode(d, 2)
     assert all(np.array_equal(p, d[0]) for p in parity)
+
+
+def test_expected_layout_helper_matches_golden_scenarios(golden):
+    """tests/helpers.expected_ec_object (the reference layout the driver tests
+    compare against) reproduces every committed reference scenario: file
+    names, sizes, parity bytes and the to_string_pretty manifest text."""
+    from helpers import expected_ec_object, scenario_body
+
+    for name, sc in golden("reference_scenarios.json").items():
+        if not isinstance(sc, dict):
+            continue  # "source" note
+        body = scenario_body(sc["body"])
+        files, manifest = expected_ec_object(body, sc["chunk_size"], sc["parity_shards"])
+        assert manifest == sc["manifest"], name
+        assert sorted(files) == sorted(sc["files"]), name
+        for fname, meta in sc["files"].items():
+            assert len(files[fname]) == meta["size"], (name, fname)
+            if "hex" in meta:
+                assert files[fname].hex() == meta["hex"], (name, fname)
