@@ -110,6 +110,47 @@ __global__ __launch_bounds__(256) void k_pattern_tile(const uint8_t* __restrict_
         }
     }
 }
+// The same 4-read : 2-write pattern with the reads as LDS-DMA (nontemporal
+// policy) into a per-wave D-stage ring.  A wave owns a contiguous run of
+// `run` 1-KiB column blocks of one object (pointers stay in SGPRs); each
+// iteration issues the 4 loads of block t+D-1, waits for block t with the
+// constant count vmcnt(6(D-1)) (every iteration issues 4 loads + 2 stores and
+// the counter retires in issue order), XORs it out of LDS and stores.
+template <int D>
+__global__ __launch_bounds__(64) void k_pattern_glds(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                     uint64_t S, uint64_t n_obj, uint32_t run) {
+    __shared__ u32x4 ring[D][4][64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t bpo = S / 1024, runs_per_obj = bpo / run, n_runs = runs_per_obj * n_obj;
+    for (uint64_t r = blockIdx.x; r < n_runs; r += gridDim.x) {
+        const uint64_t o = r / runs_per_obj, b0 = (r - o * runs_per_obj) * run;
+        const uint8_t* in0 = data + (o * 4) * S + lane * 16;
+        uint8_t* out0 = par + (o * 2) * S + lane * 16;
+        auto issue = [&](uint64_t b, int slot) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_global_load_lds(
+                    (const void __attribute__((address_space(1)))*)(in0 + j * S + b * 1024),
+                    (void __attribute__((address_space(3)))*)&ring[slot][j][0], 16, 0, 2);
+        };
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d) issue(b0 + d, d);
+        for (uint32_t t = 0; t < run; ++t) {
+            const uint64_t b = b0 + t;
+            if (t + D - 1 < run) {
+                issue(b + D - 1, int((t + D - 1) % D));
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * (D - 1)) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const int slot = int(t % D);
+            const u32x4 p = ring[slot][0][lane] ^ ring[slot][1][lane] ^ ring[slot][2][lane] ^ ring[slot][3][lane];
+            __builtin_nontemporal_store(p, reinterpret_cast<u32x4*>(out0 + b * 1024));
+            __builtin_nontemporal_store(p + 1u, reinterpret_cast<u32x4*>(out0 + S + b * 1024));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
 // RS access pattern without the math: object o, 16-B column c: read k shards,
 // write m shards (XOR of inputs), same layout as the bench.
 __global__ __launch_bounds__(256) void k_pattern(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
@@ -247,6 +288,17 @@ int main(int argc, char** argv) {
                 std::snprintf(nm, sizeof nm, "read_glds_nt_bpc%d", bpc);
                 ms = tm.median_ms([&] { hipLaunchKernelGGL(k_read_glds<2>, dim3(cus * bpc), dim3(256), 0, 0, s, d, nvec); });
                 report(nm, "pool", ms, 16.0 * nvec);
+            }
+            for (int wpc : {8, 16, 32}) {
+                for (uint32_t run : {16u, 64u}) {
+                    char nm[96];
+                    std::snprintf(nm, sizeof nm, "pattern_glds_d3_wpc%d_run%u", wpc, run);
+                    double ms = tm.median_ms([&] { hipLaunchKernelGGL(k_pattern_glds<3>, dim3(cus * wpc), dim3(64), 0, 0, buf, buf + n2 * 4 * S2, S2, n2, run); });
+                    report(nm, "k4m2 S10MiB", ms, double(n2) * 6 * S2);
+                    std::snprintf(nm, sizeof nm, "pattern_glds_d5_wpc%d_run%u", wpc, run);
+                    ms = tm.median_ms([&] { hipLaunchKernelGGL(k_pattern_glds<5>, dim3(cus * wpc), dim3(64), 0, 0, buf, buf + n2 * 4 * S2, S2, n2, run); });
+                    report(nm, "k4m2 S10MiB", ms, double(n2) * 6 * S2);
+                }
             }
             for (int bpc : {8, 16, 32}) {
                 char nm[64];
