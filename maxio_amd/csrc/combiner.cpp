@@ -13,8 +13,11 @@
 // combining, no service thread).  A request waits at most for the batch in
 // flight plus its own, and a batch of N requests costs about one request's
 // latency.
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 
 #include "ops.hpp"
 
@@ -33,6 +36,7 @@ struct ShaCombiner {
     std::condition_variable cv;
     std::vector<Req*> pending;
     bool busy = false;
+    size_t last_batch = 1;  // requests in the previous launch
     Slot slot;  // private stream, descriptor ring and digest buffers
     uint64_t batches = 0, messages = 0;
 
@@ -56,7 +60,12 @@ struct ShaCombiner {
         if (n == 0) return MXEC_OK;
         hipStream_t s = slot.stream;
         MXEC_TRY(slot.digests.ensure(n * 32));
-        MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
+        // The split (producer / consumer) form at every size: a combined
+        // batch is usually several chip-filling requests, and two waves per
+        // 64 messages spread over the SIMDs more evenly than one (a batch
+        // ends with its most loaded SIMD).
+        MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr, nullptr,
+                         nullptr, 2));
         MXEC_TRY(slot.hdig.ensure(n * 32));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
         MXEC_HIP(hipStreamSynchronize(s));
@@ -73,11 +82,37 @@ struct ShaCombiner {
     }
 };
 
-// Requests with at least this many messages are not combined.
-constexpr size_t kCombineBelow = 8192;
-bool sha_combines(size_t n) { return n < kCombineBelow; }
+// Every request is combined by default, chip-filling ones too: eight
+// concurrent 10 240-message batches (config 3c) ran 1.34x faster as one
+// split-form launch than as eight launches on eight streams
+// (profiles/r1_bench_cfg3c_w8_combine_below_*.json).  MXEC_COMBINE_BELOW=n
+// sends requests of n or more messages to their own launch on the caller's
+// stream instead.
+bool sha_combines(size_t n) {
+    static const size_t below = [] {
+        const char* e = getenv("MXEC_COMBINE_BELOW");
+        return e ? size_t(strtoull(e, nullptr, 10)) : size_t(0);
+    }();
+    return below == 0 || n < below;
+}
 
 namespace {
+
+// MXEC_GATHER_US: how long a lone leader waits for company (default 100 us);
+// MXEC_GATHER_MAX_US: the bound when waiting for the previous batch size
+// (default 2 ms).
+long env_us(const char* name, long dflt) {
+    const char* e = getenv(name);
+    return e ? long(strtol(e, nullptr, 10)) : dflt;
+}
+long gather_us() {
+    static const long us = env_us("MXEC_GATHER_US", 100);
+    return us;
+}
+long gather_max_us() {
+    static const long us = env_us("MXEC_GATHER_MAX_US", 2000);
+    return us;
+}
 
 ShaCombiner* combiner_of(Device& d) {
     std::lock_guard<std::mutex> g(d.comb_mu);
@@ -116,14 +151,28 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     me.out = out;
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&me);
+    if (c->busy) c->cv.notify_all();  // a gathering leader may be waiting for us
     while (!me.done) {
         if (c->busy) {
             c->cv.wait(lk);
             continue;
         }
         c->busy = true;
+        // Adaptive gathering: a leader waits (bounded) until as many requests
+        // are pending as the previous launch carried, so a steady stream of
+        // concurrent callers keeps landing in one launch instead of splitting
+        // into a lone first request and the rest; a lone leader waits a short
+        // window.  A launch lasts >= 1.8 us per 64-byte block of its longest
+        // message (29 ms per 1 MiB chunk), so the wait costs a few percent at
+        // most, and the previous size is forgotten as soon as fewer come.
+        const size_t want = c->last_batch;
+        const long wait_us = want > 1 ? gather_max_us() : gather_us();
+        if (c->pending.size() < std::max<size_t>(want, 2) && wait_us > 0)
+            c->cv.wait_for(lk, std::chrono::microseconds(wait_us),
+                           [&] { return c->pending.size() >= std::max<size_t>(want, 2); });
         std::vector<ShaCombiner::Req*> batch;
         batch.swap(c->pending);
+        c->last_batch = batch.size();
         lk.unlock();
         int rc = MXEC_OK;
         try {

@@ -171,7 +171,7 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
 
 int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
             const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
-            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx, DescArena* arena) {
+            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx, DescArena* arena, int form) {
     (void)dev;
     const size_t n = ptrs.size();
     if (!n) return MXEC_OK;
@@ -193,6 +193,7 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     a.exp_idx = exp_idx ? reinterpret_cast<const uint64_t*>(db + o_e) : nullptr;
     a.ok = ok_dev;
     a.n = uint32_t(n);
+    a.force = form;
     MXEC_HIP(launch_sha256(a, s));
     return w.finish(s);
 }

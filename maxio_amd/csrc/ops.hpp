@@ -32,7 +32,7 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
 int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
             const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
             uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx = nullptr,
-            DescArena* arena = nullptr);
+            DescArena* arena = nullptr, int form = 0);
 
 // SHA-256 digests (host out, n * 32 bytes) of n device-resident messages on
 // `dev`, blocking; the caller's work on `s` must have produced them (the

@@ -264,6 +264,7 @@ int main(int argc, char** argv) {
     // `kernel_lab N sha` runs the SHA-256 section only; `kernel_lab N hbm`
     // the load-form ceilings, the tile-order sweep and the SHA split form.
     const bool sha_only = argc > 2 && !std::strcmp(argv[2], "sha");
+    const bool sha_big = argc > 2 && !std::strcmp(argv[2], "shabig");
     const bool hbm_only = argc > 2 && !std::strcmp(argv[2], "hbm");
     // ---- calibration ----
     if (hbm_only) {
@@ -317,7 +318,7 @@ int main(int argc, char** argv) {
             report("copy_bpc16", "2x half pool", ms, 32.0 * half);
         }
     }
-    if (!sha_only && !hbm_only) {
+    if (!sha_only && !hbm_only && !sha_big) {
         const uint64_t half = pool / 2 / 16;
         auto* s = reinterpret_cast<const u32x4*>(buf);
         auto* d = reinterpret_cast<u32x4*>(buf + pool / 2);
@@ -411,6 +412,18 @@ int main(int argc, char** argv) {
                     ms * 1e3 / (L / 64.0));
         CK(hipFree(d));
     };
+    if (sha_big) {
+        // Many 1 MiB messages (combined GET verification): forms by batch size.
+        for (uint64_t n : {20480ull, 32768ull, 40960ull, 57344ull}) {
+            char nm[96];
+            std::snprintf(nm, sizeof nm, "%llu x 1 MiB split form", (unsigned long long)n);
+            sha(n, 1ull << 20, nm, 2);
+            std::snprintf(nm, sizeof nm, "%llu x 1 MiB one-wave form", (unsigned long long)n);
+            sha(n, 1ull << 20, nm, 1);
+        }
+        CK(hipFree(buf));
+        return 0;
+    }
     if (hbm_only) {
         sweep(Shape{4, 2, S2, n2}, "k4m2 S10MiB (cfg2)", true);
         sweep(Shape{8, 4, 1ull << 20, n2 * 60 / 12}, "k8m4 S1MiB (north star)", true);
