@@ -226,15 +226,20 @@ __device__ __forceinline__ void store16_be(uint8_t* p, u32x4 v) {
 // indices otherwise serialise on bank conflicts).  The extraction +
 // lane-bank address was two VALU per lookup before (byte extract, shift-add).
 // The tables occupy LDS bytes [0, 128 KiB) (the dynamic LDS block starts at
-// address 0: the kernel has no static __shared__); then one H^256 table and
-// reduction slots per frame group.
+// address 0: the kernel has no static __shared__); then one H^256 table per
+// frame group.
 #ifndef GCM_GROUPS
-#define GCM_GROUPS 3
+#define GCM_GROUPS 4
 #endif
 constexpr uint32_t kTeCopies = 32;
 constexpr uint32_t kGcmGroups = GCM_GROUPS;  // frames in flight per workgroup, 256 threads each
 constexpr size_t kTeWords = 4 * 256 * kTeCopies;
-constexpr size_t kGcmLdsBytes = kTeWords * 4 + kGcmGroups * (32 * 16 + 4) * sizeof(u32x4);
+// Per group: the 32 x 16 position table of H^256 (8 KiB).  Its entries
+// [p][0] (nibble 0 times anything) are zero; the workgroup's cross-wave XOR
+// reduction borrows [0..3][0] and puts the zeros back before the next frame,
+// so four groups (1 024 threads, four waves per SIMD) fit in 160 KiB.
+constexpr size_t kGcmLdsBytes = kTeWords * 4 + kGcmGroups * (32 * 16) * sizeof(u32x4);
+static_assert(kGcmLdsBytes <= 160 * 1024, "GCM LDS image exceeds 160 KiB");
 
 typedef const uint32_t __attribute__((address_space(3)))* lds_u32p;
 
@@ -246,8 +251,8 @@ __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a)
     if (size_t((lds_u32p)(smem)) != 0) __builtin_trap();
     u32x4* gbase = reinterpret_cast<u32x4*>(smem + kTeWords);
     const uint32_t g = threadIdx.x >> 8, lane = threadIdx.x & 255;
-    u32x4 (*htab)[16] = reinterpret_cast<u32x4 (*)[16]>(gbase + g * (32 * 16 + 4));
-    u32x4* red = gbase + g * (32 * 16 + 4) + 32 * 16;
+    u32x4 (*htab)[16] = reinterpret_cast<u32x4 (*)[16]>(gbase + g * (32 * 16));
+    auto red = [htab](int q) -> u32x4& { return htab[q][0]; };  // the zero entries, borrowed
     // word t = pair << 14 | x << 6 | tsel << 5 | copy  ->  Te_{2 pair + tsel}[x]
     for (uint32_t t = threadIdx.x; t < kTeWords; t += blockDim.x)
         te[t] = a.te[((t >> 14) * 2 + ((t >> 5) & 1)) * 256 + ((t >> 6) & 255)];
@@ -271,6 +276,8 @@ __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a)
         if (live && int64_t(fr.key) != cur_key) {  // a new object's H^256 table
             for (uint32_t t = lane; t < 32 * 16; t += 256) (&htab[0][0])[t] = key->htab[t / 16][t % 16];
             cur_key = fr.key;
+        } else if (lane < 4) {
+            htab[lane][0] = u32x4{0u, 0u, 0u, 0u};  // return the reduction slots
         }
         __syncthreads();
         const uint32_t* rk = key->rk;
@@ -375,11 +382,14 @@ __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a)
             acc.z ^= __shfl_xor(acc.z, s);
             acc.w ^= __shfl_xor(acc.w, s);
         }
-        if ((lane & 63) == 0) red[lane >> 6] = acc;
+        if ((lane & 63) == 0) red(int(lane >> 6)) = acc;
         __syncthreads();
         if (live && lane == 0) {
-            u32x4 y = red[0];
-            for (int q = 1; q < 4; ++q) y = u32x4{y.x ^ red[q].x, y.y ^ red[q].y, y.z ^ red[q].z, y.w ^ red[q].w};
+            u32x4 y = red(0);
+            for (int q = 1; q < 4; ++q) {
+                const u32x4 rq = red(q);
+                y = u32x4{y.x ^ rq.x, y.y ^ rq.y, y.z ^ rq.z, y.w ^ rq.w};
+            }
             uint32_t s0 = n0, s1 = n1, s2 = n2, s3 = 1u;
             aes_block(lk, rk, s0, s1, s2, s3);
             const u32x4 tag = {s0 ^ y.x, s1 ^ y.y, s2 ^ y.z, s3 ^ y.w};
@@ -401,8 +411,8 @@ __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a)
 
 hipError_t launch_gcm_frames(const GcmArgs& a, bool decrypt, int n_cus, hipStream_t s) {
     if (a.n_frames == 0) return hipSuccess;
-    // 128 KiB of T-tables + 8.06 KiB per frame group (155 KiB at three groups):
-    // one workgroup (three frames, 12 waves) per CU.
+    // 128 KiB of T-tables + 8 KiB per frame group (160 KiB at four groups):
+    // one workgroup (four frames, 16 waves) per CU.
     static const hipError_t attr = [] {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gcm_frames_kernel<true>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, int(kGcmLdsBytes));
