@@ -38,7 +38,7 @@ struct ShaCombiner {
     bool busy = false;
     size_t last_batch = 1;  // requests in the previous launch
     Slot slot;  // private stream, descriptor ring and digest buffers
-    uint64_t batches = 0, messages = 0;
+    uint64_t batches = 0, messages = 0;  // guarded by mu
 
     ~ShaCombiner() {
         if (slot.stream) (void)hipStreamSynchronize(slot.stream);
@@ -76,8 +76,6 @@ struct ShaCombiner {
             std::memcpy(r->out, h + o * 32, k * 32);
             o += k;
         }
-        ++batches;
-        messages += n;
         return MXEC_OK;
     }
 };
@@ -182,6 +180,10 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         }
         const std::string msg = rc ? std::string(last_error()) : std::string();
         lk.lock();
+        if (rc == MXEC_OK) {
+            ++c->batches;
+            for (const auto* r : batch) c->messages += r->ptrs->size();
+        }
         for (auto* r : batch) {
             r->rc = rc;
             r->msg = msg;
@@ -195,10 +197,17 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
 }
 
 void combiner_stats(Device& d, uint64_t* batches, uint64_t* messages) {
-    std::lock_guard<std::mutex> g(d.comb_mu);
-    auto* c = static_cast<ShaCombiner*>(d.comb.get());
-    *batches = c ? c->batches : 0;
-    *messages = c ? c->messages : 0;
+    std::shared_ptr<void> keep;
+    {
+        std::lock_guard<std::mutex> g(d.comb_mu);
+        keep = d.comb;
+    }
+    auto* c = static_cast<ShaCombiner*>(keep.get());
+    *batches = *messages = 0;
+    if (!c) return;
+    std::lock_guard<std::mutex> g(c->mu);
+    *batches = c->batches;
+    *messages = c->messages;
 }
 
 }  // namespace mxec
