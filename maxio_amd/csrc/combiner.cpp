@@ -128,10 +128,8 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
                     const std::vector<uint64_t>& lens, uint8_t* out) {
     if (ptrs.empty()) return MXEC_OK;
     if (!sha_combines(ptrs.size())) {
-        // Enough messages to fill the chip's SIMDs on its own (bench config 3:
-        // 10 240): its own launch on the caller's stream.  Folded into other
-        // large requests it would only cross the one-wave-per-SIMD line and
-        // make every message of the batch wait for the SIMDs that got two.
+        // Opted out by MXEC_COMBINE_BELOW: its own launch on the caller's
+        // stream (the kernel picks its form by message count).
         const size_t n = ptrs.size();
         MXEC_TRY(slot.digests.ensure(n * 32));
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
