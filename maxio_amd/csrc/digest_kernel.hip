@@ -341,13 +341,7 @@ __global__ __launch_bounds__(256) void crc_tiles_kernel(CrcArgs a) {
     const uint32_t poly = tb->poly;
     __syncthreads();
     for (uint64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-        // Body of this tile: the last body whose first tile is <= tile.
-        uint32_t lo = 0, hi = a.n_bodies - 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) / 2;
-            if (a.bodies[mid].tile0 <= tile) lo = mid; else hi = mid - 1;
-        }
-        const CrcBody bd = a.bodies[lo];
+        const CrcBody bd = a.bodies[a.tile_body[tile]];  // host-built tile -> body map
         const uint64_t t_in = tile - bd.tile0;
         // Virtual unit index of row r, lane L: t_in * kCrcRows * 256 + r * 256 + L;
         // real unit = virtual - pad (pad = leading virtual zero units).

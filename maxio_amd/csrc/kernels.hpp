@@ -99,6 +99,7 @@ struct CrcBody {
 struct CrcArgs {
     const CrcTables* tables;
     const CrcBody* bodies;  // [n_bodies], tile0 ascending
+    const uint32_t* tile_body;  // [n_tiles] body of each tile
     uint32_t* tile_crc;     // [n_tiles] scratch
     uint8_t* out;           // finished CRC of body b at out + b * out_stride
     uint64_t out_stride;

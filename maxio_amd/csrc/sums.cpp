@@ -132,15 +132,23 @@ int run_body_sums(Device& d, Slot& slot, hipStream_t s, const std::vector<const 
         bodies[i] = crc_body(ptrs[i], lens[i], tiles);
         tiles += bodies[i].n_tiles;
     }
-    size_t o_body = 0, o_tiles = 0;
+    size_t o_body = 0, o_tiles = 0, o_tb = 0;
     if (!polys.empty()) {
         o_body = w.add(n * sizeof(CrcBody));
         o_tiles = w.add(std::max<uint64_t>(1, tiles) * sizeof(uint32_t) * polys.size());
+        o_tb = w.add(std::max<uint64_t>(1, tiles) * sizeof(uint32_t));
     }
     std::memcpy(w.data() + o_ptr, ptrs.data(), n * sizeof(void*));
     std::memcpy(w.data() + o_len, lens.data(), n * sizeof(uint64_t));
     if (!algs.empty()) std::memcpy(w.data() + o_alg, algs.data(), algs.size() * sizeof(uint32_t));
-    if (!polys.empty()) std::memcpy(w.data() + o_body, bodies.data(), n * sizeof(CrcBody));
+    if (!polys.empty()) {
+        std::memcpy(w.data() + o_body, bodies.data(), n * sizeof(CrcBody));
+        // tile -> body, so a workgroup finds its body with one load instead
+        // of a search of dependent loads per tile.
+        auto* tb = reinterpret_cast<uint32_t*>(w.data() + o_tb);
+        for (size_t i = 0; i < n; ++i)
+            for (uint64_t t = 0; t < bodies[i].n_tiles; ++t) tb[bodies[i].tile0 + t] = uint32_t(i);
+    }
     char* dev = nullptr;
     MXEC_TRY(w.commit(s, &dev));
     if (!polys.empty()) {
@@ -150,6 +158,7 @@ int run_body_sums(Device& d, Slot& slot, hipStream_t s, const std::vector<const 
             CrcArgs a{};
             a.tables = tab + polys[q];
             a.bodies = reinterpret_cast<const CrcBody*>(dev + o_body);
+            a.tile_body = reinterpret_cast<const uint32_t*>(dev + o_tb);
             a.tile_crc = reinterpret_cast<uint32_t*>(dev + o_tiles) + q * std::max<uint64_t>(1, tiles);
             a.out = out_dev + (polys[q] == 0 ? offsetof(mxec_body_sums, crc32) : offsetof(mxec_body_sums, crc32c));
             a.out_stride = stride;
