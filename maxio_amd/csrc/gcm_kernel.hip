@@ -382,6 +382,10 @@ __global__ __launch_bounds__(256 * kGcmGroups) void gcm_frames_kernel(GcmArgs a)
             acc.z ^= __shfl_xor(acc.z, s);
             acc.w ^= __shfl_xor(acc.w, s);
         }
+        // The reduction slots are H^256-table entries that slower waves of
+        // this frame may still be reading in their folds: every wave of the
+        // workgroup is past its folds before any slot is written.
+        __syncthreads();
         if ((lane & 63) == 0) red(int(lane >> 6)) = acc;
         __syncthreads();
         if (live && lane == 0) {

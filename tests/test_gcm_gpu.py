@@ -121,3 +121,31 @@ def test_device_batch_many_objects(ctx):
         if first != 2:
             got = bufs[-len(back_jobs) + first][:len(pt)].cpu().numpy().tobytes()
             assert got == pt
+
+
+def test_device_batch_full_chip_every_frame(ctx):
+    """Enough frames to keep every workgroup busy for many iterations (the
+    bench's shape, scaled down): 48 objects x 41 frames with per-frame AADs,
+    every frame of every object compared with the oracle.  Catches races
+    between a workgroup's waves (they drift apart over a long grid-stride)."""
+    import torch
+
+    n_obj, n = 48, 40 * FS + 1234
+    rng = np.random.default_rng(7)
+    nfr = (n + FS - 1) // FS
+    pt = torch.randint(0, 256, (n_obj, n), dtype=torch.uint8, device="cuda")
+    fl = oracle.frames_len(n)
+    fr = torch.zeros((n_obj, fl), dtype=torch.uint8, device="cuda")
+    aad = torch.from_numpy(rng.integers(0, 256, (n_obj, nfr, 32), dtype=np.uint8)).cuda()
+    keys = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(n_obj)]
+    jobs = [{"key": keys[o], "nonce_prefix": bytes([o, 1, 2, 3]), "aad_dev": aad[o].data_ptr(), "aad_len": 32,
+             "in_dev": pt[o].data_ptr(), "len": n, "out_dev": fr[o].data_ptr()} for o in range(n_obj)]
+    for _ in range(2):  # twice: the second run starts with warm tables and clocks
+        fr.zero_()
+        ctx.frames_device(jobs)
+        torch.cuda.synchronize()
+        host_pt, host_fr, host_aad = pt.cpu().numpy(), fr.cpu().numpy(), aad.cpu().numpy()
+        for o in range(n_obj):
+            want = oracle.frames_encrypt(keys[o], bytes([o, 1, 2, 3]), host_pt[o],
+                                         [bytes(x) for x in host_aad[o]])
+            assert host_fr[o].tobytes() == want, o
