@@ -317,7 +317,17 @@ class Mixed:
             assert rc == 0
 
     def spot_check(self):
-        return None
+        """The last object of every class after the steps: its parity equals
+        the oracle's encode of its (short-last-chunk) data."""
+        import numpy as np
+
+        oracle = _oracle()
+        for (k, m, S, n, t, dl, pres) in self.classes:
+            h = t[n - 1].cpu().numpy()
+            want = oracle.encode([h[j][:dl[j]] for j in range(k)], m, S)
+            if not all(np.array_equal(h[k + i], want[i]) for i in range(m)):
+                return False
+        return True
 
     def cpu_work(self):
         return None
