@@ -139,3 +139,16 @@ def test_get_object_chunked_encrypted_ranges(ctx, tmp_path):
     # the wrong identity (another key's AAD) fails authentication
     with pytest.raises(maxio_amd.RSError):
         ctx.get_object_chunked_encrypted(ec, key, oracle.object_aad_prefix("bkt", "other", "v7"))
+
+
+def test_multipart_errors(ctx, tmp_path):
+    """A missing part file is an IO error; an encrypted part without the
+    upload key is refused; the plain driver refuses encrypted parts."""
+    parts, _ = _write_parts(tmp_path, [1000, 2000], 90)
+    parts.append({"path": str(tmp_path / "nope"), "size": 5, "etag": "00" * 16, "part_number": 3})
+    with pytest.raises(maxio_amd.RSError) as e:
+        ctx.complete_multipart_chunked(str(tmp_path / "a.ec"), 4096, 2, parts)
+    assert e.value.code == -40 and e.value.name == "Io"
+    enc = [dict(parts[0], encrypted=True)]
+    with pytest.raises(maxio_amd.RSError):
+        ctx.complete_multipart_chunked(str(tmp_path / "b.ec"), 4096, 2, enc)
