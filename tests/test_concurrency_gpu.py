@@ -1,0 +1,89 @@
+"""GPU: many host threads drive every kind of request through ONE context at
+once — PUT, healthy / degraded / ranged GET, encrypted PUT + GET, multipart
+completion, raw SHA-256 batches and device-batch reconstructs — as MaxIO's
+tokio workers would; every result is checked.  Exercises slot locking, the
+SHA-256 combiner and the per-device caches under contention."""
+from __future__ import annotations
+
+import hashlib
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import maxio_amd
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _job(ctx, base, t):
+    rng = np.random.default_rng(500 + t)
+    kind = t % 6
+    d = os.path.join(base, f"t{t}")
+    if kind == 0:  # PUT + degraded GET
+        n = int(rng.integers(1, 3 << 20))
+        body = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        ctx.put_object_chunked(d + ".ec", 1 << 18, 2, body)
+        k = (n + (1 << 18) - 1) >> 18
+        os.unlink(os.path.join(d + ".ec", f"{int(rng.integers(0, k)):06}"))
+        return ctx.get_object_chunked(d + ".ec") == body
+    if kind == 1:  # PUT + ranged reads through the streaming reader
+        n = int(rng.integers(100_000, 2 << 20))
+        body = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        ctx.put_object_chunked(d + ".ec", 65536, 3, body)
+        off, ln = int(rng.integers(0, n)), int(rng.integers(1, 300_000))
+        with ctx.open_reader(d + ".ec", off, ln, batch_bytes=1 << 18) as r:
+            got = b""
+            while True:
+                piece = r.read(77_777)
+                if not piece:
+                    break
+                got += piece
+        return got == body[off:off + ln]
+    if kind == 2:  # encrypted PUT + ranged GET
+        key, pre = rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), b"CONC"
+        idp = oracle.object_aad_prefix("b", f"k{t}", None)
+        n = int(rng.integers(1, 400_000))
+        body = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        ctx.put_object_chunked_encrypted(d + ".ec", 100_000, 2, key, pre, idp, body)
+        off = int(rng.integers(0, n))
+        return ctx.get_object_chunked_encrypted(d + ".ec", key, idp, off, 5000) == body[off:off + 5000]
+    if kind == 3:  # SHA-256 batches of odd lengths
+        bufs = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in rng.integers(0, 90_000, 9)]
+        return ctx.sha256(bufs) == [hashlib.sha256(b).digest() for b in bufs]
+    if kind == 4:  # host encode / reconstruct with verification
+        k, m, s = 6, 3, 70_001
+        data = [rng.integers(0, 256, s, dtype=np.uint8) for _ in range(k)]
+        parity, dig = ctx.encode(data, m, s)
+        shards = [x.tobytes() for x in data] + [p.tobytes() for p in parity]
+        inp = list(shards)
+        inp[1] = None
+        inp[7] = bytes(s)  # corrupt: caught by the digest
+        out, present = ctx.reconstruct(inp, k, m, s, expected=dig)
+        return present.all() and out[1].tobytes() == shards[1] and out[7].tobytes() == shards[7]
+    # multipart completion
+    sizes = [int(x) for x in rng.integers(1, 200_000, 3)]
+    parts = []
+    whole = b""
+    for i, sz in enumerate(sizes):
+        b = rng.integers(0, 256, sz, dtype=np.uint8).tobytes()
+        p = f"{d}.part{i}"
+        with open(p, "wb") as f:
+            f.write(b)
+        parts.append({"path": p, "size": sz, "etag": hashlib.md5(b).hexdigest(), "part_number": i + 1})
+        whole += b
+    etag = ctx.complete_multipart_chunked(d + ".mp", 65536, 2, parts)
+    raw = b"".join(bytes.fromhex(p["etag"]) for p in parts)
+    return etag == f'"{hashlib.md5(raw).hexdigest()}-3"' and ctx.get_object_chunked(d + ".mp") == whole
+
+
+def test_mixed_requests_many_threads(tmp_path):
+    ctx = maxio_amd.Context(streams_per_device=16)
+    try:
+        with ThreadPoolExecutor(24) as pool:
+            results = list(pool.map(lambda t: _job(ctx, str(tmp_path), t), range(96)))
+        assert all(results), [i for i, r in enumerate(results) if not r]
+    finally:
+        ctx.close()
