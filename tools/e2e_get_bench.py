@@ -162,6 +162,19 @@ def main() -> int:
             return total / GIB / best, best
 
         items = list(enumerate(dirs))
+
+        def host_read(i_d):
+            """The file reads of a healthy GET alone (no hashing, no GPU):
+            what the host side can deliver."""
+            _, d = i_d
+            total = 0
+            for j in range(k):
+                with open(os.path.join(d, f"{j:06}"), "rb") as f:
+                    total += len(f.read())
+            return total
+
+        v, el = timed(host_read, items, args.threads)
+        out["host_file_reads_only"] = {"GiBps": round(v, 3), "s": round(el, 4)}
         v, el = timed(gpu_get, items, args.threads)
         out["gpu_healthy"] = {"GiBps": round(v, 3), "s": round(el, 4)}
         v1, el1 = timed(gpu_get, items[:16], 1)
