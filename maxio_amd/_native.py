@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmaxio_ec.so")
+# MXEC_LIB: load another build of the library (A/B runs of a kernel change).
+LIB_PATH = os.environ.get("MXEC_LIB") or os.path.join(_HERE, "lib", "libmaxio_ec.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "maxio_ec.h")
 
 _lock = threading.Lock()

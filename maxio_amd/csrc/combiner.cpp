@@ -6,13 +6,13 @@
 // idle and, past GPU_MAX_HW_QUEUES streams, even queue behind each other.
 // Concurrent callers on one device (MaxIO's tokio workers serving GETs, chunk
 // verification in chunk_reader.rs:87-152 / :176-196) therefore hand their
-// device-resident messages to one combiner: the first caller that finds no
-// launch in flight becomes the leader, takes every pending request, and runs
-// ONE launch over all their messages on the combiner's private stream;
-// callers that arrive meanwhile wait and form the next batch (flat
-// combining, no service thread).  A request waits at most for the batch in
-// flight plus its own, and a batch of N requests costs about one request's
-// latency.
+// device-resident messages to one combiner: a caller that finds a launch
+// lane free and nobody gathering becomes the leader, takes every pending
+// request, and runs ONE launch over all their messages on that lane's private
+// stream; callers that arrive meanwhile form the next batch, which starts on
+// the next free lane without waiting for the first to finish (flat
+// combining, no service thread).  A batch of N requests costs about one
+// request's latency.
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -35,21 +35,28 @@ struct ShaCombiner {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<Req*> pending;
-    bool busy = false;
-    size_t last_batch = 1;  // requests in the previous launch
-    Slot slot;  // private stream, descriptor ring and digest buffers
+    bool gathering = false;  // a leader is collecting its batch
+    size_t last_batch = 1;   // requests in the previous launch
+    // Launch lanes: up to slots.size() batches in flight at once (default
+    // one), each on its own stream and buffers, so that with more than one a
+    // request arriving while a launch runs starts its own instead of queueing
+    // behind it (GPU_MAX_HW_QUEUES = 4 bounds the lanes).
+    std::vector<std::unique_ptr<Slot>> slots;
+    std::vector<Slot*> free_slots;
     uint64_t batches = 0, messages = 0;  // guarded by mu
 
     ~ShaCombiner() {
-        if (slot.stream) (void)hipStreamSynchronize(slot.stream);
-        for (auto& rb : slot.ring)
-            if (rb.done) (void)hipEventDestroy(rb.done);
-        if (slot.stream) (void)hipStreamDestroy(slot.stream);
+        for (auto& sl : slots) {
+            if (sl->stream) (void)hipStreamSynchronize(sl->stream);
+            for (auto& rb : sl->ring)
+                if (rb.done) (void)hipEventDestroy(rb.done);
+            if (sl->stream) (void)hipStreamDestroy(sl->stream);
+        }
     }
 
-    // One launch over every message of `batch`; digests land in each
-    // request's host buffer.  Called by the leader without the lock held.
-    int run(Device& d, const std::vector<Req*>& batch) {
+    // One launch over every message of `batch` on `slot`; digests land in
+    // each request's host buffer.  Called by a leader without the lock held.
+    static int run(Device& d, Slot& slot, const std::vector<Req*>& batch) {
         std::vector<const uint8_t*> ptrs;
         std::vector<uint64_t> lens;
         for (const Req* r : batch) {
@@ -61,9 +68,9 @@ struct ShaCombiner {
         hipStream_t s = slot.stream;
         MXEC_TRY(slot.digests.ensure(n * 32));
         // The split (producer / consumer) form at every size: a combined
-        // batch is usually several chip-filling requests, and two waves per
-        // 64 messages spread over the SIMDs more evenly than one (a batch
-        // ends with its most loaded SIMD).
+        // batch is often several chip-filling requests, and two waves per 64
+        // messages spread over the SIMDs more evenly than one (a batch ends
+        // with its most loaded SIMD).
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr, nullptr,
                          nullptr, 2));
         MXEC_TRY(slot.hdig.ensure(n * 32));
@@ -112,11 +119,29 @@ long gather_max_us() {
     return us;
 }
 
+// MXEC_COMBINE_STREAMS: launches in flight per device (default 1: two or
+// three lanes measured slower everywhere -- config 3c 509 -> 344 / 381
+// GiB/s, 64-thread GET 6.8 -> 5.6 / 4.2 GiB/s, profiles/r1_combine_lanes.txt
+// -- since concurrent issue-bound launches share the SIMDs and the smaller
+// batches end no sooner).
+size_t combine_streams() {
+    static const size_t n = [] {
+        const long v = env_us("MXEC_COMBINE_STREAMS", 1);
+        return size_t(v < 1 ? 1 : v > 4 ? 4 : v);
+    }();
+    return n;
+}
+
 ShaCombiner* combiner_of(Device& d) {
     std::lock_guard<std::mutex> g(d.comb_mu);
     if (!d.comb) {
         auto c = std::make_shared<ShaCombiner>();
-        if (hipStreamCreateWithFlags(&c->slot.stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        for (size_t i = 0; i < combine_streams(); ++i) {
+            auto sl = std::make_unique<Slot>();
+            if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+            c->free_slots.push_back(sl.get());
+            c->slots.push_back(std::move(sl));
+        }
         d.comb = c;
     }
     return static_cast<ShaCombiner*>(d.comb.get());
@@ -147,20 +172,22 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     me.out = out;
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&me);
-    if (c->busy) c->cv.notify_all();  // a gathering leader may be waiting for us
+    if (c->gathering) c->cv.notify_all();  // a gathering leader may be waiting for us
     while (!me.done) {
-        if (c->busy) {
+        // Lead when a launch lane is free and nobody else is gathering (a
+        // gathering leader takes this request too); else wait.
+        if (c->gathering || c->free_slots.empty()) {
             c->cv.wait(lk);
             continue;
         }
-        c->busy = true;
+        c->gathering = true;
         // Adaptive gathering: a leader waits (bounded) until as many requests
         // are pending as the previous launch carried, so a steady stream of
-        // concurrent callers keeps landing in one launch instead of splitting
-        // into a lone first request and the rest; a lone leader waits a short
-        // window.  A launch lasts >= 1.8 us per 64-byte block of its longest
-        // message (29 ms per 1 MiB chunk), so the wait costs a few percent at
-        // most, and the previous size is forgotten as soon as fewer come.
+        // concurrent callers keeps landing in few launches instead of a lone
+        // first request and the rest; a lone leader waits a short window.  A
+        // launch lasts >= 1.8 us per 64-byte block of its longest message (29
+        // ms per 1 MiB chunk), so the wait costs a few percent at most, and
+        // the previous size is forgotten as soon as fewer come.
         const size_t want = c->last_batch;
         const long wait_us = want > 1 ? gather_max_us() : gather_us();
         if (c->pending.size() < std::max<size_t>(want, 2) && wait_us > 0)
@@ -169,10 +196,14 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         std::vector<ShaCombiner::Req*> batch;
         batch.swap(c->pending);
         c->last_batch = batch.size();
+        c->gathering = false;
+        Slot* slot_run = c->free_slots.back();
+        c->free_slots.pop_back();
+        c->cv.notify_all();  // the next leader may start gathering now
         lk.unlock();
         int rc = MXEC_OK;
         try {
-            rc = c->run(d, batch);
+            rc = ShaCombiner::run(d, *slot_run, batch);
         } catch (...) {
             rc = set_error(MXEC_E_OOM, "host allocation failed");
         }
@@ -187,7 +218,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
             r->msg = msg;
             r->done = true;
         }
-        c->busy = false;
+        c->free_slots.push_back(slot_run);
         c->cv.notify_all();
     }
     if (me.rc) return set_error(me.rc, me.msg);

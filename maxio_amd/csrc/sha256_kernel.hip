@@ -161,12 +161,20 @@ __device__ __forceinline__ void message_words(const uint8_t* p, bool aligned, ui
         load_block(p, blk);
         block_words(blk, w);
     } else {
+        // Global, not flat, byte loads: a pending flat load makes the
+        // compiler drain vmcnt to 0 before every later use of a load result,
+        // which would also wait out the producer's prefetch ring.
+        typedef const uint8_t __attribute__((address_space(1)))* gbyte;
+        const gbyte q = (gbyte)(p);
 #pragma unroll
         for (int t = 0; t < 16; ++t)
-            w[t] = uint32_t(p[4 * t]) << 24 | uint32_t(p[4 * t + 1]) << 16 |
-                   uint32_t(p[4 * t + 2]) << 8 | uint32_t(p[4 * t + 3]);
+            w[t] = uint32_t(q[4 * t]) << 24 | uint32_t(q[4 * t + 1]) << 16 |
+                   uint32_t(q[4 * t + 2]) << 8 | uint32_t(q[4 * t + 3]);
     }
 }
+
+constexpr int kShaPrefetch = 4;
+__device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const* __restrict__ ptrs,
                                                            const uint64_t* __restrict__ lens,
@@ -190,35 +198,91 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
         const uint64_t o = __shfl_xor(nmax, s);
         nmax = o > nmax ? o : nmax;
     }
+    // Equal in every lane now; say so, so the loops below branch on scalars
+    // (a divergent loop exit would make every prefetch load conditional).
+    nmax = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(nmax >> 32))) << 32) |
+           __builtin_amdgcn_readfirstlane(uint32_t(nmax));
     uint32_t w[16];
-    // Producer prefetch: the raw bytes of the block after the one being
-    // scheduled stay in flight across the barrier (plain loads survive it),
-    // so the producer's step is the schedule alone, not an HBM round trip
-    // plus the schedule.
-    u32x4 nxt[4];
-    if (wave == 1 && nfull > 0) {
-        message_words(p, aligned, w);
-        if (aligned && nfull > 1) load_block(p + 64, nxt);
-        schedule_kw(w, &kw[0][0][lane]);
-    }
-    __syncthreads();
     uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                       0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    for (uint64_t b = 0; b < nmax; ++b) {
-        if (wave == 1) {
-            if (b + 1 < nfull) {
-                if (aligned) {
-                    block_words(nxt, w);
-                    if (b + 2 < nfull) load_block(p + 64 * (b + 2), nxt);
-                } else {
-                    message_words(p + 64 * (b + 1), false, w);
-                }
-                schedule_kw(w, &kw[(b + 1) & 1][0][lane]);
-            }
-        } else if (b < nfull) {
-            compress_kw(st, &kw[b & 1][0][lane]);
+    // The two roles run separate loops with one barrier per block each (the
+    // trip counts match, so the barriers pair up).
+    if (wave == 0) {
+        __syncthreads();
+        for (uint64_t b = 0; b < nmax; ++b) {
+            if (b < nfull) compress_kw(st, &kw[b & 1][0][lane]);
+            __syncthreads();
+        }
+    } else if (__all(!live || nfull == 0 || aligned)) {
+        // Producer, every message 16-byte aligned: the raw bytes of the next
+        // kShaPrefetch blocks stay in flight across the barriers in a
+        // register ring indexed at compile time (the loop is unrolled by the
+        // ring size), so the producer's step is the schedule alone.  One
+        // block ahead was not enough for a lone workgroup: with the chip
+        // otherwise idle a load's round trip can outlast a 1.8 us step, and
+        // the consumer then waited at the barrier (29-52 ms for one 1 MiB
+        // message, run to run).  Every load is unconditional -- lanes past
+        // their last block re-read it, lanes without one read a donor lane's
+        // -- because a load under a branch makes the compiler's wait before
+        // the next use drain every load in flight (it cannot count the ones
+        // that may have been skipped).
+        const uint64_t donor_mask = __ballot(nfull == nmax);
+        const int donor = __ffsll((unsigned long long)donor_mask) - 1;
+        const uint8_t* dp = reinterpret_cast<const uint8_t*>(
+            __shfl(reinterpret_cast<uintptr_t>(p), donor));
+        const bool own = live && nfull > 0;
+        const uint8_t* ps = own ? p : dp;
+        const uint64_t last = (own ? nfull : nmax) - 1;  // nmax > 0 when the loop runs
+        u32x4 ring[kShaPrefetch][4];
+        if (nmax > 0) {
+            u32x4 blk[4];
+            load_block(ps, blk);
+#pragma unroll
+            for (int j = 0; j < kShaPrefetch; ++j) load_block(ps + 64 * min_u64(j + 1, last), ring[j]);
+            block_words(blk, w);
+            schedule_kw(w, &kw[0][0][lane]);
         }
         __syncthreads();
+        // Whole groups of kShaPrefetch steps, then the rest: an exit in the
+        // middle of a group would join the loop's back edge with fewer loads
+        // issued, and the waits at the top would drain the ring again.
+        uint64_t b0 = 0;
+        for (; b0 + kShaPrefetch <= nmax; b0 += kShaPrefetch) {
+#pragma unroll
+            for (int j = 0; j < kShaPrefetch; ++j) {
+                const uint64_t b = b0 + j;
+                // ring[j] holds block b + 1 (or a clamped re-read nobody
+                // consumes: lanes compress only blocks below their nfull, and
+                // kw[nmax & 1] is never read).
+                block_words(ring[j], w);
+                load_block(ps + 64 * min_u64(b + 1 + kShaPrefetch, last), ring[j]);
+                schedule_kw(w, &kw[(b + 1) & 1][0][lane]);
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kShaPrefetch - 1; ++j) {  // the ring already holds these blocks
+            if (b0 + j < nmax) {
+                block_words(ring[j], w);
+                schedule_kw(w, &kw[(b0 + j + 1) & 1][0][lane]);
+                __syncthreads();
+            }
+        }
+    } else {
+        // Producer with an unaligned message in the wave: byte loads, one
+        // block at a time.
+        if (nfull > 0) {
+            message_words(p, aligned, w);
+            schedule_kw(w, &kw[0][0][lane]);
+        }
+        __syncthreads();
+        for (uint64_t b = 0; b < nmax; ++b) {
+            if (b + 1 < nfull) {
+                message_words(p + 64 * (b + 1), aligned, w);
+                schedule_kw(w, &kw[(b + 1) & 1][0][lane]);
+            }
+            __syncthreads();
+        }
     }
     if (wave == 1 || !live) return;
     const uint32_t rem = uint32_t(len - nfull * 64);

@@ -391,6 +391,36 @@ def test_sha256_every_kernel_form(ctx, form, monkeypatch):
     assert got == [hashlib.sha256(b).digest() for b in bufs]
 
 
+@pytest.mark.parametrize("form", ["split", "one"])
+@pytest.mark.parametrize("shift", [0, 16, 3])
+def test_sha256_device_messages_ring_edges(ctx, form, shift, monkeypatch):
+    """Device-resident messages straight into the kernel (no staging copy),
+    16-byte aligned (shift 0/16: the split form's prefetch-ring path) or not
+    (shift 3: its byte-load path): lone messages of 0..9 full blocks (every
+    ring phase and tail count), a wave whose lanes end at different blocks,
+    empty messages (their lanes borrow a donor lane's address) and a batch
+    past one workgroup."""
+    monkeypatch.setenv("MXEC_SHA_FORM", form)
+    torch = _torch()
+    rng = np.random.default_rng(21 + shift)
+    cases = [[64 * b + t] for b in range(10) for t in (0, 37)]
+    cases.append([int(x) for x in rng.integers(0, 64 * 23, 64)])
+    cases.append([0, 0, 5 * 64, 0, 64 * 9 + 1])
+    cases.append([int(x) for x in rng.integers(0, 3000, 150)])
+    for lens in cases:
+        stride = (max(lens) + 64 + 15) // 16 * 16
+        host = rng.integers(0, 256, stride * len(lens) + 64, dtype=np.uint8)
+        dev = torch.from_numpy(host).cuda()
+        ptrs = [dev.data_ptr() + i * stride + shift for i in range(len(lens))]
+        dig = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
+        ctx.sha256_batch_device(ptrs, lens, dig.data_ptr())
+        torch.cuda.synchronize()
+        got = dig.cpu().numpy().reshape(-1, 32)
+        for i, n in enumerate(lens):
+            o = i * stride + shift
+            assert bytes(got[i]) == hashlib.sha256(host[o:o + n].tobytes()).digest(), (lens, i)
+
+
 def test_concurrent_reconstruct_workers(ctx):
     """Several host threads (tokio workers) reconstruct their own batches on
     their own streams through one context at once (bench config 3c): every
