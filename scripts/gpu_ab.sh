@@ -1,4 +1,7 @@
 #!/bin/bash
+# A/B of a library change on one box: bench configs (CONFIGS) with the
+# library built from the previous kernel (build_ab/libmaxio_ec_prev.so, via
+# MXEC_LIB) and with the current one, alternating, twice.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/ab; mkdir -p $O
