@@ -110,11 +110,7 @@ void mxec_close(mxec_ctx* ctx) {
     for (auto& d : ctx->c.devs) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
-        for (auto& s : d->slots) {
-            for (auto& rb : s->ring)
-                if (rb.done) (void)hipEventDestroy(rb.done);
-            if (s->stream) (void)hipStreamDestroy(s->stream);
-        }
+        for (auto& s : d->slots) slot_destroy(*s);
     }
     delete ctx;
 }
@@ -168,12 +164,15 @@ int mxec_sha256_batch(mxec_ctx* ctx, const uint8_t* const* bufs, const size_t* l
         auto* base = static_cast<uint8_t*>(slot.shards.p);
         std::vector<const uint8_t*> ptrs(n);
         std::vector<uint64_t> l(n);
+        std::vector<UploadSeg> segs;
+        segs.reserve(n);
         for (size_t i = 0; i < n; ++i) {
-            if (lens[i]) MXEC_HIP(hipMemcpyAsync(base + off[i], bufs[i], lens[i], hipMemcpyHostToDevice, s));
+            if (lens[i]) segs.push_back({off[i], bufs[i], lens[i]});
             ptrs[i] = base + off[i];
             l[i] = lens[i];
         }
-        MXEC_HIP(hipStreamSynchronize(s));  // uploads done: the combiner hashes on its own stream
+        MXEC_TRY(upload_segments(slot, s, base, segs));
+        MXEC_TRY(slot_wait(slot, s));  // uploads done: the combiner hashes on its own stream
         return sha256_combined(*ds.d, slot, s, ptrs, l, &out[0][0]);
     });
 }
@@ -200,19 +199,20 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* c
         auto* base = static_cast<uint8_t*>(slot.shards.p);
         std::vector<const uint8_t*> in(static_cast<size_t>(k));
         std::vector<uint8_t*> out(static_cast<size_t>(m));
+        std::vector<UploadSeg> up;
         for (int j = 0; j < k; ++j) {
             in[size_t(j)] = base + sa * uint64_t(j);
-            if (len[size_t(j)])
-                MXEC_HIP(hipMemcpyAsync(base + sa * uint64_t(j), data[j], len[size_t(j)], hipMemcpyHostToDevice, s));
+            if (len[size_t(j)]) up.push_back({sa * uint64_t(j), data[j], len[size_t(j)]});
         }
+        MXEC_TRY(upload_segments(slot, s, base, up));
         for (int i = 0; i < m; ++i) out[size_t(i)] = base + sa * uint64_t(k + i);
         uint32_t off = 0;
         MXEC_TRY(encode_coef(*ds.d, k, m, &off));
         RsObject ob{in.data(), len.data(), out.data(), len.data() + k, off};
         MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, m, {ob}));
-        for (int i = 0; i < m; ++i)
-            MXEC_HIP(hipMemcpyAsync(parity[i], out[size_t(i)], shard_size, hipMemcpyDeviceToHost, s));
-        MXEC_HIP(hipStreamSynchronize(s));
+        std::vector<UploadSeg> down;
+        for (int i = 0; i < m; ++i) down.push_back({sa * uint64_t(k + i), parity[i], shard_size});
+        MXEC_TRY(download_segments(slot, s, base, down));
         if (sha256_out) {
             // write_chunk / compute_and_write_parity digests (filesystem.rs:1070,
             // :1131), combined with every concurrent caller's verification work.
@@ -249,17 +249,18 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
         std::vector<const uint8_t*> sp;
         std::vector<uint64_t> sl;
         std::vector<int> si;
+        std::vector<UploadSeg> up;
         for (int i = 0; i < total; ++i) {
             if (!present[size_t(i)]) continue;
-            if (len[size_t(i)])
-                MXEC_HIP(hipMemcpyAsync(base + sa * uint64_t(i), shards[i], len[size_t(i)], hipMemcpyHostToDevice, s));
+            if (len[size_t(i)]) up.push_back({sa * uint64_t(i), shards[i], len[size_t(i)]});
             sp.push_back(base + sa * uint64_t(i));
             sl.push_back(len[size_t(i)]);
             si.push_back(i);
         }
+        MXEC_TRY(upload_segments(slot, s, base, up));
         if (expected_sha256 && !sp.empty()) {
             // chunk_reader.rs:176-196: hash every present shard; mismatch -> erasure.
-            MXEC_HIP(hipStreamSynchronize(s));
+            MXEC_TRY(slot_wait(slot, s));
             std::vector<uint8_t> dig(sp.size() * 32);
             MXEC_TRY(sha256_combined(*ds.d, slot, s, sp, sl, dig.data()));
             for (size_t t = 0; t < si.size(); ++t)
@@ -288,10 +289,11 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
             }
             RsObject ob{in.data(), in_len.data(), out.data(), out_len.data(), off};
             MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, int(out.size()), {ob}));
+            std::vector<UploadSeg> down;
             for (size_t t = 0; t < out.size(); ++t)
-                if (out_len[t])
-                    MXEC_HIP(hipMemcpyAsync(shards[plan->missing[t]], out[t], out_len[t], hipMemcpyDeviceToHost, s));
-            MXEC_HIP(hipStreamSynchronize(s));
+                if (out_len[t]) down.push_back({sa * uint64_t(plan->missing[t]), shards[plan->missing[t]], out_len[t]});
+            // plan->missing is ascending, so are the offsets.
+            MXEC_TRY(download_segments(slot, s, base, down));
             for (int e : plan->missing) present[size_t(e)] = 1;
         }
         std::memcpy(present_inout, present.data(), size_t(total));
@@ -436,7 +438,7 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx));
                 MXEC_TRY(slot.hdig.ensure(ptrs.size()));
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok, ptrs.size(), hipMemcpyDeviceToHost, s));
-                MXEC_HIP(hipStreamSynchronize(s));
+                MXEC_TRY(slot_wait(*ds.slot, s));
                 const auto* okh = static_cast<const uint8_t*>(slot.hdig.p);
                 for (size_t t = 0; t < idx.size(); ++t)
                     if (!okh[t]) present[idx[t]] = 0;
@@ -448,7 +450,7 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 const size_t ne = size_t(n_obj) * size_t(total) * 32;
                 MXEC_TRY(slot.hdig.ensure(ne));
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, expected_sha_dev, ne, hipMemcpyDeviceToHost, s));
-                MXEC_HIP(hipStreamSynchronize(s));
+                MXEC_TRY(slot_wait(*ds.slot, s));
                 std::vector<uint8_t> exph(static_cast<const uint8_t*>(slot.hdig.p),
                                           static_cast<const uint8_t*>(slot.hdig.p) + ne);
                 std::vector<uint8_t> dig(ptrs.size() * 32);

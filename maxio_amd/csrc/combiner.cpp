@@ -33,7 +33,12 @@ struct ShaCombiner {
         bool done = false;
     };
     std::mutex mu;
-    std::condition_variable cv;
+    // Two wait queues, so that an arrival wakes only the gathering leader and
+    // a finished launch wakes the waiters once (one shared queue woke every
+    // waiting thread on every arrival: ~60 futex wake-ups per request at 64
+    // request threads).
+    std::condition_variable cv_gather;  // the gathering leader
+    std::condition_variable cv_done;    // everyone else
     std::vector<Req*> pending;
     bool gathering = false;  // a leader is collecting its batch
     size_t last_batch = 1;   // requests in the previous launch
@@ -48,9 +53,7 @@ struct ShaCombiner {
     ~ShaCombiner() {
         for (auto& sl : slots) {
             if (sl->stream) (void)hipStreamSynchronize(sl->stream);
-            for (auto& rb : sl->ring)
-                if (rb.done) (void)hipEventDestroy(rb.done);
-            if (sl->stream) (void)hipStreamDestroy(sl->stream);
+            slot_destroy(*sl);
         }
     }
 
@@ -75,7 +78,7 @@ struct ShaCombiner {
                          nullptr, 2));
         MXEC_TRY(slot.hdig.ensure(n * 32));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
-        MXEC_HIP(hipStreamSynchronize(s));
+        MXEC_TRY(slot_wait(slot, s));
         const auto* h = static_cast<const uint8_t*>(slot.hdig.p);
         size_t o = 0;
         for (Req* r : batch) {
@@ -132,13 +135,30 @@ size_t combine_streams() {
     return n;
 }
 
+// MXEC_COMBINE_PRIORITY (default 1): the combiner's streams get the highest
+// stream priority, i.e. a hardware queue of their own.  Streams share
+// GPU_MAX_HW_QUEUES = 4 queues, so a 30 ms hash launch on a normal-priority
+// stream held up the uploads of a quarter of the request streams behind it
+// (64-thread GET: host upload + wait 6.4 -> 2.7 ms per request, 7.3 -> 8.0 GiB/s).
+bool combine_priority() {
+    static const bool p = env_us("MXEC_COMBINE_PRIORITY", 1) != 0;
+    return p;
+}
+
 ShaCombiner* combiner_of(Device& d) {
     std::lock_guard<std::mutex> g(d.comb_mu);
     if (!d.comb) {
         auto c = std::make_shared<ShaCombiner>();
         for (size_t i = 0; i < combine_streams(); ++i) {
             auto sl = std::make_unique<Slot>();
-            if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+            if (combine_priority()) {
+                int lo = 0, hi = 0;
+                if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+                    hipStreamCreateWithPriority(&sl->stream, hipStreamNonBlocking, hi) != hipSuccess)
+                    return nullptr;
+            } else if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) {
+                return nullptr;
+            }
             c->free_slots.push_back(sl.get());
             c->slots.push_back(std::move(sl));
         }
@@ -160,7 +180,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
         MXEC_TRY(slot.hdig.ensure(n * 32));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
-        MXEC_HIP(hipStreamSynchronize(s));
+        MXEC_TRY(slot_wait(slot, s));
         std::memcpy(out, slot.hdig.p, n * 32);
         return MXEC_OK;
     }
@@ -172,12 +192,12 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     me.out = out;
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&me);
-    if (c->gathering) c->cv.notify_all();  // a gathering leader may be waiting for us
+    if (c->gathering) c->cv_gather.notify_one();  // the gathering leader may be waiting for us
     while (!me.done) {
         // Lead when a launch lane is free and nobody else is gathering (a
         // gathering leader takes this request too); else wait.
         if (c->gathering || c->free_slots.empty()) {
-            c->cv.wait(lk);
+            c->cv_done.wait(lk);
             continue;
         }
         c->gathering = true;
@@ -191,7 +211,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         const size_t want = c->last_batch;
         const long wait_us = want > 1 ? gather_max_us() : gather_us();
         if (c->pending.size() < std::max<size_t>(want, 2) && wait_us > 0)
-            c->cv.wait_for(lk, std::chrono::microseconds(wait_us),
+            c->cv_gather.wait_for(lk, std::chrono::microseconds(wait_us),
                            [&] { return c->pending.size() >= std::max<size_t>(want, 2); });
         std::vector<ShaCombiner::Req*> batch;
         batch.swap(c->pending);
@@ -199,7 +219,10 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         c->gathering = false;
         Slot* slot_run = c->free_slots.back();
         c->free_slots.pop_back();
-        c->cv.notify_all();  // the next leader may start gathering now
+        // Requests that arrived while this leader gathered are in its batch,
+        // so nobody waits for the gathering to end unless another lane is
+        // free for them.
+        if (!c->free_slots.empty()) c->cv_done.notify_all();
         lk.unlock();
         int rc = MXEC_OK;
         try {
@@ -219,7 +242,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
             r->done = true;
         }
         c->free_slots.push_back(slot_run);
-        c->cv.notify_all();
+        c->cv_done.notify_all();
     }
     if (me.rc) return set_error(me.rc, me.msg);
     return MXEC_OK;

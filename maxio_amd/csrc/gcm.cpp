@@ -279,13 +279,13 @@ int mxec_frames_encrypt(mxec_ctx* ctx, const uint8_t key[32], const uint8_t nonc
         const uint64_t a_aad = round_up(uint64_t(aad_len) * nf, kSlotAlign);
         MXEC_TRY(slot.shards.ensure(a_in + a_out + a_aad));
         auto* base = static_cast<uint8_t*>(slot.shards.p);
-        MXEC_HIP(hipMemcpyAsync(base, pt, len, hipMemcpyHostToDevice, s));
-        if (aad_len) MXEC_HIP(hipMemcpyAsync(base + a_in + a_out, aad, uint64_t(aad_len) * nf, hipMemcpyHostToDevice, s));
+        std::vector<UploadSeg> up{{0, pt, len}};
+        if (aad_len) up.push_back({a_in + a_out, aad, uint64_t(aad_len) * nf});
+        MXEC_TRY(upload_segments(slot, s, base, up));
         Job jb{key, prefix_word(nonce_prefix), frame_size, first_index, base + a_in + a_out, aad_len, base, len,
                base + a_in};
         MXEC_TRY(run_frames(*ds.d, slot, s, {jb}, false, nullptr));
-        MXEC_HIP(hipMemcpyAsync(out, base + a_in, total, hipMemcpyDeviceToHost, s));
-        MXEC_HIP(hipStreamSynchronize(s));
+        MXEC_TRY(download_segments(slot, s, base, {{a_in, out, total}}));
         *out_len = total;
         return MXEC_OK;
     });
@@ -312,17 +312,18 @@ int mxec_frames_decrypt(mxec_ctx* ctx, const uint8_t key[32], uint64_t first_ind
         MXEC_TRY(slot.shards.ensure(a_in + a_out + a_aad));
         MXEC_TRY(slot.digests.ensure(nf * sizeof(int32_t)));
         auto* base = static_cast<uint8_t*>(slot.shards.p);
-        MXEC_HIP(hipMemcpyAsync(base, frames, need, hipMemcpyHostToDevice, s));
-        if (aad_len) MXEC_HIP(hipMemcpyAsync(base + a_in + a_out, aad, uint64_t(aad_len) * nf, hipMemcpyHostToDevice, s));
+        std::vector<UploadSeg> up{{0, frames, need}};
+        if (aad_len) up.push_back({a_in + a_out, aad, uint64_t(aad_len) * nf});
+        MXEC_TRY(upload_segments(slot, s, base, up));
         Job jb{key, 0, frame_size, first_index, base + a_in + a_out, aad_len, base, plaintext_size, base + a_in};
         auto* st_dev = static_cast<int32_t*>(slot.digests.p);
         MXEC_TRY(run_frames(*ds.d, slot, s, {jb}, true, st_dev));
         MXEC_TRY(slot.hdig.ensure(nf * sizeof(int32_t)));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, st_dev, nf * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        MXEC_HIP(hipStreamSynchronize(s));
+        MXEC_TRY(slot_wait(slot, s));
         MXEC_TRY(frame_error(static_cast<const int32_t*>(slot.hdig.p), nf, first_index, frames, frame_size,
                              plaintext_size));
-        MXEC_HIP(hipMemcpy(out, base + a_in, plaintext_size, hipMemcpyDeviceToHost));
+        MXEC_TRY(download_segments(slot, s, base, {{a_in, out, plaintext_size}}));
         *out_len = plaintext_size;
         return MXEC_OK;
     });
@@ -372,7 +373,7 @@ int mxec_frames_decrypt_device(mxec_ctx* ctx, int dev, void* stream, const mxec_
         MXEC_TRY(run_frames(*ds.d, slot, s, js, true, st_dev));
         MXEC_TRY(slot.hdig.ensure(std::max<uint64_t>(1, nf) * sizeof(int32_t)));
         if (nf) MXEC_HIP(hipMemcpyAsync(slot.hdig.p, st_dev, nf * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        MXEC_HIP(hipStreamSynchronize(s));
+        MXEC_TRY(slot_wait(slot, s));
         const auto* st = static_cast<const int32_t*>(slot.hdig.p);
         int rc = MXEC_OK;
         for (uint64_t j = 0; j < n_jobs; ++j) {

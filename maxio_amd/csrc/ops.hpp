@@ -12,6 +12,7 @@
 
 namespace mxec {
 
+
 // One object of an RS launch: k inputs -> r outputs, device pointers.
 struct RsObject {
     const uint8_t* const* in;  // k

@@ -1,6 +1,8 @@
 // runtime.cpp — device buffers, descriptor rings, coefficient arena.
 #include "runtime.hpp"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace mxec {
@@ -38,6 +40,98 @@ int PinnedBuf::ensure(size_t n) {
     MXEC_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
     cap = want;
     return MXEC_OK;
+}
+
+int slot_wait(Slot& slot, hipStream_t s) {
+    static const bool spin = [] {
+        const char* e = getenv("MXEC_SPIN_WAIT");
+        return e && *e && *e != '0';
+    }();
+    if (spin) {
+        MXEC_HIP(hipStreamSynchronize(s));
+        return MXEC_OK;
+    }
+    if (!slot.sync_ev)
+        MXEC_HIP(hipEventCreateWithFlags(&slot.sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+    MXEC_HIP(hipEventRecord(slot.sync_ev, s));
+    MXEC_HIP(hipEventSynchronize(slot.sync_ev));
+    return MXEC_OK;
+}
+
+void slot_destroy(Slot& slot) {
+    for (auto& rb : slot.ring)
+        if (rb.done) (void)hipEventDestroy(rb.done);
+    for (auto& e : slot.stage_done)
+        if (e) (void)hipEventDestroy(e);
+    if (slot.sync_ev) (void)hipEventDestroy(slot.sync_ev);
+    if (slot.stream) (void)hipStreamDestroy(slot.stream);
+    slot.stream = nullptr;
+}
+
+int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
+    if (segs.empty()) return MXEC_OK;
+    for (auto& e : slot.stage_done)
+        if (!e) MXEC_HIP(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
+    // Walk the destination range [lo, hi) in pieces; each piece gathers the
+    // bytes of the segments it overlaps (gaps between segments are padding
+    // nobody reads) and goes up in one DMA.
+    const uint64_t lo = segs.front().dst_off;
+    const uint64_t hi = segs.back().dst_off + segs.back().len;
+    const uint64_t piece = std::min<uint64_t>(kStagePiece, hi - lo);
+    for (auto& b : slot.stage) MXEC_TRY(b.ensure(piece));
+    size_t si = 0;
+    int buf = 0;
+    for (uint64_t a = lo; a < hi; a += piece, buf ^= 1) {
+        const uint64_t b = std::min(hi, a + piece);
+        // The DMA that last read this buffer must be done before refilling it.
+        MXEC_HIP(hipEventSynchronize(slot.stage_done[buf]));
+        auto* h = static_cast<uint8_t*>(slot.stage[buf].p);
+        while (si < segs.size() && segs[si].dst_off + segs[si].len <= a) ++si;
+        for (size_t j = si; j < segs.size() && segs[j].dst_off < b; ++j) {
+            const uint64_t x = std::max(a, segs[j].dst_off), y = std::min(b, segs[j].dst_off + segs[j].len);
+            if (y > x) std::memcpy(h + (x - a), static_cast<const uint8_t*>(segs[j].src) + (x - segs[j].dst_off), y - x);
+        }
+        MXEC_HIP(hipMemcpyAsync(dev_base + a, h, b - a, hipMemcpyHostToDevice, s));
+        MXEC_HIP(hipEventRecord(slot.stage_done[buf], s));
+    }
+    return MXEC_OK;
+}
+
+int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
+    if (segs.empty()) return slot_wait(slot, s);
+    for (auto& e : slot.stage_done)
+        if (!e) MXEC_HIP(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
+    const uint64_t lo = segs.front().dst_off;
+    const uint64_t hi = segs.back().dst_off + segs.back().len;
+    const uint64_t piece = std::min<uint64_t>(kStagePiece, hi - lo);
+    for (auto& b : slot.stage) MXEC_TRY(b.ensure(piece));
+    // Piece i+1's DMA is in flight while piece i is copied out.
+    size_t si = 0;
+    auto drain = [&](uint64_t a, int buf) -> int {
+        const uint64_t b = std::min(hi, a + piece);
+        MXEC_HIP(hipEventSynchronize(slot.stage_done[buf]));
+        const auto* h = static_cast<const uint8_t*>(slot.stage[buf].p);
+        while (si < segs.size() && segs[si].dst_off + segs[si].len <= a) ++si;
+        for (size_t j = si; j < segs.size() && segs[j].dst_off < b; ++j) {
+            const uint64_t x = std::max(a, segs[j].dst_off), y = std::min(b, segs[j].dst_off + segs[j].len);
+            if (y > x)
+                std::memcpy(const_cast<uint8_t*>(static_cast<const uint8_t*>(segs[j].src)) + (x - segs[j].dst_off),
+                            h + (x - a), y - x);
+        }
+        return MXEC_OK;
+    };
+    int buf = 0;
+    uint64_t prev = UINT64_MAX;
+    for (uint64_t a = lo; a < hi; a += piece, buf ^= 1) {
+        const uint64_t b = std::min(hi, a + piece);
+        // This buffer's previous piece was drained before the one before
+        // this iteration's (strict alternation), so it is free.
+        MXEC_HIP(hipMemcpyAsync(slot.stage[buf].p, dev_base + a, b - a, hipMemcpyDeviceToHost, s));
+        MXEC_HIP(hipEventRecord(slot.stage_done[buf], s));
+        if (prev != UINT64_MAX) MXEC_TRY(drain(prev, buf ^ 1));
+        prev = a;
+    }
+    return drain(prev, buf ^ 1);
 }
 
 void PinnedBuf::release() {

@@ -69,7 +69,38 @@ struct Slot {
     static constexpr int kRing = 4;
     DescBuf ring[kRing];
     int ring_next = 0;
+    // Host-API uploads go through this pinned pair (pieces of kStagePiece,
+    // double-buffered): one DMA per piece instead of HIP's pageable staging.
+    PinnedBuf stage[2];
+    hipEvent_t stage_done[2] = {nullptr, nullptr};
+    // Blocking-sync event for the host-API waits (slot_wait).
+    hipEvent_t sync_ev = nullptr;
 };
+
+// Wait for everything enqueued on `s` so far.  An event created with
+// hipEventBlockingSync sleeps in the driver instead of spinning a core: with
+// dozens of request threads waiting on ~30 ms hash launches, spin-waiting
+// took more host cores than the data copies (MXEC_SPIN_WAIT=1 restores
+// hipStreamSynchronize).
+int slot_wait(Slot& slot, hipStream_t s);
+// Destroy a slot's events and stream (context close).
+void slot_destroy(Slot& slot);
+
+// One host -> device upload segment: len bytes from src to dst_off.
+struct UploadSeg {
+    uint64_t dst_off;
+    const void* src;
+    uint64_t len;
+};
+constexpr uint64_t kStagePiece = uint64_t(8) << 20;
+// Copy pageable host segments to dev_base + dst_off through the slot's pinned
+// pair, enqueued on `s` (the caller waits or orders later work on `s`).
+// Segments must be sorted by dst_off and not overlap.
+int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs);
+// The reverse: dev_base + src_off (UploadSeg::dst_off) -> host UploadSeg::src
+// (written), through the same pinned pair; returns when every byte has
+// landed (waits for everything enqueued on `s` before it, too).
+int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<UploadSeg>& segs);
 
 struct Device {
     int id = 0;

@@ -13,12 +13,18 @@
 // in one GPU batch instead of chunk by chunk, parity is encoded from the body
 // already in memory instead of re-reading the data chunk files (:1108-1113),
 // and a GET verifies every chunk of the range in one batch.
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <filesystem>
 #include <fstream>
 #include <map>
+#include <mutex>
+#include <new>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -73,16 +79,137 @@ int write_file(const fs::path& p, const uint8_t* data, size_t len) {
     return MXEC_OK;
 }
 
+// Byte buffers whose resize() leaves new bytes uninitialised: a chunk about
+// to be overwritten by read(2) or a decode need not be zero-filled first.
+//
+// Large buffers come from a process-wide free list by power-of-two class: a
+// GET allocates a chunk-sized buffer per shard, and fresh mmap'd memory costs
+// a page fault per 4 KiB on first touch and a TLB shoot-down across every
+// request thread on munmap -- with 64 request threads that took more host
+// CPU than the data copies.  Pages past the requested size are never
+// touched, so the rounding costs address space, not memory.
+class BigPool {
+public:
+    static constexpr size_t kMin = size_t(256) << 10;
+    static BigPool& get() {
+        static BigPool* p = new BigPool;  // never destroyed: used from static destructors
+        return *p;
+    }
+    static size_t cls(size_t n) {
+        size_t c = kMin;
+        while (c < n) c <<= 1;
+        return c;
+    }
+    void* take(size_t c) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto it = free_.find(c);
+            if (it != free_.end() && !it->second.empty()) {
+                void* p = it->second.back();
+                it->second.pop_back();
+                cached_ -= c;
+                return p;
+            }
+        }
+        void* p = std::malloc(c);
+        if (!p) throw std::bad_alloc();
+        return p;
+    }
+    void give(void* p, size_t c) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (cached_ + c <= kCap) {
+                free_[c].push_back(p);
+                cached_ += c;
+                return;
+            }
+        }
+        std::free(p);
+    }
+
+private:
+    static constexpr size_t kCap = size_t(2) << 30;  // bytes kept for reuse
+    std::mutex mu_;
+    std::map<size_t, std::vector<void*>> free_;
+    size_t cached_ = 0;
+};
+
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    using value_type = T;
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    T* allocate(size_t n) {
+        const size_t b = n * sizeof(T);
+        if (b < BigPool::kMin) return std::allocator<T>::allocate(n);
+        return static_cast<T*>(BigPool::get().take(BigPool::cls(b)));
+    }
+    void deallocate(T* p, size_t n) {
+        const size_t b = n * sizeof(T);
+        if (b < BigPool::kMin) return std::allocator<T>::deallocate(p, n);
+        BigPool::get().give(p, BigPool::cls(b));
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        if constexpr (sizeof...(A) == 0) ::new (static_cast<void*>(p)) U;
+        else ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+using Bytes = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
+
 // std::fs::read: whole file or an io::Error.
-int read_file(const fs::path& p, std::vector<uint8_t>& out) {
-    std::ifstream f(p, std::ios::binary);
-    if (!f) return set_error(MXEC_E_IO, "IO error: " + p.string() + ": " + std::strerror(errno));
-    f.seekg(0, std::ios::end);
-    const std::streamoff n = f.tellg();
-    f.seekg(0, std::ios::beg);
-    out.resize(size_t(n < 0 ? 0 : n));
-    if (n > 0) f.read(reinterpret_cast<char*>(out.data()), n);
-    if (!f) return set_error(MXEC_E_IO, "IO error: read failed for " + p.string());
+template <class Vec>
+int read_file(const fs::path& p, Vec& out) {
+    const int fd = ::open(p.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return set_error(MXEC_E_IO, "IO error: " + p.string() + ": " + std::strerror(errno));
+    struct stat st;
+    if (::fstat(fd, &st) != 0) {
+        const int e = errno;
+        ::close(fd);
+        return set_error(MXEC_E_IO, "IO error: " + p.string() + ": " + std::strerror(e));
+    }
+    out.resize(size_t(st.st_size));
+    size_t got = 0;
+    while (got < out.size()) {
+        const ssize_t r = ::read(fd, out.data() + got, out.size() - got);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) break;
+        got += size_t(r);
+    }
+    ::close(fd);
+    if (got != out.size()) return set_error(MXEC_E_IO, "IO error: read failed for " + p.string());
+    return MXEC_OK;
+}
+
+// read_file into a caller buffer of exactly `want` bytes; *size gets the
+// file's size (when it differs, nothing is read and MXEC_OK is returned so
+// the caller can report the mismatch like read_file + size check would).
+int read_file_to(const fs::path& p, uint8_t* dst, uint64_t want, uint64_t* size) {
+    const int fd = ::open(p.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return set_error(MXEC_E_IO, "IO error: " + p.string() + ": " + std::strerror(errno));
+    struct stat st;
+    if (::fstat(fd, &st) != 0) {
+        const int e = errno;
+        ::close(fd);
+        return set_error(MXEC_E_IO, "IO error: " + p.string() + ": " + std::strerror(e));
+    }
+    *size = uint64_t(st.st_size);
+    uint64_t got = 0;
+    if (*size == want) {
+        while (got < want) {
+            const ssize_t r = ::read(fd, dst + got, size_t(want - got));
+            if (r < 0 && errno == EINTR) continue;
+            if (r <= 0) break;
+            got += uint64_t(r);
+        }
+    }
+    ::close(fd);
+    if (*size == want && got != want) return set_error(MXEC_E_IO, "IO error: read failed for " + p.string());
     return MXEC_OK;
 }
 
@@ -609,9 +736,16 @@ int mxec_put_object_chunked_sums(mxec_ctx* ctx, const char* ec_dir, uint64_t chu
 namespace {
 
 struct LoadedChunk {
-    std::vector<uint8_t> data;
+    Bytes data;
+    // When set, the chunk's bytes go straight to this caller buffer of
+    // exactly the manifest's size instead of `data` (one-shot GET: the chunk
+    // lands where it is served, no intermediate copy).
+    uint8_t* dst = nullptr;
+    uint64_t dst_size = 0;  // the file's size as read into dst
     int err = MXEC_OK;  // non-zero: this chunk fails the read that reaches it
     std::string msg;
+    const uint8_t* ptr() const { return dst ? dst : data.data(); }
+    uint64_t size() const { return dst ? dst_size : data.size(); }
 };
 
 // load_chunk_sync (:87-152) for chunks [first, last]: read, size check, one
@@ -625,10 +759,15 @@ struct LoadedChunk {
 // hashed in the SAME pass as the range; a chunk that only fails its digest
 // costs one more pass over the shards not yet hashed.  Either way each shard
 // is hashed once and every bad chunk of the range comes out of one decode.
+//
+// `dsts` (optional, one per chunk of the range, nullptr = none) places chunks
+// in caller memory (LoadedChunk::dst).
 int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_t first, uint32_t last,
-                std::vector<LoadedChunk>& out) {
+                std::vector<LoadedChunk>& out, const std::vector<uint8_t*>* dsts = nullptr) {
     const uint32_t n = last - first + 1;
     out.assign(n, LoadedChunk{});
+    if (dsts)
+        for (uint32_t c = 0; c < n; ++c) out[c].dst = (*dsts)[c];
     const bool parity = man.has_parity && man.parity_shards > 0;
     const int k = int(man.chunk_count);
     const int m = parity ? int(man.parity_shards) : 0;
@@ -638,16 +777,18 @@ int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_
     for (uint32_t c = 0; c < n; ++c) {
         const uint32_t idx = first + c;
         LoadedChunk& lc = out[c];
-        if (read_file(dir / chunk_name(idx), lc.data) != MXEC_OK) {
+        const int rc = lc.dst ? read_file_to(dir / chunk_name(idx), lc.dst, man.chunks[idx].size, &lc.dst_size)
+                              : read_file(dir / chunk_name(idx), lc.data);
+        if (rc != MXEC_OK) {
             lc.err = MXEC_E_IO;
             lc.msg = "failed to read chunk " + std::to_string(idx) + ": " + mxec::last_error();
             known_bad = true;
             continue;
         }
-        if (lc.data.size() != man.chunks[idx].size) {
+        if (lc.size() != man.chunks[idx].size) {
             lc.err = MXEC_E_INTEGRITY;
             lc.msg = "chunk " + std::to_string(idx) + " size mismatch: expected " +
-                     std::to_string(man.chunks[idx].size) + ", got " + std::to_string(lc.data.size());
+                     std::to_string(man.chunks[idx].size) + ", got " + std::to_string(lc.size());
             known_bad = true;
         }
     }
@@ -658,14 +799,14 @@ int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_
     auto want_len = [&](int i) {
         return size_t(i < k ? std::min<uint64_t>(man.chunks[size_t(i)].size, shard) : shard);
     };
-    std::vector<std::vector<uint8_t>> extra(parity ? size_t(total) : 0);
+    std::vector<Bytes> extra(parity ? size_t(total) : 0);
     std::vector<uint8_t> extra_loaded(extra.size(), 0), verified(extra.size(), 0);
     bool extra_read = false;
     auto read_extra = [&] {
         extra_read = true;
         for (int i = 0; i < total; ++i) {
             if (i >= int(first) && i <= int(last)) continue;
-            std::vector<uint8_t>& d = extra[size_t(i)];
+            Bytes& d = extra[size_t(i)];
             extra_loaded[size_t(i)] =
                 read_file(dir / chunk_name(uint32_t(i)), d) == MXEC_OK && d.size() == want_len(i);
         }
@@ -679,8 +820,8 @@ int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_
         if (range)
             for (uint32_t c = 0; c < n; ++c)
                 if (!out[c].err) {
-                    hp.push_back(out[c].data.empty() ? reinterpret_cast<const uint8_t*>("") : out[c].data.data());
-                    hl.push_back(out[c].data.size());
+                    hp.push_back(out[c].size() == 0 ? reinterpret_cast<const uint8_t*>("") : out[c].ptr());
+                    hl.push_back(out[c].size());
                     who.push_back(int(c));
                 }
         for (size_t i = 0; i < extra.size(); ++i)
@@ -709,6 +850,85 @@ int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_
         }
         return MXEC_OK;
     };
+    // try_reconstruct_data_chunk (:157-226) over every shard at once: the
+    // buffers hold each shard's real bytes (the kernels read past a shard's
+    // length as zero = Vec::resize(shard_size)).  Present shards are passed
+    // in place (the decode only reads them); missing ones get uninitialised
+    // buffers the decode overwrites whole.  verify = true: the shards are not
+    // hashed yet, so mxec_reconstruct hashes every present one against the
+    // manifest in the same upload (a mismatch is one more erasure) -- one
+    // upload, one hash launch, one decode for a range with a known-bad chunk.
+    // Returns MXEC_OK with every range chunk good or carrying its error;
+    // with verify, 1 when too few shards verified (the caller then finds out
+    // chunk by chunk).
+    auto decode = [&](bool verify) -> int {
+        std::vector<Bytes> bufs(static_cast<size_t>(total));
+        std::vector<uint8_t*> ptrs(static_cast<size_t>(total));
+        std::vector<size_t> lens(static_cast<size_t>(total));
+        std::vector<uint8_t> present(static_cast<size_t>(total), 0);
+        std::vector<uint8_t> expected(verify ? size_t(total) * 32 : 0);
+        for (int i = 0; i < total; ++i) {
+            const size_t w = want_len(i);
+            Bytes* b = &bufs[size_t(i)];
+            bool have = false;
+            uint8_t* ext = nullptr;
+            if (i >= int(first) && i <= int(last)) {
+                LoadedChunk& lc = out[size_t(i) - first];
+                have = !lc.err;
+                if (lc.dst) ext = lc.dst;  // exactly chunks[i].size == want_len(i) bytes
+                else if (have) b = &lc.data;
+            } else if (verify ? extra_loaded[size_t(i)] : verified[size_t(i)]) {
+                have = true;
+                b = &extra[size_t(i)];
+            }
+            if (have && verify && !unhex32(man.chunks[size_t(i)].sha256, &expected[size_t(i) * 32]))
+                have = false;  // an unparsable digest never matches
+            present[size_t(i)] = have ? 1 : 0;
+            lens[size_t(i)] = w;
+            if (ext) {
+                ptrs[size_t(i)] = w ? ext : nullptr;
+                continue;
+            }
+            if (!have) b->resize(w);
+            ptrs[size_t(i)] = b->empty() ? nullptr : b->data();
+        }
+        // Zero-length shards still need a non-null pointer for the C API.
+        uint8_t dummy = 0;
+        for (auto& p : ptrs)
+            if (!p) p = &dummy;
+        int np = 0;
+        const int rc = mxec_reconstruct(ctx, k, m, shard, ptrs.data(), lens.data(),
+                                        verify ? reinterpret_cast<const uint8_t(*)[32]>(expected.data()) : nullptr,
+                                        present.data(), MXEC_F_DATA_ONLY, &np);
+        if (verify && rc == MXEC_E_TOO_FEW_SHARDS_PRESENT) return 1;
+        const std::string msg = rc ? std::string(mxec::last_error()) : std::string();
+        for (uint32_t c = 0; c < n; ++c) {
+            LoadedChunk& lc = out[c];
+            if (!lc.err) continue;  // good, or (verify) rebuilt in place after a mismatch
+            if (rc) {
+                lc.msg = msg;
+                lc.err = rc;
+                continue;
+            }
+            const uint32_t idx = first + c;
+            const size_t real = size_t(std::min<uint64_t>(man.chunks[idx].size, shard));
+            if (lc.dst) {
+                lc.dst_size = real;
+            } else {
+                bufs[idx].resize(real);
+                lc.data.swap(bufs[idx]);
+            }
+            lc.err = MXEC_OK;
+            lc.msg.clear();
+        }
+        return MXEC_OK;
+    };
+    if (parity && known_bad) {
+        const int rc = decode(true);
+        if (rc <= 0) return rc;
+        // Too few shards verified: hash shard by shard to give each range
+        // chunk its own error (or rebuild from what did verify).
+    }
     MXEC_TRY(hash_pass(true));
     if (!parity) return MXEC_OK;
     std::vector<uint32_t> bad;
@@ -719,52 +939,7 @@ int load_chunks(mxec_ctx* ctx, const fs::path& dir, const Manifest& man, uint32_
         read_extra();
         MXEC_TRY(hash_pass(false));
     }
-    // try_reconstruct_data_chunk (:157-226) from the verified shards: the
-    // buffers hold each shard's real bytes (the kernels read past a shard's
-    // length as zero = Vec::resize(shard_size)); no digest is recomputed.
-    std::vector<std::vector<uint8_t>> bufs(static_cast<size_t>(total));
-    std::vector<uint8_t*> ptrs(static_cast<size_t>(total));
-    std::vector<size_t> lens(static_cast<size_t>(total));
-    std::vector<uint8_t> present(static_cast<size_t>(total), 0);
-    for (int i = 0; i < total; ++i) {
-        const size_t w = want_len(i);
-        std::vector<uint8_t>& b = bufs[size_t(i)];
-        if (i >= int(first) && i <= int(last)) {
-            LoadedChunk& lc = out[size_t(i) - first];
-            if (!lc.err) {
-                b = lc.data;  // size == chunks[i].size == want_len(i)
-                present[size_t(i)] = 1;
-            }
-        } else if (verified[size_t(i)]) {
-            b.swap(extra[size_t(i)]);
-            present[size_t(i)] = 1;
-        }
-        if (!present[size_t(i)]) b.assign(w, 0);
-        lens[size_t(i)] = w;
-        ptrs[size_t(i)] = b.empty() ? nullptr : b.data();
-    }
-    // Zero-length shards still need a non-null pointer for the C API.
-    uint8_t dummy = 0;
-    for (auto& p : ptrs)
-        if (!p) p = &dummy;
-    int np = 0;
-    const int rc = mxec_reconstruct(ctx, k, m, shard, ptrs.data(), lens.data(), nullptr, present.data(),
-                                    MXEC_F_DATA_ONLY, &np);
-    const std::string msg = rc ? std::string(mxec::last_error()) : std::string();
-    for (uint32_t c : bad) {
-        LoadedChunk& lc = out[c];
-        if (rc) {
-            lc.err = rc;
-            lc.msg = msg;
-            continue;
-        }
-        const uint32_t idx = first + c;
-        const size_t real = size_t(std::min<uint64_t>(man.chunks[idx].size, shard));
-        lc.data.assign(bufs[idx].begin(), bufs[idx].begin() + long(real));
-        lc.err = MXEC_OK;
-        lc.msg.clear();
-    }
-    return MXEC_OK;
+    return decode(false);
 }
 
 }  // namespace
@@ -836,7 +1011,7 @@ int64_t mxec_reader_read(mxec_reader* r, uint8_t* buf, uint64_t cap) {
         r->pos += take;
         r->remaining -= take;
         if (r->pos >= c.data.size()) {
-            c.data = std::vector<uint8_t>();
+            c.data = Bytes();
             ++r->bi;
             r->pos = 0;
         }
@@ -850,17 +1025,47 @@ int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, 
                             uint64_t out_cap, uint64_t* out_len) {
     if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
     *out_len = 0;
+    // The reader's semantics (mxec_reader_open / _read over the whole range
+    // in one batch), with every chunk the range covers whole read straight
+    // into its place in `out`: no intermediate chunk buffer, no copy out.
     mxec_reader* r = nullptr;
     MXEC_TRY(mxec_reader_open(ctx, ec_dir, offset, length, uint64_t(1) << 40, &r));
     std::unique_ptr<mxec_reader, void (*)(mxec_reader*)> guard(r, mxec_reader_close);
     if (r->remaining > out_cap || (r->remaining && !out))
         return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
-    while (r->remaining > 0) {
-        const int64_t n = mxec_reader_read(r, out + *out_len, out_cap - *out_len);
-        if (n < 0) return int(n);
-        if (n == 0) break;
-        *out_len += uint64_t(n);
+    if (r->remaining == 0) return MXEC_OK;
+    const Manifest& man = r->man;
+    const uint32_t first = r->next, last = r->end;
+    // Where each chunk's bytes are served: the first from `skip`, the rest
+    // whole, in order, until `remaining` runs out (mxec_reader_read).
+    std::vector<uint8_t*> dsts(last - first + 1, nullptr);
+    uint64_t pos = 0, left = r->remaining;
+    for (uint32_t c = first; c <= last && left; ++c) {
+        const uint64_t sz = man.chunks[c].size;
+        const uint64_t from = c == first ? r->skip : 0;
+        const uint64_t take = std::min(sz > from ? sz - from : 0, left);
+        if (from == 0 && take == sz && sz > 0) dsts[c - first] = out + pos;
+        pos += take;
+        left -= take;
     }
+    std::vector<LoadedChunk> batch;
+    MXEC_TRY(load_chunks(ctx, r->dir, man, first, last, batch, &dsts));
+    pos = 0;
+    left = r->remaining;
+    for (uint32_t c = first; c <= last && left; ++c) {
+        const LoadedChunk& lc = batch[c - first];
+        if (lc.err) {  // bytes before it are served, then the error (reader semantics)
+            *out_len = pos;
+            return set_error(lc.err, lc.msg);
+        }
+        const uint64_t from = c == first ? r->skip : 0;
+        const uint64_t sz = lc.size();
+        const uint64_t take = std::min(sz > from ? sz - from : 0, left);
+        if (!lc.dst && take) std::memcpy(out + pos, lc.data.data() + from, take);
+        pos += take;
+        left -= take;
+    }
+    *out_len = pos;
     return MXEC_OK;
 }
 

@@ -224,15 +224,17 @@ int mxec_body_sums_batch(mxec_ctx* ctx, const uint8_t* const* bodies, const uint
         auto* base = static_cast<uint8_t*>(slot.shards.p);
         std::vector<const uint8_t*> p(n);
         std::vector<uint64_t> l(lens, lens + n);
+        std::vector<UploadSeg> up;
         for (uint64_t i = 0; i < n; ++i) {
             p[i] = base + off[i];
-            if (lens[i]) MXEC_HIP(hipMemcpyAsync(base + off[i], bodies[i], lens[i], hipMemcpyHostToDevice, s));
+            if (lens[i]) up.push_back({off[i], bodies[i], lens[i]});
         }
+        MXEC_TRY(upload_segments(slot, s, base, up));
         auto* rec = static_cast<uint8_t*>(slot.digests.p);
         MXEC_TRY(run_body_sums(*ds.d, slot, s, p, l, which, rec, sizeof(mxec_body_sums)));
         MXEC_TRY(slot.hdig.ensure(n * sizeof(mxec_body_sums)));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, rec, n * sizeof(mxec_body_sums), hipMemcpyDeviceToHost, s));
-        MXEC_HIP(hipStreamSynchronize(s));
+        MXEC_TRY(slot_wait(slot, s));
         const auto* h = static_cast<const mxec_body_sums*>(slot.hdig.p);
         for (uint64_t i = 0; i < n; ++i) {
             if (which & MXEC_SUM_MD5) std::memcpy(out[i].md5, h[i].md5, 16);

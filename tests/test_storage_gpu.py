@@ -227,3 +227,81 @@ def test_reader_serves_healthy_prefix_then_fails(ctx, tmp_path):
     # a range that ends before the bad chunk never touches it
     with ctx.open_reader(str(ec), 10, 300) as r:
         assert _drain(r, 64) == body[10:310]
+
+
+def _get_raw(ctx, ec, off, ln, cap):
+    """mxec_get_object_chunked as called from C: (rc, bytes written)."""
+    import ctypes
+
+    import numpy as np
+
+    out = np.full(max(cap, 1), 0xEE, np.uint8)
+    n = ctypes.c_uint64(0)
+    rc = maxio_amd.lib().mxec_get_object_chunked(ctx.handle, str(ec).encode(), off,
+                                                  (1 << 64) - 1 if ln is None else ln,
+                                                  out.ctypes.data, cap, ctypes.byref(n))
+    return rc, out[: n.value].tobytes()
+
+
+def _drain_raw(ctx, ec, off, ln):
+    """The streaming reader over the same range: (rc, bytes before the error)."""
+    got = bytearray()
+    try:
+        with ctx.open_reader(str(ec), off, ln, 1 << 40) as r:
+            while True:
+                b = r.read(333)
+                if not b:
+                    return 0, bytes(got)
+                got += b
+    except maxio_amd.RSError as e:
+        return e.code, bytes(got)
+
+
+@pytest.mark.parametrize("damage", ["none", "missing", "corrupt", "short", "missing+corrupt",
+                                    "missing+parity", "too_many", "no_parity_corrupt"])
+def test_one_shot_get_matches_streaming_reader(ctx, tmp_path, damage):
+    """The one-shot GET reads whole chunks straight into the caller's buffer
+    and, with a chunk known bad before hashing, verifies and rebuilds in one
+    mxec_reconstruct call; the streaming reader goes chunk buffer by chunk
+    buffer.  Same bytes, same length, same error, over ranges that start and
+    end mid-chunk, for every kind of damage."""
+    import numpy as np
+
+    body = np.random.default_rng(9).integers(0, 256, 1000, dtype=np.uint8).tobytes()
+    ec = tmp_path / "o.ec"
+    ctx.put_object_chunked(str(ec), 128, 0 if damage == "no_parity_corrupt" else 3, body)  # k = 8
+
+    def corrupt(i):
+        raw = bytearray((ec / f"{i:06}").read_bytes())
+        raw[5] ^= 0x40
+        (ec / f"{i:06}").write_bytes(raw)
+
+    if damage == "missing":
+        os.remove(ec / "000002")
+    elif damage == "corrupt":
+        corrupt(4)
+    elif damage == "short":
+        (ec / "000001").write_bytes(bytes(7))
+    elif damage == "missing+corrupt":
+        os.remove(ec / "000002")
+        corrupt(6)
+    elif damage == "missing+parity":
+        os.remove(ec / "000000")
+        corrupt(9)
+        os.remove(ec / "000010")
+    elif damage == "too_many":
+        os.remove(ec / "000002")
+        corrupt(3)
+        corrupt(5)
+        os.remove(ec / "000008")
+    elif damage == "no_parity_corrupt":
+        corrupt(3)
+    for off, ln in [(0, None), (0, 1000), (130, 1), (127, 2), (200, 700), (256, 384), (999, 1), (5, 995)]:
+        want_len = len(body[off:] if ln is None else body[off:off + ln])
+        rc, got = _get_raw(ctx, ec, off, ln, want_len)
+        rrc, rgot = _drain_raw(ctx, ec, off, ln)
+        assert (rc, got) == (rrc, rgot), (damage, off, ln, rc, rrc, len(got), len(rgot))
+        if rc == 0:
+            assert got == (body[off:] if ln is None else body[off:off + ln])
+    if damage in ("none", "missing", "corrupt", "short", "missing+corrupt", "missing+parity"):
+        assert ctx.get_object_chunked(str(ec)) == body

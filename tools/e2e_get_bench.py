@@ -18,6 +18,7 @@ algorithm) over all k+m shard files, as chunk_reader.rs:157-226 does.
 from __future__ import annotations
 
 import argparse
+import threading
 import ctypes
 import hashlib
 import json
@@ -87,7 +88,7 @@ def main() -> int:
     base = tempfile.mkdtemp(prefix="mxec_get_", dir=args.dir)
     out = {"what": "GET end to end (page-cached shard files -> verified host buffer)",
            "k": k, "m": m, "chunk_size": S, "object_bytes": size, "objects": n,
-           "threads": args.threads, "scratch": base}
+           "threads": args.threads, "scratch": base, "host_cpus_allowed": len(os.sched_getaffinity(0))}
     try:
         ctx = maxio_amd.Context(streams_per_device=args.threads)
         rng = np.random.default_rng(7)
@@ -139,11 +140,13 @@ def main() -> int:
             out[f"cpu_reference_put_{threads}t"] = {"GiBps": round(total / GIB / el, 3),
                                                    "objects": args.cpu_objects}
         lib = maxio_amd.lib()
-        bufs = [np.zeros(size, np.uint8) for _ in range(args.threads)]
+        tls = threading.local()  # one output buffer per request thread
 
         def gpu_get(i_d):
             i, d = i_d
-            b = bufs[i % args.threads]
+            b = getattr(tls, "buf", None)
+            if b is None:
+                b = tls.buf = np.zeros(size, np.uint8)
             got = ctypes.c_uint64(0)
             rc = lib.mxec_get_object_chunked(ctx.handle, d.encode(), 0, (1 << 64) - 1,
                                              b.ctypes.data, size, ctypes.byref(got))
@@ -155,11 +158,18 @@ def main() -> int:
                 list(pool.map(fn, items[: threads]))  # warm
                 best = None
                 for _ in range(args.reps):
+                    c0 = os.times()
                     t = time.perf_counter()
                     total = sum(pool.map(fn, items))
                     el = time.perf_counter() - t
-                    best = el if best is None or el < best else best
+                    c1 = os.times()
+                    if best is None or el < best:
+                        best = el
+                        # host cores kept busy (user + system CPU time / wall)
+                        cores[0] = round((c1.user + c1.system - c0.user - c0.system) / el, 2)
             return total / GIB / best, best
+
+        cores = [None]
 
         items = list(enumerate(dirs))
 
@@ -174,9 +184,9 @@ def main() -> int:
             return total
 
         v, el = timed(host_read, items, args.threads)
-        out["host_file_reads_only"] = {"GiBps": round(v, 3), "s": round(el, 4)}
+        out["host_file_reads_only"] = {"GiBps": round(v, 3), "s": round(el, 4), "host_cores_busy": cores[0]}
         v, el = timed(gpu_get, items, args.threads)
-        out["gpu_healthy"] = {"GiBps": round(v, 3), "s": round(el, 4)}
+        out["gpu_healthy"] = {"GiBps": round(v, 3), "s": round(el, 4), "host_cores_busy": cores[0]}
         v1, el1 = timed(gpu_get, items[:16], 1)
         out["gpu_healthy_1thread"] = {"GiBps": round(v1, 3), "ms_per_object": round(el1 * 1e3 / 16, 2)}
         # degraded: delete `erasures` data chunks of every object
@@ -184,7 +194,8 @@ def main() -> int:
             for i in np.random.default_rng(o).choice(k, args.erasures, replace=False):
                 os.unlink(os.path.join(d, f"{int(i):06}"))
         v, el = timed(gpu_get, items, args.threads)
-        out["gpu_degraded"] = {"GiBps": round(v, 3), "s": round(el, 4), "erasures_per_object": args.erasures}
+        out["gpu_degraded"] = {"GiBps": round(v, 3), "s": round(el, 4), "erasures_per_object": args.erasures,
+                               "host_cores_busy": cores[0]}
         # bit-exactness of one degraded GET against the body written
         got = ctx.get_object_chunked(dirs[1])
         out["degraded_roundtrip_ok"] = got == block[1: 1 + size].tobytes()
