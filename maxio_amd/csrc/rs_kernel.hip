@@ -124,6 +124,94 @@ __device__ __forceinline__ void gstore16(gptr p, const uint32_t (&w)[4]) {
     else *q = v;
 }
 
+// Edge tiles: the list entries (object << 32 | fast tile index) are the fast
+// tiles that a length boundary or the shard end cuts through, or every tile
+// when a pointer is unaligned.  Each is walked in kEdgeTile steps with
+// byte-exact bounds on every input and output.  One step:
+template <int R>
+__device__ __forceinline__ void edge_step(
+    const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
+    const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
+    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
+    uint32_t k, uint32_t r_total, uint32_t row0, const uint64_t* __restrict__ edge_list,
+    uint32_t steps_per_tile, uint64_t tile_bytes, uint32_t aligned, uint64_t step) {
+    const uint64_t e = edge_list[step / steps_per_tile];
+    const uint32_t obj = uint32_t(e >> 32);
+    const uint64_t col = uint64_t(uint32_t(e)) * tile_bytes + (step % steps_per_tile) * kEdgeTile +
+                         threadIdx.x * 16;
+    if (col >= shard_size) return;
+    const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
+    uint32_t acc[1][4][R];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[0][w][i] = 0;
+    // Four inputs' loads in flight before their multiply-accumulates.
+    // Whole vectors load unconditionally from a global address (a safe
+    // dummy when the lane's vector is not whole) so the waits stay
+    // counted; the lane whose vector a length boundary cuts, and
+    // unaligned launches, take the byte path afterwards.
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(coef);
+    auto issue = [&](uint32_t j, Vec4& x, const uint8_t*& p, int64_t& valid) {
+        const uint64_t len = in_len[uint64_t(obj) * k + j];
+        valid = col < len ? int64_t(len - col) : 0;
+        p = in_ptrs[uint64_t(obj) * k + j] + col;
+        const bool full = aligned && valid >= 16;
+        x = gload16<false>(gcptr(full ? p : safe));
+    };
+    // After all four loads are issued: zero what was not a whole vector
+    // (selects, no branch), then the rare cut lane reads its bytes.
+    auto fixup = [&](Vec4& x, const uint8_t* p, int64_t valid) {
+        const bool full = aligned && valid >= 16;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) x.w[w] = full ? x.w[w] : 0u;
+        if (valid > 0 && !full) x = load_partial(p, valid, aligned != 0);
+    };
+    uint32_t j = 0;
+    for (; j + 4 <= k; j += 4) {
+        Vec4 x[4][1];
+        const uint8_t* p[4];
+        int64_t valid[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) issue(j + u, x[u][0], p[u], valid[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) fixup(x[u][0], p[u], valid[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mac_column<R, 1>(acc, x[u], tab + (j + u) * r_total * 8);
+    }
+    for (; j < k; ++j) {
+        Vec4 x[1];
+        const uint8_t* p;
+        int64_t valid;
+        issue(j, x[0], p, valid);
+        fixup(x[0], p, valid);
+        mac_column<R, 1>(acc, x, tab + j * r_total * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        uint64_t olen = out_len[uint64_t(obj) * r_total + row0 + i];
+        if (olen > shard_size) olen = shard_size;
+        if (col < olen) {
+            uint32_t o[4] = {acc[0][0][i], acc[0][1][i], acc[0][2][i], acc[0][3][i]};
+            store_partial(out_ptrs[uint64_t(obj) * r_total + row0 + i] + col, o, int64_t(olen - col),
+                          aligned != 0);
+        }
+    }
+}
+
+// The edge steps alone (unaligned launches: every tile is an edge tile).
+template <int R>
+__global__ __launch_bounds__(kThreads) void rs_apply_edge(
+    const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
+    const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
+    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
+    uint32_t k, uint32_t r_total, uint32_t row0, const uint64_t* __restrict__ edge_list,
+    uint32_t steps_per_tile, uint64_t tile_bytes, uint32_t aligned, uint64_t n_steps) {
+    for (uint64_t step = blockIdx.x; step < n_steps; step += gridDim.x)
+        edge_step<R>(in_ptrs, out_ptrs, in_len, out_len, coef, coef_off, shard_size, k, r_total, row0, edge_list,
+                     steps_per_tile, tile_bytes, aligned, step);
+}
+
 // Fast tiles: every tile of every object that no length boundary cuts
 // through (those are in the edge list and skipped here).  An input whose
 // length ends at or before the tile reads as zero without a load; an output
@@ -133,9 +221,18 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
     const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
-    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles) {
+    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles,
+    const uint64_t* __restrict__ edge_list, uint64_t n_edge_steps) {
     constexpr uint32_t kTile = kThreads * 16 * V;
-    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    // The edge steps come first in the grid-stride order, so they run side
+    // by side with the interior tiles instead of as a launch of their own
+    // (a few hundred latency-bound steps after the interior kernel drained:
+    // ~11 % of config 5's kernel time).
+    uint64_t item = blockIdx.x;
+    for (; item < n_edge_steps; item += gridDim.x)
+        edge_step<R>(in_ptrs, out_ptrs, in_len, out_len, coef, coef_off, shard_size, k, r_total, row0, edge_list,
+                     uint32_t(kTile / kEdgeTile), kTile, 1u, item);
+    for (uint64_t tile = item - n_edge_steps; tile < n_tiles; tile += gridDim.x) {
         const uint32_t obj = uint32_t(tile / tiles_per_obj);
         const uint64_t base = (tile - uint64_t(obj) * tiles_per_obj) * kTile;
         const uint64_t end = base + kTile;
@@ -196,89 +293,13 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     }
 }
 
-// Edge tiles: the list entries (object << 32 | fast tile index) are the fast
-// tiles that a length boundary or the shard end cuts through, or every tile
-// when a pointer is unaligned.  Each is walked in kEdgeTile steps with
-// byte-exact bounds on every input and output.
-template <int R>
-__global__ __launch_bounds__(kThreads) void rs_apply_edge(
-    const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
-    const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
-    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
-    uint32_t k, uint32_t r_total, uint32_t row0, const uint64_t* __restrict__ edge_list,
-    uint32_t steps_per_tile, uint64_t tile_bytes, uint32_t aligned, uint64_t n_steps) {
-    for (uint64_t step = blockIdx.x; step < n_steps; step += gridDim.x) {
-        const uint64_t e = edge_list[step / steps_per_tile];
-        const uint32_t obj = uint32_t(e >> 32);
-        const uint64_t col = uint64_t(uint32_t(e)) * tile_bytes + (step % steps_per_tile) * kEdgeTile +
-                             threadIdx.x * 16;
-        if (col >= shard_size) continue;
-        const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
-        uint32_t acc[1][4][R];
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-#pragma unroll
-            for (int i = 0; i < R; ++i) acc[0][w][i] = 0;
-        // Four inputs' loads in flight before their multiply-accumulates.
-        // Whole vectors load unconditionally from a global address (a safe
-        // dummy when the lane's vector is not whole) so the waits stay
-        // counted; the lane whose vector a length boundary cuts, and
-        // unaligned launches, take the byte path afterwards.
-        const uint8_t* safe = reinterpret_cast<const uint8_t*>(coef);
-        auto issue = [&](uint32_t j, Vec4& x, const uint8_t*& p, int64_t& valid) {
-            const uint64_t len = in_len[uint64_t(obj) * k + j];
-            valid = col < len ? int64_t(len - col) : 0;
-            p = in_ptrs[uint64_t(obj) * k + j] + col;
-            const bool full = aligned && valid >= 16;
-            x = gload16<false>(gcptr(full ? p : safe));
-        };
-        // After all four loads are issued: zero what was not a whole vector
-        // (selects, no branch), then the rare cut lane reads its bytes.
-        auto fixup = [&](Vec4& x, const uint8_t* p, int64_t valid) {
-            const bool full = aligned && valid >= 16;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) x.w[w] = full ? x.w[w] : 0u;
-            if (valid > 0 && !full) x = load_partial(p, valid, aligned != 0);
-        };
-        uint32_t j = 0;
-        for (; j + 4 <= k; j += 4) {
-            Vec4 x[4][1];
-            const uint8_t* p[4];
-            int64_t valid[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) issue(j + u, x[u][0], p[u], valid[u]);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) fixup(x[u][0], p[u], valid[u]);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) mac_column<R, 1>(acc, x[u], tab + (j + u) * r_total * 8);
-        }
-        for (; j < k; ++j) {
-            Vec4 x[1];
-            const uint8_t* p;
-            int64_t valid;
-            issue(j, x[0], p, valid);
-            fixup(x[0], p, valid);
-            mac_column<R, 1>(acc, x, tab + j * r_total * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            uint64_t olen = out_len[uint64_t(obj) * r_total + row0 + i];
-            if (olen > shard_size) olen = shard_size;
-            if (col < olen) {
-                uint32_t o[4] = {acc[0][0][i], acc[0][1][i], acc[0][2][i], acc[0][3][i]};
-                store_partial(out_ptrs[uint64_t(obj) * r_total + row0 + i] + col, o,
-                              int64_t(olen - col), aligned != 0);
-            }
-        }
-    }
-}
-
 template <int R, int V, bool NT>
 hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
+    const uint64_t n_edge_steps = a.n_edge * (uint64_t(kThreads) * 16 * V / kEdgeTile);
     hipLaunchKernelGGL((rs_apply_fast<R, V, NT>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                        a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.shard_size,
-                       a.k, a.r_total, a.row0, tiles_per_obj, n_tiles);
+                       a.k, a.r_total, a.row0, tiles_per_obj, n_tiles, a.edge_list, n_edge_steps);
     return hipGetLastError();
 }
 
@@ -289,8 +310,9 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
     if (a.aligned) {
         const uint32_t tiles_per_obj = uint32_t((a.shard_size + tile - 1) / tile);
         const uint64_t n_tiles = uint64_t(tiles_per_obj) * a.n_obj;
+        const uint64_t n_items = n_tiles + a.n_edge * (tile / kEdgeTile);
         uint64_t blocks = uint64_t(n_cus) * uint64_t(var.blocks_per_cu);
-        if (blocks > n_tiles) blocks = n_tiles;
+        if (blocks > n_items) blocks = n_items;
         hipError_t e = hipErrorInvalidValue;
         if (var.vecs == 1) e = var.nt ? launch_fast<R, 1, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                       : launch_fast<R, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
@@ -298,7 +320,7 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
                                            : launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                            : launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
-        if (e != hipSuccess) return e;
+        return e;  // edge steps ran inside the fast launch
     }
     if (a.n_edge) {
         const uint32_t steps = uint32_t(tile / kEdgeTile);
