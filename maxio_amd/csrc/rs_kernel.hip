@@ -22,8 +22,10 @@
 //  * Zero padding (the crate pads the short last chunk, filesystem.rs:1111)
 //    is never materialised: in the fast kernel an input whose length ends at
 //    or before a tile contributes zero and is not loaded; only the few tiles
-//    that a length boundary cuts through go to the byte-exact edge kernel,
-//    from a per-launch list built by the host (edge_tiles()).
+//    that a length boundary cuts through take the byte-exact edge path, from
+//    a per-launch list built by the host (run_rs) -- as the first items of
+//    the same grid-stride launch when every pointer is aligned, as a launch
+//    of their own otherwise.
 #include "kernels.hpp"
 
 namespace mxec {
