@@ -71,11 +71,17 @@ std::string chunk_name(uint32_t index) {
 }
 
 int write_file(const fs::path& p, const uint8_t* data, size_t len) {
-    std::ofstream f(p, std::ios::binary | std::ios::trunc);
-    if (!f) return set_error(MXEC_E_IO, "IO error: cannot create " + p.string() + ": " + std::strerror(errno));
-    if (len) f.write(reinterpret_cast<const char*>(data), std::streamsize(len));
-    f.flush();
-    if (!f) return set_error(MXEC_E_IO, "IO error: write failed for " + p.string());
+    const int fd = ::open(p.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) return set_error(MXEC_E_IO, "IO error: cannot create " + p.string() + ": " + std::strerror(errno));
+    size_t put = 0;
+    while (put < len) {
+        const ssize_t w = ::write(fd, data + put, len - put);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) break;
+        put += size_t(w);
+    }
+    const bool ok = put == len;
+    if (::close(fd) != 0 || !ok) return set_error(MXEC_E_IO, "IO error: write failed for " + p.string());
     return MXEC_OK;
 }
 
@@ -478,7 +484,7 @@ int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir, uint64_t ch
         return MXEC_OK;
     }());
     const fs::path dir(ec_dir);
-    std::vector<std::vector<uint8_t>> data(static_cast<size_t>(k));
+    std::vector<Bytes> data(static_cast<size_t>(k));
     std::vector<const uint8_t*> dp(static_cast<size_t>(k));
     std::vector<size_t> dl(static_cast<size_t>(k));
     for (int j = 0; j < k; ++j) {
@@ -487,7 +493,9 @@ int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir, uint64_t ch
         dp[size_t(j)] = data[size_t(j)].data();
         dl[size_t(j)] = data[size_t(j)].size();
     }
-    std::vector<std::vector<uint8_t>> parity(static_cast<size_t>(m > 0 ? m : 0), std::vector<uint8_t>(chunk_size));
+    // Parity buffers: the encode writes every byte (no zero-fill needed).
+    std::vector<Bytes> parity(static_cast<size_t>(m > 0 ? m : 0));
+    for (auto& b : parity) b.resize(chunk_size);
     std::vector<uint8_t*> pp(parity.size());
     for (size_t i = 0; i < parity.size(); ++i) pp[i] = parity[i].data();
     std::vector<uint8_t> dig(size_t(k + m) * 32);
@@ -539,7 +547,7 @@ int put_chunked_buffer(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, u
     man.chunk_size = chunk_size;
     man.chunk_count = uint32_t(k);
     std::vector<uint8_t> dig(size_t(k + m) * 32);
-    std::vector<std::vector<uint8_t>> parity;
+    std::vector<Bytes> parity;
     if (has_parity) {
         // The reference writes the data chunks first (write_chunk), then
         // hits the k+m guard inside compute_and_write_parity.
@@ -548,7 +556,8 @@ int put_chunked_buffer(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, u
             return set_error(MXEC_E_TOO_MANY_SHARDS_255,
                              "too many shards: " + std::to_string(k) + " data + " + std::to_string(m) + " parity = " +
                                  std::to_string(k + m) + " > 255 (GF(2^8) limit). Increase --chunk-size");
-        parity.assign(size_t(m), std::vector<uint8_t>(chunk_size));
+        parity.resize(size_t(m));  // the encode writes every byte
+        for (auto& b : parity) b.resize(chunk_size);
         std::vector<uint8_t*> pp(static_cast<size_t>(m));
         for (int i = 0; i < m; ++i) pp[size_t(i)] = parity[size_t(i)].data();
         MXEC_TRY(mxec_encode(ctx, k, m, chunk_size, dp.data(), dl.data(), pp.data(),

@@ -107,10 +107,33 @@ def main() -> int:
         # overwrites the same files.
         with ThreadPoolExecutor(args.threads) as pool:
             list(pool.map(gpu_put, range(n)))
+            c0 = os.times()
             t = time.perf_counter()
             total = sum(pool.map(gpu_put, range(n)))
             el = time.perf_counter() - t
-        out["gpu_put"] = {"GiBps": round(total / GIB / el, 3), "s": round(el, 4)}
+            c1 = os.times()
+        out["gpu_put"] = {"GiBps": round(total / GIB / el, 3), "s": round(el, 4),
+                          "host_cores_busy": round((c1.user + c1.system - c0.user - c0.system) / el, 2)}
+
+        def host_write(o):
+            """The file writes of a PUT alone (k data + m parity-sized chunk
+            files, rewritten in place as the timed PUT pass does): what the
+            filesystem can take."""
+            body = block[o % 4096: o % 4096 + size]
+            for i in range(k + m):
+                with open(os.path.join(dirs[o], f"{i:06}"), "wb") as f:
+                    f.write(body[(i % k) * S:(i % k + 1) * S])
+            return size
+
+        with ThreadPoolExecutor(args.threads) as pool:
+            c0 = os.times()
+            t = time.perf_counter()
+            total = sum(pool.map(host_write, range(n)))
+            el = time.perf_counter() - t
+            c1 = os.times()
+        out["host_file_writes_only"] = {"GiBps": round(total / GIB / el, 3), "s": round(el, 4),
+                                        "host_cores_busy": round((c1.user + c1.system - c0.user - c0.system) / el, 2)}
+        list(ThreadPoolExecutor(args.threads).map(gpu_put, range(n)))  # restore the objects
 
         def ref_put(o):
             """filesystem.rs:686-828 with the crate algorithm (oracle/) and
