@@ -151,14 +151,11 @@ ShaCombiner* combiner_of(Device& d) {
         auto c = std::make_shared<ShaCombiner>();
         for (size_t i = 0; i < combine_streams(); ++i) {
             auto sl = std::make_unique<Slot>();
-            if (combine_priority()) {
-                int lo = 0, hi = 0;
-                if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-                    hipStreamCreateWithPriority(&sl->stream, hipStreamNonBlocking, hi) != hipSuccess)
-                    return nullptr;
-            } else if (hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) {
-                return nullptr;
-            }
+            int least = 0, greatest = 0;
+            const bool prio = combine_priority() &&
+                              hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+                              hipStreamCreateWithPriority(&sl->stream, hipStreamNonBlocking, greatest) == hipSuccess;
+            if (!prio && hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
             c->free_slots.push_back(sl.get());
             c->slots.push_back(std::move(sl));
         }
