@@ -266,6 +266,9 @@ int main(int argc, char** argv) {
     const bool sha_only = argc > 2 && !std::strcmp(argv[2], "sha");
     const bool sha_big = argc > 2 && !std::strcmp(argv[2], "shabig");
     const bool hbm_only = argc > 2 && !std::strcmp(argv[2], "hbm");
+    // `kernel_lab N ns`: every geometry of the north-star shape (k=8 m=4, 1 MiB)
+    // against the 2:1 no-math pattern, two rounds.
+    const bool ns_only = argc > 2 && !std::strcmp(argv[2], "ns");
     // ---- calibration ----
     if (hbm_only) {
         const uint64_t nvec = pool / 16, half = pool / 2 / 16;
@@ -351,6 +354,9 @@ int main(int argc, char** argv) {
             // order were measured here and dropped: profiles/r1_lab_rs_glds_variants.jsonl,
             // profiles/r1_lab_hbm_ceilings_tile_order.jsonl.)
             for (int bpc : {8, 16, 32}) vs.push_back(mxec::RsVariant{4, true, bpc});
+        } else if (ns_only) {
+            for (int v : {2, 4})
+                for (int bpc : {8, 16, 32, 64}) vs.push_back(mxec::RsVariant{v, true, bpc});
         } else if (full) {
             for (int v : {1, 2, 4})
                 for (bool nt : {false, true})
@@ -420,6 +426,14 @@ int main(int argc, char** argv) {
             sha(n, 1ull << 20, nm, 2);
             std::snprintf(nm, sizeof nm, "%llu x 1 MiB one-wave form", (unsigned long long)n);
             sha(n, 1ull << 20, nm, 1);
+        }
+        CK(hipFree(buf));
+        return 0;
+    }
+    if (ns_only) {
+        for (int rep = 0; rep < 2; ++rep) {
+            sweep(Shape{8, 4, 1ull << 20, n2 * 60 / 12}, "k8m4 S1MiB (north star)", true);
+            sweep(Shape{4, 2, S2, n2}, "k4m2 S10MiB (cfg2)", true);
         }
         CK(hipFree(buf));
         return 0;
