@@ -370,7 +370,11 @@ int mxec_complete_multipart_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir,
  * chunk_reader.rs:35-152): verified chunks, RS recovery of bad ones.
  * out must hold manifest total_size bytes; *out_len receives it.
  * offset/length select a range as with_range (:52-82); length UINT64_MAX = to
- * the end. */
+ * the end.  Chunks the range covers whole are read straight into out and
+ * verified there, so out must not be touched by anyone else during the call;
+ * on an error *out_len is the number of bytes served before the bad chunk
+ * (the streaming reader's prefix) and the bytes of out past it are
+ * unspecified. */
 int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset,
                             uint64_t length, uint8_t* out, uint64_t out_cap,
                             uint64_t* out_len);
