@@ -420,7 +420,7 @@ int main(int argc, char** argv) {
     };
     if (sha_big) {
         // Many 1 MiB messages (combined GET verification): forms by batch size.
-        for (uint64_t n : {20480ull, 32768ull, 40960ull, 57344ull}) {
+        for (uint64_t n : {16384ull, 49152ull, 65536ull, 81920ull}) {
             char nm[96];
             std::snprintf(nm, sizeof nm, "%llu x 1 MiB split form", (unsigned long long)n);
             sha(n, 1ull << 20, nm, 2);
