@@ -691,7 +691,7 @@ def main() -> int:
     if args.extra and rank == 0 and args.config == "2":
         extra = secondary(ctx, torch, dev, sh, w)
     cpu = cpu_all = None
-    if rank == 0 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the CPU leg runs at N=1 only
         spec = w.cpu_work()
         if spec is not None:
             work, per_call, what = spec
