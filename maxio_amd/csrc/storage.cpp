@@ -19,6 +19,7 @@
 
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <filesystem>
 #include <fstream>
@@ -1057,22 +1058,38 @@ int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, 
         pos += take;
         left -= take;
     }
+    // Windows of at most kGetWindow bytes of chunks (at least one chunk): one
+    // hash round trip per window, and a slot's device staging stays bounded
+    // however large the object.
+    // MXEC_GET_WINDOW (bytes) overrides the window (tests).
+    const char* we = getenv("MXEC_GET_WINDOW");
+    const uint64_t kGetWindow = we && *we ? std::max<uint64_t>(1, strtoull(we, nullptr, 10)) : uint64_t(1) << 30;
     std::vector<LoadedChunk> batch;
-    MXEC_TRY(load_chunks(ctx, r->dir, man, first, last, batch, &dsts));
     pos = 0;
     left = r->remaining;
-    for (uint32_t c = first; c <= last && left; ++c) {
-        const LoadedChunk& lc = batch[c - first];
-        if (lc.err) {  // bytes before it are served, then the error (reader semantics)
+    for (uint32_t w0 = first; w0 <= last && left;) {
+        uint32_t w1 = w0;
+        uint64_t bytes = man.chunks[w0].size;
+        while (w1 < last && bytes + man.chunks[w1 + 1].size <= kGetWindow) bytes += man.chunks[++w1].size;
+        const std::vector<uint8_t*> wd(dsts.begin() + (w0 - first), dsts.begin() + (w1 - first) + 1);
+        if (const int rc = load_chunks(ctx, r->dir, man, w0, w1, batch, &wd)) {
             *out_len = pos;
-            return set_error(lc.err, lc.msg);
+            return rc;
         }
-        const uint64_t from = c == first ? r->skip : 0;
-        const uint64_t sz = lc.size();
-        const uint64_t take = std::min(sz > from ? sz - from : 0, left);
-        if (!lc.dst && take) std::memcpy(out + pos, lc.data.data() + from, take);
-        pos += take;
-        left -= take;
+        for (uint32_t c = w0; c <= w1 && left; ++c) {
+            const LoadedChunk& lc = batch[c - w0];
+            if (lc.err) {  // bytes before it are served, then the error (reader semantics)
+                *out_len = pos;
+                return set_error(lc.err, lc.msg);
+            }
+            const uint64_t from = c == first ? r->skip : 0;
+            const uint64_t sz = lc.size();
+            const uint64_t take = std::min(sz > from ? sz - from : 0, left);
+            if (!lc.dst && take) std::memcpy(out + pos, lc.data.data() + from, take);
+            pos += take;
+            left -= take;
+        }
+        w0 = w1 + 1;
     }
     *out_len = pos;
     return MXEC_OK;

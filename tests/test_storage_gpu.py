@@ -257,15 +257,20 @@ def _drain_raw(ctx, ec, off, ln):
         return e.code, bytes(got)
 
 
+@pytest.mark.parametrize("window", [None, "1", "300"])
 @pytest.mark.parametrize("damage", ["none", "missing", "corrupt", "short", "missing+corrupt",
                                     "missing+parity", "too_many", "no_parity_corrupt"])
-def test_one_shot_get_matches_streaming_reader(ctx, tmp_path, damage):
+def test_one_shot_get_matches_streaming_reader(ctx, tmp_path, damage, window, monkeypatch):
     """The one-shot GET reads whole chunks straight into the caller's buffer
     and, with a chunk known bad before hashing, verifies and rebuilds in one
     mxec_reconstruct call; the streaming reader goes chunk buffer by chunk
     buffer.  Same bytes, same length, same error, over ranges that start and
-    end mid-chunk, for every kind of damage."""
+    end mid-chunk, for every kind of damage, with the one-shot GET's chunk
+    window at its default, one chunk (window 1) and two chunks (300)."""
     import numpy as np
+
+    if window is not None:
+        monkeypatch.setenv("MXEC_GET_WINDOW", window)
 
     body = np.random.default_rng(9).integers(0, 256, 1000, dtype=np.uint8).tobytes()
     ec = tmp_path / "o.ec"
