@@ -42,6 +42,9 @@ struct ShaCombiner {
     std::vector<Req*> pending;
     bool gathering = false;  // a leader is collecting its batch
     size_t last_batch = 1;   // requests in the previous launch
+    size_t pending_msgs = 0;   // messages of `pending`
+    size_t inflight_msgs = 0;  // messages of the launches running now
+    size_t lane_limit = 0;     // a second lane opens only below this (see below)
     // Launch lanes: up to slots.size() batches in flight at once (default
     // one), each on its own stream and buffers, so that with more than one a
     // request arriving while a launch runs starts its own instead of queueing
@@ -122,14 +125,17 @@ long gather_max_us() {
     return us;
 }
 
-// MXEC_COMBINE_STREAMS: launches in flight per device (default 1: two or
-// three lanes measured slower everywhere -- config 3c 509 -> 344 / 381
-// GiB/s, 64-thread GET 6.8 -> 5.6 / 4.2 GiB/s, profiles/r1_combine_lanes.txt
-// -- since concurrent issue-bound launches share the SIMDs and the smaller
-// batches end no sooner).
+// MXEC_COMBINE_STREAMS: launches in flight per device (default 2).  A second
+// launch starts beside a running one only while both together stay under
+// one workgroup per CU of messages (lane_limit): light request traffic then
+// no longer waits out the batch in flight (16-thread GET 2.5 -> 3.5 GiB/s,
+// profiles/r1_combine_lanes2.txt), while chip-filling batches still go one
+// at a time -- unconditional lanes split them and issue-bound launches side
+// by side share the SIMDs (config 3c 509 -> 344 GiB/s with two lanes,
+// profiles/r1_combine_lanes.txt).
 size_t combine_streams() {
     static const size_t n = [] {
-        const long v = env_us("MXEC_COMBINE_STREAMS", 1);
+        const long v = env_us("MXEC_COMBINE_STREAMS", 2);
         return size_t(v < 1 ? 1 : v > 4 ? 4 : v);
     }();
     return n;
@@ -159,6 +165,7 @@ ShaCombiner* combiner_of(Device& d) {
             c->free_slots.push_back(sl.get());
             c->slots.push_back(std::move(sl));
         }
+        c->lane_limit = size_t(d.n_cus) * 64;
         d.comb = c;
     }
     return static_cast<ShaCombiner*>(d.comb.get());
@@ -189,11 +196,13 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     me.out = out;
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&me);
+    c->pending_msgs += ptrs.size();
     if (c->gathering) c->cv_gather.notify_one();  // the gathering leader may be waiting for us
     while (!me.done) {
         // Lead when a launch lane is free and nobody else is gathering (a
         // gathering leader takes this request too); else wait.
-        if (c->gathering || c->free_slots.empty()) {
+        if (c->gathering || c->free_slots.empty() ||
+            (c->inflight_msgs > 0 && c->inflight_msgs + c->pending_msgs > c->lane_limit)) {
             c->cv_done.wait(lk);
             continue;
         }
@@ -212,6 +221,9 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
                            [&] { return c->pending.size() >= std::max<size_t>(want, 2); });
         std::vector<ShaCombiner::Req*> batch;
         batch.swap(c->pending);
+        size_t batch_msgs = c->pending_msgs;
+        c->pending_msgs = 0;
+        c->inflight_msgs += batch_msgs;
         c->last_batch = batch.size();
         c->gathering = false;
         Slot* slot_run = c->free_slots.back();
@@ -219,7 +231,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // Requests that arrived while this leader gathered are in its batch,
         // so nobody waits for the gathering to end unless another lane is
         // free for them.
-        if (!c->free_slots.empty()) c->cv_done.notify_all();
+        if (!c->free_slots.empty() && c->inflight_msgs + c->pending_msgs <= c->lane_limit) c->cv_done.notify_all();
         lk.unlock();
         int rc = MXEC_OK;
         try {
@@ -239,6 +251,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
             r->done = true;
         }
         c->free_slots.push_back(slot_run);
+        c->inflight_msgs -= batch_msgs;
         c->cv_done.notify_all();
     }
     if (me.rc) return set_error(me.rc, me.msg);

@@ -1119,14 +1119,14 @@ int mxec_get_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, const u
     const uint64_t ct_off = f0 * fl;
     const uint64_t ct_len = std::min<uint64_t>(man.total_size - std::min(man.total_size, ct_off), (f1 - f0 + 1) * fl);
     if (end - offset > out_cap || !out) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
-    std::vector<uint8_t> ct(size_t(ct_len) + 1);
+    Bytes ct(size_t(ct_len) + 1);  // every byte written by the GET below
     uint64_t got = 0;
     MXEC_TRY(mxec_get_object_chunked(ctx, ec_dir, ct_off, ct_len, ct.data(), ct_len, &got));
     const uint64_t nf = f1 - f0 + 1;
     const uint64_t pt_lo = f0 * frame_size, pt_hi = std::min<uint64_t>(plaintext_size, (f1 + 1) * uint64_t(frame_size));
     std::vector<uint8_t> aads(size_t(nf) * 32);
     MXEC_TRY(mxec_frame_aads(ctx, aad_prefix, aad_prefix_len, f0, nf, reinterpret_cast<uint8_t(*)[32]>(aads.data())));
-    std::vector<uint8_t> pt(size_t(pt_hi - pt_lo) + 1);
+    Bytes pt(size_t(pt_hi - pt_lo) + 1);
     uint64_t n = 0;
     MXEC_TRY(mxec_frames_decrypt(ctx, key, f0, aads.data(), 32, frame_size, ct.data(), got, pt_hi - pt_lo, pt.data(),
                                  pt.size(), &n));
