@@ -46,9 +46,9 @@ struct ShaCombiner {
     size_t inflight_msgs = 0;  // messages of the launches running now
     size_t lane_limit = 0;     // a second lane opens only below this (see below)
     // Launch lanes: up to slots.size() batches in flight at once (default
-    // one), each on its own stream and buffers, so that with more than one a
-    // request arriving while a launch runs starts its own instead of queueing
-    // behind it (GPU_MAX_HW_QUEUES = 4 bounds the lanes).
+    // two), each on its own stream and buffers, so that a request arriving
+    // while a small launch runs starts its own instead of queueing behind it
+    // (lane_limit keeps chip-filling batches one at a time).
     std::vector<std::unique_ptr<Slot>> slots;
     std::vector<Slot*> free_slots;
     uint64_t batches = 0, messages = 0;  // guarded by mu
