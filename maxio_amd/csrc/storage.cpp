@@ -29,9 +29,11 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/maxio_ec.h"
+#include "ops.hpp"
 #include "runtime.hpp"
 
 namespace fs = std::filesystem;
@@ -463,51 +465,55 @@ extern "C" {
 
 int mxec_write_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t index, const uint8_t* data, size_t len,
                      mxec_chunk_info* out) {
-    if (!ec_dir || !out || (len && !data)) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    uint8_t dig[1][32];
-    const uint8_t* b = data ? data : reinterpret_cast<const uint8_t*>("");
-    MXEC_TRY(mxec_sha256_batch(ctx, &b, &len, 1, dig));
-    MXEC_TRY(write_file(fs::path(ec_dir) / chunk_name(index), data, len));
-    fill_info(out, index, len, dig[0], 0);
-    return MXEC_OK;
+    return mxec::guarded([&]() -> int {
+        if (!ec_dir || !out || (len && !data)) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        uint8_t dig[1][32];
+        const uint8_t* b = data ? data : reinterpret_cast<const uint8_t*>("");
+        MXEC_TRY(mxec_sha256_batch(ctx, &b, &len, 1, dig));
+        MXEC_TRY(write_file(fs::path(ec_dir) / chunk_name(index), data, len));
+        fill_info(out, index, len, dig[0], 0);
+        return MXEC_OK;
+    });
 }
 
 int mxec_compute_and_write_parity(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
                                   uint32_t parity_shards, const mxec_chunk_info* data_chunks, int k,
                                   mxec_chunk_info* parity_out) {
-    if (!ec_dir || (k > 0 && !data_chunks) || !parity_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    const int m = int(parity_shards);
-    MXEC_TRY([&] {
-        if (k + m > 255)
-            return set_error(MXEC_E_TOO_MANY_SHARDS_255,
-                             "too many shards: " + std::to_string(k) + " data + " + std::to_string(m) + " parity = " +
-                                 std::to_string(k + m) + " > 255 (GF(2^8) limit). Increase --chunk-size");
+    return mxec::guarded([&]() -> int {
+        if (!ec_dir || (k > 0 && !data_chunks) || !parity_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        const int m = int(parity_shards);
+        MXEC_TRY([&] {
+            if (k + m > 255)
+                return set_error(MXEC_E_TOO_MANY_SHARDS_255,
+                                 "too many shards: " + std::to_string(k) + " data + " + std::to_string(m) + " parity = " +
+                                     std::to_string(k + m) + " > 255 (GF(2^8) limit). Increase --chunk-size");
+            return MXEC_OK;
+        }());
+        const fs::path dir(ec_dir);
+        std::vector<Bytes> data(static_cast<size_t>(k));
+        std::vector<const uint8_t*> dp(static_cast<size_t>(k));
+        std::vector<size_t> dl(static_cast<size_t>(k));
+        for (int j = 0; j < k; ++j) {
+            MXEC_TRY(read_file(dir / chunk_name(data_chunks[j].index), data[size_t(j)]));
+            if (data[size_t(j)].size() > chunk_size) data[size_t(j)].resize(chunk_size);  // Vec::resize
+            dp[size_t(j)] = data[size_t(j)].data();
+            dl[size_t(j)] = data[size_t(j)].size();
+        }
+        // Parity buffers: the encode writes every byte (no zero-fill needed).
+        std::vector<Bytes> parity(static_cast<size_t>(m > 0 ? m : 0));
+        for (auto& b : parity) b.resize(chunk_size);
+        std::vector<uint8_t*> pp(parity.size());
+        for (size_t i = 0; i < parity.size(); ++i) pp[i] = parity[i].data();
+        std::vector<uint8_t> dig(size_t(k + m) * 32);
+        int rc = mxec_encode(ctx, k, m, chunk_size, dp.data(), dl.data(), pp.data(),
+                             reinterpret_cast<uint8_t(*)[32]>(dig.data()));
+        if (rc) return rc;
+        for (int i = 0; i < m; ++i) {
+            MXEC_TRY(write_file(dir / chunk_name(uint32_t(k + i)), pp[size_t(i)], chunk_size));
+            fill_info(&parity_out[i], uint32_t(k + i), chunk_size, &dig[size_t(k + i) * 32], 1);
+        }
         return MXEC_OK;
-    }());
-    const fs::path dir(ec_dir);
-    std::vector<Bytes> data(static_cast<size_t>(k));
-    std::vector<const uint8_t*> dp(static_cast<size_t>(k));
-    std::vector<size_t> dl(static_cast<size_t>(k));
-    for (int j = 0; j < k; ++j) {
-        MXEC_TRY(read_file(dir / chunk_name(data_chunks[j].index), data[size_t(j)]));
-        if (data[size_t(j)].size() > chunk_size) data[size_t(j)].resize(chunk_size);  // Vec::resize
-        dp[size_t(j)] = data[size_t(j)].data();
-        dl[size_t(j)] = data[size_t(j)].size();
-    }
-    // Parity buffers: the encode writes every byte (no zero-fill needed).
-    std::vector<Bytes> parity(static_cast<size_t>(m > 0 ? m : 0));
-    for (auto& b : parity) b.resize(chunk_size);
-    std::vector<uint8_t*> pp(parity.size());
-    for (size_t i = 0; i < parity.size(); ++i) pp[i] = parity[i].data();
-    std::vector<uint8_t> dig(size_t(k + m) * 32);
-    int rc = mxec_encode(ctx, k, m, chunk_size, dp.data(), dl.data(), pp.data(),
-                         reinterpret_cast<uint8_t(*)[32]>(dig.data()));
-    if (rc) return rc;
-    for (int i = 0; i < m; ++i) {
-        MXEC_TRY(write_file(dir / chunk_name(uint32_t(k + i)), pp[size_t(i)], chunk_size));
-        fill_info(&parity_out[i], uint32_t(k + i), chunk_size, &dig[size_t(k + i) * 32], 1);
-    }
-    return MXEC_OK;
+    });
 }
 
 }  // extern "C"
@@ -552,17 +558,41 @@ int put_chunked_buffer(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, u
     if (has_parity) {
         // The reference writes the data chunks first (write_chunk), then
         // hits the k+m guard inside compute_and_write_parity.
-        for (int j = 0; j < k; ++j) MXEC_TRY(write_file(dir / chunk_name(uint32_t(j)), dp[size_t(j)], dl[size_t(j)]));
-        if (k + m > 255)
+        auto write_data = [&]() -> int {
+            for (int j = 0; j < k; ++j) MXEC_TRY(write_file(dir / chunk_name(uint32_t(j)), dp[size_t(j)], dl[size_t(j)]));
+            return MXEC_OK;
+        };
+        if (k + m > 255) {
+            MXEC_TRY(write_data());
             return set_error(MXEC_E_TOO_MANY_SHARDS_255,
                              "too many shards: " + std::to_string(k) + " data + " + std::to_string(m) + " parity = " +
                                  std::to_string(k + m) + " > 255 (GF(2^8) limit). Increase --chunk-size");
+        }
+        // The data chunk files are written on a helper thread while the
+        // device encodes and hashes (the ~30 ms SHA-256 chain of a 1 MiB
+        // chunk hides the writes); a write error still wins over anything
+        // the encode reports, as the reference writes them first.
+        int wrc = MXEC_OK;
+        std::string wmsg;
+        std::thread writer([&] {
+            try {
+                wrc = write_data();
+                if (wrc) wmsg = mxec::last_error();
+            } catch (...) {
+                wrc = MXEC_E_IO;
+                wmsg = "IO error: data chunk write failed";
+            }
+        });
         parity.resize(size_t(m));  // the encode writes every byte
         for (auto& b : parity) b.resize(chunk_size);
         std::vector<uint8_t*> pp(static_cast<size_t>(m));
         for (int i = 0; i < m; ++i) pp[size_t(i)] = parity[size_t(i)].data();
-        MXEC_TRY(mxec_encode(ctx, k, m, chunk_size, dp.data(), dl.data(), pp.data(),
-                             reinterpret_cast<uint8_t(*)[32]>(dig.data())));
+        const int erc = mxec_encode(ctx, k, m, chunk_size, dp.data(), dl.data(), pp.data(),
+                                    reinterpret_cast<uint8_t(*)[32]>(dig.data()));
+        const std::string emsg = erc ? std::string(mxec::last_error()) : std::string();
+        writer.join();
+        if (wrc) return set_error(wrc, wmsg);
+        if (erc) return set_error(erc, emsg);
         for (int i = 0; i < m; ++i)
             MXEC_TRY(write_file(dir / chunk_name(uint32_t(k + i)), pp[size_t(i)], chunk_size));
     } else {
@@ -666,35 +696,41 @@ extern "C" {
 
 int mxec_put_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
                             const uint8_t* body, size_t len) {
-    return put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, body, len, -1);
+    return mxec::guarded([&]() -> int {
+        return put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, body, len, -1);
+    });
 }
 
 int mxec_put_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
                                       uint32_t parity_shards, const uint8_t key[32], const uint8_t nonce_prefix[4],
                                       const uint8_t* aad_prefix, uint32_t aad_prefix_len, const uint8_t* body,
                                       size_t len, uint32_t which, mxec_body_sums* sums_out) {
-    if (!key || !nonce_prefix || (len && !body) || (aad_prefix_len && !aad_prefix) || (which && !sums_out))
-        return set_error(MXEC_E_INVALID_ARG, "null argument");
-    std::vector<uint8_t> ct;
-    MXEC_TRY(encrypt_frames(ctx, key, nonce_prefix, aad_prefix, aad_prefix_len, body, len, ct));
-    MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, ct.data(), ct.size(), int64_t(len)));
-    if (!which) return MXEC_OK;
-    // Md5 / ChecksumHasher over the plaintext as it arrives (:878-884).
-    const uint8_t* b = body ? body : reinterpret_cast<const uint8_t*>("");
-    const uint64_t l = len;
-    return mxec_body_sums_batch(ctx, &b, &l, 1, which, sums_out);
+    return mxec::guarded([&]() -> int {
+        if (!key || !nonce_prefix || (len && !body) || (aad_prefix_len && !aad_prefix) || (which && !sums_out))
+            return set_error(MXEC_E_INVALID_ARG, "null argument");
+        std::vector<uint8_t> ct;
+        MXEC_TRY(encrypt_frames(ctx, key, nonce_prefix, aad_prefix, aad_prefix_len, body, len, ct));
+        MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, ct.data(), ct.size(), int64_t(len)));
+        if (!which) return MXEC_OK;
+        // Md5 / ChecksumHasher over the plaintext as it arrives (:878-884).
+        const uint8_t* b = body ? body : reinterpret_cast<const uint8_t*>("");
+        const uint64_t l = len;
+        return mxec_body_sums_batch(ctx, &b, &l, 1, which, sums_out);
+    });
 }
 
 int mxec_complete_multipart_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
                                     uint32_t parity_shards, const mxec_multipart_part* parts, uint32_t n_parts,
                                     char etag_out[48]) {
-    if ((n_parts && !parts) || !etag_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    std::vector<uint8_t> body;
-    for (uint32_t p = 0; p < n_parts; ++p)
-        if (parts[p].encrypted) return set_error(MXEC_E_INVALID_ARG, "encrypted part: use the _encrypted driver");
-    MXEC_TRY(read_parts(ctx, parts, n_parts, nullptr, nullptr, body));
-    MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, body.data(), body.size(), -1));
-    return multipart_etag(ctx, parts, n_parts, etag_out);
+    return mxec::guarded([&]() -> int {
+        if ((n_parts && !parts) || !etag_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        std::vector<uint8_t> body;
+        for (uint32_t p = 0; p < n_parts; ++p)
+            if (parts[p].encrypted) return set_error(MXEC_E_INVALID_ARG, "encrypted part: use the _encrypted driver");
+        MXEC_TRY(read_parts(ctx, parts, n_parts, nullptr, nullptr, body));
+        MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, body.data(), body.size(), -1));
+        return multipart_etag(ctx, parts, n_parts, etag_out);
+    });
 }
 
 int mxec_complete_multipart_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
@@ -703,40 +739,46 @@ int mxec_complete_multipart_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir,
                                               const uint8_t key[32], const uint8_t nonce_prefix[4],
                                               const uint8_t* aad_prefix, uint32_t aad_prefix_len,
                                               char etag_out[48]) {
-    if ((n_parts && !parts) || !etag_out || !key || !nonce_prefix || (aad_prefix_len && !aad_prefix))
-        return set_error(MXEC_E_INVALID_ARG, "null argument");
-    std::vector<uint8_t> plain, ct;
-    MXEC_TRY(read_parts(ctx, parts, n_parts, upload_key, upload_id, plain));
-    MXEC_TRY(encrypt_frames(ctx, key, nonce_prefix, aad_prefix, aad_prefix_len, plain.data(), plain.size(), ct));
-    MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, ct.data(), ct.size(), int64_t(plain.size())));
-    return multipart_etag(ctx, parts, n_parts, etag_out);
+    return mxec::guarded([&]() -> int {
+        if ((n_parts && !parts) || !etag_out || !key || !nonce_prefix || (aad_prefix_len && !aad_prefix))
+            return set_error(MXEC_E_INVALID_ARG, "null argument");
+        std::vector<uint8_t> plain, ct;
+        MXEC_TRY(read_parts(ctx, parts, n_parts, upload_key, upload_id, plain));
+        MXEC_TRY(encrypt_frames(ctx, key, nonce_prefix, aad_prefix, aad_prefix_len, plain.data(), plain.size(), ct));
+        MXEC_TRY(put_chunked_buffer(ctx, ec_dir, chunk_size, parity_shards, ct.data(), ct.size(), int64_t(plain.size())));
+        return multipart_etag(ctx, parts, n_parts, etag_out);
+    });
 }
 
 
 int mxec_try_reconstruct_data_chunk(mxec_ctx* ctx, const char* ec_dir, uint32_t target, uint8_t* out,
                                     uint64_t out_cap, uint64_t* out_len) {
-    if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    Manifest man;
-    MXEC_TRY(read_manifest(ec_dir, man));
-    if (target >= man.chunk_count) return set_error(MXEC_E_INVALID_INDEX, "target is not a data chunk");
-    std::vector<uint8_t> buf;
-    MXEC_TRY(reconstruct_from_dir(ctx, ec_dir, man, {target}, {&buf}));
-    *out_len = buf.size();
-    if (buf.size() > out_cap || (buf.size() && !out)) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
-    if (!buf.empty()) std::memcpy(out, buf.data(), buf.size());
-    return MXEC_OK;
+    return mxec::guarded([&]() -> int {
+        if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        Manifest man;
+        MXEC_TRY(read_manifest(ec_dir, man));
+        if (target >= man.chunk_count) return set_error(MXEC_E_INVALID_INDEX, "target is not a data chunk");
+        std::vector<uint8_t> buf;
+        MXEC_TRY(reconstruct_from_dir(ctx, ec_dir, man, {target}, {&buf}));
+        *out_len = buf.size();
+        if (buf.size() > out_cap || (buf.size() && !out)) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
+        if (!buf.empty()) std::memcpy(out, buf.data(), buf.size());
+        return MXEC_OK;
+    });
 }
 
 int mxec_put_object_chunked_sums(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
                                  const uint8_t* body, size_t len, uint32_t which, mxec_body_sums* sums_out) {
-    if (which && !sums_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    MXEC_TRY(mxec_put_object_chunked(ctx, ec_dir, chunk_size, parity_shards, body, len));
-    if (!which) return MXEC_OK;
-    // The reference feeds the same bytes to Md5 / ChecksumHasher as it
-    // chunks them (:722-725); here one batched pass over the whole body.
-    const uint8_t* b = body ? body : reinterpret_cast<const uint8_t*>("");
-    const uint64_t l = len;
-    return mxec_body_sums_batch(ctx, &b, &l, 1, which, sums_out);
+    return mxec::guarded([&]() -> int {
+        if (which && !sums_out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        MXEC_TRY(mxec_put_object_chunked(ctx, ec_dir, chunk_size, parity_shards, body, len));
+        if (!which) return MXEC_OK;
+        // The reference feeds the same bytes to Md5 / ChecksumHasher as it
+        // chunks them (:722-725); here one batched pass over the whole body.
+        const uint8_t* b = body ? body : reinterpret_cast<const uint8_t*>("");
+        const uint64_t l = len;
+        return mxec_body_sums_batch(ctx, &b, &l, 1, which, sums_out);
+    });
 }
 
 }  // extern "C"
@@ -969,130 +1011,142 @@ extern "C" {
 
 int mxec_reader_open(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, uint64_t length, uint64_t batch_bytes,
                      mxec_reader** out) {
-    if (!ec_dir || !out) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    *out = nullptr;
-    auto r = std::make_unique<mxec_reader>();
-    MXEC_TRY(read_manifest(ec_dir, r->man));
-    r->ctx = ctx;
-    r->dir = ec_dir;
-    r->batch_bytes = batch_bytes ? batch_bytes : (uint64_t(64) << 20);
-    const Manifest& man = r->man;
-    if (length == UINT64_MAX) length = offset < man.total_size ? man.total_size - offset : 0;
-    if (offset + length > man.total_size) length = man.total_size > offset ? man.total_size - offset : 0;
-    if (length > 0 && man.total_size > 0) {  // else Done at once (:40, :53-65)
-        if (man.chunk_size == 0) return set_error(MXEC_E_JSON, "JSON error: chunk_size is 0");
-        r->next = uint32_t(offset / man.chunk_size);
-        r->end = uint32_t((offset + length - 1) / man.chunk_size);
-        r->skip = offset % man.chunk_size;
-        if (r->end >= man.chunk_count || r->end >= man.chunks.size())
-            return set_error(MXEC_E_JSON, "JSON error: range past chunk_count");
-        r->remaining = length;
-    }
-    *out = r.release();
-    return MXEC_OK;
+    return mxec::guarded([&]() -> int {
+        if (!ec_dir || !out) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        *out = nullptr;
+        auto r = std::make_unique<mxec_reader>();
+        MXEC_TRY(read_manifest(ec_dir, r->man));
+        r->ctx = ctx;
+        r->dir = ec_dir;
+        r->batch_bytes = batch_bytes ? batch_bytes : (uint64_t(64) << 20);
+        const Manifest& man = r->man;
+        if (length == UINT64_MAX) length = offset < man.total_size ? man.total_size - offset : 0;
+        if (offset + length > man.total_size) length = man.total_size > offset ? man.total_size - offset : 0;
+        if (length > 0 && man.total_size > 0) {  // else Done at once (:40, :53-65)
+            if (man.chunk_size == 0) return set_error(MXEC_E_JSON, "JSON error: chunk_size is 0");
+            r->next = uint32_t(offset / man.chunk_size);
+            r->end = uint32_t((offset + length - 1) / man.chunk_size);
+            r->skip = offset % man.chunk_size;
+            if (r->end >= man.chunk_count || r->end >= man.chunks.size())
+                return set_error(MXEC_E_JSON, "JSON error: range past chunk_count");
+            r->remaining = length;
+        }
+        *out = r.release();
+        return MXEC_OK;
+    });
 }
 
 int64_t mxec_reader_read(mxec_reader* r, uint8_t* buf, uint64_t cap) {
-    if (!r || (cap && !buf)) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    uint64_t copied = 0;
-    while (copied < cap && r->remaining > 0) {
-        if (r->bi >= r->batch.size()) {
-            // NeedLoad: the next chunks up to batch_bytes (at least one)
-            uint32_t last = r->next;
-            uint64_t bytes = r->man.chunks[r->next].size;
-            while (last < r->end && bytes + r->man.chunks[last + 1].size <= r->batch_bytes)
-                bytes += r->man.chunks[++last].size;
-            const int rc = load_chunks(r->ctx, r->dir, r->man, r->next, last, r->batch);
-            if (rc) return copied ? int64_t(copied) : int64_t(rc);
-            r->next = last + 1;
-            r->bi = 0;
-            r->pos = r->skip;  // skip applies to the first chunk of the range only
-            r->skip = 0;
+    try {
+        if (!r || (cap && !buf)) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        uint64_t copied = 0;
+        while (copied < cap && r->remaining > 0) {
+            if (r->bi >= r->batch.size()) {
+                // NeedLoad: the next chunks up to batch_bytes (at least one)
+                uint32_t last = r->next;
+                uint64_t bytes = r->man.chunks[r->next].size;
+                while (last < r->end && bytes + r->man.chunks[last + 1].size <= r->batch_bytes)
+                    bytes += r->man.chunks[++last].size;
+                const int rc = load_chunks(r->ctx, r->dir, r->man, r->next, last, r->batch);
+                if (rc) return copied ? int64_t(copied) : int64_t(rc);
+                r->next = last + 1;
+                r->bi = 0;
+                r->pos = r->skip;  // skip applies to the first chunk of the range only
+                r->skip = 0;
+            }
+            LoadedChunk& c = r->batch[r->bi];
+            if (c.err) {  // serve everything before it first, as the reference streams
+                if (copied) return int64_t(copied);
+                return set_error(c.err, c.msg);
+            }
+            const uint64_t avail = c.data.size() > r->pos ? c.data.size() - r->pos : 0;
+            const uint64_t take = std::min(std::min(avail, cap - copied), r->remaining);
+            if (take) std::memcpy(buf + copied, c.data.data() + r->pos, take);
+            copied += take;
+            r->pos += take;
+            r->remaining -= take;
+            if (r->pos >= c.data.size()) {
+                c.data = Bytes();
+                ++r->bi;
+                r->pos = 0;
+            }
         }
-        LoadedChunk& c = r->batch[r->bi];
-        if (c.err) {  // serve everything before it first, as the reference streams
-            if (copied) return int64_t(copied);
-            return set_error(c.err, c.msg);
-        }
-        const uint64_t avail = c.data.size() > r->pos ? c.data.size() - r->pos : 0;
-        const uint64_t take = std::min(std::min(avail, cap - copied), r->remaining);
-        if (take) std::memcpy(buf + copied, c.data.data() + r->pos, take);
-        copied += take;
-        r->pos += take;
-        r->remaining -= take;
-        if (r->pos >= c.data.size()) {
-            c.data = Bytes();
-            ++r->bi;
-            r->pos = 0;
-        }
+        return int64_t(copied);
+    } catch (const std::bad_alloc&) {
+        return set_error(MXEC_E_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return set_error(MXEC_E_INVALID_ARG, e.what());
+    } catch (...) {
+        return set_error(MXEC_E_INVALID_ARG, "unknown exception");
     }
-    return int64_t(copied);
 }
 
 void mxec_reader_close(mxec_reader* r) { delete r; }
 
 int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, uint64_t length, uint8_t* out,
                             uint64_t out_cap, uint64_t* out_len) {
-    if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
-    *out_len = 0;
-    // The reader's semantics (mxec_reader_open / _read over the whole range
-    // in one batch), with every chunk the range covers whole read straight
-    // into its place in `out`: no intermediate chunk buffer, no copy out.
-    mxec_reader* r = nullptr;
-    MXEC_TRY(mxec_reader_open(ctx, ec_dir, offset, length, uint64_t(1) << 40, &r));
-    std::unique_ptr<mxec_reader, void (*)(mxec_reader*)> guard(r, mxec_reader_close);
-    if (r->remaining > out_cap || (r->remaining && !out))
-        return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
-    if (r->remaining == 0) return MXEC_OK;
-    const Manifest& man = r->man;
-    const uint32_t first = r->next, last = r->end;
-    // Where each chunk's bytes are served: the first from `skip`, the rest
-    // whole, in order, until `remaining` runs out (mxec_reader_read).
-    std::vector<uint8_t*> dsts(last - first + 1, nullptr);
-    uint64_t pos = 0, left = r->remaining;
-    for (uint32_t c = first; c <= last && left; ++c) {
-        const uint64_t sz = man.chunks[c].size;
-        const uint64_t from = c == first ? r->skip : 0;
-        const uint64_t take = std::min(sz > from ? sz - from : 0, left);
-        if (from == 0 && take == sz && sz > 0) dsts[c - first] = out + pos;
-        pos += take;
-        left -= take;
-    }
-    // Windows of at most kGetWindow bytes of chunks (at least one chunk): one
-    // hash round trip per window, and a slot's device staging stays bounded
-    // however large the object.
-    // MXEC_GET_WINDOW (bytes) overrides the window (tests).
-    const char* we = getenv("MXEC_GET_WINDOW");
-    const uint64_t kGetWindow = we && *we ? std::max<uint64_t>(1, strtoull(we, nullptr, 10)) : uint64_t(1) << 30;
-    std::vector<LoadedChunk> batch;
-    pos = 0;
-    left = r->remaining;
-    for (uint32_t w0 = first; w0 <= last && left;) {
-        uint32_t w1 = w0;
-        uint64_t bytes = man.chunks[w0].size;
-        while (w1 < last && bytes + man.chunks[w1 + 1].size <= kGetWindow) bytes += man.chunks[++w1].size;
-        const std::vector<uint8_t*> wd(dsts.begin() + (w0 - first), dsts.begin() + (w1 - first) + 1);
-        if (const int rc = load_chunks(ctx, r->dir, man, w0, w1, batch, &wd)) {
-            *out_len = pos;
-            return rc;
-        }
-        for (uint32_t c = w0; c <= w1 && left; ++c) {
-            const LoadedChunk& lc = batch[c - w0];
-            if (lc.err) {  // bytes before it are served, then the error (reader semantics)
-                *out_len = pos;
-                return set_error(lc.err, lc.msg);
-            }
+    return mxec::guarded([&]() -> int {
+        if (!ec_dir || !out_len) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        *out_len = 0;
+        // The reader's semantics (mxec_reader_open / _read over the whole range
+        // in one batch), with every chunk the range covers whole read straight
+        // into its place in `out`: no intermediate chunk buffer, no copy out.
+        mxec_reader* r = nullptr;
+        MXEC_TRY(mxec_reader_open(ctx, ec_dir, offset, length, uint64_t(1) << 40, &r));
+        std::unique_ptr<mxec_reader, void (*)(mxec_reader*)> guard(r, mxec_reader_close);
+        if (r->remaining > out_cap || (r->remaining && !out))
+            return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
+        if (r->remaining == 0) return MXEC_OK;
+        const Manifest& man = r->man;
+        const uint32_t first = r->next, last = r->end;
+        // Where each chunk's bytes are served: the first from `skip`, the rest
+        // whole, in order, until `remaining` runs out (mxec_reader_read).
+        std::vector<uint8_t*> dsts(last - first + 1, nullptr);
+        uint64_t pos = 0, left = r->remaining;
+        for (uint32_t c = first; c <= last && left; ++c) {
+            const uint64_t sz = man.chunks[c].size;
             const uint64_t from = c == first ? r->skip : 0;
-            const uint64_t sz = lc.size();
             const uint64_t take = std::min(sz > from ? sz - from : 0, left);
-            if (!lc.dst && take) std::memcpy(out + pos, lc.data.data() + from, take);
+            if (from == 0 && take == sz && sz > 0) dsts[c - first] = out + pos;
             pos += take;
             left -= take;
         }
-        w0 = w1 + 1;
-    }
-    *out_len = pos;
-    return MXEC_OK;
+        // Windows of at most kGetWindow bytes of chunks (at least one chunk): one
+        // hash round trip per window, and a slot's device staging stays bounded
+        // however large the object.
+        // MXEC_GET_WINDOW (bytes) overrides the window (tests).
+        const char* we = getenv("MXEC_GET_WINDOW");
+        const uint64_t kGetWindow = we && *we ? std::max<uint64_t>(1, strtoull(we, nullptr, 10)) : uint64_t(1) << 30;
+        std::vector<LoadedChunk> batch;
+        pos = 0;
+        left = r->remaining;
+        for (uint32_t w0 = first; w0 <= last && left;) {
+            uint32_t w1 = w0;
+            uint64_t bytes = man.chunks[w0].size;
+            while (w1 < last && bytes + man.chunks[w1 + 1].size <= kGetWindow) bytes += man.chunks[++w1].size;
+            const std::vector<uint8_t*> wd(dsts.begin() + (w0 - first), dsts.begin() + (w1 - first) + 1);
+            if (const int rc = load_chunks(ctx, r->dir, man, w0, w1, batch, &wd)) {
+                *out_len = pos;
+                return rc;
+            }
+            for (uint32_t c = w0; c <= w1 && left; ++c) {
+                const LoadedChunk& lc = batch[c - w0];
+                if (lc.err) {  // bytes before it are served, then the error (reader semantics)
+                    *out_len = pos;
+                    return set_error(lc.err, lc.msg);
+                }
+                const uint64_t from = c == first ? r->skip : 0;
+                const uint64_t sz = lc.size();
+                const uint64_t take = std::min(sz > from ? sz - from : 0, left);
+                if (!lc.dst && take) std::memcpy(out + pos, lc.data.data() + from, take);
+                pos += take;
+                left -= take;
+            }
+            w0 = w1 + 1;
+        }
+        *out_len = pos;
+        return MXEC_OK;
+    });
 }
 
 
@@ -1100,39 +1154,41 @@ int mxec_get_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, const u
                                       const uint8_t* aad_prefix, uint32_t aad_prefix_len, uint32_t frame_size,
                                       uint64_t plaintext_size, uint64_t offset, uint64_t length, uint8_t* out,
                                       uint64_t out_cap, uint64_t* out_len) {
-    if (!ec_dir || !key || !out_len || (aad_prefix_len && !aad_prefix))
-        return set_error(MXEC_E_INVALID_ARG, "null argument");
-    if (frame_size == 0 || frame_size % 16) return set_error(MXEC_E_INVALID_ARG, "frame_size must be a positive multiple of 16");
-    *out_len = 0;
-    Manifest man;
-    MXEC_TRY(read_manifest(ec_dir, man));
-    if (plaintext_size == UINT64_MAX) {
-        if (!man.has_plain) return set_error(MXEC_E_JSON, "JSON error: manifest has no plaintext_size");
-        plaintext_size = man.plaintext_size;
-    }
-    if (offset >= plaintext_size || length == 0) return MXEC_OK;
-    const uint64_t end = length == UINT64_MAX || length > plaintext_size - offset ? plaintext_size : offset + length;
-    // FrameDecryptor::ciphertext_offset / for_range: the frames that cover
-    // [offset, end), read through the verified chunk reader (with_range).
-    const uint64_t fl = uint64_t(frame_size) + MXEC_FRAME_OVERHEAD;
-    const uint64_t f0 = offset / frame_size, f1 = (end - 1) / frame_size;
-    const uint64_t ct_off = f0 * fl;
-    const uint64_t ct_len = std::min<uint64_t>(man.total_size - std::min(man.total_size, ct_off), (f1 - f0 + 1) * fl);
-    if (end - offset > out_cap || !out) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
-    Bytes ct(size_t(ct_len) + 1);  // every byte written by the GET below
-    uint64_t got = 0;
-    MXEC_TRY(mxec_get_object_chunked(ctx, ec_dir, ct_off, ct_len, ct.data(), ct_len, &got));
-    const uint64_t nf = f1 - f0 + 1;
-    const uint64_t pt_lo = f0 * frame_size, pt_hi = std::min<uint64_t>(plaintext_size, (f1 + 1) * uint64_t(frame_size));
-    std::vector<uint8_t> aads(size_t(nf) * 32);
-    MXEC_TRY(mxec_frame_aads(ctx, aad_prefix, aad_prefix_len, f0, nf, reinterpret_cast<uint8_t(*)[32]>(aads.data())));
-    Bytes pt(size_t(pt_hi - pt_lo) + 1);
-    uint64_t n = 0;
-    MXEC_TRY(mxec_frames_decrypt(ctx, key, f0, aads.data(), 32, frame_size, ct.data(), got, pt_hi - pt_lo, pt.data(),
-                                 pt.size(), &n));
-    std::memcpy(out, pt.data() + (offset - pt_lo), size_t(end - offset));
-    *out_len = end - offset;
-    return MXEC_OK;
+    return mxec::guarded([&]() -> int {
+        if (!ec_dir || !key || !out_len || (aad_prefix_len && !aad_prefix))
+            return set_error(MXEC_E_INVALID_ARG, "null argument");
+        if (frame_size == 0 || frame_size % 16) return set_error(MXEC_E_INVALID_ARG, "frame_size must be a positive multiple of 16");
+        *out_len = 0;
+        Manifest man;
+        MXEC_TRY(read_manifest(ec_dir, man));
+        if (plaintext_size == UINT64_MAX) {
+            if (!man.has_plain) return set_error(MXEC_E_JSON, "JSON error: manifest has no plaintext_size");
+            plaintext_size = man.plaintext_size;
+        }
+        if (offset >= plaintext_size || length == 0) return MXEC_OK;
+        const uint64_t end = length == UINT64_MAX || length > plaintext_size - offset ? plaintext_size : offset + length;
+        // FrameDecryptor::ciphertext_offset / for_range: the frames that cover
+        // [offset, end), read through the verified chunk reader (with_range).
+        const uint64_t fl = uint64_t(frame_size) + MXEC_FRAME_OVERHEAD;
+        const uint64_t f0 = offset / frame_size, f1 = (end - 1) / frame_size;
+        const uint64_t ct_off = f0 * fl;
+        const uint64_t ct_len = std::min<uint64_t>(man.total_size - std::min(man.total_size, ct_off), (f1 - f0 + 1) * fl);
+        if (end - offset > out_cap || !out) return set_error(MXEC_E_INVALID_ARG, "output buffer too small");
+        Bytes ct(size_t(ct_len) + 1);  // every byte written by the GET below
+        uint64_t got = 0;
+        MXEC_TRY(mxec_get_object_chunked(ctx, ec_dir, ct_off, ct_len, ct.data(), ct_len, &got));
+        const uint64_t nf = f1 - f0 + 1;
+        const uint64_t pt_lo = f0 * frame_size, pt_hi = std::min<uint64_t>(plaintext_size, (f1 + 1) * uint64_t(frame_size));
+        std::vector<uint8_t> aads(size_t(nf) * 32);
+        MXEC_TRY(mxec_frame_aads(ctx, aad_prefix, aad_prefix_len, f0, nf, reinterpret_cast<uint8_t(*)[32]>(aads.data())));
+        Bytes pt(size_t(pt_hi - pt_lo) + 1);
+        uint64_t n = 0;
+        MXEC_TRY(mxec_frames_decrypt(ctx, key, f0, aads.data(), 32, frame_size, ct.data(), got, pt_hi - pt_lo, pt.data(),
+                                     pt.size(), &n));
+        std::memcpy(out, pt.data() + (offset - pt_lo), size_t(end - offset));
+        *out_len = end - offset;
+        return MXEC_OK;
+    });
 }
 
 }  // extern "C"
