@@ -1181,11 +1181,17 @@ int mxec_get_object_chunked_encrypted(mxec_ctx* ctx, const char* ec_dir, const u
         const uint64_t pt_lo = f0 * frame_size, pt_hi = std::min<uint64_t>(plaintext_size, (f1 + 1) * uint64_t(frame_size));
         std::vector<uint8_t> aads(size_t(nf) * 32);
         MXEC_TRY(mxec_frame_aads(ctx, aad_prefix, aad_prefix_len, f0, nf, reinterpret_cast<uint8_t(*)[32]>(aads.data())));
-        Bytes pt(size_t(pt_hi - pt_lo) + 1);
         uint64_t n = 0;
-        MXEC_TRY(mxec_frames_decrypt(ctx, key, f0, aads.data(), 32, frame_size, ct.data(), got, pt_hi - pt_lo, pt.data(),
-                                     pt.size(), &n));
-        std::memcpy(out, pt.data() + (offset - pt_lo), size_t(end - offset));
+        if (offset == pt_lo && end == pt_hi) {
+            // The range is whole frames (a full GET): decrypt straight into out.
+            MXEC_TRY(mxec_frames_decrypt(ctx, key, f0, aads.data(), 32, frame_size, ct.data(), got, pt_hi - pt_lo,
+                                         out, out_cap, &n));
+        } else {
+            Bytes pt(size_t(pt_hi - pt_lo) + 1);
+            MXEC_TRY(mxec_frames_decrypt(ctx, key, f0, aads.data(), 32, frame_size, ct.data(), got, pt_hi - pt_lo,
+                                         pt.data(), pt.size(), &n));
+            std::memcpy(out, pt.data() + (offset - pt_lo), size_t(end - offset));
+        }
         *out_len = end - offset;
         return MXEC_OK;
     });
