@@ -210,7 +210,7 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* c
         MXEC_TRY(encode_coef(*ds.d, k, m, &off));
         RsObject ob{in.data(), len.data(), out.data(), len.data() + k, off};
         MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, m, {ob}));
-        std::vector<UploadSeg> down;
+        std::vector<DownloadSeg> down;
         for (int i = 0; i < m; ++i) down.push_back({sa * uint64_t(k + i), parity[i], shard_size});
         MXEC_TRY(download_segments(slot, s, base, down));
         if (sha256_out) {
@@ -289,7 +289,7 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
             }
             RsObject ob{in.data(), in_len.data(), out.data(), out_len.data(), off};
             MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, int(out.size()), {ob}));
-            std::vector<UploadSeg> down;
+            std::vector<DownloadSeg> down;
             for (size_t t = 0; t < out.size(); ++t)
                 if (out_len[t]) down.push_back({sa * uint64_t(plan->missing[t]), shards[plan->missing[t]], out_len[t]});
             // plan->missing is ascending, so are the offsets.

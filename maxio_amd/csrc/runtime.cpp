@@ -97,12 +97,12 @@ int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vec
     return MXEC_OK;
 }
 
-int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
+int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs) {
     if (segs.empty()) return slot_wait(slot, s);
     for (auto& e : slot.stage_done)
         if (!e) MXEC_HIP(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
-    const uint64_t lo = segs.front().dst_off;
-    const uint64_t hi = segs.back().dst_off + segs.back().len;
+    const uint64_t lo = segs.front().src_off;
+    const uint64_t hi = segs.back().src_off + segs.back().len;
     const uint64_t piece = std::min<uint64_t>(kStagePiece, hi - lo);
     for (auto& b : slot.stage) MXEC_TRY(b.ensure(piece));
     // Piece i+1's DMA is in flight while piece i is copied out.
@@ -111,11 +111,11 @@ int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const 
         const uint64_t b = std::min(hi, a + piece);
         MXEC_HIP(hipEventSynchronize(slot.stage_done[buf]));
         const auto* h = static_cast<const uint8_t*>(slot.stage[buf].p);
-        while (si < segs.size() && segs[si].dst_off + segs[si].len <= a) ++si;
-        for (size_t j = si; j < segs.size() && segs[j].dst_off < b; ++j) {
-            const uint64_t x = std::max(a, segs[j].dst_off), y = std::min(b, segs[j].dst_off + segs[j].len);
+        while (si < segs.size() && segs[si].src_off + segs[si].len <= a) ++si;
+        for (size_t j = si; j < segs.size() && segs[j].src_off < b; ++j) {
+            const uint64_t x = std::max(a, segs[j].src_off), y = std::min(b, segs[j].src_off + segs[j].len);
             if (y > x)
-                std::memcpy(const_cast<uint8_t*>(static_cast<const uint8_t*>(segs[j].src)) + (x - segs[j].dst_off),
+                std::memcpy(static_cast<uint8_t*>(segs[j].dst) + (x - segs[j].src_off),
                             h + (x - a), y - x);
         }
         return MXEC_OK;

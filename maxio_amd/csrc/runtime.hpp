@@ -97,10 +97,16 @@ constexpr uint64_t kStagePiece = uint64_t(8) << 20;
 // pair, enqueued on `s` (the caller waits or orders later work on `s`).
 // Segments must be sorted by dst_off and not overlap.
 int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs);
-// The reverse: dev_base + src_off (UploadSeg::dst_off) -> host UploadSeg::src
-// (written), through the same pinned pair; returns when every byte has
-// landed (waits for everything enqueued on `s` before it, too).
-int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<UploadSeg>& segs);
+// One device -> host download segment: len bytes from src_off to dst.
+struct DownloadSeg {
+    uint64_t src_off;
+    void* dst;
+    uint64_t len;
+};
+// The reverse of upload_segments, through the same pinned pair; returns when
+// every byte has landed (waits for everything enqueued on `s` before it,
+// too).  Segments sorted by src_off, not overlapping.
+int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs);
 
 struct Device {
     int id = 0;
