@@ -100,6 +100,14 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
  * the device's combiner (concurrent small requests share one launch) and the
  * messages they hashed. */
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages);
+/* Page-locked host memory for request bodies and GET buffers (the Axum body
+ * MaxIO hands to a PUT, the buffer a GET fills).  Every host-pointer entry
+ * point accepts any host memory; when a buffer comes from here, its bytes
+ * move by DMA straight to and from the device instead of through the
+ * library's pinned staging copy.  NULL on failure; free with
+ * mxec_host_free. */
+void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes);
+void mxec_host_free(mxec_ctx* ctx, void* p);
 
 /* ---- ReedSolomon::new ----------------------------------------------------- */
 /* 0 if new(k, m) would succeed; otherwise the crate's error

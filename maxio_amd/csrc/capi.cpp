@@ -129,6 +129,22 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
     return MXEC_OK;
 }
 
+void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes) {
+    if (!ctx || bytes == 0) return nullptr;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error(MXEC_E_OOM, "pinned host allocation failed");
+        return nullptr;
+    }
+    return p;
+}
+
+void mxec_host_free(mxec_ctx* ctx, void* p) {
+    (void)ctx;
+    if (p) (void)hipHostFree(p);
+}
+
 int mxec_rs_check(int k, int m) { return rs_check(k, m); }
 
 int mxec_rs_parity_matrix(int k, int m, uint8_t* out) {
@@ -295,6 +311,10 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
             // plan->missing is ascending, so are the offsets.
             MXEC_TRY(download_segments(slot, s, base, down));
             for (int e : plan->missing) present[size_t(e)] = 1;
+        } else {
+            // Nothing to rebuild: the uploads may still be reading the
+            // caller's buffers (direct DMA from page-locked memory).
+            MXEC_TRY(slot_wait(slot, s));
         }
         std::memcpy(present_inout, present.data(), size_t(total));
         return MXEC_OK;

@@ -68,8 +68,28 @@ void slot_destroy(Slot& slot) {
     slot.stream = nullptr;
 }
 
+namespace {
+// True when [p, p + n) is page-locked host memory HIP can DMA from directly
+// (mxec_host_alloc, hipHostMalloc / hipHostRegister).
+bool pinned_host(const void* p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory is reported as an error
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+}  // namespace
+
 int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
     if (segs.empty()) return MXEC_OK;
+    bool all_pinned = true;
+    for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_host(g.src));
+    if (all_pinned) {  // DMA straight from the caller's page-locked buffers
+        for (const auto& g : segs)
+            if (g.len) MXEC_HIP(hipMemcpyAsync(dev_base + g.dst_off, g.src, g.len, hipMemcpyHostToDevice, s));
+        return MXEC_OK;
+    }
     for (auto& e : slot.stage_done)
         if (!e) MXEC_HIP(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
     // Walk the destination range [lo, hi) in pieces; each piece gathers the
@@ -99,6 +119,13 @@ int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vec
 
 int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs) {
     if (segs.empty()) return slot_wait(slot, s);
+    bool all_pinned = true;
+    for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_host(g.dst));
+    if (all_pinned) {  // DMA straight into the caller's page-locked buffers
+        for (const auto& g : segs)
+            if (g.len) MXEC_HIP(hipMemcpyAsync(g.dst, dev_base + g.src_off, g.len, hipMemcpyDeviceToHost, s));
+        return slot_wait(slot, s);
+    }
     for (auto& e : slot.stage_done)
         if (!e) MXEC_HIP(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
     const uint64_t lo = segs.front().src_off;

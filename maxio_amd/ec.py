@@ -172,6 +172,21 @@ class Context:
         _check(self._lib.mxec_ctx_combiner_stats(self._h, dev, ctypes.byref(b), ctypes.byref(m)))
         return {"batches": b.value, "messages": m.value}
 
+    def host_array(self, n: int) -> np.ndarray:
+        """A uint8 array of n bytes in page-locked memory (mxec_host_alloc):
+        uploads from it and downloads into it skip the staging copy.  The
+        memory is freed when the array is garbage collected."""
+        p = self._lib.mxec_host_alloc(self._h, max(1, n))
+        if not p:
+            raise MemoryError("mxec_host_alloc failed")
+        buf = (ctypes.c_uint8 * max(1, n)).from_address(p)
+        a = np.frombuffer(buf, dtype=np.uint8, count=n)
+        lib, h = self._lib, self._h
+        import weakref
+
+        weakref.finalize(buf, lib.mxec_host_free, h, p)
+        return a
+
     def device_ids(self) -> list[int]:
         n = self._lib.mxec_ctx_device_count(self._h)
         return [self._lib.mxec_ctx_device_id(self._h, i) for i in range(n)]

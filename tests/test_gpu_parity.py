@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import hashlib
 import itertools
+import os
 
 import numpy as np
 import pytest
@@ -490,3 +491,51 @@ def test_concurrent_small_sha_requests_are_combined(ctx):
         assert stats["batches"] <= 4 * 48  # some requests rode in another's launch
     finally:
         c.close()
+
+
+def test_pinned_host_buffers_take_the_direct_dma_path(ctx, tmp_path):
+    """Buffers from mxec_host_alloc (Context.host_array) move by DMA straight
+    to and from the device: same results as pageable buffers for hashing,
+    encode, reconstruct and a file-layer GET into a pinned output."""
+    import ctypes
+
+    rng = np.random.default_rng(31)
+    k, m, S = 4, 2, 100_003
+    pinned = [ctx.host_array(S) for _ in range(k + m)]
+    for j in range(k):
+        pinned[j][:] = rng.integers(0, 256, S, dtype=np.uint8)
+    pageable = [p.copy() for p in pinned[:k]]
+    assert ctx.sha256(pinned[:k]) == [hashlib.sha256(p.tobytes()).digest() for p in pageable]
+    par_pg, dig_pg = ctx.encode(pageable, m, S)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    ins = (ctypes.c_void_p * k)(*[p.ctypes.data for p in pinned[:k]])
+    outs = (ctypes.c_void_p * m)(*[p.ctypes.data for p in pinned[k:]])
+    dig = np.zeros((k + m, 32), np.uint8)
+    assert maxio_amd.lib().mxec_encode(ctx.handle, k, m, S, ins, None, outs, dig.ctypes.data_as(u8p)) == 0
+    for i in range(m):
+        assert np.array_equal(pinned[k + i], par_pg[i])
+    assert [bytes(d) for d in dig] == dig_pg
+    # reconstruct two lost data shards in place, in pinned memory
+    want = [p.copy() for p in pinned]
+    pinned[1][:] = 0
+    pinned[3][:] = 0
+    present = np.array([0 if i in (1, 3) else 1 for i in range(k + m)], np.uint8)
+    ptrs = (ctypes.c_void_p * (k + m))(*[f.ctypes.data for f in pinned])
+    n = ctypes.c_int(0)
+    assert maxio_amd.lib().mxec_reconstruct(ctx.handle, k, m, S, ptrs, None, None, present.ctypes.data_as(u8p), 0,
+                                            ctypes.byref(n)) == 0
+    for i in range(k + m):
+        assert np.array_equal(pinned[i], want[i]), i
+    # every shard present, nothing to rebuild: returns only after the uploads
+    assert maxio_amd.lib().mxec_reconstruct(ctx.handle, k, m, S, ptrs, None, None, present.ctypes.data_as(u8p), 0,
+                                            ctypes.byref(n)) == 0
+    # file-layer GET into a pinned buffer
+    body = rng.integers(0, 256, 5 * 4096 + 17, dtype=np.uint8)
+    ec = str(tmp_path / "p.ec")
+    ctx.put_object_chunked(ec, 4096, 2, body)
+    os.remove(os.path.join(ec, "000002"))
+    out = ctx.host_array(body.size)
+    got = ctypes.c_uint64(0)
+    assert maxio_amd.lib().mxec_get_object_chunked(ctx.handle, ec.encode(), 0, (1 << 64) - 1, out.ctypes.data,
+                                                   body.size, ctypes.byref(got)) == 0
+    assert got.value == body.size and np.array_equal(out, body)

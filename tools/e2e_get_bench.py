@@ -77,6 +77,8 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-objects", type=int, default=32)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--pinned", action="store_true",
+                    help="PUT bodies and GET buffers in page-locked memory (mxec_host_alloc)")
     args = ap.parse_args()
 
     import maxio_amd
@@ -93,6 +95,11 @@ def main() -> int:
         ctx = maxio_amd.Context(streams_per_device=args.threads)
         rng = np.random.default_rng(7)
         block = rng.integers(0, 256, size + 4096, dtype=np.uint8)
+        if args.pinned:
+            pb = ctx.host_array(block.size)
+            pb[:] = block
+            block = pb
+        out["pinned_buffers"] = bool(args.pinned)
         dirs = [os.path.join(base, f"obj{o}.ec") for o in range(n)]
         lib0 = maxio_amd.lib()
 
@@ -169,7 +176,7 @@ def main() -> int:
             i, d = i_d
             b = getattr(tls, "buf", None)
             if b is None:
-                b = tls.buf = np.zeros(size, np.uint8)
+                b = tls.buf = ctx.host_array(size) if args.pinned else np.zeros(size, np.uint8)
             got = ctypes.c_uint64(0)
             rc = lib.mxec_get_object_chunked(ctx.handle, d.encode(), 0, (1 << 64) - 1,
                                              b.ctypes.data, size, ctypes.byref(got))
