@@ -583,6 +583,12 @@ int put_chunked_buffer(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, u
                 wmsg = "IO error: data chunk write failed";
             }
         });
+        struct Joiner {  // joined on every path, an exception included
+            std::thread& t;
+            ~Joiner() {
+                if (t.joinable()) t.join();
+            }
+        } joiner{writer};
         parity.resize(size_t(m));  // the encode writes every byte
         for (auto& b : parity) b.resize(chunk_size);
         std::vector<uint8_t*> pp(static_cast<size_t>(m));
