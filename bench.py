@@ -46,14 +46,25 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident RS encode+reconstruct GiB/s (k+m, chunk_size); % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GIB = float(1 << 30)
+# INT32-VALU roofline of the SHA-256 kernels (configs 3 / 3c):
+# lane-ops per 64-byte block = the wave-instructions each form issues per
+# block (one wave instruction serves 64 messages, one block each), counted in
+# the gfx950 ISA of the loop bodies (tools/isa_count.py): split form =
+# consumer 905 (64 rounds x 14 + 9) + producer 565 (2261 per 4-block step);
+# one-wave form 1536.
+SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1536}
+# Chip INT32 issue ceiling for those instructions (v_alignbit / v_bitop3 /
+# v_add3 / v_add / v_perm): CUs x 4 SIMDs x lanes per cycle x 2.4 GHz, lanes
+# per cycle measured with tools/valu_lab chip (profiles/r2_lab_valu_chip.jsonl).
+VALU_LANES_PER_SIMD_CYCLE = 16
+CLOCK_GHZ = 2.4
 SEED = 0x6D6178696F  # "maxio"
 
 
 def shard_objects(n_total: int, rank: int, world: int) -> range:
-    """Objects of the global batch owned by `rank` (contiguous block)."""
-    per = (n_total + world - 1) // world
-    lo = min(n_total, rank * per)
-    return range(lo, min(n_total, lo + per))
+    """Objects of the global batch owned by `rank`: object i -> GPU i mod G
+    (DESIGN §6)."""
+    return range(rank, n_total, world)
 
 
 def reduce_max(value: float) -> float:
@@ -123,6 +134,7 @@ class Encode:
         self.parity = torch.zeros((n, m, S), dtype=torch.uint8, device=dev)
         self.payload = n * k * S
         self.alg_bytes = n * (k + m) * S
+        self.rw_ratio = k // m if k % m == 0 else None  # read:write of the stream
         r = min(m, 8)
         self.kernel = f"rs_apply_fast<R={r},V={4 if r <= 4 else 2},NT=1>"
         self.name = label
@@ -549,45 +561,188 @@ def pmc_traffic(tag: str, alg_bytes: float):
     return None, None
 
 
-def secondary(ctx, torch, dev, sh, w) -> dict:
-    """Reference-equivalent PUT path (encode + SHA-256 of all k+m chunks) on
-    the same batch, config 3 reconstruct + verify and the device copy peak.
-    Reported, not the headline."""
+def probe_lib():
+    """libmaxio_probe.so: HBM calibration streams (same load/store forms as
+    the RS kernel), bench-only."""
+    import ctypes
+
+    p = os.path.join(ROOT, "maxio_amd", "lib", "libmaxio_probe.so")
+    lib = ctypes.CDLL(p)
+    for fn, args in (("mxprobe_copy", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+                     ("mxprobe_read2_write1", [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]),
+                     ("mxprobe_read", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p])):
+        getattr(lib, fn).argtypes = args
+        getattr(lib, fn).restype = ctypes.c_int
+    return lib
+
+
+def event_ms(torch, stream, fn, reps: int) -> float:
+    """Average HIP-event time of fn() on `stream` (one warm-up call first)."""
+    fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    torch.cuda.synchronize()
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / reps
+
+
+def calibrate(torch, dev, stream) -> dict:
+    """This box's HBM rates for plain streams of the RS kernel's load/store
+    forms (nt dwordx4, 4 loads in flight per lane, 16 WG/CU): the second
+    denominator of SURVEY §8(d)."""
+    lib = probe_lib()
+    sh = stream.cuda_stream
+    n = 2 << 30
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    c = torch.empty(n, dtype=torch.uint8, device=dev)
+    a.random_(0, 256)
+    b.random_(0, 256)
+    sink = torch.zeros(16, dtype=torch.uint8, device=dev)
     out = {}
 
-    def timed(fn, reps):
-        fn()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            fn()
-        torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / reps
+    def run(rc):
+        assert rc == 0, rc
 
-    buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
-    dst = torch.empty_like(buf)
-    t = timed(lambda: dst.copy_(buf), 5)
-    out["copy_peak_GBps"] = round(2 * buf.numel() / t / 1e9, 1)
-    del buf, dst
+    ms = event_ms(torch, stream, lambda: run(lib.mxprobe_copy(c.data_ptr(), a.data_ptr(), n, sh)), 5)
+    out["copy_GBps"] = round(2 * n / (ms * 1e-3) / 1e9, 1)
+    ms = event_ms(torch, stream, lambda: run(lib.mxprobe_read2_write1(c.data_ptr(), a.data_ptr(), b.data_ptr(), n, sh)), 5)
+    out["read2_write1_GBps"] = round(3 * n / (ms * 1e-3) / 1e9, 1)
+    ms = event_ms(torch, stream, lambda: run(lib.mxprobe_read(a.data_ptr(), n, sink.data_ptr(), sh)), 5)
+    out["read_GBps"] = round(n / (ms * 1e-3) / 1e9, 1)
+    out["what"] = ("libmaxio_probe.so streams over 2 GiB buffers: nontemporal global_load_dwordx4, 4 loads in "
+                   "flight per lane, nontemporal stores, 16 WG x 256 lanes per CU; HIP-event timed, 5 launches")
+    del a, b, c, sink
+    torch.cuda.empty_cache()
+    return out
 
-    k, m, S, n = w.k, w.m, w.S, w.n
-    dig = torch.empty((n, k + m, 32), dtype=torch.uint8, device=dev)
 
-    def put_path():
-        ctx.encode_strided_device(k, m, S, n, w.data.data_ptr(), k * S, S, w.parity.data_ptr(),
-                                  m * S, S, digests_ptr=dig.data_ptr(), stream=sh)
+def valu_bound_GBps(form: str, n_cus: int) -> float:
+    """Hashed-bytes ceiling of the SHA-256 form when every SIMD issues INT32
+    VALU at its measured rate: 64 B per block / lane-ops per block."""
+    lane_ops = n_cus * 4 * VALU_LANES_PER_SIMD_CYCLE * CLOCK_GHZ * 1e9
+    return lane_ops / SHA_VALU_PER_BLOCK[form] * 64 / 1e9
 
-    t = timed(put_path, 2)
-    out["put_path_encode_plus_sha256"] = {
-        "GiBps_payload": round(n * k * S / GIB / t, 3), "ms": round(t * 1e3, 2),
-        "what": "RS encode + SHA-256 of every data and parity chunk (write_chunk + "
-                "compute_and_write_parity compute)"}
-    del dig
+
+def hbm_block(alg_bytes: float, ms: float, kernel: str, cal: dict, ratio_key: str) -> dict:
+    ach = alg_bytes / (ms * 1e-3) / 1e9
+    d = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBPS, 4), "kernel": kernel, "bytes_per_launch": float(alg_bytes),
+         "ms_per_launch": round(ms, 4)}
+    if cal and cal.get(ratio_key):
+        d["box_stream_GBps"] = cal[ratio_key]
+        d["frac_of_box_stream"] = round(ach / cal[ratio_key], 4)
+        d["box_stream"] = ratio_key
+    return d
+
+
+def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
+    """Driver-timed secondary measurements beside the headline (VERDICT r1
+    item 1), each with its own roofline block: the north-star shape (encode
+    k=8 m=4, 1 MiB chunks), config 3 (verify + rebuild) with the SHA kernel
+    timed alone against the INT32-VALU bound, config 3c (8 concurrent
+    batches), and the reference-equivalent PUT compute (encode + SHA-256 of
+    all k+m chunks)."""
+    sh = stream.cuda_stream
+    n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    out = {}
+    # -- north star: encode k=8 m=4, 1 MiB, 4096 objects -------------------
+    w = make_workload("ns", torch, ctx, dev, sh, 0, 0)
+    torch.cuda.synchronize()
+    ms = event_ms(torch, stream, w.step, max(5, steps // 2))
+    ok = w.spot_check()
+    out["ns"] = {"workload": w.name, "GiBps_payload": round(w.payload / GIB / (ms * 1e-3), 3),
+                 "spot_check_vs_oracle": ok,
+                 "roofline": hbm_block(w.alg_bytes, ms, w.kernel, cal, "read2_write1_GBps")}
+    tr, src = pmc_traffic("k8m4", w.alg_bytes)
+    out["ns"]["roofline"]["traffic"], out["ns"]["roofline"]["traffic_source"] = tr, src
+    w.drop()
+    del w
+    torch.cuda.empty_cache()
+    # -- config 3: reconstruct 8+4, 2 erasures + verify, 1024 objects --------
     r = Reconstruct(torch, ctx, dev, sh, 1024, SEED)
-    t = timed(r.step, 3)
-    out["config3_reconstruct_verify"] = {
-        "GiBps_payload": round(r.payload / GIB / t, 3), "ms": round(t * 1e3, 2), "what": r.name}
+    ms_call = event_ms(torch, stream, r.step, 5)
+    ok = r.spot_check()
+    k, m, S, n = r.k, r.m, r.S, r.n
+    present_ptrs, present_lens = [], []
+    for o in range(n):
+        for i in range(k + m):
+            if r.present0[o * (k + m) + i]:
+                present_ptrs.append(r.obj[o, i].data_ptr())
+                present_lens.append(S)
+    dig = torch.empty((len(present_ptrs), 32), dtype=torch.uint8, device=dev)
+    ms_sha = event_ms(torch, stream, lambda: ctx.sha256_batch_device(present_ptrs, present_lens, dig.data_ptr(),
+                                                                     stream=sh), 3)
+    hashed = float(len(present_ptrs)) * S
+    form = "split" if len(present_ptrs) <= 32768 else "one"
+    sha_GBps = hashed / (ms_sha * 1e-3) / 1e9
+    vb = valu_bound_GBps(form, n_cus)
+    # decode alone: the same erasures, no digests (RS over the 8 survivors -> 2)
+    def decode_only():
+        pr = r.present0.copy()
+        rc, _ = ctx.reconstruct_strided_device(k, m, S, n, r.obj.data_ptr(), (k + m) * S, S, pr, stream=sh)
+        assert rc == 0
+    ms_rs = event_ms(torch, stream, decode_only, 3)
+    out["config3"] = {
+        "workload": r.name, "GiBps_payload": round(r.payload / GIB / (ms_call * 1e-3), 3),
+        "ms_per_call": round(ms_call, 3), "spot_check_vs_original": ok,
+        "roofline": {"bound": "valu", "kernel": f"sha256_{form}_kernel (alone, {len(present_ptrs)} x 1 MiB)",
+                     "achieved": round(sha_GBps, 1), "unit": "GB/s hashed",
+                     "peak": round(vb, 1), "frac": round(sha_GBps / vb, 4),
+                     "valu_lane_ops_per_block": SHA_VALU_PER_BLOCK[form],
+                     "valu_peak_lane_ops_per_s": n_cus * 4 * VALU_LANES_PER_SIMD_CYCLE * CLOCK_GHZ * 1e9,
+                     "ms_per_launch": round(ms_sha, 3), "us_per_block": round(ms_sha * 1e3 / (S / 64), 4),
+                     "frac_of_hbm": round(sha_GBps / HBM_PEAK_GBPS, 4),
+                     "note": ("10 240 messages fill 160 of 1024 SIMDs: this launch is bound by the serial "
+                              "chain of one 1 MiB message (16 384 blocks), not by chip-wide VALU issue")},
+        "rs_decode": hbm_block(float(n) * (k + 2) * S, ms_rs, "rs_apply_fast<R=2> (decode 8 -> 2, no verify)",
+                               cal, "copy_GBps"),
+    }
+    del dig
     r.drop()
+    del r
+    torch.cuda.empty_cache()
+    # -- config 3c: 8 concurrent batches -----------------------------------
+    rs = ReconstructStream(torch, ctx, dev, sh, 1024, 8, SEED)
+    torch.cuda.synchronize()
+    rs.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        rs.step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    hashed = 8 * 1024 * 10 * float(1 << 20)
+    sha_GBps = hashed / (ms * 1e-3) / 1e9
+    vb = valu_bound_GBps("one" if 8 * 10240 > 32768 else "split", n_cus)
+    out["config3c"] = {"workload": rs.name, "GiBps_payload": round(rs.payload / GIB / (ms * 1e-3), 3),
+                       "ms_per_step": round(ms, 2), "spot_check_vs_original": rs.spot_check(),
+                       "roofline": {"bound": "valu", "achieved": round(sha_GBps, 1), "unit": "GB/s hashed",
+                                    "peak": round(vb, 1), "frac": round(sha_GBps / vb, 4),
+                                    "what": "whole step (hash + decode + host work) against the hashing bound"},
+                       "breakdown": rs.breakdown()}
+    rs.drop()
+    del rs
+    torch.cuda.empty_cache()
+    # -- PUT compute: encode + SHA-256 of all k+m chunks, config 2 shape -----
+    w = make_workload("2", torch, ctx, dev, sh, 256, 0)
+    kk, mm, SS, nn = w.k, w.m, w.S, w.n
+    dig = torch.empty((nn, kk + mm, 32), dtype=torch.uint8, device=dev)
+    ms = event_ms(torch, stream, lambda: ctx.encode_strided_device(
+        kk, mm, SS, nn, w.data.data_ptr(), kk * SS, SS, w.parity.data_ptr(), mm * SS, SS,
+        digests_ptr=dig.data_ptr(), stream=sh), 2)
+    out["put_path_encode_plus_sha256"] = {
+        "GiBps_payload": round(nn * kk * SS / GIB / (ms * 1e-3), 3), "ms": round(ms, 2),
+        "what": (f"RS encode + SHA-256 of every data and parity chunk, {nn} x 4+2 x 10 MiB (write_chunk + "
+                 "compute_and_write_parity compute); bound by one 10 MiB chunk's SHA chain (163 840 blocks)")}
+    del dig
+    w.drop()
+    del w
+    torch.cuda.empty_cache()
     return out
 
 
@@ -600,10 +755,9 @@ def main() -> int:
     ap.add_argument("--workers", type=int, default=8, help="config 3c: concurrent batches")
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--extra", action="store_true",
-                    help="also time the secondary paths (PUT path with SHA-256, config 3 "
-                         "reconstruct + verify, copy peak); off by default so a rocprofv3 "
-                         "run of the default command profiles only the headline kernel")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the secondary measurements that the default config-2 run adds "
+                         "at N=1 (north-star shape, config 3 / 3c, PUT compute)")
     args = ap.parse_args()
 
     import torch
@@ -630,8 +784,11 @@ def main() -> int:
 
     import maxio_amd
 
+    # config 3c (and the default run's extras, which include it) needs one
+    # slot per concurrent batch.
+    with_extra = args.config == "2" and world == 1 and not args.no_extra
     ctx = maxio_amd.Context(device_mask=1 << (local if world > 1 else 0),
-                            streams_per_device=max(2, args.workers if args.config == "3c" else 2))
+                            streams_per_device=max(2, args.workers if args.config == "3c" or with_extra else 2))
     dev = torch.device("cuda", torch.cuda.current_device())
     # A dedicated stream: the kernels and the HIP events that time them are
     # on the same queue.
@@ -664,19 +821,11 @@ def main() -> int:
     value = float(w.payload) * world * args.steps / GIB / elapsed  # weak scaling: all ranks
     achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
 
-    # §8(d) second denominator: this box's device copy rate (read + write).
-    copy_peak = None
-    if rank == 0:
-        src = torch.empty(2 << 30, dtype=torch.uint8, device=dev)
-        dst = torch.empty_like(src)
-        dst.copy_(src)
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        for _ in range(5):
-            dst.copy_(src)
-        torch.cuda.synchronize()
-        copy_peak = 2 * src.numel() * 5 / (time.perf_counter() - t) / 1e9
-        del src, dst
+    # §8(d) second denominator: this box's rates for plain streams of the RS
+    # kernel's own load/store forms (libmaxio_probe.so).
+    cal = calibrate(torch, dev, stream) if rank == 0 else None
+    box_key = "read2_write1_GBps" if getattr(w, "rw_ratio", None) == 2 else "copy_GBps"
+    copy_peak = cal.get(box_key) if cal else None
 
     extra = None
     if rank == 0 and hasattr(w, "breakdown"):
@@ -688,8 +837,13 @@ def main() -> int:
         ms_launch = crc["ms"]
         achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
         w.kernel = "crc_tiles_kernel + crc_finish_kernel (CRC32C alone)"
-    if args.extra and rank == 0 and args.config == "2":
-        extra = secondary(ctx, torch, dev, sh, w)
+    dropped = False
+    if rank == 0 and with_extra:
+        w.drop()  # HBM for the secondary workloads
+        dropped = True
+        torch.cuda.empty_cache()
+        extra = extras(ctx, torch, dev, stream, args.steps, cal)
+        extra["calibration"] = cal
     cpu = cpu_all = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the CPU leg runs at N=1 only
         spec = w.cpu_work()
@@ -706,7 +860,8 @@ def main() -> int:
             cpu_all = {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
                        "sample": f"{n} calls in {el:.1f}s on {threads} threads "
                                  f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={nc})"}
-    w.drop()
+    if not dropped:
+        w.drop()
     torch.cuda.empty_cache()
 
     if rank == 0:
@@ -742,8 +897,9 @@ def main() -> int:
                 "bytes_per_launch": float(w.alg_bytes),
                 "ms_per_launch": round(ms_launch, 4),
                 "traffic_source": tsrc,
-                "box_copy_GBps": round(copy_peak, 1) if copy_peak else None,
-                "frac_of_box_copy": round(achieved / copy_peak, 4) if copy_peak else None,
+                "box_stream": box_key if copy_peak else None,
+                "box_stream_GBps": round(copy_peak, 1) if copy_peak else None,
+                "frac_of_box_stream": round(achieved / copy_peak, 4) if copy_peak else None,
             },
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,

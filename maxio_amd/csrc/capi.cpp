@@ -2,6 +2,7 @@
 // pointer drop-ins, device-resident batches).  No exception crosses the ABI.
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <unordered_map>
 #include <cstring>
 #include <map>
@@ -73,8 +74,15 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
             return nullptr;
         }
         if (streams_per_device < 1) streams_per_device = 1;
+        // MXEC_LOGICAL_DEVICES=L (tests): open every selected device L times,
+        // each copy with its own slots, streams, arenas, combiner and
+        // pipeline, so the multi-device paths (per-device workers, round
+        // robin, error aggregation) run on a one-GPU box.
+        int logical = 1;
+        if (const char* e = getenv("MXEC_LOGICAL_DEVICES")) logical = std::max(1, std::min(8, atoi(e)));
         auto* ctx = new mxec_ctx();
-        for (int d = 0; d < n && d < 32; ++d) {
+        for (int dl = 0; dl < n * logical && dl < 32 * logical; ++dl) {
+            const int d = dl / logical;
             if (device_mask && !(device_mask & (1u << d))) continue;
             auto dev = std::make_unique<Device>();
             dev->id = d;
@@ -137,12 +145,15 @@ void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes) {
         set_error(MXEC_E_OOM, "pinned host allocation failed");
         return nullptr;
     }
+    pinned_register(p, bytes);
     return p;
 }
 
 void mxec_host_free(mxec_ctx* ctx, void* p) {
     (void)ctx;
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    pinned_unregister(p);
+    (void)hipHostFree(p);
 }
 
 int mxec_rs_check(int k, int m) { return rs_check(k, m); }

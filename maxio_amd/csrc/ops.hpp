@@ -77,10 +77,26 @@ int guarded(F&& f) {
 
 // A device of the context (dev_index < 0: round robin) with one of its slots
 // locked for the duration of a call.
+// On the way out (any path, the lock still held) it waits for DMAs still
+// reading the caller's page-locked buffers (Slot::borrowed).
 struct DevScope {
     Device* d = nullptr;
     std::unique_lock<std::mutex> lk;
     Slot* slot = nullptr;
+    DevScope() = default;
+    DevScope(const DevScope&) = delete;
+    DevScope& operator=(const DevScope&) = delete;
+    ~DevScope() {
+        if (slot && slot->borrowed) {
+            const std::string keep = last_error();  // an early return's message stays
+            (void)slot_wait(*slot, slot->borrowed);
+            if (slot->borrowed) {  // the wait itself failed: drain the device
+                (void)hipStreamSynchronize(slot->borrowed);
+                slot->borrowed = nullptr;
+            }
+            set_error(0, keep);
+        }
+    }
     int open(mxec_ctx* ctx, int dev_index) {
         if (!ctx) return set_error(MXEC_E_INVALID_ARG, "null context");
         d = pick_device(&ctx->c, dev_index);

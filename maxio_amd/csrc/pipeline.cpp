@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <system_error>
 #include <thread>
 #include <tuple>
 #include <vector>
@@ -40,18 +41,7 @@ constexpr int kComputeStreams = 2;  // RS stream + SHA stream (4 HW queues per p
 
 uint64_t rup(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-bool pinned_addr(const void* p) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeHost;
-}
-
-bool is_pinned(const void* p, uint64_t len) {
-    return p && len && pinned_addr(p) && pinned_addr(static_cast<const uint8_t*>(p) + len - 1);
-}
+bool is_pinned(const void* p, uint64_t len) { return pinned_range(p, len); }
 
 struct HostObj {
     int k, m;
@@ -397,10 +387,18 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
         }
         std::vector<int> rcs(D, MXEC_OK);
         std::vector<std::string> errs(D);
-        std::vector<std::thread> th;
-        for (size_t d = 0; d < D; ++d) {
-            if (per[d].empty()) continue;
-            th.emplace_back([&, d] {
+        // One worker per device.  Every thread is joined on every path (a
+        // joinable std::thread destroyed during unwinding would terminate the
+        // process), and no exception leaves a worker.
+        struct Joiner {
+            std::vector<std::thread> th;
+            ~Joiner() {
+                for (auto& t : th)
+                    if (t.joinable()) t.join();
+            }
+        } j;
+        auto work = [&](size_t d) {
+            try {
                 Device& dev = *ctx->c.devs[d];
                 rcs[d] = [&]() -> int {
                     MXEC_HIP(hipSetDevice(dev.id));
@@ -412,9 +410,23 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
                     return p.run(per[d]);
                 }();
                 if (rcs[d] != MXEC_OK) errs[d] = last_error();
-            });
+            } catch (const std::bad_alloc&) {
+                rcs[d] = MXEC_E_OOM;
+                errs[d] = "host allocation failed";
+            } catch (const std::exception& e) {
+                rcs[d] = MXEC_E_INVALID_ARG;
+                errs[d] = e.what();
+            }
+        };
+        for (size_t d = 0; d < D; ++d) {
+            if (per[d].empty()) continue;
+            try {
+                j.th.emplace_back(work, d);
+            } catch (const std::system_error&) {
+                work(d);  // no thread to be had: run this device's share here
+            }
         }
-        for (auto& t : th) t.join();
+        for (auto& t : j.th) t.join();
         for (size_t d = 0; d < D; ++d)
             if (rcs[d] != MXEC_OK) return set_error(rcs[d], errs[d]);
         if (first_err != MXEC_OK) return set_error(first_err, first_msg);

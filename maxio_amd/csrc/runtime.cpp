@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 
 namespace mxec {
 
@@ -49,12 +50,14 @@ int slot_wait(Slot& slot, hipStream_t s) {
     }();
     if (spin) {
         MXEC_HIP(hipStreamSynchronize(s));
+        if (slot.borrowed == s) slot.borrowed = nullptr;
         return MXEC_OK;
     }
     if (!slot.sync_ev)
         MXEC_HIP(hipEventCreateWithFlags(&slot.sync_ev, hipEventBlockingSync | hipEventDisableTiming));
     MXEC_HIP(hipEventRecord(slot.sync_ev, s));
     MXEC_HIP(hipEventSynchronize(slot.sync_ev));
+    if (slot.borrowed == s) slot.borrowed = nullptr;
     return MXEC_OK;
 }
 
@@ -69,9 +72,7 @@ void slot_destroy(Slot& slot) {
 }
 
 namespace {
-// True when [p, p + n) is page-locked host memory HIP can DMA from directly
-// (mxec_host_alloc, hipHostMalloc / hipHostRegister).
-bool pinned_host(const void* p) {
+bool hip_says_pinned(const void* p) {
     hipPointerAttribute_t at{};
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();  // pageable memory is reported as an error
@@ -79,13 +80,41 @@ bool pinned_host(const void* p) {
     }
     return at.type == hipMemoryTypeHost;
 }
+
+std::mutex g_pinned_mu;
+std::map<uintptr_t, size_t> g_pinned;  // base -> bytes (mxec_host_alloc)
 }  // namespace
+
+void pinned_register(const void* p, size_t n) {
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    g_pinned[reinterpret_cast<uintptr_t>(p)] = n;
+}
+
+void pinned_unregister(const void* p) {
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+}
+
+bool pinned_range(const void* p, uint64_t len) {
+    if (!p || !len) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    {
+        std::lock_guard<std::mutex> g(g_pinned_mu);
+        auto it = g_pinned.upper_bound(a);
+        if (it != g_pinned.begin()) {
+            --it;
+            if (a - it->first < it->second) return len <= it->second - (a - it->first);
+        }
+    }
+    return hip_says_pinned(p) && hip_says_pinned(static_cast<const uint8_t*>(p) + len - 1);
+}
 
 int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
     if (segs.empty()) return MXEC_OK;
     bool all_pinned = true;
-    for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_host(g.src));
+    for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.src, g.len));
     if (all_pinned) {  // DMA straight from the caller's page-locked buffers
+        slot.borrowed = s;  // from here on every exit of the call waits on s
         for (const auto& g : segs)
             if (g.len) MXEC_HIP(hipMemcpyAsync(dev_base + g.dst_off, g.src, g.len, hipMemcpyHostToDevice, s));
         return MXEC_OK;
@@ -120,7 +149,7 @@ int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vec
 int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs) {
     if (segs.empty()) return slot_wait(slot, s);
     bool all_pinned = true;
-    for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_host(g.dst));
+    for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.dst, g.len));
     if (all_pinned) {  // DMA straight into the caller's page-locked buffers
         for (const auto& g : segs)
             if (g.len) MXEC_HIP(hipMemcpyAsync(g.dst, dev_base + g.src_off, g.len, hipMemcpyDeviceToHost, s));

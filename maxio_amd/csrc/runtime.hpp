@@ -75,6 +75,10 @@ struct Slot {
     hipEvent_t stage_done[2] = {nullptr, nullptr};
     // Blocking-sync event for the host-API waits (slot_wait).
     hipEvent_t sync_ev = nullptr;
+    // Set by upload_segments when it queued DMAs straight from the caller's
+    // page-locked memory (no staging copy): the call must not return before
+    // they finish, on any path.  slot_wait clears it; DevScope waits on it.
+    hipStream_t borrowed = nullptr;
 };
 
 // Wait for everything enqueued on `s` so far.  An event created with
@@ -93,9 +97,12 @@ struct UploadSeg {
     uint64_t len;
 };
 constexpr uint64_t kStagePiece = uint64_t(8) << 20;
-// Copy pageable host segments to dev_base + dst_off through the slot's pinned
-// pair, enqueued on `s` (the caller waits or orders later work on `s`).
-// Segments must be sorted by dst_off and not overlap.
+// Copy host segments to dev_base + dst_off, enqueued on `s`: pageable ones
+// through the slot's pinned pair, page-locked ones by direct DMA from the
+// caller's memory.  In the direct case the slot is marked `borrowed` and the
+// call must wait on `s` before it returns to its caller (slot_wait, or the
+// DevScope destructor on an early error return).  Segments must be sorted by
+// dst_off and not overlap.
 int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs);
 // One device -> host download segment: len bytes from src_off to dst.
 struct DownloadSeg {
@@ -107,6 +114,15 @@ struct DownloadSeg {
 // every byte has landed (waits for everything enqueued on `s` before it,
 // too).  Segments sorted by src_off, not overlapping.
 int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs);
+
+// Page-locked host ranges.  mxec_host_alloc registers its allocations so the
+// copy paths recognise them without a hipPointerGetAttributes call per
+// segment; other page-locked memory (hipHostRegister) is asked of HIP, at both
+// ends of the range.
+void pinned_register(const void* p, size_t n);
+void pinned_unregister(const void* p);
+// True when every byte of [p, p + len) is page-locked host memory.
+bool pinned_range(const void* p, uint64_t len);
 
 struct Device {
     int id = 0;

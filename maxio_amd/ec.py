@@ -258,17 +258,21 @@ class Context:
             _u64p(data_len) if data_len is not None else None, _pp(parity_ptrs), digests_ptr))
 
     def encode_batch_host(self, objs: Sequence[tuple], data_ptrs, parity_ptrs, data_len=None,
-                          digests: Optional[np.ndarray] = None):
+                          digests: Optional[np.ndarray] = None, return_rc: bool = False):
         """mxec_encode_batch_host: host pointers in and out (ints), pipelined
         over every device.  digests: uint8 array of sum(k+m)*32 or None.
-        Returns the per-object status array."""
+        Returns the per-object status array (with return_rc: (rc, status),
+        no exception on a failing object)."""
         arr = (N.Object * len(objs))(*[N.Object(k, m, s) for (k, m, s) in objs])
         status = np.zeros(max(1, len(objs)), np.int32)
-        _check(self._lib.mxec_encode_batch_host(
+        rc = self._lib.mxec_encode_batch_host(
             self._h, arr, len(objs), _pp(data_ptrs),
             _u64p(data_len) if data_len is not None else None, _pp(parity_ptrs),
             digests.ctypes.data_as(N.U8P) if digests is not None else None,
-            status.ctypes.data_as(N.I32P)))
+            status.ctypes.data_as(N.I32P))
+        if return_rc:
+            return rc, status[: len(objs)]
+        _check(rc)
         return status[: len(objs)]
 
     def reconstruct_strided_device(self, k, m, shard_size, n_obj, shards_ptr, obj_stride,

@@ -64,5 +64,6 @@ def test_shard_objects_edges():
     assert list(bench.shard_objects(0, 0, 2)) == []
     assert list(bench.shard_objects(3, 1, 4)) == [1]
     assert list(bench.shard_objects(3, 3, 4)) == []
+    assert list(bench.shard_objects(10, 1, 4)) == [1, 5, 9]  # object i -> GPU i mod G
     covered = [o for r in range(8) for o in bench.shard_objects(1024 * 8, r, 8)]
-    assert covered == list(range(1024 * 8))
+    assert sorted(covered) == list(range(1024 * 8))

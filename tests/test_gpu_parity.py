@@ -539,3 +539,68 @@ def test_pinned_host_buffers_take_the_direct_dma_path(ctx, tmp_path):
     assert maxio_amd.lib().mxec_get_object_chunked(ctx.handle, ec.encode(), 0, (1 << 64) - 1, out.ctypes.data,
                                                    body.size, ctypes.byref(got)) == 0
     assert got.value == body.size and np.array_equal(out, body)
+
+
+def test_pinned_error_paths_wait_for_the_dma(ctx):
+    """A call whose uploads read the caller's page-locked buffers directly
+    returns only after those DMAs finished, on its error paths too: too few
+    shards present (no digests given, a routine result) frees the buffers at
+    once; the next call on the context still works and its results are
+    exact."""
+    import ctypes
+
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    k, m, S = 6, 3, 1 << 20
+    rng = np.random.default_rng(41)
+    for _ in range(4):
+        bufs = [ctx.host_array(S) for _ in range(k + m)]
+        for b in bufs:
+            b[:] = rng.integers(0, 256, S, dtype=np.uint8)
+        present = np.array([1] * (k - 1) + [0] * (m + 1), np.uint8)
+        ptrs = (ctypes.c_void_p * (k + m))(*[b.ctypes.data for b in bufs])
+        n = ctypes.c_int(0)
+        rc = maxio_amd.lib().mxec_reconstruct(ctx.handle, k, m, S, ptrs, None, None,
+                                              present.ctypes.data_as(u8p), 0, ctypes.byref(n))
+        assert rc == -10 and n.value == k - 1
+        assert b"too many missing" in maxio_amd.lib().mxec_last_error()
+        del bufs, ptrs  # page-locked memory handed back right away
+        import gc
+
+        gc.collect()
+    data = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(4)]
+    par, _ = ctx.encode(data, 2, 4096)
+    want = oracle.encode(data, 2, 4096)
+    assert all(np.array_equal(par[i], want[i]) for i in range(2))
+
+
+def test_sha256_mixed_pinned_and_pageable(ctx):
+    """One batch with page-locked and pageable buffers (the staging path takes
+    the whole call) and a range that starts inside a pinned allocation but
+    runs past its end is never sent by direct DMA."""
+    rng = np.random.default_rng(43)
+    pinned = [ctx.host_array(n) for n in (5000, 64, 1 << 20)]
+    for p in pinned:
+        p[:] = rng.integers(0, 256, p.size, dtype=np.uint8)
+    pageable = [rng.integers(0, 256, n, dtype=np.uint8) for n in (1, 99_999)]
+    bufs = [pinned[0], pageable[0], pinned[1], pageable[1], pinned[2]]
+    assert ctx.sha256(bufs) == [hashlib.sha256(b.tobytes()).digest() for b in bufs]
+    # slices: inside one pinned allocation (direct) and the tail of one
+    parts = [pinned[2][100:200_000], pinned[2][-7:], pinned[0][4999:]]
+    assert ctx.sha256(parts) == [hashlib.sha256(b.tobytes()).digest() for b in parts]
+
+
+def test_put_data_chunk_write_error_wins(ctx, tmp_path):
+    """PUT whose data-chunk write fails (a directory squats on 000001): the
+    I/O error is what the call reports — the reference writes the data chunks
+    before compute_and_write_parity (filesystem.rs:729-750) — and the writer
+    thread is joined (the context keeps working)."""
+    ec = tmp_path / "w.ec"
+    (ec / "000001").mkdir(parents=True)
+    body = np.random.default_rng(44).integers(0, 256, 3 * 4096 + 5, dtype=np.uint8)
+    with pytest.raises(maxio_amd.RSError) as ei:
+        ctx.put_object_chunked(str(ec), 4096, 2, body)
+    assert ei.value.code == -40 and "000001" in str(ei.value)
+    assert not (ec / "manifest.json").exists()
+    ok = tmp_path / "ok.ec"
+    ctx.put_object_chunked(str(ok), 4096, 2, body)
+    assert ctx.get_object_chunked(str(ok)) == body.tobytes()
