@@ -134,7 +134,6 @@ class Encode:
         self.parity = torch.zeros((n, m, S), dtype=torch.uint8, device=dev)
         self.payload = n * k * S
         self.alg_bytes = n * (k + m) * S
-        self.rw_ratio = k // m if k % m == 0 else None  # read:write of the stream
         r = min(m, 8)
         self.kernel = f"rs_apply_fast<R={r},V={4 if r <= 4 else 2},NT=1>"
         self.name = label
@@ -570,7 +569,9 @@ def probe_lib():
     lib = ctypes.CDLL(p)
     for fn, args in (("mxprobe_copy", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
                      ("mxprobe_read2_write1", [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]),
-                     ("mxprobe_read", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p])):
+                     ("mxprobe_read", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+                     ("mxprobe_rs_pattern", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p])):
         getattr(lib, fn).argtypes = args
         getattr(lib, fn).restype = ctypes.c_int
     return lib
@@ -613,9 +614,21 @@ def calibrate(torch, dev, stream) -> dict:
     out["read2_write1_GBps"] = round(3 * n / (ms * 1e-3) / 1e9, 1)
     ms = event_ms(torch, stream, lambda: run(lib.mxprobe_read(a.data_ptr(), n, sink.data_ptr(), sh)), 5)
     out["read_GBps"] = round(n / (ms * 1e-3) / 1e9, 1)
-    out["what"] = ("libmaxio_probe.so streams over 2 GiB buffers: nontemporal global_load_dwordx4, 4 loads in "
-                   "flight per lane, nontemporal stores, 16 WG x 256 lanes per CU; HIP-event timed, 5 launches")
     del a, b, c, sink
+    torch.cuda.empty_cache()
+    # The RS kernel's own access pattern (same tile, same loads in flight,
+    # 32 WG per CU) with XOR for the GF math, at the two encode shapes.
+    for k, m, S, n in ((4, 2, 10 << 20, 64), (8, 4, 1 << 20, 512)):
+        d = torch.empty((n, k, S), dtype=torch.uint8, device=dev)
+        d.random_(0, 256)
+        p = torch.empty((n, m, S), dtype=torch.uint8, device=dev)
+        ms = event_ms(torch, stream, lambda: run(lib.mxprobe_rs_pattern(d.data_ptr(), p.data_ptr(), k, m, S, n, sh)), 5)
+        out[f"rs_pattern_k{k}m{m}_GBps"] = round(n * (k + m) * S / (ms * 1e-3) / 1e9, 1)
+        del d, p
+    out["what"] = ("libmaxio_probe.so streams, HIP-event timed, 5 launches each: copy / read2_write1 / read over 2 GiB "
+                   "buffers (nontemporal global_load_dwordx4, 4 loads in flight per lane, nontemporal stores, 16 WG "
+                   "x 256 lanes per CU); rs_pattern_kXmY = the RS kernel's tile and load schedule with XOR for the "
+                   "GF math, 32 WG per CU, over 3.75 GiB (k=4 m=2, 10 MiB) / 6 GiB (k=8 m=4, 1 MiB)")
     torch.cuda.empty_cache()
     return out
 
@@ -656,7 +669,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     ok = w.spot_check()
     out["ns"] = {"workload": w.name, "GiBps_payload": round(w.payload / GIB / (ms * 1e-3), 3),
                  "spot_check_vs_oracle": ok,
-                 "roofline": hbm_block(w.alg_bytes, ms, w.kernel, cal, "read2_write1_GBps")}
+                 "roofline": hbm_block(w.alg_bytes, ms, w.kernel, cal, "rs_pattern_k8m4_GBps")}
     tr, src = pmc_traffic("k8m4", w.alg_bytes)
     out["ns"]["roofline"]["traffic"], out["ns"]["roofline"]["traffic_source"] = tr, src
     w.drop()
@@ -824,7 +837,10 @@ def main() -> int:
     # §8(d) second denominator: this box's rates for plain streams of the RS
     # kernel's own load/store forms (libmaxio_probe.so).
     cal = calibrate(torch, dev, stream) if rank == 0 else None
-    box_key = "read2_write1_GBps" if getattr(w, "rw_ratio", None) == 2 else "copy_GBps"
+    box_key = {(4, 2): "rs_pattern_k4m2_GBps", (8, 4): "rs_pattern_k8m4_GBps"}.get(
+        (getattr(w, "k", 0), getattr(w, "m", 0)), "copy_GBps")
+    if not isinstance(w, Encode):
+        box_key = "copy_GBps"
     copy_peak = cal.get(box_key) if cal else None
 
     extra = None

@@ -11,6 +11,11 @@
 //   mxprobe_read2_write1  read 2n bytes (two sources), write n (2:1, the
 //                      encode stream of k=4 m=2 and k=8 m=4)
 //   mxprobe_read       read n bytes                            (read-only)
+//   mxprobe_rs_pattern the RS kernel's own access pattern with the GF math
+//                      replaced by XOR: object-major [n][k][S] in,
+//                      [n][m][S] out, tiles of 256 lanes x 16 B x 4 vectors,
+//                      4 inputs x 4 vectors of loads in flight, 32 WG per CU
+//                      (the ceiling the RS kernel is measured against)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -60,6 +65,39 @@ __global__ __launch_bounds__(256) void probe_read(const u32x4* __restrict__ s, u
     if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) sink[0] = acc;  // keeps the loads; never true for the probe's data
 }
 
+template <int R>
+__global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                     uint32_t k, uint64_t S, uint64_t n_obj) {
+    constexpr uint64_t kTile = 256 * 16 * 4;
+    const uint64_t tpo = S / kTile, n_tiles = tpo * n_obj;
+    for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint64_t o = t / tpo, base = (t - o * tpo) * kTile + threadIdx.x * 16;
+        u32x4 acc[4][R];
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int i = 0; i < R; ++i) acc[v][i] = u32x4{0, 0, 0, 0};
+        for (uint32_t j = 0; j < k; j += 4) {
+            u32x4 x[4][4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    x[jj][v] = __builtin_nontemporal_load(
+                        reinterpret_cast<const u32x4*>(data + (o * k + j + jj) * S + base + v * 4096));
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int i = 0; i < R; ++i) acc[v][i] ^= (x[0][v] ^ x[1][v]) + (x[2][v] ^ x[3][v]) * (i + 1u);
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                __builtin_nontemporal_store(acc[v][i], reinterpret_cast<u32x4*>(par + (o * R + i) * S + base + v * 4096));
+    }
+}
+
 int grid() {
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
@@ -94,5 +132,22 @@ extern "C" int mxprobe_read(const void* src, uint64_t bytes, void* sink16, void*
         return int(hipErrorInvalidValue);
     hipLaunchKernelGGL(probe_read, dim3(grid()), dim3(256), 0, static_cast<hipStream_t>(stream),
                        static_cast<const u32x4*>(src), static_cast<u32x4*>(sink16), bytes / 16);
+    return int(hipGetLastError());
+}
+
+// k a multiple of 4, m in {1, 2, 4}, S a multiple of 16 KiB.
+extern "C" int mxprobe_rs_pattern(const void* data, void* parity, uint32_t k, uint32_t m, uint64_t S, uint64_t n_obj,
+                                  void* stream) {
+    if (k == 0 || (k & 3) || S == 0 || (S % 16384) ||
+        ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
+        return int(hipErrorInvalidValue);
+    const dim3 g(uint32_t(grid() * 2)), b(256);  // 32 WG per CU, as the RS kernel
+    const auto* in = static_cast<const uint8_t*>(data);
+    auto* out = static_cast<uint8_t*>(parity);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (m == 1) hipLaunchKernelGGL(probe_pattern<1>, g, b, 0, s, in, out, k, S, n_obj);
+    else if (m == 2) hipLaunchKernelGGL(probe_pattern<2>, g, b, 0, s, in, out, k, S, n_obj);
+    else if (m == 4) hipLaunchKernelGGL(probe_pattern<4>, g, b, 0, s, in, out, k, S, n_obj);
+    else return int(hipErrorInvalidValue);
     return int(hipGetLastError());
 }

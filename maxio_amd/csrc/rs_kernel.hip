@@ -102,6 +102,44 @@ __device__ __forceinline__ void mac_column(uint32_t (&acc)[V][4][R], const Vec4 
         for (int w = 0; w < 4; ++w) mac_dword<R>(acc[v][w], x[v].w[w], t, hi);
 }
 
+// Two input columns at once: the six partial products of each output fold
+// into the accumulator with three XOR3s (1.5 per input instead of an XOR3
+// and an XOR), the VALU saving that matters at R = 4, where the kernel's
+// VALU issue sits near the HBM stream's pace.
+template <int R, int V>
+__device__ __forceinline__ void mac_column_pair(uint32_t (&acc)[V][4][R], const Vec4 (&xa)[V], const Vec4 (&xb)[V],
+                                                const uint32_t* __restrict__ ta, const uint32_t* __restrict__ tb) {
+    uint32_t ha[R][2], hb[R][2];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        ha[i][0] = __builtin_amdgcn_readfirstlane(ta[8 * i + 1]);
+        ha[i][1] = __builtin_amdgcn_readfirstlane(ta[8 * i + 3]);
+        hb[i][0] = __builtin_amdgcn_readfirstlane(tb[8 * i + 1]);
+        hb[i][1] = __builtin_amdgcn_readfirstlane(tb[8 * i + 3]);
+        asm volatile("" : "+v"(ha[i][0]), "+v"(ha[i][1]), "+v"(hb[i][0]), "+v"(hb[i][1]));
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t a = xa[v].w[w], b = xb[v].w[w];
+            const uint32_t a0 = a & 0x07070707u, a1 = (a >> 3) & 0x07070707u, a2 = (a >> 6) & 0x03030303u;
+            const uint32_t b0 = b & 0x07070707u, b1 = (b >> 3) & 0x07070707u, b2 = (b >> 6) & 0x03030303u;
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const uint32_t pa0 = __builtin_amdgcn_perm(ha[i][0], ta[8 * i + 0], a0);
+                const uint32_t pa1 = __builtin_amdgcn_perm(ha[i][1], ta[8 * i + 2], a1);
+                const uint32_t pa2 = __builtin_amdgcn_perm(a2, ta[8 * i + 4], a2);
+                const uint32_t pb0 = __builtin_amdgcn_perm(hb[i][0], tb[8 * i + 0], b0);
+                const uint32_t pb1 = __builtin_amdgcn_perm(hb[i][1], tb[8 * i + 2], b1);
+                const uint32_t pb2 = __builtin_amdgcn_perm(b2, tb[8 * i + 4], b2);
+                uint32_t t = __builtin_amdgcn_bitop3_b32(acc[v][w][i], pa0, pa1, 0x96);
+                t = __builtin_amdgcn_bitop3_b32(t, pa2, pb0, 0x96);
+                acc[v][w][i] = __builtin_amdgcn_bitop3_b32(t, pb1, pb2, 0x96);
+            }
+        }
+}
+
 // Global-address-space views: pointers fetched from the descriptor tables are
 // generic in HIP; casting them lets the backend emit global_load/store
 // (vmcnt only) instead of flat_* (vmcnt + lgkmcnt).
@@ -263,16 +301,29 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
         uint32_t j = 0;
         for (; j + 4 <= k; j += 4) {
             Vec4 x[4][V];
+            // Wave-uniform: all four inputs reach past this tile (every tile
+            // but the few past a short last chunk).  The common case loads
+            // unconditionally; the per-input select would zero 4V registers
+            // and branch around every load, one VALU per input dword.
+            if (il[j] >= end && il[j + 1] >= end && il[j + 2] >= end && il[j + 3] >= end) {
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                gcptr p = ((gcptr)(ip[j + jj])) + lane;
-                const bool live = il[j + jj] >= end;  // else ends at/before base: zero
+                for (int jj = 0; jj < 4; ++jj) {
+                    gcptr p = ((gcptr)(ip[j + jj])) + lane;
 #pragma unroll
-                for (int v = 0; v < V; ++v)
-                    x[jj][v] = live ? gload16<NT>(p + v * kThreads * 16) : Vec4{{0, 0, 0, 0}};
+                    for (int v = 0; v < V; ++v) x[jj][v] = gload16<NT>(p + v * kThreads * 16);
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    gcptr p = ((gcptr)(ip[j + jj])) + lane;
+                    const bool live = il[j + jj] >= end;  // else ends at/before base: zero
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        x[jj][v] = live ? gload16<NT>(p + v * kThreads * 16) : Vec4{{0, 0, 0, 0}};
+                }
             }
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * r_total * 8);
+            mac_column_pair<R, V>(acc, x[0], x[1], tab + (j + 0) * r_total * 8, tab + (j + 1) * r_total * 8);
+            mac_column_pair<R, V>(acc, x[2], x[3], tab + (j + 2) * r_total * 8, tab + (j + 3) * r_total * 8);
         }
         for (; j < k; ++j) {
             if (il[j] < end) continue;  // zero column: contributes nothing

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "../../include/maxio_ec.h"
+#include "manifest.hpp"
 #include "ops.hpp"
 #include "runtime.hpp"
 
@@ -230,175 +231,20 @@ void fill_info(mxec_chunk_info* ci, uint32_t index, uint64_t size, const uint8_t
     ci->kind = kind;
 }
 
-// ---- ChunkManifest JSON --------------------------------------------------
-struct Manifest {
-    uint32_t version = 1;
-    uint64_t total_size = 0, chunk_size = 0;
-    uint32_t chunk_count = 0;
-    struct Chunk {
-        uint32_t index = 0;
-        uint64_t size = 0;
-        std::string sha256;
-        uint8_t kind = 0;
-    };
-    std::vector<Chunk> chunks;
-    bool has_parity = false, has_shard = false, has_plain = false;
-    uint32_t parity_shards = 0;
-    uint64_t shard_size = 0, plaintext_size = 0;
-};
-
-// serde_json::to_string_pretty layout (two-space indent, "key": value, no
-// trailing newline), fields in ChunkManifest declaration order; `kind` only
-// for parity (skip_serializing_if = is_data), Option fields only when Some.
-std::string manifest_json(const Manifest& m) {
-    std::ostringstream o;
-    o << "{\n  \"version\": " << m.version << ",\n  \"total_size\": " << m.total_size
-      << ",\n  \"chunk_size\": " << m.chunk_size << ",\n  \"chunk_count\": " << m.chunk_count
-      << ",\n  \"chunks\": [";
-    for (size_t i = 0; i < m.chunks.size(); ++i) {
-        const auto& c = m.chunks[i];
-        o << (i ? ",\n" : "\n") << "    {\n      \"index\": " << c.index << ",\n      \"size\": " << c.size
-          << ",\n      \"sha256\": \"" << c.sha256 << "\"";
-        if (c.kind == 1) o << ",\n      \"kind\": \"parity\"";
-        o << "\n    }";
-    }
-    o << (m.chunks.empty() ? "]" : "\n  ]");
-    if (m.has_parity) o << ",\n  \"parity_shards\": " << m.parity_shards;
-    if (m.has_shard) o << ",\n  \"shard_size\": " << m.shard_size;
-    if (m.has_plain) o << ",\n  \"plaintext_size\": " << m.plaintext_size;
-    o << "\n}";
-    return o.str();
-}
-
-// Minimal JSON reader for the manifest schema (serde accepts any field
-// order and whitespace, so this does too).
-class Json {
-public:
-    explicit Json(const std::string& s) : s_(s) {}
-    bool parse(Manifest& m) {
-        ws();
-        if (!eat('{')) return false;
-        ws();
-        if (eat('}')) return true;
-        for (;;) {
-            std::string key;
-            ws();
-            if (!str(key)) return false;
-            ws();
-            if (!eat(':')) return false;
-            ws();
-            if (key == "chunks") {
-                if (!chunks(m.chunks)) return false;
-            } else if (key == "version") {
-                uint64_t v; if (!num(v)) return false; m.version = uint32_t(v);
-            } else if (key == "total_size") {
-                if (!num(m.total_size)) return false;
-            } else if (key == "chunk_size") {
-                if (!num(m.chunk_size)) return false;
-            } else if (key == "chunk_count") {
-                uint64_t v; if (!num(v)) return false; m.chunk_count = uint32_t(v);
-            } else if (key == "parity_shards") {
-                if (null()) { m.has_parity = false; }
-                else { uint64_t v; if (!num(v)) return false; m.parity_shards = uint32_t(v); m.has_parity = true; }
-            } else if (key == "shard_size") {
-                if (null()) { m.has_shard = false; }
-                else { if (!num(m.shard_size)) return false; m.has_shard = true; }
-            } else if (key == "plaintext_size") {
-                if (null()) { m.has_plain = false; }
-                else { if (!num(m.plaintext_size)) return false; m.has_plain = true; }
-            } else if (!skip()) {
-                return false;
-            }
-            ws();
-            if (eat(',')) continue;
-            if (eat('}')) return true;
-            return false;
-        }
-    }
-
-private:
-    const std::string& s_;
-    size_t i_ = 0;
-    void ws() { while (i_ < s_.size() && std::isspace(static_cast<unsigned char>(s_[i_]))) ++i_; }
-    bool eat(char c) { if (i_ < s_.size() && s_[i_] == c) { ++i_; return true; } return false; }
-    bool null() { if (s_.compare(i_, 4, "null") == 0) { i_ += 4; return true; } return false; }
-    bool str(std::string& out) {
-        if (!eat('"')) return false;
-        while (i_ < s_.size() && s_[i_] != '"') {
-            if (s_[i_] == '\\' && i_ + 1 < s_.size()) ++i_;
-            out.push_back(s_[i_++]);
-        }
-        return eat('"');
-    }
-    bool num(uint64_t& v) {
-        size_t st = i_;
-        v = 0;
-        while (i_ < s_.size() && std::isdigit(static_cast<unsigned char>(s_[i_]))) v = v * 10 + uint64_t(s_[i_++] - '0');
-        return i_ > st;
-    }
-    bool skip() {
-        ws();
-        if (i_ >= s_.size()) return false;
-        char c = s_[i_];
-        if (c == '"') { std::string t; return str(t); }
-        if (c == '{' || c == '[') {
-            char close = c == '{' ? '}' : ']';
-            ++i_;
-            ws();
-            if (eat(close)) return true;
-            for (;;) {
-                if (c == '{') { std::string t; ws(); if (!str(t)) return false; ws(); if (!eat(':')) return false; }
-                if (!skip()) return false;
-                ws();
-                if (eat(',')) continue;
-                return eat(close);
-            }
-        }
-        while (i_ < s_.size() && (std::isalnum(static_cast<unsigned char>(s_[i_])) || s_[i_] == '-' || s_[i_] == '.' || s_[i_] == '+')) ++i_;
-        return true;
-    }
-    bool chunks(std::vector<Manifest::Chunk>& out) {
-        if (!eat('[')) return false;
-        ws();
-        if (eat(']')) return true;
-        for (;;) {
-            ws();
-            if (!eat('{')) return false;
-            Manifest::Chunk c;
-            ws();
-            if (!eat('}')) {
-                for (;;) {
-                    std::string key;
-                    ws();
-                    if (!str(key)) return false;
-                    ws();
-                    if (!eat(':')) return false;
-                    ws();
-                    if (key == "index") { uint64_t v; if (!num(v)) return false; c.index = uint32_t(v); }
-                    else if (key == "size") { if (!num(c.size)) return false; }
-                    else if (key == "sha256") { if (!str(c.sha256)) return false; }
-                    else if (key == "kind") { std::string k; if (!str(k)) return false; c.kind = k == "parity" ? 1 : 0; }
-                    else if (!skip()) return false;
-                    ws();
-                    if (eat(',')) continue;
-                    if (eat('}')) break;
-                    return false;
-                }
-            }
-            out.push_back(c);
-            ws();
-            if (eat(',')) continue;
-            return eat(']');
-        }
-    }
-};
+// ---- ChunkManifest JSON (manifest.cpp) ------------------------------------
+using mxec::Manifest;
+using mxec::manifest_json;
 
 int read_manifest(const fs::path& ec_dir, Manifest& m) {
     std::vector<uint8_t> raw;
     MXEC_TRY(read_file(ec_dir / "manifest.json", raw));
+    // fs::read_to_string fails with an I/O error (InvalidData) on bytes that
+    // are not UTF-8; then serde_json::from_str (filesystem.rs:3164-3171).
+    if (!mxec::utf8_valid(raw.data(), raw.size()))
+        return set_error(MXEC_E_IO, "IO error: stream did not contain valid UTF-8");
     std::string s(raw.begin(), raw.end());
-    Json j(s);
-    if (!j.parse(m)) return set_error(MXEC_E_JSON, "JSON error: malformed manifest.json");
+    std::string why;
+    if (!mxec::parse_manifest(s, m, &why)) return set_error(MXEC_E_JSON, "JSON error: " + why);
     if (m.chunks.size() < m.chunk_count) return set_error(MXEC_E_JSON, "JSON error: manifest lists fewer chunks than chunk_count");
     return MXEC_OK;
 }
