@@ -104,7 +104,7 @@ __device__ __forceinline__ void mac_column(uint32_t (&acc)[V][4][R], const Vec4 
 
 // Two input columns at once: the six partial products of each output fold
 // into the accumulator with three XOR3s (1.5 per input instead of an XOR3
-// and an XOR), the VALU saving that matters at R = 4, where the kernel's
+// and an XOR), the VALU saving that matters at R >= 3, where the kernel's
 // VALU issue sits near the HBM stream's pace.
 template <int R, int V>
 __device__ __forceinline__ void mac_column_pair(uint32_t (&acc)[V][4][R], const Vec4 (&xa)[V], const Vec4 (&xb)[V],
@@ -322,8 +322,13 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
                         x[jj][v] = live ? gload16<NT>(p + v * kThreads * 16) : Vec4{{0, 0, 0, 0}};
                 }
             }
-            mac_column_pair<R, V>(acc, x[0], x[1], tab + (j + 0) * r_total * 8, tab + (j + 1) * r_total * 8);
-            mac_column_pair<R, V>(acc, x[2], x[3], tab + (j + 2) * r_total * 8, tab + (j + 3) * r_total * 8);
+            if constexpr (R >= 3) {
+                mac_column_pair<R, V>(acc, x[0], x[1], tab + (j + 0) * r_total * 8, tab + (j + 1) * r_total * 8);
+                mac_column_pair<R, V>(acc, x[2], x[3], tab + (j + 2) * r_total * 8, tab + (j + 3) * r_total * 8);
+            } else {  // VALU has slack at R <= 2; one column at a time needs fewer VGPRs
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * r_total * 8);
+            }
         }
         for (; j < k; ++j) {
             if (il[j] < end) continue;  // zero column: contributes nothing

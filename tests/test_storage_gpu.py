@@ -8,6 +8,7 @@ import hashlib
 import json
 import os
 
+import numpy as np
 import pytest
 
 import maxio_amd
@@ -310,3 +311,45 @@ def test_one_shot_get_matches_streaming_reader(ctx, tmp_path, damage, window, mo
             assert got == (body[off:] if ln is None else body[off:off + ln])
     if damage in ("none", "missing", "corrupt", "short", "missing+corrupt", "missing+parity"):
         assert ctx.get_object_chunked(str(ec)) == body
+
+
+@pytest.mark.parametrize("edit,code", [
+    (lambda j: j.replace('"version": 2,', ""), -42),                      # missing required field
+    (lambda j: j.replace('"kind": "parity"', '"kind": "Parity"', 1), -42),  # unknown variant
+    (lambda j: j.replace('"chunk_count": 3', '"chunk_count": 4294967299'), -42),  # u32 overflow
+    (lambda j: j.replace('"chunk_size": 4096', '"chunk_size": 4096.0'), -42),     # float for u64
+    (lambda j: j + " x", -42),                                            # trailing characters
+    (lambda j: j.replace('"total_size"', '"extra": ' + "[" * 200 + "]" * 200 + ', "total_size"'), -42),
+    (lambda j: j.replace('"version": 2', '"versio\\u006e": 2'), 0),       # escaped key is the same key
+    (lambda j: j.replace('"version": 2,', '"version": 2, "future_field": {"a": [1, 2.5]},'), 0),
+])
+def test_get_manifest_parsed_like_serde(ctx, tmp_path, edit, code):
+    """GET reads manifest.json with the serde-exact reader (manifest.cpp):
+    what serde_json::from_str::<ChunkManifest> rejects is MXEC_E_JSON
+    (StorageError::Json, filesystem.rs:3171), what it accepts reads back."""
+    body = np.random.default_rng(51).integers(0, 256, 3 * 4096 - 5, dtype=np.uint8)
+    ec = tmp_path / "m.ec"
+    ctx.put_object_chunked(str(ec), 4096, 2, body)
+    mpath = ec / "manifest.json"
+    text = mpath.read_text()
+    assert '"chunk_count": 3' in text and '"version": 2' in text
+    mpath.write_text(edit(text))
+    if code == 0:
+        assert ctx.get_object_chunked(str(ec)) == body.tobytes()
+    else:
+        with pytest.raises(maxio_amd.RSError) as ei:
+            ctx.get_object_chunked(str(ec), capacity=body.size)
+        assert ei.value.code == code, str(ei.value)
+        assert "JSON error" in str(ei.value)
+
+
+def test_get_manifest_not_utf8_is_io_error(ctx, tmp_path):
+    body = np.random.default_rng(52).integers(0, 256, 5000, dtype=np.uint8)
+    ec = tmp_path / "u.ec"
+    ctx.put_object_chunked(str(ec), 4096, 1, body)
+    mpath = ec / "manifest.json"
+    raw = mpath.read_bytes().replace(b'"version"', b'"v\xffersion"')
+    mpath.write_bytes(raw)
+    with pytest.raises(maxio_amd.RSError) as ei:
+        ctx.get_object_chunked(str(ec), capacity=body.size)
+    assert ei.value.code == -40
