@@ -466,10 +466,17 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 // message t against expected[idx[t]]), n flags read back.
                 MXEC_TRY(slot.digests.ensure(ptrs.size()));
                 auto* ok = static_cast<uint8_t*>(slot.digests.p);
-                MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx));
-                MXEC_TRY(slot.hdig.ensure(ptrs.size()));
+                const uint32_t* tmo = nullptr;
+                MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx, nullptr, 0, &tmo));
+                const size_t fo = (ptrs.size() + 15) & ~size_t(15);
+                MXEC_TRY(slot.hdig.ensure(fo + 16));
+                auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + fo);
+                *hflag = 0;
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok, ptrs.size(), hipMemcpyDeviceToHost, s));
+                if (tmo) MXEC_HIP(hipMemcpyAsync(hflag, tmo, 4, hipMemcpyDeviceToHost, s));
                 MXEC_TRY(slot_wait(*ds.slot, s));
+                if (*hflag != 0)
+                    return set_error(MXEC_E_DEVICE, "SHA-256 stream kernel: a wave timed out waiting for its predecessor segment");
                 const auto* okh = static_cast<const uint8_t*>(slot.hdig.p);
                 for (size_t t = 0; t < idx.size(); ++t)
                     if (!okh[t]) present[idx[t]] = 0;

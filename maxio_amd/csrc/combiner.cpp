@@ -73,15 +73,23 @@ struct ShaCombiner {
         if (n == 0) return MXEC_OK;
         hipStream_t s = slot.stream;
         MXEC_TRY(slot.digests.ensure(n * 32));
-        // The split (producer / consumer) form at every size: a combined
-        // batch is often several chip-filling requests, and two waves per 64
-        // messages spread over the SIMDs more evenly than one (a batch ends
-        // with its most loaded SIMD).
+        // The split (producer / consumer) form up to one 64-message group per
+        // SIMD: a combined batch is often several chip-filling requests, and
+        // two waves per 64 messages spread over the SIMDs more evenly than
+        // one.  Past that the stream form (segments of every chain dealt to
+        // persistent waves) keeps every SIMD busy to the end; its timeout
+        // word comes back with the digests.
+        const uint32_t* tmo = nullptr;
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr, nullptr,
-                         nullptr, 2));
-        MXEC_TRY(slot.hdig.ensure(n * 32));
+                         nullptr, (n + 63) / 64 > size_t(d.n_cus) * 4 ? 0 : 2, &tmo));
+        MXEC_TRY(slot.hdig.ensure(n * 32 + 16));
+        auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + n * 32);
+        *hflag = 0;
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
+        if (tmo) MXEC_HIP(hipMemcpyAsync(hflag, tmo, 4, hipMemcpyDeviceToHost, s));
         MXEC_TRY(slot_wait(slot, s));
+        if (*hflag != 0)
+            return set_error(MXEC_E_DEVICE, "SHA-256 stream kernel: a wave timed out waiting for its predecessor segment");
         const auto* h = static_cast<const uint8_t*>(slot.hdig.p);
         size_t o = 0;
         for (Req* r : batch) {

@@ -56,8 +56,23 @@ struct ShaArgs {
                                  //   (null: expected[i])
     uint8_t* ok;                 // [n] or null
     uint32_t n;
-    int force = 0;               // 0 auto, 1 one wave per 64 messages, 2 split
+    int force = 0;               // 0 auto, 1 one wave per 64 messages, 2 split,
+                                 // 3 stream (needs the fields below)
+    // Stream form (batches of more 64-message groups than the chip has
+    // SIMDs): persistent waves take (group, segment) items in segment-major
+    // order; a group's running state is handed from segment to segment
+    // through `state`.  Every message 16-byte aligned.
+    uint32_t* work = nullptr;    // [4 + groups] zeroed before the launch:
+                                 //   [0] next item, [1] timeout code, [4 + g] segments of group g done
+    uint32_t* state = nullptr;   // [n][8]
+    uint32_t waves = 0;          // persistent waves (one workgroup each)
+    uint32_t seg_max = 0;        // segments of the longest message
 };
+// Blocks per stream-form segment (32 KiB of each message).
+constexpr uint32_t kShaSegBlocks = 512;
+// Timeout code the stream form leaves in work[1] when a wave gave up
+// waiting for a predecessor segment (the digests are then incomplete).
+constexpr uint32_t kShaStreamTimeout = 0x5AA5u;
 
 hipError_t launch_sha256(const ShaArgs& a, hipStream_t s);
 

@@ -1,4 +1,7 @@
 // ops.cpp — descriptor planning and kernel launches over device pointers.
+#include <cstdlib>
+#include <cstring>
+
 #include "ops.hpp"
 
 #include <algorithm>
@@ -171,14 +174,35 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
 
 int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
             const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
-            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx, DescArena* arena, int form) {
-    (void)dev;
+            uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx, DescArena* arena, int form,
+            const uint32_t** tmo_dev) {
     const size_t n = ptrs.size();
+    if (tmo_dev) *tmo_dev = nullptr;
     if (!n) return MXEC_OK;
+    // The stream form: more 64-message groups than SIMDs, every message
+    // 16-byte aligned, a caller that checks the timeout word, ring tables.
+    // MXEC_SHA_FORM=stream forces it whenever it is allowed (tests).
+    const uint64_t groups = (n + 63) / 64, simds = uint64_t(dev.n_cus) * 4;
+    static const int env_form = [] {
+        const char* e = getenv("MXEC_SHA_FORM");
+        return e && !strcmp(e, "stream") ? 3 : 0;
+    }();
+    bool stream = false;
+    if (tmo_dev && !arena && (form == 0 || form == 3) && n < (uint64_t(1) << 31)) {
+        bool aligned = true;
+        for (const uint8_t* p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+        stream = aligned && (groups > simds || form == 3 || env_form == 3);
+    } else if (tmo_dev && !arena && env_form == 3 && n < (uint64_t(1) << 31)) {
+        bool aligned = true;
+        for (const uint8_t* p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+        stream = aligned;
+    }
     DescWriter w(slot, arena);
     const size_t o_p = w.add(sizeof(void*) * n);
     const size_t o_l = w.add(8 * n);
     const size_t o_e = exp_idx ? w.add(8 * n) : 0;
+    // Zeroed by the upload: [0] item counter, [1] timeout code, [4 + g] progress.
+    const size_t o_w = stream ? w.add(4 * (4 + groups)) : 0;
     char* hb = w.data();
     std::memcpy(hb + o_p, ptrs.data(), sizeof(void*) * n);
     std::memcpy(hb + o_l, lens.data(), 8 * n);
@@ -193,7 +217,20 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     a.exp_idx = exp_idx ? reinterpret_cast<const uint64_t*>(db + o_e) : nullptr;
     a.ok = ok_dev;
     a.n = uint32_t(n);
-    a.force = form;
+    a.force = form == 3 && !stream ? 0 : form;
+    if (stream) {
+        void* st = nullptr;
+        MXEC_TRY(w.scratch(32 * n, &st));
+        uint64_t longest = 0;
+        for (uint64_t l : lens) longest = std::max(longest, l);
+        a.force = 3;
+        a.work = reinterpret_cast<uint32_t*>(db + o_w);
+        a.state = static_cast<uint32_t*>(st);
+        // One wave per SIMD; two once every SIMD would hold two groups.
+        a.waves = uint32_t(groups >= 2 * simds ? 2 * simds : simds);
+        a.seg_max = uint32_t(longest / 64 / kShaSegBlocks + 1);
+        *tmo_dev = a.work + 1;
+    }
     MXEC_HIP(launch_sha256(a, s));
     return w.finish(s);
 }

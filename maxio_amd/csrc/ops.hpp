@@ -30,10 +30,14 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
 
 // SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be
 // null (see ShaArgs).
+// tmo_dev: a caller that reads back a 4-byte device word after the launch
+// (and fails the call if it is not 0) passes this; only then may a batch of
+// more 64-message groups than SIMDs take the stream form (sha256_kernel.hip),
+// whose word it is.  Set to null when another form ran.
 int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
             const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
             uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx = nullptr,
-            DescArena* arena = nullptr, int form = 0);
+            DescArena* arena = nullptr, int form = 0, const uint32_t** tmo_dev = nullptr);
 
 // SHA-256 digests (host out, n * 32 bytes) of n device-resident messages on
 // `dev`, blocking; the caller's work on `s` must have produced them (the

@@ -231,6 +231,13 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
     return MXEC_OK;
 }
 
+int DescWriter::scratch(size_t bytes, void** dev) {
+    if (arena_ || !buf_) return set_error(MXEC_E_INVALID_ARG, "descriptor scratch needs a committed ring entry");
+    MXEC_TRY(buf_->scratch.ensure(bytes));
+    *dev = buf_->scratch.p;
+    return MXEC_OK;
+}
+
 int DescWriter::finish(hipStream_t stream) {
     if (arena_ || !buf_) return MXEC_OK;
     MXEC_HIP(hipEventRecord(buf_->done, stream));

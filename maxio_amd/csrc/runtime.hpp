@@ -56,6 +56,7 @@ struct PinnedBuf {
 struct DescBuf {
     PinnedBuf host;
     DevBuf dev;
+    DevBuf scratch;  // per-launch device scratch (DescWriter::scratch), same lifetime
     hipEvent_t done = nullptr;
     bool pending = false;
 };
@@ -195,6 +196,10 @@ public:
     char* data() { return tmp_.data(); }
     // Upload; dev_base receives the device base to add offsets to.
     int commit(hipStream_t stream, char** dev_base);
+    // Device scratch of `bytes` that lives as long as this launch's tables
+    // (the ring entry is not reused before finish()'s event): after commit,
+    // slot ring only (not with an arena).
+    int scratch(size_t bytes, void** dev);
     // Record completion after the launches that read the tables.
     int finish(hipStream_t stream);
 

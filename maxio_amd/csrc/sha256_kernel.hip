@@ -308,6 +308,156 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
     if (ok) ok[i] = match ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Stream form for batches with more 64-message groups than the chip has SIMDs
+// (e.g. config 3c: eight concurrent 10 240-chunk verifications = 1 280 groups
+// on 1 024 SIMDs).  Whole-chain scheduling ends with the SIMDs that hold two
+// groups running at half speed while the rest idle (81 920 x 1 MiB: 87.6 ms
+// split form vs 53.3 for 65 536).  Here a group's chain is cut into segments
+// of kShaSegBlocks blocks; persistent one-wave workgroups (one per SIMD, or
+// two) take (group, segment) items from a counter in segment-major order, so
+// a SIMD that finishes early takes the next segment of some other group and
+// the load evens out to within one segment.
+//
+// Hand-off between the waves that run consecutive segments of a group
+// (MI355X_MICROARCH.md, visibility; cdna_hip_programming.md Guideline 16,
+// recipe R1): each lane stores its 8 state words with agent-scope relaxed
+// atomic stores (write-through), the wave drains them (vmcnt(0)), then lane
+// 0 stores the group's progress word (agent-scope relaxed); the next wave's
+// lane 0 polls that word relaxed with s_sleep, bounded, then one agent
+// acquire, then the lanes read the state with agent-scope loads.  Item t's
+// predecessor is item t - groups, taken earlier by a resident wave, so every
+// wait ends; a wave that still waits ~4 s gives up, leaves
+// kShaStreamTimeout in work[1] and every other wave drains the queue without
+// hashing (the host checks the word).
+// ---------------------------------------------------------------------------
+typedef uint32_t __attribute__((address_space(1))) gu32;
+
+__device__ __forceinline__ bool stream_wait(gu32* prog, uint32_t want, gu32* tmo) {
+    for (uint32_t spins = 0;; ++spins) {
+        if (__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) return true;
+        if ((spins & 63) == 0 && __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+            return false;
+        if (spins > (1u << 24)) {  // ~4 s of s_sleep 2
+            __hip_atomic_store(tmo, kShaStreamTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+__global__ __launch_bounds__(64) void sha256_stream_kernel(const uint8_t* const* __restrict__ ptrs,
+                                                           const uint64_t* __restrict__ lens,
+                                                           uint8_t* __restrict__ digests,
+                                                           const uint8_t* __restrict__ expected,
+                                                           const uint64_t* __restrict__ exp_idx,
+                                                           uint8_t* __restrict__ ok, uint32_t n,
+                                                           uint32_t* work_p, uint32_t* state_p,
+                                                           uint32_t seg_max) {
+    gu32* work = (gu32*)(work_p);
+    gu32* state = (gu32*)(state_p);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t groups = (n + 63) / 64;
+    const uint32_t n_items = groups * seg_max;
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t >= n_items) break;
+        const uint32_t sg = t / groups, g = t - sg * groups;
+        const uint32_t i = g * 64 + lane;
+        const bool live = i < n;
+        const uint8_t* p = live ? ptrs[i] : nullptr;
+        const uint64_t len = live ? lens[i] : 0;
+        const uint64_t nfull = len / 64;
+        const uint32_t last = uint32_t(nfull / kShaSegBlocks);  // the segment holding this lane's tail
+        uint32_t segs = last;
+#pragma unroll
+        for (int x = 32; x >= 1; x >>= 1) segs = max(segs, uint32_t(__shfl_xor(int(segs), x)));
+        segs = __builtin_amdgcn_readfirstlane(segs) + 1;
+        if (sg >= segs) continue;  // this group has no such segment
+        gu32* prog = work + 4 + g;
+        if (sg > 0) {
+            uint32_t okw = 1;
+            if (lane == 0) okw = stream_wait(prog, sg, work + 1) ? 1u : 0u;
+            if (!__builtin_amdgcn_readfirstlane(okw)) continue;  // timed out: drain
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        } else if (__hip_atomic_load(work + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            continue;  // another wave timed out: drain without hashing
+        }
+        uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                          0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+        gu32* my = state + uint64_t(live ? i : 0) * 8;
+        if (sg > 0 && live && sg <= last) {
+#pragma unroll
+            for (int w = 0; w < 8; ++w) st[w] = __hip_atomic_load(my + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // Blocks [b0, b1) of this segment; the trip count is the wave's
+        // longest, loads are unconditional (clamped to a block the lane
+        // owns, or a donor lane's) so the prefetch is never drained by a
+        // branch, and a lane compresses only its own blocks.
+        const uint64_t b0 = uint64_t(sg) * kShaSegBlocks;
+        const uint64_t b1 = sg <= last ? min(b0 + kShaSegBlocks, nfull) : b0;
+        uint32_t cnt = uint32_t(b1 > b0 ? b1 - b0 : 0), cmax = cnt;
+#pragma unroll
+        for (int x = 32; x >= 1; x >>= 1) cmax = max(cmax, uint32_t(__shfl_xor(int(cmax), x)));
+        cmax = __builtin_amdgcn_readfirstlane(cmax);
+        if (cmax > 0) {
+            const uint64_t dmask = __ballot(cnt == cmax);
+            const int donor = __ffsll((unsigned long long)dmask) - 1;
+            const uint8_t* dp = reinterpret_cast<const uint8_t*>(__shfl(reinterpret_cast<uintptr_t>(p), donor));
+            const uint64_t db0 = uint64_t(__shfl(int64_t(b0), donor));
+            const bool own = cnt > 0;
+            const uint8_t* base = own ? p + 64 * b0 : dp + 64 * db0;
+            const uint32_t lastb = (own ? cnt : cmax) - 1;
+            u32x4 cur[4], nxt[4];
+            load_block(base, cur);
+            uint32_t w[16];
+            for (uint32_t b = 0; b < cmax; ++b) {
+                load_block(base + 64 * uint64_t(min(b + 1, lastb)), nxt);
+                if (b < cnt) {
+                    block_words(cur, w);
+                    compress(st, w);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+            }
+        }
+        if (live && sg == last) {
+            // Padding blocks, digest, expected-digest check (as the other forms).
+            const uint32_t rem = uint32_t(len - nfull * 64);
+            const uint8_t* tp = p + nfull * 64;
+            const int nblk = (rem + 9 <= 64) ? 1 : 2;
+            const uint64_t bits = len * 8;
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) w[q] = tail_word(tp, rem, q, nblk, bits);
+            compress(st, w);
+            if (nblk == 2) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) w[q] = tail_word(tp, rem, 16 + q, nblk, bits);
+                compress(st, w);
+            }
+            bool match = true;
+            const uint64_t ei = exp_idx ? exp_idx[i] : i;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t be = bswap(st[q]);
+                if (digests) reinterpret_cast<uint32_t*>(digests + 32 * uint64_t(i))[q] = be;
+                if (expected) match &= reinterpret_cast<const uint32_t*>(expected + 32 * ei)[q] == be;
+            }
+            if (ok) ok[i] = match ? 1 : 0;
+        } else if (live && sg < last) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) __hip_atomic_store(my + q, st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (sg + 1 < segs) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's state stores have landed
+            if (lane == 0) __hip_atomic_store(prog, sg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 }  // namespace
 
 // Messages at or below this count run the split (two waves per 64 messages)
@@ -326,6 +476,12 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         if (env && !strcmp(env, "one")) form = 1;
         else if (env && !strcmp(env, "split")) form = 2;
         else form = a.n <= kSplitMaxMessages ? 2 : 1;
+    }
+    if (form == 3) {
+        if (!a.work || !a.state || a.waves == 0 || a.seg_max == 0) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(sha256_stream_kernel, dim3(a.waves), dim3(64), 0, s, a.ptrs, a.lens, a.digests,
+                           a.expected, a.exp_idx, a.ok, a.n, a.work, a.state, a.seg_max);
+        return hipGetLastError();
     }
     const bool split = form == 2;
     if (split)
