@@ -145,6 +145,44 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size,
                      const uint8_t (*expected_sha256)[32],
                      uint8_t* present_inout, uint32_t flags, int* n_present);
 
+/* ---- completion handles (non-blocking host calls) -------------------------
+ * The *_async forms queue the blocking call of the same name on the
+ * context's worker threads and return at once (MXEC_OK and *ticket set), or
+ * return an argument error without a ticket.  Pointer arrays, digests to
+ * compare and directory strings are copied at submission; data buffers and
+ * out-parameters (parity, shards, present_inout, n_present, out, out_len)
+ * must stay valid until the ticket completes.  A tokio caller registers
+ * mxec_ticket_fd (an eventfd, readable once the call is done) with AsyncFd
+ * and awaits it instead of parking a blocking-pool thread for the ~30 ms a
+ * 1 MiB chunk's SHA-256 chain takes (chunk_reader.rs:244-249, main.rs:81). */
+typedef struct mxec_ticket mxec_ticket;
+/* eventfd that becomes readable when the call completes. */
+int mxec_ticket_fd(const mxec_ticket* t);
+/* 1 when complete, 0 while running (never blocks). */
+int mxec_ticket_poll(mxec_ticket* t);
+/* Blocks until complete; returns the call's status and sets the calling
+ * thread's mxec_last_error to its message. */
+int mxec_ticket_wait(mxec_ticket* t);
+/* The failed call's message ("" on success or while running). */
+const char* mxec_ticket_error(const mxec_ticket* t);
+/* Waits for completion if needed, then frees the ticket and its fd. */
+void mxec_ticket_free(mxec_ticket* t);
+int mxec_sha256_batch_async(mxec_ctx* ctx, const uint8_t* const* bufs, const size_t* lens,
+                            size_t n, uint8_t (*out)[32], mxec_ticket** ticket);
+int mxec_encode_async(mxec_ctx* ctx, int k, int m, size_t shard_size,
+                      const uint8_t* const* data, const size_t* data_len,
+                      uint8_t* const* parity, uint8_t (*sha256_out)[32], mxec_ticket** ticket);
+int mxec_reconstruct_async(mxec_ctx* ctx, int k, int m, size_t shard_size,
+                           uint8_t* const* shards, const size_t* shard_len,
+                           const uint8_t (*expected_sha256)[32], uint8_t* present_inout,
+                           uint32_t flags, int* n_present, mxec_ticket** ticket);
+int mxec_put_object_chunked_async(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size,
+                                  uint32_t parity_shards, const uint8_t* body, size_t len,
+                                  mxec_ticket** ticket);
+int mxec_get_object_chunked_async(mxec_ctx* ctx, const char* ec_dir, uint64_t offset,
+                                  uint64_t length, uint8_t* out, uint64_t out_cap,
+                                  uint64_t* out_len, mxec_ticket** ticket);
+
 /* ---- device-resident batches ---------------------------------------------
  * All data pointers below are HIP device pointers on ctx device `dev`
  * (index into the ctx's devices).  `stream` is a hipStream_t of that device;

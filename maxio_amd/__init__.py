@@ -17,6 +17,7 @@ from .ec import (  # noqa: F401
     Context,
     ReedSolomon,
     RSError,
+    Ticket,
     device_count,
     parity_matrix,
     rs_check,

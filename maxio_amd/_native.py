@@ -141,6 +141,19 @@ _SIGS = {
     "mxec_reader_open": (INT, [P, ctypes.c_char_p, U64, U64, U64, ctypes.POINTER(ctypes.c_void_p)]),
     "mxec_reader_read": (ctypes.c_int64, [P, P, U64]),
     "mxec_reader_close": (None, [P]),
+    "mxec_ticket_fd": (INT, [P]),
+    "mxec_ticket_poll": (INT, [P]),
+    "mxec_ticket_wait": (INT, [P]),
+    "mxec_ticket_error": (ctypes.c_char_p, [P]),
+    "mxec_ticket_free": (None, [P]),
+    "mxec_sha256_batch_async": (INT, [P, PP, SZP, SZ, U8P, ctypes.POINTER(ctypes.c_void_p)]),
+    "mxec_encode_async": (INT, [P, INT, INT, SZ, PP, SZP, PP, U8P, ctypes.POINTER(ctypes.c_void_p)]),
+    "mxec_reconstruct_async": (INT, [P, INT, INT, SZ, PP, SZP, U8P, U8P, ctypes.c_uint32, ctypes.POINTER(INT),
+                                     ctypes.POINTER(ctypes.c_void_p)]),
+    "mxec_put_object_chunked_async": (INT, [P, ctypes.c_char_p, U64, ctypes.c_uint32, P, SZ,
+                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "mxec_get_object_chunked_async": (INT, [P, ctypes.c_char_p, U64, U64, P, U64, U64P,
+                                            ctypes.POINTER(ctypes.c_void_p)]),
 }
 
 

@@ -115,6 +115,7 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
 
 void mxec_close(mxec_ctx* ctx) {
     if (!ctx) return;
+    async_shutdown(ctx->c);  // every queued *_async call finishes first
     for (auto& d : ctx->c.devs) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();

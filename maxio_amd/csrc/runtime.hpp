@@ -169,7 +169,12 @@ struct Device {
 struct Ctx {
     std::vector<std::unique_ptr<Device>> devs;
     std::atomic<unsigned> rr{0};
+    // Worker threads of the *_async entry points (async.cpp), created on
+    // first use; async_shutdown drains and joins them (mxec_close).
+    std::mutex pool_mu;
+    std::shared_ptr<void> pool;
 };
+void async_shutdown(Ctx& c);
 
 // Descriptor tables of many launches in flight at once (host pipeline): one
 // pinned + device region, bump-allocated, never reused until reset().

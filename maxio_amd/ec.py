@@ -241,6 +241,71 @@ class Context:
         out = [bufs[i][: int(shard_len[i])] if present[i] else None for i in range(total)]
         return out, present
 
+    # ---- completion-handle forms (mxec_*_async) -----------------------------
+    def _submit(self, fn, args, keep, result) -> "Ticket":
+        t = ctypes.c_void_p(0)
+        _check(fn(*args, ctypes.byref(t)))
+        return Ticket(self._lib, t, keep, result)
+
+    def sha256_async(self, bufs: Sequence) -> "Ticket":
+        arrs = [_u8(b) for b in bufs]
+        out = np.zeros((max(1, len(arrs)), 32), np.uint8)
+        ptrs, lens = _pp([_ptr(a) for a in arrs]), _szp([a.size for a in arrs])
+        return self._submit(self._lib.mxec_sha256_batch_async,
+                            (self._h, ptrs, lens, len(arrs), out.ctypes.data_as(N.U8P)), (arrs, out, ptrs, lens),
+                            lambda: [bytes(out[i]) for i in range(len(arrs))])
+
+    def encode_async(self, data: Sequence, m: int, shard_size: int) -> "Ticket":
+        arrs = [_u8(d) for d in data]
+        k = len(arrs)
+        parity = [np.zeros(shard_size, np.uint8) for _ in range(max(m, 0))]
+        dig = np.zeros((max(1, k + m), 32), np.uint8)
+        args = (self._h, k, m, shard_size, _pp([_ptr(a) for a in arrs]), _szp([a.size for a in arrs]),
+                _pp([p.ctypes.data for p in parity]), dig.ctypes.data_as(N.U8P))
+        return self._submit(self._lib.mxec_encode_async, args, (arrs, parity, dig),
+                            lambda: (parity, [bytes(dig[i]) for i in range(k + m)]))
+
+    def reconstruct_async(self, shards: Sequence[Optional[object]], k: int, m: int, shard_size: int,
+                          shard_len: Optional[Sequence[int]] = None,
+                          expected: Optional[Sequence[bytes]] = None) -> "Ticket":
+        total = k + m
+        if shard_len is None:
+            shard_len = [shard_size] * total
+        bufs, present = [], np.zeros(total, np.uint8)
+        for i in range(total):
+            s = shards[i] if i < len(shards) else None
+            if s is None:
+                bufs.append(np.zeros(max(int(shard_len[i]), 1), np.uint8))
+            else:
+                a = np.array(_u8(s), dtype=np.uint8, copy=True)
+                bufs.append(a if a.size else np.zeros(1, np.uint8))
+                present[i] = 1
+        exp = None
+        if expected is not None:
+            exp = np.frombuffer(b"".join(bytes(e) for e in expected), np.uint8).copy()
+        npres = ctypes.c_int(0)
+        args = (self._h, k, m, shard_size, _pp([b.ctypes.data for b in bufs]), _szp(list(shard_len)),
+                exp.ctypes.data_as(N.U8P) if exp is not None else None, present.ctypes.data_as(N.U8P), 0,
+                ctypes.byref(npres))
+        return self._submit(self._lib.mxec_reconstruct_async, args, (bufs, present, exp, npres),
+                            lambda: ([bufs[i][: int(shard_len[i])] if present[i] else None for i in range(total)],
+                                     present))
+
+    def put_object_chunked_async(self, ec_dir: str, chunk_size: int, parity_shards: int, body) -> "Ticket":
+        b = _u8(body)
+        return self._submit(self._lib.mxec_put_object_chunked_async,
+                            (self._h, ec_dir.encode(), chunk_size, parity_shards, _ptr(b) if b.size else None,
+                             b.size), (b,), None)
+
+    def get_object_chunked_async(self, ec_dir: str, capacity: int, offset: int = 0,
+                                 length: Optional[int] = None) -> "Ticket":
+        out = np.zeros(max(1, capacity), np.uint8)
+        n = ctypes.c_uint64(0)
+        args = (self._h, ec_dir.encode(), offset, (1 << 64) - 1 if length is None else length, out.ctypes.data,
+                capacity, ctypes.byref(n))
+        return self._submit(self._lib.mxec_get_object_chunked_async, args, (out, n),
+                            lambda: out[: n.value].tobytes())
+
     # ---- device-resident batches (integer device pointers) ------------------
     def encode_strided_device(self, k, m, shard_size, n_obj, data_ptr, data_obj_stride,
                               data_shard_stride, parity_ptr, parity_obj_stride, parity_shard_stride,
@@ -506,6 +571,43 @@ class Context:
         _check(self._lib.mxec_try_reconstruct_data_chunk(self._h, ec_dir.encode(), target,
                                                          out.ctypes.data, capacity, ctypes.byref(n)))
         return out[: n.value].tobytes()
+
+
+class Ticket:
+    """An mxec_ticket (completion handle of an *_async call).  `fd` is an
+    eventfd that becomes readable when the call is done (select / asyncio
+    add_reader); `wait()` returns the result or raises RSError.  Keeps the
+    call's buffers alive until it completes."""
+
+    def __init__(self, lib, handle, keep, result):
+        self._lib, self._h, self._keep, self._result = lib, handle, keep, result
+
+    @property
+    def fd(self) -> int:
+        return self._lib.mxec_ticket_fd(self._h)
+
+    def done(self) -> bool:
+        return self._lib.mxec_ticket_poll(self._h) == 1
+
+    def wait(self):
+        rc = self._lib.mxec_ticket_wait(self._h)
+        msg = self._lib.mxec_ticket_error(self._h).decode()
+        self.close()
+        if rc != 0:
+            raise RSError(rc, msg)
+        return self._result() if self._result else None
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.mxec_ticket_free(self._h)
+            self._h = None
+            self._keep = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class ChunkReader:

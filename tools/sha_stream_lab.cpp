@@ -1,0 +1,185 @@
+// sha_stream_lab — the SHA-256 stream form (persistent waves over segments)
+// against the split form on the same messages: digests compared, the work
+// words (item counter, timeout code, per-group progress) dumped, and the
+// big-batch timings (81 920 x 1 MiB etc.) beside the split / one-wave forms.
+//
+//   tools/sha_stream_lab check     small ragged batches, forced stream form
+//   tools/sha_stream_lab big       timing: n x 1 MiB for n in 65536, 81920, 98304, 131072
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../maxio_amd/csrc/kernels.hpp"
+
+#define CK(x)                                                                                       \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) {                                                                     \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(1);                                                                           \
+        }                                                                                           \
+    } while (0)
+
+namespace {
+
+struct Batch {
+    uint8_t* data = nullptr;  // device, messages back to back (16-byte aligned starts)
+    std::vector<const uint8_t*> ptrs;
+    std::vector<uint64_t> lens;
+    void* tables = nullptr;  // ptrs, lens
+    uint8_t* dig = nullptr;
+    uint32_t* work = nullptr;
+    uint32_t* state = nullptr;
+    int cus = 256;
+
+    void make(const std::vector<uint64_t>& L, uint64_t seed, bool random = true) {
+        uint64_t total = 0;
+        for (uint64_t l : L) total += (l + 255) / 256 * 256 + 256;
+        CK(hipMalloc(&data, total));
+        if (random) {
+            std::vector<uint8_t> h(total);
+            uint64_t x = seed;
+            for (auto& b : h) {
+                x ^= x << 13;
+                x ^= x >> 7;
+                x ^= x << 17;
+                b = uint8_t(x);
+            }
+            CK(hipMemcpy(data, h.data(), total, hipMemcpyHostToDevice));
+        } else {
+            CK(hipMemset(data, 0x5A, total));  // timing only: SHA-256's work does not depend on the bytes
+        }
+        uint64_t o = 0;
+        for (uint64_t l : L) {
+            ptrs.push_back(data + o);
+            lens.push_back(l);
+            o += (l + 255) / 256 * 256 + 256;
+        }
+        const size_t n = L.size();
+        CK(hipMalloc(&tables, n * 16));
+        CK(hipMemcpy(tables, ptrs.data(), n * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(static_cast<char*>(tables) + n * 8, lens.data(), n * 8, hipMemcpyHostToDevice));
+        CK(hipMalloc(&dig, n * 32));
+        CK(hipMalloc(&work, 4 * (4 + (n + 63) / 64)));
+        CK(hipMalloc(&state, 32 * n));
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    }
+    mxec::ShaArgs args(int form) {
+        const size_t n = lens.size();
+        mxec::ShaArgs a{};
+        a.ptrs = static_cast<const uint8_t* const*>(tables);
+        a.lens = reinterpret_cast<const uint64_t*>(static_cast<char*>(tables) + n * 8);
+        a.digests = dig;
+        a.n = uint32_t(n);
+        a.force = form;
+        if (form == 3) {
+            const uint64_t groups = (n + 63) / 64, simds = uint64_t(cus) * 4;
+            uint64_t longest = 0;
+            for (uint64_t l : lens) longest = l > longest ? l : longest;
+            a.work = work;
+            a.state = state;
+            a.waves = uint32_t(groups >= 2 * simds ? 2 * simds : simds);
+            if (const char* e = getenv("LAB_WAVES")) a.waves = uint32_t(atoi(e));
+            a.seg_max = uint32_t(longest / 64 / mxec::kShaSegBlocks + 1);
+        }
+        return a;
+    }
+    double run(int form) {
+        const size_t n = lens.size();
+        CK(hipMemset(work, 0, 4 * (4 + (n + 63) / 64)));
+        CK(hipMemset(dig, 0, n * 32));
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        CK(hipEventRecord(a, 0));
+        CK(mxec::launch_sha256(args(form), 0));
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms;
+    }
+    std::vector<uint8_t> digests() {
+        std::vector<uint8_t> h(lens.size() * 32);
+        CK(hipMemcpy(h.data(), dig, h.size(), hipMemcpyDeviceToHost));
+        return h;
+    }
+    std::vector<uint32_t> work_words() {
+        std::vector<uint32_t> h(4 + (lens.size() + 63) / 64);
+        CK(hipMemcpy(h.data(), work, h.size() * 4, hipMemcpyDeviceToHost));
+        return h;
+    }
+    void free_all() {
+        (void)hipFree(data);
+        (void)hipFree(tables);
+        (void)hipFree(dig);
+        (void)hipFree(work);
+        (void)hipFree(state);
+    }
+};
+
+int check(const char* name, const std::vector<uint64_t>& L) {
+    Batch b;
+    b.make(L, 0x6D6178696Full + L.size());
+    b.run(2);
+    const auto ref = b.digests();
+    const double ms = b.run(3);
+    const auto got = b.digests();
+    const auto w = b.work_words();
+    size_t bad = 0, first = SIZE_MAX;
+    for (size_t i = 0; i < L.size(); ++i)
+        if (std::memcmp(&ref[i * 32], &got[i * 32], 32)) {
+            ++bad;
+            if (first == SIZE_MAX) first = i;
+        }
+    std::string prog;
+    for (size_t g = 0; g < w.size() - 4 && g < 16; ++g) prog += (g ? "," : "") + std::to_string(w[4 + g]);
+    std::printf("{\"case\": \"%s\", \"n\": %zu, \"ms\": %.3f, \"items_taken\": %u, \"timeout\": %u, \"prog\": [%s], "
+                "\"mismatch\": %zu, \"first_bad\": %lld}\n",
+                name, L.size(), ms, w[0], w[1], prog.c_str(), bad, first == SIZE_MAX ? -1ll : (long long)first);
+    b.free_all();
+    return bad || w[1] ? 1 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "check";
+    int fails = 0;
+    if (mode == "check") {
+        const uint64_t SEG = 512 * 64;
+        fails += check("one 1 MiB message", {1 << 20});
+        fails += check("one message of 2 segments", {2 * SEG});
+        fails += check("64 messages of 3 segments", std::vector<uint64_t>(64, 3 * SEG));
+        std::vector<uint64_t> ragged = {0, 1, 55, 56, 63, 64, 119, 120, SEG - 64, SEG - 1, SEG, SEG + 1, SEG + 64,
+                                        2 * SEG, 3 * SEG - 9, 1 << 20, (1 << 20) + 5, 5 * SEG + 100};
+        uint64_t x = 7;
+        for (int i = 0; i < 150; ++i) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            ragged.push_back((x >> 33) % (4 * SEG));
+        }
+        fails += check("ragged 168", ragged);
+        fails += check("1100 groups x 2 segments", std::vector<uint64_t>(1100 * 64, 2 * SEG));
+    } else {
+        for (uint64_t n : {65536ull, 81920ull, 98304ull, 131072ull}) {
+            Batch b;
+            b.make(std::vector<uint64_t>(n, 1 << 20), n, false);
+            for (int form : {2, 1, 3}) {
+                b.run(form);  // warm
+                const double ms = b.run(form);
+                const auto w = b.work_words();
+                std::printf("{\"n\": %llu, \"form\": \"%s\", \"ms\": %.3f, \"GBps_hashed\": %.1f, \"timeout\": %u}\n",
+                            (unsigned long long)n, form == 1 ? "one" : form == 2 ? "split" : "stream", ms,
+                            double(n) * (1 << 20) / (ms * 1e-3) / 1e9, form == 3 ? w[1] : 0u);
+                std::fflush(stdout);
+            }
+            b.free_all();
+        }
+    }
+    return fails ? 1 : 0;
+}
