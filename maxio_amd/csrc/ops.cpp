@@ -191,7 +191,7 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     if (tmo_dev && !arena && (form == 0 || form == 3) && n < (uint64_t(1) << 31)) {
         bool aligned = true;
         for (const uint8_t* p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-        stream = aligned && (groups > simds || form == 3 || env_form == 3);
+        stream = aligned && (groups >= simds || form == 3 || env_form == 3);
     } else if (tmo_dev && !arena && env_form == 3 && n < (uint64_t(1) << 31)) {
         bool aligned = true;
         for (const uint8_t* p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
@@ -226,8 +226,11 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
         a.force = 3;
         a.work = reinterpret_cast<uint32_t*>(db + o_w);
         a.state = static_cast<uint32_t*>(st);
-        // One wave per SIMD; two once every SIMD would hold two groups.
-        a.waves = uint32_t(groups >= 2 * simds ? 2 * simds : simds);
+        // One persistent wave per SIMD: 1.54 TB/s hashed from 65 536 to
+        // 98 304 x 1 MiB, the chip's INT32 issue ceiling for this mix; two
+        // per SIMD measured slower (131 072 x 1 MiB: 132.5 vs 92.8 ms for the
+        // one-wave form; profiles/r2_sha_stream_lab.txt).
+        a.waves = uint32_t(simds);
         a.seg_max = uint32_t(longest / 64 / kShaSegBlocks + 1);
         *tmo_dev = a.work + 1;
     }

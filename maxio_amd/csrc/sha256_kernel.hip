@@ -333,12 +333,36 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
 // ---------------------------------------------------------------------------
 typedef uint32_t __attribute__((address_space(1))) gu32;
 
+#ifndef SHA_STREAM_SPIN_LIMIT
+#define SHA_STREAM_SPIN_LIMIT (1u << 24)
+#endif
+// Lab builds (tools/sha_stream_lab) define SHA_STREAM_DEBUG: per item, eight
+// words after the n x 8 state words record (taken, waited ok, progress word
+// seen, published, and s_memtime / 16 at start, publish, wait end, loop end).
+#ifdef SHA_STREAM_DEBUG
+#define SHA_DBG(t, k, v) (state_p[uint64_t(n) * 8 + uint64_t(t) * 8 + (k)] = (v))
+#else
+#define SHA_DBG(t, k, v) ((void)0)
+#endif
+
+__device__ __forceinline__ uint32_t prog_read(gu32* prog) {
+    return __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave-uniform wait: every lane polls the same word (one request per
+// instruction) and the exit test is on scalars, so no divergent loop sits
+// inside a lane-0 branch.  (A lane-0-only spin loop let the compiler's
+// control-flow structurizer fold the previous item's lane-0 publish into the
+// next item's wait region: a wave with two or more live lanes then held its
+// publish until its own next wait timed out — measured in
+// tools/sha_stream_lab, profiles/r2_sha_stream_lab.txt.)
 __device__ __forceinline__ bool stream_wait(gu32* prog, uint32_t want, gu32* tmo) {
     for (uint32_t spins = 0;; ++spins) {
-        if (__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) return true;
-        if ((spins & 63) == 0 && __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        if (uint32_t(__builtin_amdgcn_readfirstlane(prog_read(prog))) == want) return true;
+        if ((spins & 63) == 0 &&
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
             return false;
-        if (spins > (1u << 24)) {  // ~4 s of s_sleep 2
+        if (spins > SHA_STREAM_SPIN_LIMIT) {
             __hip_atomic_store(tmo, kShaStreamTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
         }
@@ -377,10 +401,14 @@ __global__ __launch_bounds__(64) void sha256_stream_kernel(const uint8_t* const*
         segs = __builtin_amdgcn_readfirstlane(segs) + 1;
         if (sg >= segs) continue;  // this group has no such segment
         gu32* prog = work + 4 + g;
+        if (lane == 0) SHA_DBG(t, 0, 1u + sg);
+        if (lane == 0) SHA_DBG(t, 4, uint32_t(__builtin_amdgcn_s_memtime() >> 4));
         if (sg > 0) {
-            uint32_t okw = 1;
-            if (lane == 0) okw = stream_wait(prog, sg, work + 1) ? 1u : 0u;
-            if (!__builtin_amdgcn_readfirstlane(okw)) continue;  // timed out: drain
+            const bool okw = stream_wait(prog, sg, work + 1);
+            if (lane == 0) SHA_DBG(t, 1, okw ? 1u : 0u);
+            if (lane == 0) SHA_DBG(t, 6, uint32_t(__builtin_amdgcn_s_memtime() >> 4));
+            if (lane == 0) SHA_DBG(t, 2, prog_read(prog));
+            if (!okw) continue;  // timed out: drain
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         } else if (__hip_atomic_load(work + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
             continue;  // another wave timed out: drain without hashing
@@ -423,6 +451,7 @@ __global__ __launch_bounds__(64) void sha256_stream_kernel(const uint8_t* const*
                 for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
             }
         }
+        if (lane == 0) SHA_DBG(t, 7, uint32_t(__builtin_amdgcn_s_memtime() >> 4));
         if (live && sg == last) {
             // Padding blocks, digest, expected-digest check (as the other forms).
             const uint32_t rem = uint32_t(len - nfull * 64);
@@ -453,7 +482,10 @@ __global__ __launch_bounds__(64) void sha256_stream_kernel(const uint8_t* const*
         }
         if (sg + 1 < segs) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's state stores have landed
-            if (lane == 0) __hip_atomic_store(prog, sg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) SHA_DBG(t, 5, uint32_t(__builtin_amdgcn_s_memtime() >> 4));
+            // Every lane, the same word and value: no divergent region.
+            __hip_atomic_store(prog, sg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) SHA_DBG(t, 3, sg + 1);
         }
     }
 }

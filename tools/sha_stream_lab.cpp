@@ -66,7 +66,7 @@ struct Batch {
         CK(hipMemcpy(static_cast<char*>(tables) + n * 8, lens.data(), n * 8, hipMemcpyHostToDevice));
         CK(hipMalloc(&dig, n * 32));
         CK(hipMalloc(&work, 4 * (4 + (n + 63) / 64)));
-        CK(hipMalloc(&state, 32 * n));
+        CK(hipMalloc(&state, 32 * n + 32 * 4096));  // + SHA_STREAM_DEBUG records  // + SHA_STREAM_DEBUG records
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     }
     mxec::ShaArgs args(int form) {
@@ -83,7 +83,8 @@ struct Batch {
             for (uint64_t l : lens) longest = l > longest ? l : longest;
             a.work = work;
             a.state = state;
-            a.waves = uint32_t(groups >= 2 * simds ? 2 * simds : simds);
+            a.waves = uint32_t(simds);
+            (void)groups;
             if (const char* e = getenv("LAB_WAVES")) a.waves = uint32_t(atoi(e));
             a.seg_max = uint32_t(longest / 64 / mxec::kShaSegBlocks + 1);
         }
@@ -93,6 +94,7 @@ struct Batch {
         const size_t n = lens.size();
         CK(hipMemset(work, 0, 4 * (4 + (n + 63) / 64)));
         CK(hipMemset(dig, 0, n * 32));
+        CK(hipMemset(state, 0, 32 * n + 32 * 4096));
         hipEvent_t a, b;
         CK(hipEventCreate(&a));
         CK(hipEventCreate(&b));
@@ -126,9 +128,11 @@ struct Batch {
 int check(const char* name, const std::vector<uint64_t>& L) {
     Batch b;
     b.make(L, 0x6D6178696Full + L.size());
-    b.run(2);
+    const double ms_split = b.run(2);
     const auto ref = b.digests();
+    const double ms_one = b.run(1);
     const double ms = b.run(3);
+    std::printf("{\"case\": \"%s\", \"ms_split\": %.3f, \"ms_one\": %.3f}\n", name, ms_split, ms_one);
     const auto got = b.digests();
     const auto w = b.work_words();
     size_t bad = 0, first = SIZE_MAX;
@@ -142,6 +146,20 @@ int check(const char* name, const std::vector<uint64_t>& L) {
     std::printf("{\"case\": \"%s\", \"n\": %zu, \"ms\": %.3f, \"items_taken\": %u, \"timeout\": %u, \"prog\": [%s], "
                 "\"mismatch\": %zu, \"first_bad\": %lld}\n",
                 name, L.size(), ms, w[0], w[1], prog.c_str(), bad, first == SIZE_MAX ? -1ll : (long long)first);
+    {
+        std::vector<uint32_t> dbg(8 * 64);
+        CK(hipMemcpy(dbg.data(), b.state + L.size() * 8, dbg.size() * 4, hipMemcpyDeviceToHost));
+        std::string d;
+        const uint32_t t0 = dbg[4];
+        for (int t = 0; t < 12; ++t)
+            d += (t ? " | " : "") + std::to_string(dbg[8 * t]) + "/" + std::to_string(dbg[8 * t + 1]) + "/" +
+                 std::to_string(dbg[8 * t + 2]) + "/" + std::to_string(dbg[8 * t + 3]) + " start " +
+                 std::to_string(int(dbg[8 * t + 4] - t0)) + " waited " + std::to_string(int(dbg[8 * t + 6] - t0)) +
+                 " loopdone " + std::to_string(int(dbg[8 * t + 7] - t0)) + " pub " + std::to_string(int(dbg[8 * t + 5] - t0));
+        std::printf("{\"case\": \"%s\", \"items (taken 1+sg / waited / prog seen / published)\": \"%s\"}\n", name,
+                    d.c_str());
+    }
+    std::fflush(stdout);
     b.free_all();
     return bad || w[1] ? 1 : 0;
 }
@@ -164,7 +182,9 @@ int main(int argc, char** argv) {
             ragged.push_back((x >> 33) % (4 * SEG));
         }
         fails += check("ragged 168", ragged);
-        fails += check("1100 groups x 2 segments", std::vector<uint64_t>(1100 * 64, 2 * SEG));
+        fails += check("64 messages of 1 segment", std::vector<uint64_t>(64, SEG - 64));
+        fails += check("2 messages of 2 segments", std::vector<uint64_t>(2, 2 * SEG));
+        if (getenv("LAB_BIGCHECK")) fails += check("1100 groups x 2 segments", std::vector<uint64_t>(1100 * 64, 2 * SEG));
     } else {
         for (uint64_t n : {65536ull, 81920ull, 98304ull, 131072ull}) {
             Batch b;
