@@ -198,7 +198,7 @@ int mxec_encode_async(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint
                       const size_t* data_len, uint8_t* const* parity, uint8_t (*sha256_out)[32],
                       mxec_ticket** ticket) {
     return guarded([&] {
-        if (k <= 0 || m < 0 || k + m > 256) return mxec_encode(ctx, k, m, shard_size, data, data_len, parity, sha256_out);
+        MXEC_TRY(check_km(k, m));  // the crate / k+m>255 guards answer at once, as the blocking call would
         auto d = copy_n(data, size_t(k));
         auto dl = copy_n(data_len, size_t(k));
         auto p = copy_n(parity, size_t(m));
@@ -214,9 +214,7 @@ int mxec_reconstruct_async(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8
                            const size_t* shard_len, const uint8_t (*expected_sha256)[32], uint8_t* present_inout,
                            uint32_t flags, int* n_present, mxec_ticket** ticket) {
     return guarded([&] {
-        if (k <= 0 || m < 0 || k + m > 256)
-            return mxec_reconstruct(ctx, k, m, shard_size, shards, shard_len, expected_sha256, present_inout, flags,
-                                    n_present);
+        if (int rc = mxec_rs_check(k, m)) return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
         const size_t total = size_t(k + m);
         auto s = copy_n(shards, total);
         auto sl = copy_n(shard_len, total);
