@@ -52,7 +52,9 @@ GIB = float(1 << 30)
 # the gfx950 ISA of the loop bodies (tools/isa_count.py): split form =
 # consumer 905 (64 rounds x 14 + 9) + producer 565 (2261 per 4-block step);
 # one-wave form 1536.
-SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1536}
+# stream form 1541 (its block loop: the one-wave rounds plus the clamped
+# prefetch).
+SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1536, "stream": 1541}
 # Chip INT32 issue ceiling for those instructions (v_alignbit / v_bitop3 /
 # v_add3 / v_add / v_perm): CUs x 4 SIMDs x lanes per cycle x 2.4 GHz, lanes
 # per cycle measured with tools/valu_lab chip (profiles/r2_lab_valu_chip.jsonl).
@@ -265,10 +267,14 @@ class ReconstructStream:
 
     def breakdown(self):
         lat = sorted(self.lat)
+        st = self.parts[0].ctx.combiner_stats()
         return {"workers": len(self.parts),
                 "batch_call_ms_median": round(1e3 * lat[len(lat) // 2], 2) if lat else None,
+                "combiner_launches": st["batches"], "combiner_messages": st["messages"],
+                "messages_per_launch": round(st["messages"] / max(1, st["batches"]), 1),
                 "what": "host-side duration of one worker's reconstruct call (verify kernel + "
-                        "readback + decode enqueue)"}
+                        "readback + decode enqueue); SHA-256 launches of the device's combiner since "
+                        "the context opened"}
 
     def spot_check(self):
         return all(p.spot_check() for p in self.parts)
@@ -640,6 +646,30 @@ def valu_bound_GBps(form: str, n_cus: int) -> float:
     return lane_ops / SHA_VALU_PER_BLOCK[form] * 64 / 1e9
 
 
+def stream_step_roofline(ms: float, workers: int, n: int, n_cus: int) -> dict:
+    """Config 3c's step against its bound: every present shard hashed in one
+    combined stream-form launch at the INT32-VALU ceiling, then the decodes
+    (read 8, write 2 shards per object) at HBM peak -- the step's digests
+    decide what the decodes rebuild, and the next step's hashes read what
+    they wrote, so the two phases are serial.  frac_hash_only sets the whole
+    step against the hashing bound alone."""
+    S = float(1 << 20)
+    hashed = workers * n * 10 * S
+    decoded = workers * n * 10 * S
+    vb = valu_bound_GBps("stream", n_cus)
+    bound_ms = hashed / (vb * 1e9) * 1e3 + decoded / (HBM_PEAK_GBPS * 1e9) * 1e3
+    sha_GBps = hashed / (ms * 1e-3) / 1e9
+    return {"bound": "valu+hbm", "kernel": "sha256_stream_kernel (combined) + rs_apply_fast<R=2> x workers",
+            "achieved_ms_per_step": round(ms, 2), "bound_ms_per_step": round(bound_ms, 2),
+            "frac": round(bound_ms / ms, 4),
+            "hash_GBps_over_step": round(sha_GBps, 1), "valu_bound_GBps_hashed": round(vb, 1),
+            "frac_hash_only": round(sha_GBps / vb, 4),
+            "valu_lane_ops_per_block": SHA_VALU_PER_BLOCK["stream"],
+            "what": (f"{workers} x {n} objects 8+4 x 1 MiB per step: {hashed / 1e9:.1f} GB hashed at the "
+                     f"INT32-VALU bound ({vb:.0f} GB/s) + {decoded / 1e9:.1f} GB decode traffic at "
+                     f"{HBM_PEAK_GBPS:.0f} GB/s, serial")}
+
+
 def hbm_block(alg_bytes: float, ms: float, kernel: str, cal: dict, ratio_key: str) -> dict:
     ach = alg_bytes / (ms * 1e-3) / 1e9
     d = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -690,7 +720,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     ms_sha = event_ms(torch, stream, lambda: ctx.sha256_batch_device(present_ptrs, present_lens, dig.data_ptr(),
                                                                      stream=sh), 3)
     hashed = float(len(present_ptrs)) * S
-    form = "split" if len(present_ptrs) <= 32768 else "one"
+    form = "split" if len(present_ptrs) <= 49152 else "stream"
     sha_GBps = hashed / (ms_sha * 1e-3) / 1e9
     vb = valu_bound_GBps(form, n_cus)
     # decode alone: the same erasures, no digests (RS over the 8 survivors -> 2)
@@ -729,14 +759,9 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
         rs.step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / reps
-    hashed = 8 * 1024 * 10 * float(1 << 20)
-    sha_GBps = hashed / (ms * 1e-3) / 1e9
-    vb = valu_bound_GBps("one" if 8 * 10240 > 32768 else "split", n_cus)
     out["config3c"] = {"workload": rs.name, "GiBps_payload": round(rs.payload / GIB / (ms * 1e-3), 3),
                        "ms_per_step": round(ms, 2), "spot_check_vs_original": rs.spot_check(),
-                       "roofline": {"bound": "valu", "achieved": round(sha_GBps, 1), "unit": "GB/s hashed",
-                                    "peak": round(vb, 1), "frac": round(sha_GBps / vb, 4),
-                                    "what": "whole step (hash + decode + host work) against the hashing bound"},
+                       "roofline": stream_step_roofline(ms, 8, 1024, n_cus),
                        "breakdown": rs.breakdown()}
     rs.drop()
     del rs
@@ -922,6 +947,10 @@ def main() -> int:
             "spot_check_vs_oracle": spot_ok,
             "extra": extra,
         }
+        if isinstance(w, ReconstructStream):
+            n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            line["roofline"] = dict(stream_step_roofline(elapsed * 1e3 / args.steps, len(w.parts), w.parts[0].n, n_cus),
+                                    traffic=None)
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:

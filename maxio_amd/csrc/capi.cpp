@@ -486,16 +486,18 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 // every concurrent caller's verification (combiner.cpp), once
                 // the work queued on `stream` has produced the shards; digests
                 // compared on the host.
+                // The combined launch waits on the device for the work
+                // already on `stream` (an event), so the host does not wait
+                // here first; the expected digests travel meanwhile.
                 const size_t ne = size_t(n_obj) * size_t(total) * 32;
                 MXEC_TRY(slot.hdig.ensure(ne));
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, expected_sha_dev, ne, hipMemcpyDeviceToHost, s));
-                MXEC_TRY(slot_wait(*ds.slot, s));
-                std::vector<uint8_t> exph(static_cast<const uint8_t*>(slot.hdig.p),
-                                          static_cast<const uint8_t*>(slot.hdig.p) + ne);
                 std::vector<uint8_t> dig(ptrs.size() * 32);
                 MXEC_TRY(sha256_combined(*ds.d, slot, s, ptrs, lens, dig.data()));
+                MXEC_TRY(slot_wait(*ds.slot, s));  // the digest copy (long done)
+                const auto* exph = static_cast<const uint8_t*>(slot.hdig.p);
                 for (size_t t = 0; t < idx.size(); ++t)
-                    if (std::memcmp(&dig[t * 32], exph.data() + idx[t] * 32, 32) != 0) present[idx[t]] = 0;
+                    if (std::memcmp(&dig[t * 32], exph + idx[t] * 32, 32) != 0) present[idx[t]] = 0;
             }
         }
         const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;

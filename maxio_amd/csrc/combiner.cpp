@@ -15,6 +15,7 @@
 // request's latency.
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
@@ -28,6 +29,7 @@ struct ShaCombiner {
         const std::vector<const uint8_t*>* ptrs = nullptr;
         const std::vector<uint64_t>* lens = nullptr;
         uint8_t* out = nullptr;  // host, n * 32
+        hipEvent_t ready = nullptr;  // on the caller's stream: its messages are complete
         int rc = MXEC_OK;
         std::string msg;
         bool done = false;
@@ -72,17 +74,21 @@ struct ShaCombiner {
         const size_t n = ptrs.size();
         if (n == 0) return MXEC_OK;
         hipStream_t s = slot.stream;
+        // Each caller's shards are complete once its stream reaches its
+        // event; the launch waits on the device, not on the host, so
+        // callers whose preceding work finishes at different times still
+        // arrive together (config 3c: the decodes of the previous step).
+        for (const Req* r : batch)
+            if (r->ready) MXEC_HIP(hipStreamWaitEvent(s, r->ready, 0));
         MXEC_TRY(slot.digests.ensure(n * 32));
-        // The split (producer / consumer) form below one 64-message group per
-        // SIMD: a combined batch is often several chip-filling requests, and
-        // two waves per 64 messages spread over the SIMDs more evenly than
-        // one.  From there the stream form (segments of every chain dealt to
-        // persistent waves) keeps every SIMD busy to the end (81 920 x 1 MiB:
-        // 55.7 ms vs 77.8 split); its timeout word comes back with the
-        // digests.
+        // The split (producer / consumer) form up to 3/4 of a 64-message
+        // group per SIMD; beyond, the stream form (segments of every chain
+        // dealt to persistent waves) keeps every SIMD busy to the end
+        // (81 920 x 1 MiB: 55.8 ms vs 96.1 split); its timeout word comes
+        // back with the digests.
         const uint32_t* tmo = nullptr;
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr, nullptr,
-                         nullptr, (n + 63) / 64 >= size_t(d.n_cus) * 4 ? 0 : 2, &tmo));
+                         nullptr, sha_stream_size((n + 63) / 64, uint64_t(d.n_cus) * 4) ? 0 : 2, &tmo));
         MXEC_TRY(slot.hdig.ensure(n * 32 + 16));
         auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + n * 32);
         *hflag = 0;
@@ -132,6 +138,18 @@ long gather_us() {
 long gather_max_us() {
     static const long us = env_us("MXEC_GATHER_MAX_US", 2000);
     return us;
+}
+// MXEC_GATHER_IDLE_US: once a batch is forming, how long a gap between
+// arrivals still counts as "more are coming" (default 300 us).
+long gather_idle_us() {
+    static const long us = env_us("MXEC_GATHER_IDLE_US", 300);
+    return us;
+}
+// MXEC_COMBINE_LOG=1: one stderr line per combined launch (requests,
+// messages, gathering and launch times) -- for tuning the windows above.
+bool combine_log() {
+    static const bool on = env_us("MXEC_COMBINE_LOG", 0) != 0;
+    return on;
 }
 
 // MXEC_COMBINE_STREAMS: launches in flight per device (default 2).  A second
@@ -203,6 +221,9 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     me.ptrs = &ptrs;
     me.lens = &lens;
     me.out = out;
+    if (!slot.ready_ev) MXEC_HIP(hipEventCreateWithFlags(&slot.ready_ev, hipEventDisableTiming));
+    MXEC_HIP(hipEventRecord(slot.ready_ev, s));
+    me.ready = slot.ready_ev;
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&me);
     c->pending_msgs += ptrs.size();
@@ -225,9 +246,25 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // the previous size is forgotten as soon as fewer come.
         const size_t want = c->last_batch;
         const long wait_us = want > 1 ? gather_max_us() : gather_us();
+        const auto t0 = std::chrono::steady_clock::now();
         if (c->pending.size() < std::max<size_t>(want, 2) && wait_us > 0)
             c->cv_gather.wait_for(lk, std::chrono::microseconds(wait_us),
                            [&] { return c->pending.size() >= std::max<size_t>(want, 2); });
+        // Then, while requests keep arriving (each within gather_idle_us of
+        // the last), keep gathering up to gather_max_us in all: the previous
+        // batch size is a floor, not a cap.  Without this, eight concurrent
+        // 10 240-chunk verifications (config 3c) settled into two launches of
+        // four (split form, 640 groups each) instead of one of 81 920
+        // messages, which takes the stream form.
+        if (c->pending.size() >= 2) {
+            const auto hard = t0 + std::chrono::microseconds(gather_max_us());
+            for (size_t seen = c->pending.size(); std::chrono::steady_clock::now() < hard;) {
+                c->cv_gather.wait_for(lk, std::chrono::microseconds(gather_idle_us()),
+                                      [&] { return c->pending.size() > seen; });
+                if (c->pending.size() == seen) break;
+                seen = c->pending.size();
+            }
+        }
         std::vector<ShaCombiner::Req*> batch;
         batch.swap(c->pending);
         size_t batch_msgs = c->pending_msgs;
@@ -243,10 +280,18 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         if (!c->free_slots.empty() && c->inflight_msgs + c->pending_msgs <= c->lane_limit) c->cv_done.notify_all();
         lk.unlock();
         int rc = MXEC_OK;
+        const auto t1 = std::chrono::steady_clock::now();
         try {
             rc = ShaCombiner::run(d, *slot_run, batch);
         } catch (...) {
             rc = set_error(MXEC_E_OOM, "host allocation failed");
+        }
+        if (combine_log()) {
+            const auto t2 = std::chrono::steady_clock::now();
+            using us = std::chrono::microseconds;
+            std::fprintf(stderr, "[mxec combine] requests %zu messages %zu gather_us %lld run_us %lld rc %d\n",
+                         batch.size(), batch_msgs, (long long)std::chrono::duration_cast<us>(t1 - t0).count(),
+                         (long long)std::chrono::duration_cast<us>(t2 - t1).count(), rc);
         }
         const std::string msg = rc ? std::string(last_error()) : std::string();
         lk.lock();

@@ -65,7 +65,8 @@ struct ShaArgs {
     uint32_t* work = nullptr;    // [4 + groups] zeroed before the launch:
                                  //   [0] next item, [1] timeout code, [4 + g] segments of group g done
     uint32_t* state = nullptr;   // [n][8]
-    uint32_t waves = 0;          // persistent waves (one workgroup each)
+    uint32_t waves = 0;          // persistent waves
+    uint32_t wg_waves = 1;       // waves per workgroup (1 or 4; waves divisible by it)
     uint32_t seg_max = 0;        // segments of the longest message
 };
 // Blocks per stream-form segment (32 KiB of each message).

@@ -191,7 +191,7 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     if (tmo_dev && !arena && (form == 0 || form == 3) && n < (uint64_t(1) << 31)) {
         bool aligned = true;
         for (const uint8_t* p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-        stream = aligned && (groups >= simds || form == 3 || env_form == 3);
+        stream = aligned && (sha_stream_size(groups, simds) || form == 3 || env_form == 3);
     } else if (tmo_dev && !arena && env_form == 3 && n < (uint64_t(1) << 31)) {
         bool aligned = true;
         for (const uint8_t* p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
@@ -231,6 +231,14 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
         // per SIMD measured slower (131 072 x 1 MiB: 132.5 vs 92.8 ms for the
         // one-wave form; profiles/r2_sha_stream_lab.txt).
         a.waves = uint32_t(simds);
+        // Four waves per workgroup: the dispatcher spreads a workgroup's
+        // waves over the CU's four SIMDs, while one-wave workgroups after an
+        // HBM-heavy kernel landed two to a SIMD on ~100 SIMDs and none on as
+        // many, and the segment chains through the doubled SIMDs ran the
+        // launch at half speed (81 920 x 1 MiB after an 8 GiB write kernel:
+        // 110 ms vs 56; tools/sha_stream_lab place / repeat,
+        // profiles/r2_sha_stream_placement.txt).
+        a.wg_waves = simds % 4 == 0 ? 4 : 1;
         a.seg_max = uint32_t(longest / 64 / kShaSegBlocks + 1);
         *tmo_dev = a.work + 1;
     }

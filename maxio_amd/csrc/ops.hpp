@@ -44,6 +44,10 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
 // caller synchronises `s` first).  Concurrent small requests on one device
 // share one launch on the combiner's stream (combiner.cpp); large ones run on
 // the caller's slot and stream.
+// The stream form pays once a batch has more 64-message groups than 3/4 of
+// the SIMDs (sha256_kernel.hip kSplitMaxMessages).
+inline bool sha_stream_size(uint64_t groups, uint64_t simds) { return groups * 4 > simds * 3; }
+
 int sha256_combined(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
                     const std::vector<uint64_t>& lens, uint8_t* out);
 void combiner_stats(Device& dev, uint64_t* batches, uint64_t* messages);

@@ -67,6 +67,7 @@ void slot_destroy(Slot& slot) {
     for (auto& e : slot.stage_done)
         if (e) (void)hipEventDestroy(e);
     if (slot.sync_ev) (void)hipEventDestroy(slot.sync_ev);
+    if (slot.ready_ev) (void)hipEventDestroy(slot.ready_ev);
     if (slot.stream) (void)hipStreamDestroy(slot.stream);
     slot.stream = nullptr;
 }

@@ -76,6 +76,10 @@ struct Slot {
     hipEvent_t stage_done[2] = {nullptr, nullptr};
     // Blocking-sync event for the host-API waits (slot_wait).
     hipEvent_t sync_ev = nullptr;
+    // Recorded on the caller's stream when it hands messages to the SHA-256
+    // combiner: the combined launch waits for it on the device, so a caller
+    // need not wait on the host for the work that produces its shards.
+    hipEvent_t ready_ev = nullptr;
     // Set by upload_segments when it queued DMAs straight from the caller's
     // page-locked memory (no staging copy): the call must not return before
     // they finish, on any path.  slot_wait clears it; DevScope waits on it.

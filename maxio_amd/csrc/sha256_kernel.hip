@@ -370,7 +370,7 @@ __device__ __forceinline__ bool stream_wait(gu32* prog, uint32_t want, gu32* tmo
     }
 }
 
-__global__ __launch_bounds__(64) void sha256_stream_kernel(const uint8_t* const* __restrict__ ptrs,
+__global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* const* __restrict__ ptrs,
                                                            const uint64_t* __restrict__ lens,
                                                            uint8_t* __restrict__ digests,
                                                            const uint8_t* __restrict__ expected,
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64) void sha256_stream_kernel(const uint8_t* const*
                                                            uint32_t seg_max) {
     gu32* work = (gu32*)(work_p);
     gu32* state = (gu32*)(state_p);
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;  // every wave of a workgroup works alone
     const uint32_t groups = (n + 63) / 64;
     const uint32_t n_items = groups * seg_max;
     for (;;) {
@@ -493,10 +493,13 @@ __global__ __launch_bounds__(64) void sha256_stream_kernel(const uint8_t* const*
 }  // namespace
 
 // Messages at or below this count run the split (two waves per 64 messages)
-// form: with fewer messages than SIMD slots, a message's latency is the
-// kernel's time; above it, one wave per 64 messages keeps every slot doing
-// rounds (throughput form).
-constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 / 2;
+// form: while its waves fit about one per SIMD, a message's latency is the
+// kernel's time; above it, one wave per 64 messages (or the stream form,
+// chosen by the caller) keeps every SIMD doing rounds.  Up to 3/4 of a
+// group per SIMD the split form still led (40 960 x 1 MiB: 42.8 ms vs 51.2
+// one-wave, 44.9 stream); at 51 200 the stream form led (44.8 vs 53.9 split;
+// profiles/r2_sha_stream_lab_sizes.jsonl).
+constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 
 hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
@@ -510,8 +513,9 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         else form = a.n <= kSplitMaxMessages ? 2 : 1;
     }
     if (form == 3) {
-        if (!a.work || !a.state || a.waves == 0 || a.seg_max == 0) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(sha256_stream_kernel, dim3(a.waves), dim3(64), 0, s, a.ptrs, a.lens, a.digests,
+        const uint32_t per = a.wg_waves ? a.wg_waves : 1;
+        if (!a.work || !a.state || a.waves == 0 || a.seg_max == 0 || per > 4 || a.waves % per) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(sha256_stream_kernel, dim3(a.waves / per), dim3(64 * per), 0, s, a.ptrs, a.lens, a.digests,
                            a.expected, a.exp_idx, a.ok, a.n, a.work, a.state, a.seg_max);
         return hipGetLastError();
     }

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -26,6 +27,30 @@
     } while (0)
 
 namespace {
+
+__global__ void fill_random(uint64_t* p, uint64_t n, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) {
+        uint64_t x = (i + 1) * 0x9E3779B97F4A7C15ull ^ seed;
+        x ^= x >> 31;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 29;
+        p[i] = x;
+    }
+}
+
+// Placement probe: every wave records HW_ID and XCC_ID, then stays resident
+// ~`hold` s_memtime ticks so the dispatcher places the whole grid at once.
+__global__ void placement(uint32_t* out, uint64_t hold) {
+    const uint32_t w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    if ((threadIdx.x & 63) == 0) {
+        out[2 * w] = hw;
+        out[2 * w + 1] = xcc;
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < hold) __builtin_amdgcn_s_sleep(10);
+}
 
 struct Batch {
     uint8_t* data = nullptr;  // device, messages back to back (16-byte aligned starts)
@@ -51,8 +76,11 @@ struct Batch {
                 b = uint8_t(x);
             }
             CK(hipMemcpy(data, h.data(), total, hipMemcpyHostToDevice));
+        } else if (getenv("LAB_CONST")) {
+            CK(hipMemset(data, 0x5A, total));  // constant bytes (lower switching activity)
         } else {
-            CK(hipMemset(data, 0x5A, total));  // timing only: SHA-256's work does not depend on the bytes
+            hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t*>(data), total / 8, seed);
+            CK(hipDeviceSynchronize());
         }
         uint64_t o = 0;
         for (uint64_t l : L) {
@@ -71,6 +99,8 @@ struct Batch {
     }
     mxec::ShaArgs args(int form) {
         const size_t n = lens.size();
+        const bool wg4 = form == 4;  // stream form, four waves per workgroup
+        if (wg4) form = 3;
         mxec::ShaArgs a{};
         a.ptrs = static_cast<const uint8_t* const*>(tables);
         a.lens = reinterpret_cast<const uint64_t*>(static_cast<char*>(tables) + n * 8);
@@ -86,6 +116,7 @@ struct Batch {
             a.waves = uint32_t(simds);
             (void)groups;
             if (const char* e = getenv("LAB_WAVES")) a.waves = uint32_t(atoi(e));
+            if (wg4) a.wg_waves = 4;
             a.seg_max = uint32_t(longest / 64 / mxec::kShaSegBlocks + 1);
         }
         return a;
@@ -100,6 +131,7 @@ struct Batch {
         CK(hipEventCreate(&b));
         CK(hipEventRecord(a, 0));
         CK(mxec::launch_sha256(args(form), 0));
+        CK(hipGetLastError());
         CK(hipEventRecord(b, 0));
         CK(hipEventSynchronize(b));
         float ms = 0;
@@ -159,9 +191,16 @@ int check(const char* name, const std::vector<uint64_t>& L) {
         std::printf("{\"case\": \"%s\", \"items (taken 1+sg / waited / prog seen / published)\": \"%s\"}\n", name,
                     d.c_str());
     }
+    // the same with four waves per workgroup
+    b.run(4);
+    const auto got4 = b.digests();
+    const auto w4 = b.work_words();
+    size_t bad4 = 0;
+    for (size_t i = 0; i < L.size(); ++i) bad4 += std::memcmp(&ref[i * 32], &got4[i * 32], 32) != 0;
+    std::printf("{\"case\": \"%s\", \"wg4_mismatch\": %zu, \"wg4_timeout\": %u}\n", name, bad4, w4[1]);
     std::fflush(stdout);
     b.free_all();
-    return bad || w[1] ? 1 : 0;
+    return bad || w[1] || bad4 || w4[1] ? 1 : 0;
 }
 
 }  // namespace
@@ -185,17 +224,80 @@ int main(int argc, char** argv) {
         fails += check("64 messages of 1 segment", std::vector<uint64_t>(64, SEG - 64));
         fails += check("2 messages of 2 segments", std::vector<uint64_t>(2, 2 * SEG));
         if (getenv("LAB_BIGCHECK")) fails += check("1100 groups x 2 segments", std::vector<uint64_t>(1100 * 64, 2 * SEG));
+    } else if (mode == "place") {
+        // Where do W persistent waves land (waves per SIMD), after nothing
+        // and after an 8 GiB HBM write kernel?
+        const uint32_t W = getenv("LAB_WAVES") ? uint32_t(atoi(getenv("LAB_WAVES"))) : 1024;
+        uint32_t* out = nullptr;
+        CK(hipMalloc(&out, 8 * 8192));
+        uint64_t* junk = nullptr;
+        const uint64_t jn = (8ull << 30) / 8;
+        CK(hipMalloc(&junk, jn * 8));
+        for (int per : {1, 4})
+            for (int between : {0, 1, 0, 1}) {
+                if (between) hipLaunchKernelGGL(fill_random, dim3(8192), dim3(256), 0, 0, junk, jn, 1ull);
+                CK(hipMemset(out, 0xFF, 8 * 8192));
+                hipLaunchKernelGGL(placement, dim3(W / per), dim3(64 * per), 0, 0, out, 2000000ull);
+                CK(hipDeviceSynchronize());
+                std::vector<uint32_t> h(2 * W);
+                CK(hipMemcpy(h.data(), out, 8 * W, hipMemcpyDeviceToHost));
+                std::map<uint64_t, int> simd, cu;
+                for (uint32_t w = 0; w < W; ++w) {
+                    const uint64_t key = (uint64_t(h[2 * w + 1] & 0xF) << 32) | (h[2 * w] & 0xFF30u);
+                    ++simd[key];
+                    ++cu[key & ~uint64_t(0x30)];
+                }
+                std::map<int, int> hist;
+                for (auto& kv : simd) ++hist[kv.second];
+                std::string hs;
+                for (auto& kv : hist) hs += (hs.empty() ? "" : ", ") + std::to_string(kv.first) + " waves: " + std::to_string(kv.second);
+                std::printf("{\"waves\": %u, \"per_wg\": %d, \"after_hbm_kernel\": %d, \"simds_used\": %zu, \"cus_used\": %zu, \"simds by waves\": \"%s\", \"hw0\": \"%08x\"}\n",
+                            W, per, between, simd.size(), cu.size(), hs.c_str(), h[0]);
+                std::fflush(stdout);
+            }
+        (void)hipFree(out);
+        (void)hipFree(junk);
+    } else if (mode == "repeat") {
+        // n x 1 MiB stream-form launches back to back; LAB_BETWEEN=1 puts an
+        // 8 GiB HBM write kernel between launches (as config 3c's decodes).
+        const uint64_t n = getenv("LAB_N") ? strtoull(getenv("LAB_N"), nullptr, 10) : 81920;
+        Batch b;
+        b.make(std::vector<uint64_t>(n, 1 << 20), n, false);
+        uint64_t* junk = nullptr;
+        const uint64_t jn = (8ull << 30) / 8;
+        const bool between = getenv("LAB_BETWEEN") != nullptr;
+        if (between) CK(hipMalloc(&junk, jn * 8));
+        for (int r = 0; r < 8; ++r) {
+            if (between) {
+                hipLaunchKernelGGL(fill_random, dim3(8192), dim3(256), 0, 0, junk, jn, uint64_t(r));
+                CK(hipDeviceSynchronize());
+            }
+            const double ms = b.run(getenv("LAB_FORM") ? atoi(getenv("LAB_FORM")) : 3);
+            std::printf("{\"repeat\": %d, \"n\": %llu, \"between\": %d, \"ms\": %.3f, \"timeout\": %u}\n", r,
+                        (unsigned long long)n, int(between), ms, b.work_words()[1]);
+            std::fflush(stdout);
+        }
+        if (junk) (void)hipFree(junk);
+        b.free_all();
     } else {
-        for (uint64_t n : {65536ull, 81920ull, 98304ull, 131072ull}) {
+        std::vector<uint64_t> sizes = {20480, 32768, 40960, 51200, 65536, 81920, 98304, 131072};
+        if (const char* e = getenv("LAB_SIZES")) {
+            sizes.clear();
+            for (const char* q = e; *q;) {
+                sizes.push_back(strtoull(q, const_cast<char**>(&q), 10));
+                if (*q == ',') ++q;
+            }
+        }
+        for (uint64_t n : sizes) {
             Batch b;
             b.make(std::vector<uint64_t>(n, 1 << 20), n, false);
-            for (int form : {2, 1, 3}) {
+            for (int form : {2, 1, 3, 4}) {
                 b.run(form);  // warm
                 const double ms = b.run(form);
                 const auto w = b.work_words();
                 std::printf("{\"n\": %llu, \"form\": \"%s\", \"ms\": %.3f, \"GBps_hashed\": %.1f, \"timeout\": %u}\n",
-                            (unsigned long long)n, form == 1 ? "one" : form == 2 ? "split" : "stream", ms,
-                            double(n) * (1 << 20) / (ms * 1e-3) / 1e9, form == 3 ? w[1] : 0u);
+                            (unsigned long long)n, form == 1 ? "one" : form == 2 ? "split" : form == 3 ? "stream" : "stream_wg4", ms,
+                            double(n) * (1 << 20) / (ms * 1e-3) / 1e9, form >= 3 ? w[1] : 0u);
                 std::fflush(stdout);
             }
             b.free_all();
