@@ -51,10 +51,9 @@ GIB = float(1 << 30)
 # block (one wave instruction serves 64 messages, one block each), counted in
 # the gfx950 ISA of the loop bodies (tools/isa_count.py): split form =
 # consumer 905 (64 rounds x 14 + 9) + producer 565 (2261 per 4-block step);
-# one-wave form 1536.
-# stream form 1541 (its block loop: the one-wave rounds plus the clamped
-# prefetch).
-SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1536, "stream": 1541}
+# one-wave form 1410 (64 x 14 rounds + 48 x 10 schedule + 16 byte swaps + 18);
+# stream form 1415 (the one-wave rounds plus the clamped prefetch).
+SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415}
 # Chip INT32 issue ceiling for those instructions (v_alignbit / v_bitop3 /
 # v_add3 / v_add / v_perm): CUs x 4 SIMDs x lanes per cycle x 2.4 GHz, lanes
 # per cycle measured with tools/valu_lab chip (profiles/r2_lab_valu_chip.jsonl).
