@@ -116,8 +116,24 @@ int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vec
     for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.src, g.len));
     if (all_pinned) {  // DMA straight from the caller's page-locked buffers
         slot.borrowed = s;  // from here on every exit of the call waits on s
-        for (const auto& g : segs)
-            if (g.len) MXEC_HIP(hipMemcpyAsync(dev_base + g.dst_off, g.src, g.len, hipMemcpyHostToDevice, s));
+        // Segments contiguous on both sides (a GET range's chunks land back
+        // to back in the caller's buffer and in 256-byte-aligned slots) go
+        // up as one DMA: per-copy submission cost, not bytes, is what the
+        // direct path pays over staging.
+        for (size_t i = 0; i < segs.size();) {
+            if (!segs[i].len) {
+                ++i;
+                continue;
+            }
+            const auto* src = static_cast<const uint8_t*>(segs[i].src);
+            const uint64_t dst = segs[i].dst_off;
+            uint64_t len = segs[i].len;
+            size_t j = i + 1;
+            while (j < segs.size() && segs[j].len && segs[j].src == src + len && segs[j].dst_off == dst + len)
+                len += segs[j++].len;
+            MXEC_HIP(hipMemcpyAsync(dev_base + dst, src, len, hipMemcpyHostToDevice, s));
+            i = j;
+        }
         return MXEC_OK;
     }
     for (auto& e : slot.stage_done)
@@ -152,8 +168,20 @@ int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const 
     bool all_pinned = true;
     for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.dst, g.len));
     if (all_pinned) {  // DMA straight into the caller's page-locked buffers
-        for (const auto& g : segs)
-            if (g.len) MXEC_HIP(hipMemcpyAsync(g.dst, dev_base + g.src_off, g.len, hipMemcpyDeviceToHost, s));
+        for (size_t i = 0; i < segs.size();) {  // contiguous runs as one DMA (as uploads)
+            if (!segs[i].len) {
+                ++i;
+                continue;
+            }
+            auto* dst = static_cast<uint8_t*>(segs[i].dst);
+            const uint64_t src = segs[i].src_off;
+            uint64_t len = segs[i].len;
+            size_t j = i + 1;
+            while (j < segs.size() && segs[j].len && segs[j].dst == dst + len && segs[j].src_off == src + len)
+                len += segs[j++].len;
+            MXEC_HIP(hipMemcpyAsync(dst, dev_base + src, len, hipMemcpyDeviceToHost, s));
+            i = j;
+        }
         return slot_wait(slot, s);
     }
     for (auto& e : slot.stage_done)
