@@ -554,7 +554,8 @@ def pmc_traffic(tag: str, alg_bytes: float):
     correction + WRITE_SIZE; tools/pmc_summary.py): the measured
     traffic / algorithmic ratio applied to this launch's algorithmic bytes
     (the summary may come from a smaller batch of the same kernel)."""
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{tag}*.json"))):
+    # newest round first (profiles/rNN_…)
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{tag}*.json")), reverse=True):
         try:
             with open(p) as f:
                 d = json.load(f)

@@ -87,3 +87,54 @@ def test_mixed_requests_many_threads(tmp_path):
         assert all(results), [i for i, r in enumerate(results) if not r]
     finally:
         ctx.close()
+
+
+def test_combined_verify_waits_for_callers_stream_work():
+    """The combined SHA-256 launch waits on the device for the work each
+    caller queued on its own stream before handing over its shards
+    (combiner.cpp: an event per caller, hipStreamWaitEvent): four threads
+    each zero their objects, queue a copy that restores them on their own
+    stream, and call the device verify + rebuild at once, without a host
+    sync.  Hashing before the copies land would see zeros, turn every shard
+    into an erasure and fail the call."""
+    import torch
+
+    k, m, S, n, W = 8, 4, 1 << 20, 96, 4
+    ctx = maxio_amd.Context(streams_per_device=W)
+    try:
+        streams = [torch.cuda.Stream() for _ in range(W)]
+        g = torch.Generator(device="cuda").manual_seed(91)
+        objs, refs, digs = [], [], []
+        for w in range(W):
+            o = torch.randint(0, 256, (n, k + m, S), dtype=torch.uint8, device="cuda", generator=g)
+            d = torch.zeros((n, k + m, 32), dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            ctx.encode_strided_device(k, m, S, n, o.data_ptr(), (k + m) * S, S, o[:, k:].data_ptr(),
+                                      (k + m) * S, S, digests_ptr=d.data_ptr())
+            torch.cuda.synchronize()
+            objs.append(o)
+            refs.append(o.clone())
+            digs.append(d)
+        want = [hashlib.sha256(refs[0][0, i].cpu().numpy().tobytes()).digest() for i in range(k + m)]
+        assert [bytes(x) for x in digs[0][0].cpu().numpy()] == want
+
+        def one(w):
+            st = streams[w]
+            with torch.cuda.stream(st):
+                objs[w].zero_()
+                objs[w].copy_(refs[w])  # queued, not waited for
+            present = np.ones(n * (k + m), np.uint8)
+            present[0::k + m] = 0  # one data erasure per object
+            rc, _ = ctx.reconstruct_strided_device(k, m, S, n, objs[w].data_ptr(), (k + m) * S, S, present,
+                                                   expected_ptr=digs[w].data_ptr(), stream=st.cuda_stream)
+            return rc, present
+
+        with ThreadPoolExecutor(W) as pool:
+            res = list(pool.map(one, range(W)))
+        torch.cuda.synchronize()
+        for w, (rc, present) in enumerate(res):
+            assert rc == 0, (w, rc)
+            assert present.all(), w
+            assert torch.equal(objs[w], refs[w]), w
+    finally:
+        ctx.close()
