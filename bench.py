@@ -289,14 +289,23 @@ class ReconstructStream:
 
 class Mixed:
     """configs[4]: mixed (k, m) and chunk sizes with short last chunks;
-    a step encodes the batch and reconstructs it with seeded erasures."""
+    a step encodes the batch and reconstructs it with seeded erasures.
+
+    The 15 (k, m, S) classes are independent, as concurrent requests of a
+    server are: class i runs on stream i mod `streams` (encode then
+    reconstruct, in order on that stream), and the bench's stream waits for
+    all of them, so its HIP events still bracket the whole step.  One stream
+    serialises ~65 launches per step with an idle gap and a drain tail each
+    (the smallest run 40-100 us)."""
 
     bound = "hbm"
 
-    def __init__(self, torch, ctx, dev, sh, budget, seed):
+    def __init__(self, torch, ctx, dev, sh, budget, seed, streams=4):
         import numpy as np
 
         self.torch, self.ctx, self.sh = torch, ctx, sh
+        self.main = torch.cuda.ExternalStream(sh, device=dev)
+        self.streams = [self.main] if streams <= 1 else [torch.cuda.Stream(device=dev) for _ in range(streams)]
         rng = np.random.default_rng(seed)
         kms = [(4, 2), (8, 4), (10, 4)]
         sizes = [64 << 10, 256 << 10, 1 << 20, 4 << 20, 10 << 20]
@@ -323,14 +332,22 @@ class Mixed:
                      "(BASELINE configs[4], per GPU)")
 
     def step(self):
-        for (k, m, S, n, t, dl, pres) in self.classes:
+        ns = len(self.streams)
+        for st in self.streams:
+            if st is not self.main:
+                st.wait_stream(self.main)
+        for c, (k, m, S, n, t, dl, pres) in enumerate(self.classes):
             self.ctx.encode_strided_device(k, m, S, n, t.data_ptr(), (k + m) * S, S, t[:, k:].data_ptr(),
-                                           (k + m) * S, S, data_len=dl, stream=self.sh)
-        for (k, m, S, n, t, dl, pres) in self.classes:
+                                           (k + m) * S, S, data_len=dl, stream=self.streams[c % ns].cuda_stream)
+        for c, (k, m, S, n, t, dl, pres) in enumerate(self.classes):
             pr = pres.copy()
             rc, _ = self.ctx.reconstruct_strided_device(k, m, S, n, t.data_ptr(), (k + m) * S, S, pr,
-                                                        shard_len=dl + [S] * m, stream=self.sh)
+                                                        shard_len=dl + [S] * m,
+                                                        stream=self.streams[c % ns].cuda_stream)
             assert rc == 0
+        for st in self.streams:
+            if st is not self.main:
+                self.main.wait_stream(st)
 
     def spot_check(self):
         """The last object of every class after the steps: its parity equals
@@ -540,7 +557,7 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank, workers=8):
                       f"RS encode k=64 m=4, chunk_size=1 MiB (literal 64 MiB objects), {n} objects per "
                       "GPU (BASELINE configs[3], literal reading)", seed)
     if cfg == "5":
-        return Mixed(torch, ctx, dev, sh, 24 << 30, seed)
+        return Mixed(torch, ctx, dev, sh, 24 << 30, seed, int(os.environ.get("BENCH_MIXED_STREAMS", "4")))
     if cfg == "sums":
         return BodySums(torch, ctx, dev, sh, n_objects or 1024, 40 << 20, seed)
     if cfg == "frames":
