@@ -12,6 +12,7 @@
 // submission; data buffers and out-parameters must stay valid until the
 // ticket completes.
 #include <sys/eventfd.h>
+#include <cerrno>
 #include <unistd.h>
 
 #include <condition_variable>
@@ -99,14 +100,13 @@ AsyncPool* pool_of(Ctx& c) {
     return static_cast<AsyncPool*>(c.pool.get());
 }
 
+// Everything under the ticket's lock, `done` last: mxec_ticket_free frees
+// the ticket (and closes its eventfd) as soon as it sees `done`, so the
+// eventfd write and the notify must not follow the unlock.
 void complete(mxec_ticket* t, int rc) {
-    {
-        std::lock_guard<std::mutex> g(t->mu);
-        t->rc = rc;
-        t->msg = rc ? std::string(last_error()) : std::string();
-        t->done = true;
-    }
-    t->cv.notify_all();
+    std::lock_guard<std::mutex> g(t->mu);
+    t->rc = rc;
+    t->msg = rc ? std::string(last_error()) : std::string();
     if (t->efd >= 0) {
         const uint64_t one = 1;
         ssize_t w;
@@ -114,6 +114,8 @@ void complete(mxec_ticket* t, int rc) {
             w = ::write(t->efd, &one, sizeof one);
         } while (w < 0 && errno == EINTR);
     }
+    t->done = true;
+    t->cv.notify_all();
 }
 
 // Queue `op` (returns an mxec status) on ctx's workers; *out gets the ticket.

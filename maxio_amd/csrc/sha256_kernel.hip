@@ -333,8 +333,10 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
 // ---------------------------------------------------------------------------
 typedef uint32_t __attribute__((address_space(1))) gu32;
 
-#ifndef SHA_STREAM_SPIN_LIMIT
-#define SHA_STREAM_SPIN_LIMIT (1u << 24)
+// A wait gives up after this many ticks of the 100 MHz s_memrealtime clock
+// (4 s): a predecessor segment takes ~1.4 ms, so only a fault gets there.
+#ifndef SHA_STREAM_WAIT_TICKS
+#define SHA_STREAM_WAIT_TICKS (400ull * 1000 * 1000)
 #endif
 // Lab builds (tools/sha_stream_lab) define SHA_STREAM_DEBUG: per item, eight
 // words after the n x 8 state words record (taken, waited ok, progress word
@@ -357,14 +359,16 @@ __device__ __forceinline__ uint32_t prog_read(gu32* prog) {
 // publish until its own next wait timed out — measured in
 // tools/sha_stream_lab, profiles/r2_sha_stream_lab.txt.)
 __device__ __forceinline__ bool stream_wait(gu32* prog, uint32_t want, gu32* tmo) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spins = 0;; ++spins) {
         if (uint32_t(__builtin_amdgcn_readfirstlane(prog_read(prog))) == want) return true;
-        if ((spins & 63) == 0 &&
-            __builtin_amdgcn_readfirstlane(__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
-            return false;
-        if (spins > SHA_STREAM_SPIN_LIMIT) {
-            __hip_atomic_store(tmo, kShaStreamTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
+        if ((spins & 63) == 0) {
+            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0)
+                return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > SHA_STREAM_WAIT_TICKS) {
+                __hip_atomic_store(tmo, kShaStreamTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
         }
         __builtin_amdgcn_s_sleep(2);
     }
