@@ -125,9 +125,14 @@ class Encode:
 
     bound = "hbm"
 
-    def __init__(self, torch, ctx, dev, sh, k, m, S, n, label, seed):
+    def __init__(self, torch, ctx, dev, sh, k, m, S, n, label, seed, streams=1):
         self.torch, self.ctx, self.sh = torch, ctx, sh
         self.k, self.m, self.S, self.n = k, m, S, n
+        # streams > 1 (BENCH_ENCODE_STREAMS, lab): the batch as that many
+        # launches over consecutive object ranges on their own streams,
+        # joined on the bench's stream.
+        self.main = torch.cuda.ExternalStream(sh, device=dev)
+        self.streams = [self.main] if streams <= 1 else [torch.cuda.Stream(device=dev) for _ in range(streams)]
         g = torch.Generator(device=dev).manual_seed(seed)
         self.data = torch.empty((n, k, S), dtype=torch.uint8, device=dev)
         for o in range(n):  # per object keeps the randint temporary small
@@ -141,8 +146,19 @@ class Encode:
 
     def step(self):
         k, m, S = self.k, self.m, self.S
-        self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), k * S, S,
-                                       self.parity.data_ptr(), m * S, S, stream=self.sh)
+        if len(self.streams) == 1:
+            self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), k * S, S,
+                                           self.parity.data_ptr(), m * S, S, stream=self.sh)
+            return
+        ns = len(self.streams)
+        for st in self.streams:
+            st.wait_stream(self.main)
+        for i, st in enumerate(self.streams):
+            a, b = self.n * i // ns, self.n * (i + 1) // ns
+            self.ctx.encode_strided_device(k, m, S, b - a, self.data[a].data_ptr(), k * S, S,
+                                           self.parity[a].data_ptr(), m * S, S, stream=st.cuda_stream)
+        for st in self.streams:
+            self.main.wait_stream(st)
 
     def spot_check(self):
         import numpy as np
@@ -536,7 +552,7 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank, workers=8):
         n = n_objects or 1024
         return Encode(torch, ctx, dev, sh, 4, 2, 10 << 20, n,
                       f"RS encode k=4 m=2, chunk_size=10485760 B, {n} objects per GPU, device-resident "
-                      "(BASELINE configs[1])", seed)
+                      "(BASELINE configs[1])", seed, int(os.environ.get("BENCH_ENCODE_STREAMS", "1")))
     if cfg == "3":
         return Reconstruct(torch, ctx, dev, sh, n_objects or 1024, seed)
     if cfg == "3c":
@@ -593,6 +609,7 @@ def probe_lib():
     for fn, args in (("mxprobe_copy", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
                      ("mxprobe_read2_write1", [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]),
                      ("mxprobe_read", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+                     ("mxprobe_write", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
                      ("mxprobe_rs_pattern", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p])):
         getattr(lib, fn).argtypes = args

@@ -11,6 +11,7 @@
 //   mxprobe_read2_write1  read 2n bytes (two sources), write n (2:1, the
 //                      encode stream of k=4 m=2 and k=8 m=4)
 //   mxprobe_read       read n bytes                            (read-only)
+//   mxprobe_write      write n bytes (policy 0 nontemporal, 1 plain)
 //   mxprobe_rs_pattern the RS kernel's own access pattern with the GF math
 //                      replaced by XOR: object-major [n][k][S] in,
 //                      [n][m][S] out, tiles of 256 lanes x 16 B x 4 vectors,
@@ -63,6 +64,16 @@ __global__ __launch_bounds__(256) void probe_read(const u32x4* __restrict__ s, u
     }
     for (; i < n; i += stride) acc ^= __builtin_nontemporal_load(s + i);
     if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) sink[0] = acc;  // keeps the loads; never true for the probe's data
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void probe_write(u32x4* __restrict__ d, uint64_t n) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    const u32x4 v = {blockIdx.x, threadIdx.x, 0x5A5A5A5Au, 0xA5A5A5A5u};
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += stride) {
+        if (NT) __builtin_nontemporal_store(v, d + i);
+        else d[i] = v;
+    }
 }
 
 template <int R>
@@ -132,6 +143,18 @@ extern "C" int mxprobe_read(const void* src, uint64_t bytes, void* sink16, void*
         return int(hipErrorInvalidValue);
     hipLaunchKernelGGL(probe_read, dim3(grid()), dim3(256), 0, static_cast<hipStream_t>(stream),
                        static_cast<const u32x4*>(src), static_cast<u32x4*>(sink16), bytes / 16);
+    return int(hipGetLastError());
+}
+
+extern "C" int mxprobe_write(void* dst, uint64_t bytes, int policy, void* stream) {
+    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || policy < 0 || policy > 1)
+        return int(hipErrorInvalidValue);
+    if (policy == 0)
+        hipLaunchKernelGGL(probe_write<true>, dim3(grid()), dim3(256), 0, static_cast<hipStream_t>(stream),
+                           static_cast<u32x4*>(dst), bytes / 16);
+    else
+        hipLaunchKernelGGL(probe_write<false>, dim3(grid()), dim3(256), 0, static_cast<hipStream_t>(stream),
+                           static_cast<u32x4*>(dst), bytes / 16);
     return int(hipGetLastError());
 }
 
