@@ -7,10 +7,13 @@
 // only parallelism is across messages: one lane per chunk.  A lane streams its
 // own message 64 bytes at a time with four global_load_dwordx4, prefetching the
 // next block while compressing the current one.  The 64 rounds are fully
-// unrolled (K in literals), the schedule rolls through 16 VGPRs, rotates are
-// v_alignbit_b32, Ch / Maj are v_bfi_b32.  Workgroups are one wave so the
-// waves of a batch spread over all SIMDs; the kernel is VALU-latency bound per
-// message (see DESIGN.md for the roofline), not HBM-bound.
+// unrolled (K from SGPRs), the schedule rolls through 16 VGPRs, rotates are
+// v_alignbit_b32, Σ/σ XOR3, Ch and Maj are one v_bitop3_b32 each (14 VALU per
+// round).  Three forms: one wave per 64 messages, the split (producer /
+// consumer) form for latency-bound batches, and the persistent stream form for
+// batches of more groups than the chip has SIMDs (below).  Per message the
+// work is a VALU-latency chain (see DESIGN.md for the roofline), not
+// HBM-bound.
 #include <cstdlib>
 #include <cstring>
 
@@ -309,27 +312,27 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
 }
 
 // ---------------------------------------------------------------------------
-// Stream form for batches with more 64-message groups than the chip has SIMDs
-// (e.g. config 3c: eight concurrent 10 240-chunk verifications = 1 280 groups
-// on 1 024 SIMDs).  Whole-chain scheduling ends with the SIMDs that hold two
-// groups running at half speed while the rest idle (81 920 x 1 MiB: 87.6 ms
-// split form vs 53.3 for 65 536).  Here a group's chain is cut into segments
-// of kShaSegBlocks blocks; persistent one-wave workgroups (one per SIMD, or
-// two) take (group, segment) items from a counter in segment-major order, so
-// a SIMD that finishes early takes the next segment of some other group and
-// the load evens out to within one segment.
+// Stream form for batches with more 64-message groups than 3/4 of the chip's
+// SIMDs (e.g. config 3c: eight concurrent 10 240-chunk verifications = 1 280
+// groups on 1 024 SIMDs).  Whole-chain scheduling ends with the SIMDs that
+// hold two groups running at half speed while the rest idle (81 920 x 1 MiB:
+// 78-96 ms split form vs 53 for 65 536).  Here a group's chain is cut into
+// segments of kShaSegBlocks blocks; persistent waves (one per SIMD, four per
+// workgroup so each lands on its own SIMD) take (group, segment) items from a
+// counter in segment-major order, so a SIMD that finishes early takes the next
+// segment of some other group and the load evens out to within one segment.
 //
 // Hand-off between the waves that run consecutive segments of a group
 // (MI355X_MICROARCH.md, visibility; cdna_hip_programming.md Guideline 16,
 // recipe R1): each lane stores its 8 state words with agent-scope relaxed
-// atomic stores (write-through), the wave drains them (vmcnt(0)), then lane
-// 0 stores the group's progress word (agent-scope relaxed); the next wave's
-// lane 0 polls that word relaxed with s_sleep, bounded, then one agent
-// acquire, then the lanes read the state with agent-scope loads.  Item t's
-// predecessor is item t - groups, taken earlier by a resident wave, so every
-// wait ends; a wave that still waits ~4 s gives up, leaves
-// kShaStreamTimeout in work[1] and every other wave drains the queue without
-// hashing (the host checks the word).
+// atomic stores (write-through), the wave drains them (vmcnt(0)), then every
+// lane stores the same value to the group's progress word (agent-scope
+// relaxed); the next wave polls that word with all lanes (relaxed, s_sleep,
+// bounded), then one agent acquire, then the lanes read the state with
+// agent-scope loads.  Item t's predecessor is item t - groups, taken earlier
+// by a resident wave, so every wait ends; a wave that still waits 4 s
+// (s_memrealtime) gives up, leaves kShaStreamTimeout in work[1] and every
+// other wave drains the queue without hashing (the host checks the word).
 // ---------------------------------------------------------------------------
 typedef uint32_t __attribute__((address_space(1))) gu32;
 

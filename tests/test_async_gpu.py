@@ -101,3 +101,32 @@ def test_close_drains_queued_calls():
     for t in tickets:
         assert t.done()
         assert t.wait() == want
+
+
+def test_async_storage_errors_and_ticket_lifecycle(ctx, tmp_path):
+    """File-layer errors come back on the ticket with the blocking call's
+    code and message (GET of a missing object: the manifest read fails,
+    −40; PUT into a path whose parent is a file: −40), the eventfd is not
+    readable before completion and is after, and a ticket freed without a
+    wait (close) still waits for its call first."""
+    g = ctx.get_object_chunked_async(str(tmp_path / "missing.ec"), 1024)
+    with pytest.raises(maxio_amd.RSError) as ei:
+        g.wait()
+    assert ei.value.code == -40
+    blocker = tmp_path / "file"
+    blocker.write_bytes(b"x")
+    p = ctx.put_object_chunked_async(str(blocker / "obj.ec"), 4096, 2, np.zeros(10000, np.uint8))
+    with pytest.raises(maxio_amd.RSError) as ei:
+        p.wait()
+    assert ei.value.code == -40
+    rng = np.random.default_rng(83)
+    bufs = [rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes() for _ in range(4)]
+    t = ctx.sha256_async(bufs)
+    r, _, _ = select.select([t.fd], [], [], 0)
+    if not t.done():  # a 1 MiB chain takes ~29 ms: normally still running here
+        assert not r, "eventfd readable before the call completed"
+    r, _, _ = select.select([t.fd], [], [], 120)
+    assert r and t.done()
+    assert t.wait() == [hashlib.sha256(b).digest() for b in bufs]
+    t2 = ctx.sha256_async(bufs)
+    t2.close()  # frees only after the call finished; no crash, no leak of the fd
