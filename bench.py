@@ -680,28 +680,41 @@ def valu_bound_GBps(form: str, n_cus: int) -> float:
     return lane_ops / SHA_VALU_PER_BLOCK[form] * 64 / 1e9
 
 
+# RS decode (R = 2) VALU lane-ops per input byte, from PMC: config 2's
+# rs_apply_fast<2,4,true> retires 2.84e9 wave-instructions x 64 lanes per
+# launch over 42.9 GB of input (profiles/r2_pmc_valu.json).
+RS_R2_VALU_PER_INPUT_BYTE = 4.24
+
+
 def stream_step_roofline(ms: float, workers: int, n: int, n_cus: int) -> dict:
-    """Config 3c's step against its bound: every present shard hashed in one
-    combined stream-form launch at the INT32-VALU ceiling, then the decodes
-    (read 8, write 2 shards per object) at HBM peak -- the step's digests
-    decide what the decodes rebuild, and the next step's hashes read what
-    they wrote, so the two phases are serial.  frac_hash_only sets the whole
-    step against the hashing bound alone."""
+    """Config 3c's step against its bound.  The step hashes every present
+    shard (one combined stream-form launch) and rebuilds 2 of 12 shards per
+    object; the rebuild runs speculatively beside the hash (capi.cpp), so the
+    two share the SIMDs: the bound is the larger of the step's INT32-VALU
+    work (hash lane-ops per block x blocks + decode lane-ops per input byte x
+    input bytes) at the chip's issue rate and its HBM traffic at 8 TB/s.
+    frac_hash_only sets the step against the hash's VALU time alone."""
     S = float(1 << 20)
     hashed = workers * n * 10 * S
-    decoded = workers * n * 10 * S
-    vb = valu_bound_GBps("stream", n_cus)
-    bound_ms = hashed / (vb * 1e9) * 1e3 + decoded / (HBM_PEAK_GBPS * 1e9) * 1e3
-    sha_GBps = hashed / (ms * 1e-3) / 1e9
-    return {"bound": "valu+hbm", "kernel": "sha256_stream_kernel (combined) + rs_apply_fast<R=2> x workers",
+    dec_in = workers * n * 8 * S  # the decode reads 8 shards, writes 2
+    traffic = hashed + workers * n * 10 * S
+    lane_ops_s = n_cus * 4 * VALU_LANES_PER_SIMD_CYCLE * CLOCK_GHZ * 1e9
+    hash_ms = hashed / 64 * SHA_VALU_PER_BLOCK["stream"] / lane_ops_s * 1e3
+    dec_ms = dec_in * RS_R2_VALU_PER_INPUT_BYTE / lane_ops_s * 1e3
+    hbm_ms = traffic / (HBM_PEAK_GBPS * 1e9) * 1e3
+    bound_ms = max(hash_ms + dec_ms, hbm_ms)
+    return {"bound": "valu", "kernel": "sha256_stream_kernel (combined) + rs_apply_fast<R=2> x workers beside it",
             "achieved_ms_per_step": round(ms, 2), "bound_ms_per_step": round(bound_ms, 2),
             "frac": round(bound_ms / ms, 4),
-            "hash_GBps_over_step": round(sha_GBps, 1), "valu_bound_GBps_hashed": round(vb, 1),
-            "frac_hash_only": round(sha_GBps / vb, 4),
+            "hash_valu_ms": round(hash_ms, 2), "decode_valu_ms": round(dec_ms, 2), "hbm_ms": round(hbm_ms, 2),
+            "frac_hash_only": round(hash_ms / ms, 4),
+            "hash_GBps_over_step": round(hashed / (ms * 1e-3) / 1e9, 1),
             "valu_lane_ops_per_block": SHA_VALU_PER_BLOCK["stream"],
-            "what": (f"{workers} x {n} objects 8+4 x 1 MiB per step: {hashed / 1e9:.1f} GB hashed at the "
-                     f"INT32-VALU bound ({vb:.0f} GB/s) + {decoded / 1e9:.1f} GB decode traffic at "
-                     f"{HBM_PEAK_GBPS:.0f} GB/s, serial")}
+            "decode_valu_lane_ops_per_input_byte": RS_R2_VALU_PER_INPUT_BYTE,
+            "valu_peak_lane_ops_per_s": lane_ops_s,
+            "what": (f"{workers} x {n} objects 8+4 x 1 MiB per step: {hashed / 1e9:.1f} GB hashed + "
+                     f"{dec_in / 1e9:.1f} GB decoded on the INT32 VALU (the decode runs beside the hash), "
+                     f"{traffic / 1e9:.1f} GB of HBM traffic")}
 
 
 def hbm_block(alg_bytes: float, ms: float, kernel: str, cal: dict, ratio_key: str) -> dict:

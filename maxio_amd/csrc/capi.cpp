@@ -450,6 +450,52 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
         for (int i = 0; i < total; ++i)
             len[size_t(i)] = shard_len ? std::min<uint64_t>(shard_len[i], shard_size) : shard_size;
         auto shard_ptr = [&](uint64_t o, int i) { return shards + o * obj_stride + uint64_t(i) * shard_stride; };
+        const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
+        std::vector<int32_t> st(static_cast<size_t>(n_obj), MXEC_OK);
+        // Rebuild `objs` from the present mask as it stands: one decode plan
+        // per object, one launch per number of shards to rebuild; rebuilt
+        // shards become present, an object short of k shards gets
+        // MXEC_E_TOO_FEW_SHARDS_PRESENT in st.
+        auto rebuild = [&](const std::vector<uint64_t>& objs) -> int {
+            std::map<int, std::vector<uint64_t>> groups;
+            std::vector<std::shared_ptr<const DecodePlan>> plans(objs.size());
+            std::vector<uint32_t> offs(objs.size());
+            for (size_t t = 0; t < objs.size(); ++t) {
+                const uint64_t o = objs[t];
+                MXEC_TRY(decode_plan(*ds.d, k, m, present + o * total, data_only, &plans[t], &offs[t]));
+                st[o] = plans[t] ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
+                if (plans[t] && !plans[t]->missing.empty()) groups[int(plans[t]->missing.size())].push_back(t);
+            }
+            for (auto& g : groups) {
+                const int r = g.first;
+                const size_t n = g.second.size();
+                std::vector<const uint8_t*> in(n * k);
+                std::vector<uint64_t> il(n * k), ol(n * r);
+                std::vector<uint8_t*> out(n * r);
+                std::vector<RsObject> ro(n);
+                for (size_t u = 0; u < n; ++u) {
+                    const size_t t = g.second[u];
+                    const uint64_t o = objs[t];
+                    const DecodePlan& p = *plans[t];
+                    for (int v = 0; v < k; ++v) {
+                        in[u * k + v] = shard_ptr(o, p.valid[size_t(v)]);
+                        il[u * k + v] = len[size_t(p.valid[size_t(v)])];
+                    }
+                    for (int e = 0; e < r; ++e) {
+                        out[u * r + e] = shard_ptr(o, p.missing[size_t(e)]);
+                        ol[u * r + e] = len[size_t(p.missing[size_t(e)])];
+                    }
+                    ro[u] = RsObject{&in[u * k], &il[u * k], &out[u * r], &ol[u * r], offs[t]};
+                }
+                MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, r, ro));
+                for (size_t t : g.second)
+                    for (int e : plans[t]->missing) present[objs[t] * total + e] = 1;
+            }
+            return MXEC_OK;
+        };
+        std::vector<uint64_t> all(static_cast<size_t>(n_obj));
+        for (uint64_t o = 0; o < n_obj; ++o) all[o] = o;
+        bool rebuilt = false;
         if (expected_sha_dev) {
             std::vector<const uint8_t*> ptrs;
             std::vector<uint64_t> lens;
@@ -485,68 +531,60 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 // A small batch: hashed by the device's combiner together with
                 // every concurrent caller's verification (combiner.cpp), once
                 // the work queued on `stream` has produced the shards; digests
-                // compared on the host.
-                // The combined launch waits on the device for the work
-                // already on `stream` (an event), so the host does not wait
-                // here first; the expected digests travel meanwhile.
+                // compared on the host.  The combined launch waits for that
+                // work on the device (an event recorded here), not the host.
+                //
+                // Speculative rebuild: the decode from the present mask as
+                // given is queued right behind that event, so it runs beside
+                // the hash instead of after it (the hash is a VALU-bound
+                // chain, the decode an HBM stream).  It reads only present
+                // shards and writes only missing ones, which the hash does not
+                // read.  Objects whose digests all match keep it -- exactly
+                // what verify-then-rebuild produces; an object with a
+                // mismatch is rebuilt again from its original mask minus the
+                // mismatched shards, over the same output shards, in stream
+                // order (chunk_reader.rs:176-211 semantics).  An object that
+                // ends up short of k shards may have its missing shards
+                // overwritten by the speculative decode.
                 const size_t ne = size_t(n_obj) * size_t(total) * 32;
                 MXEC_TRY(slot.hdig.ensure(ne));
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, expected_sha_dev, ne, hipMemcpyDeviceToHost, s));
+                if (!slot.ready_ev) MXEC_HIP(hipEventCreateWithFlags(&slot.ready_ev, hipEventDisableTiming));
+                MXEC_HIP(hipEventRecord(slot.ready_ev, s));
+                const std::vector<uint8_t> orig(present, present + n_obj * uint64_t(total));
+                // Queued by the combiner's leader right after the hash launch,
+                // so the host work of the plans does not hold back the hash
+                // (or this caller's arrival with it).
+                const std::function<int()> spec = [&] { return rebuild(all); };
+                rebuilt = true;
                 std::vector<uint8_t> dig(ptrs.size() * 32);
-                MXEC_TRY(sha256_combined(*ds.d, slot, s, ptrs, lens, dig.data()));
-                MXEC_TRY(slot_wait(*ds.slot, s));  // the digest copy (long done)
+                MXEC_TRY(sha256_combined(*ds.d, slot, s, ptrs, lens, dig.data(), slot.ready_ev, &spec));
+                MXEC_TRY(slot_wait(*ds.slot, s));  // the digest copy (long done), the speculative decode
                 const auto* exph = static_cast<const uint8_t*>(slot.hdig.p);
+                std::vector<uint64_t> redo;
+                for (size_t t = 0; t < idx.size(); ++t) {
+                    if (std::memcmp(&dig[t * 32], exph + idx[t] * 32, 32) == 0) continue;
+                    const uint64_t o = idx[t] / uint64_t(total);
+                    if (redo.empty() || redo.back() != o) {
+                        redo.push_back(o);  // idx ascends: objects arrive in order
+                        std::memcpy(present + o * total, &orig[o * total], size_t(total));
+                    }
+                }
                 for (size_t t = 0; t < idx.size(); ++t)
                     if (std::memcmp(&dig[t * 32], exph + idx[t] * 32, 32) != 0) present[idx[t]] = 0;
+                MXEC_TRY(rebuild(redo));
             }
         }
-        const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
+        if (!rebuilt) MXEC_TRY(rebuild(all));
         int first_err = MXEC_OK;
-        // Group objects by (number of shards to rebuild); each object keeps
-        // its own decode table.
-        std::map<int, std::vector<uint64_t>> groups;
-        std::vector<std::shared_ptr<const DecodePlan>> plans(static_cast<size_t>(n_obj));
-        std::vector<uint32_t> offs(static_cast<size_t>(n_obj));
         for (uint64_t o = 0; o < n_obj; ++o) {
-            const uint8_t* pr = present + o * total;
-            int st = MXEC_OK;
-            MXEC_TRY(decode_plan(*ds.d, k, m, pr, data_only, &plans[o], &offs[o]));
-            if (!plans[o]) {
-                st = MXEC_E_TOO_FEW_SHARDS_PRESENT;
-                if (first_err == MXEC_OK) {
-                    int np = 0;
-                    for (int i = 0; i < total; ++i) np += pr[i] != 0;
-                    first_err = st;
-                    set_error(st, too_few_msg(np, k, total));
-                }
-            } else if (!plans[o]->missing.empty()) {
-                groups[int(plans[o]->missing.size())].push_back(o);
+            if (status_out) status_out[o] = st[o];
+            if (st[o] != MXEC_OK && first_err == MXEC_OK) {
+                int np = 0;
+                for (int i = 0; i < total; ++i) np += present[o * total + i] != 0;
+                first_err = st[o];
+                set_error(first_err, too_few_msg(np, k, total));
             }
-            if (status_out) status_out[o] = st;
-        }
-        for (auto& g : groups) {
-            const int r = g.first;
-            const size_t n = g.second.size();
-            std::vector<const uint8_t*> in(n * k);
-            std::vector<uint64_t> il(n * k), ol(n * r);
-            std::vector<uint8_t*> out(n * r);
-            std::vector<RsObject> ro(n);
-            for (size_t t = 0; t < n; ++t) {
-                const uint64_t o = g.second[t];
-                const DecodePlan& p = *plans[o];
-                for (int v = 0; v < k; ++v) {
-                    in[t * k + v] = shard_ptr(o, p.valid[size_t(v)]);
-                    il[t * k + v] = len[size_t(p.valid[size_t(v)])];
-                }
-                for (int e = 0; e < r; ++e) {
-                    out[t * r + e] = shard_ptr(o, p.missing[size_t(e)]);
-                    ol[t * r + e] = len[size_t(p.missing[size_t(e)])];
-                }
-                ro[t] = RsObject{&in[t * k], &il[t * k], &out[t * r], &ol[t * r], offs[o]};
-            }
-            MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, r, ro));
-            for (uint64_t o : g.second)
-                for (int e : plans[o]->missing) present[o * total + e] = 1;
         }
         return first_err;
     });

@@ -19,10 +19,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <functional>
 
 #include "ops.hpp"
 
 namespace mxec {
+
+bool combine_log();
 
 struct ShaCombiner {
     struct Req {
@@ -30,6 +33,12 @@ struct ShaCombiner {
         const std::vector<uint64_t>* lens = nullptr;
         uint8_t* out = nullptr;  // host, n * 32
         hipEvent_t ready = nullptr;  // on the caller's stream: its messages are complete
+        // Run by the leader right after the hash launch is queued, before it
+        // waits for the digests (the caller is blocked meanwhile, so its slot
+        // and stream are free to use): work that should run beside the hash.
+        const std::function<int()>* after_launch = nullptr;
+        int after_rc = MXEC_OK;
+        std::string after_msg;
         int rc = MXEC_OK;
         std::string msg;
         bool done = false;
@@ -89,6 +98,25 @@ struct ShaCombiner {
         const uint32_t* tmo = nullptr;
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr, nullptr,
                          nullptr, sha_stream_size((n + 63) / 64, uint64_t(d.n_cus) * 4) ? 0 : 2, &tmo));
+        // The callers' work to run beside the hash is queued before this
+        // launch's digest copy: copies of different streams can share a copy
+        // engine queue in submission order, and work queued behind the
+        // digest copy (which waits for the hash) would wait for the hash too
+        // -- the speculative decodes' descriptor uploads did, measured.
+        const auto ta = std::chrono::steady_clock::now();
+        for (Req* r : batch) {
+            if (!r->after_launch) continue;
+            try {
+                r->after_rc = (*r->after_launch)();
+            } catch (...) {
+                r->after_rc = set_error(MXEC_E_OOM, "host allocation failed");
+            }
+            if (r->after_rc) r->after_msg = last_error();
+        }
+        if (combine_log())
+            std::fprintf(stderr, "[mxec combine] after-launch work %lld us\n",
+                         (long long)std::chrono::duration_cast<std::chrono::microseconds>(
+                             std::chrono::steady_clock::now() - ta).count());
         MXEC_TRY(slot.hdig.ensure(n * 32 + 16));
         auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + n * 32);
         *hflag = 0;
@@ -147,10 +175,14 @@ long gather_idle_us() {
 }
 // MXEC_COMBINE_LOG=1: one stderr line per combined launch (requests,
 // messages, gathering and launch times) -- for tuning the windows above.
+}  // namespace
+
 bool combine_log() {
     static const bool on = env_us("MXEC_COMBINE_LOG", 0) != 0;
     return on;
 }
+
+namespace {
 
 // MXEC_COMBINE_STREAMS: launches in flight per device (default 2).  A second
 // launch starts beside a running one only while both together stay under
@@ -201,7 +233,8 @@ ShaCombiner* combiner_of(Device& d) {
 }  // namespace
 
 int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
-                    const std::vector<uint64_t>& lens, uint8_t* out) {
+                    const std::vector<uint64_t>& lens, uint8_t* out, hipEvent_t ready,
+                    const std::function<int()>* after_launch) {
     if (ptrs.empty()) return MXEC_OK;
     if (!sha_combines(ptrs.size())) {
         // Opted out by MXEC_COMBINE_BELOW: its own launch on the caller's
@@ -211,6 +244,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
         MXEC_TRY(slot.hdig.ensure(n * 32));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
+        if (after_launch) MXEC_TRY((*after_launch)());  // same stream: after the hash, not beside it
         MXEC_TRY(slot_wait(slot, s));
         std::memcpy(out, slot.hdig.p, n * 32);
         return MXEC_OK;
@@ -221,9 +255,13 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     me.ptrs = &ptrs;
     me.lens = &lens;
     me.out = out;
-    if (!slot.ready_ev) MXEC_HIP(hipEventCreateWithFlags(&slot.ready_ev, hipEventDisableTiming));
-    MXEC_HIP(hipEventRecord(slot.ready_ev, s));
-    me.ready = slot.ready_ev;
+    if (!ready) {
+        if (!slot.ready_ev) MXEC_HIP(hipEventCreateWithFlags(&slot.ready_ev, hipEventDisableTiming));
+        MXEC_HIP(hipEventRecord(slot.ready_ev, s));
+        ready = slot.ready_ev;
+    }
+    me.ready = ready;
+    me.after_launch = after_launch;
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&me);
     c->pending_msgs += ptrs.size();
@@ -309,6 +347,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         c->cv_done.notify_all();
     }
     if (me.rc) return set_error(me.rc, me.msg);
+    if (me.after_rc) return set_error(me.after_rc, me.after_msg);
     return MXEC_OK;
 }
 

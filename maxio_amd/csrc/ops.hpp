@@ -5,6 +5,7 @@
 #include <exception>
 #include <mutex>
 #include <new>
+#include <functional>
 #include <vector>
 
 #include "gf256.hpp"
@@ -48,8 +49,14 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
 // the SIMDs (sha256_kernel.hip kSplitMaxMessages).
 inline bool sha_stream_size(uint64_t groups, uint64_t simds) { return groups * 4 > simds * 3; }
 
+// `ready` (optional): an event the caller recorded on `s` when its messages
+// were complete; without one the call records it now.  `after_launch`
+// (optional) runs once the hash launch is queued, before the wait for its
+// digests -- work to queue on `s` beside the hash; its status is the call's
+// if the hash itself succeeded.
 int sha256_combined(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
-                    const std::vector<uint64_t>& lens, uint8_t* out);
+                    const std::vector<uint64_t>& lens, uint8_t* out, hipEvent_t ready = nullptr,
+                    const std::function<int()>* after_launch = nullptr);
 void combiner_stats(Device& dev, uint64_t* batches, uint64_t* messages);
 // Whether a request of n messages goes through the combiner.
 bool sha_combines(size_t n);

@@ -25,12 +25,23 @@ namespace {
 
 using namespace hashdev;
 
+// Wave priority of the hash waves.  A hash wave issues one VALU every ~4.5
+// cycles for tens of ms; decode waves sharing its SIMD (the speculative
+// rebuild beside the combined hash, capi.cpp) should take the remaining
+// issue slots rather than stretch the chain.
+__device__ __forceinline__ void sha_priority(uint32_t prio) {
+    if (prio >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (prio == 1) __builtin_amdgcn_s_setprio(1);
+}
+
 __global__ __launch_bounds__(64) void sha256_kernel(const uint8_t* const* __restrict__ ptrs,
                                                     const uint64_t* __restrict__ lens,
                                                     uint8_t* __restrict__ digests,
                                                     const uint8_t* __restrict__ expected,
                                                     const uint64_t* __restrict__ exp_idx,
-                                                    uint8_t* __restrict__ ok, uint32_t n) {
+                                                    uint8_t* __restrict__ ok, uint32_t n, uint32_t prio) {
+    sha_priority(prio);
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     if (i >= n) return;
     const uint8_t* p = ptrs[i];
@@ -184,7 +195,8 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
                                                            uint8_t* __restrict__ digests,
                                                            const uint8_t* __restrict__ expected,
                                                            const uint64_t* __restrict__ exp_idx,
-                                                           uint8_t* __restrict__ ok, uint32_t n) {
+                                                           uint8_t* __restrict__ ok, uint32_t n, uint32_t prio) {
+    sha_priority(prio);
     __shared__ u32x4 kw[2][16][64];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * 64 + lane;
@@ -384,7 +396,8 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* const
                                                            const uint64_t* __restrict__ exp_idx,
                                                            uint8_t* __restrict__ ok, uint32_t n,
                                                            uint32_t* work_p, uint32_t* state_p,
-                                                           uint32_t seg_max) {
+                                                           uint32_t seg_max, uint32_t prio) {
+    sha_priority(prio);
     gu32* work = (gu32*)(work_p);
     gu32* state = (gu32*)(state_p);
     const uint32_t lane = threadIdx.x & 63;  // every wave of a workgroup works alone
@@ -508,6 +521,12 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* const
 // profiles/r2_sha_stream_lab_sizes.jsonl).
 constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 
+// MXEC_SHA_PRIO=0..3 (lab A/B; read per launch), default 3.
+uint32_t sha_prio() {
+    const char* e = getenv("MXEC_SHA_PRIO");
+    return e ? uint32_t(atoi(e)) : 3u;
+}
+
 hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const uint32_t blocks = (a.n + 63) / 64;
@@ -523,16 +542,16 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         const uint32_t per = a.wg_waves ? a.wg_waves : 1;
         if (!a.work || !a.state || a.waves == 0 || a.seg_max == 0 || per > 4 || a.waves % per) return hipErrorInvalidValue;
         hipLaunchKernelGGL(sha256_stream_kernel, dim3(a.waves / per), dim3(64 * per), 0, s, a.ptrs, a.lens, a.digests,
-                           a.expected, a.exp_idx, a.ok, a.n, a.work, a.state, a.seg_max);
+                           a.expected, a.exp_idx, a.ok, a.n, a.work, a.state, a.seg_max, sha_prio());
         return hipGetLastError();
     }
     const bool split = form == 2;
     if (split)
         hipLaunchKernelGGL(sha256_split_kernel, dim3(blocks), dim3(128), 0, s, a.ptrs, a.lens,
-                           a.digests, a.expected, a.exp_idx, a.ok, a.n);
+                           a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
     else
         hipLaunchKernelGGL(sha256_kernel, dim3(blocks), dim3(64), 0, s, a.ptrs, a.lens, a.digests,
-                           a.expected, a.exp_idx, a.ok, a.n);
+                           a.expected, a.exp_idx, a.ok, a.n, sha_prio());
     return hipGetLastError();
 }
 
