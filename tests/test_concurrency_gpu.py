@@ -138,3 +138,77 @@ def test_combined_verify_waits_for_callers_stream_work():
             assert torch.equal(objs[w], refs[w]), w
     finally:
         ctx.close()
+
+
+def test_speculative_rebuild_matches_verify_then_rebuild():
+    """mxec_reconstruct_strided_device with expected digests rebuilds
+    speculatively beside the hash (capi.cpp); the result must equal verify-
+    then-rebuild (chunk_reader.rs:176-211) in every case: no corruption;
+    a corrupt data shard among the first k present (the speculative decode
+    used it and must be redone); a corrupt parity shard past the first k
+    (not used); two corruptions that leave exactly k; corruptions that
+    leave fewer than k (the object fails with -10, its present shards
+    untouched).  A rebuildable object must come back equal to the object
+    as encoded (the reconstruction from any k valid shards is unique), with
+    every shard present."""
+    import torch
+
+    k, m, S, n = 8, 4, 40_000 + 48, 64
+    total = k + m
+    rng = np.random.default_rng(95)
+    ctx = maxio_amd.Context(streams_per_device=2)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(96)
+        obj = torch.randint(0, 256, (n, total, S), dtype=torch.uint8, device="cuda", generator=g)
+        dig = torch.zeros((n, total, 32), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        ctx.encode_strided_device(k, m, S, n, obj.data_ptr(), total * S, S, obj[:, k:].data_ptr(), total * S, S,
+                                  digests_ptr=dig.data_ptr())
+        torch.cuda.synchronize()
+        ref = obj.clone()
+        present = np.ones(n * total, np.uint8)
+        corrupt = {}
+        for o in range(n):
+            erased = [int(x) for x in rng.choice(k, 2, replace=False)]
+            for i in erased:
+                present[o * total + i] = 0
+                obj[o, i].fill_(0x5A)
+            case = o % 5
+            live = [i for i in range(total) if i not in erased]
+            if case == 1:
+                bad = [live[0]]                       # used by the first-k decode
+            elif case == 2:
+                bad = [total - 1]                     # a parity shard past the first k
+            elif case == 3:
+                bad = [live[1], live[5]]              # leaves exactly k
+            elif case == 4:
+                bad = [live[0], live[2], live[4]]     # leaves k - 1: fails
+            else:
+                bad = []
+            for i in bad:
+                obj[o, i, 7] ^= 0x80
+            corrupt[o] = (erased, bad)
+        before = obj.clone()
+        torch.cuda.synchronize()
+        rc, status = ctx.reconstruct_strided_device(k, m, S, n, obj.data_ptr(), total * S, S, present,
+                                                    expected_ptr=dig.data_ptr())
+        torch.cuda.synchronize()
+        assert rc == -10  # the first failing object's status
+        got = obj.cpu()
+        for o in range(n):
+            erased, bad = corrupt[o]
+            row = present[o * total:(o + 1) * total]
+            if len(bad) >= 3:
+                assert status[o] == -10, o
+                # present shards untouched; the flags show the mismatches
+                for i in range(total):
+                    if i not in erased and i not in bad:
+                        assert row[i] == 1 and torch.equal(got[o, i], before[o, i].cpu()), (o, i)
+                    if i in bad:
+                        assert row[i] == 0, (o, i)
+                continue
+            assert status[o] == 0, o
+            assert row.all(), o
+            assert torch.equal(got[o], ref[o].cpu()), (o, erased, bad)
+    finally:
+        ctx.close()
