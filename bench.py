@@ -134,10 +134,19 @@ class Encode:
         self.main = torch.cuda.ExternalStream(sh, device=dev)
         self.streams = [self.main] if streams <= 1 else [torch.cuda.Stream(device=dev) for _ in range(streams)]
         g = torch.Generator(device=dev).manual_seed(seed)
-        self.data = torch.empty((n, k, S), dtype=torch.uint8, device=dev)
+        # Object-major [n][k+m][S]: each object's parity right after its data
+        # (an object's shards staged together, the layout the reconstruct
+        # configs use).  With data [n][k][S] and parity [n][m][S] as two
+        # allocations the rate followed the parity buffer's physical
+        # placement (5.25-6.29 TB/s from one allocation to the next); parity
+        # interleaved with data measured 5.85-6.08 (tools/alloc_lab.py,
+        # profiles/r2_cfg2_allocation_spread.txt).
+        self.obj = torch.empty((n, k + m, S), dtype=torch.uint8, device=dev)
         for o in range(n):  # per object keeps the randint temporary small
-            self.data[o].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
-        self.parity = torch.zeros((n, m, S), dtype=torch.uint8, device=dev)
+            self.obj[o, :k].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
+        self.obj[:, k:].zero_()
+        self.data, self.parity = self.obj[:, :k], self.obj[:, k:]
+        self.stride = (k + m) * S
         self.payload = n * k * S
         self.alg_bytes = n * (k + m) * S
         r = min(m, 8)
@@ -147,16 +156,16 @@ class Encode:
     def step(self):
         k, m, S = self.k, self.m, self.S
         if len(self.streams) == 1:
-            self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), k * S, S,
-                                           self.parity.data_ptr(), m * S, S, stream=self.sh)
+            self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), self.stride, S,
+                                           self.parity.data_ptr(), self.stride, S, stream=self.sh)
             return
         ns = len(self.streams)
         for st in self.streams:
             st.wait_stream(self.main)
         for i, st in enumerate(self.streams):
             a, b = self.n * i // ns, self.n * (i + 1) // ns
-            self.ctx.encode_strided_device(k, m, S, b - a, self.data[a].data_ptr(), k * S, S,
-                                           self.parity[a].data_ptr(), m * S, S, stream=st.cuda_stream)
+            self.ctx.encode_strided_device(k, m, S, b - a, self.data[a].data_ptr(), self.stride, S,
+                                           self.parity[a].data_ptr(), self.stride, S, stream=st.cuda_stream)
         for st in self.streams:
             self.main.wait_stream(st)
 
@@ -178,7 +187,7 @@ class Encode:
             "(crate 6.0.0 pure-Rust mul_slice restated: 64 KiB MUL_TABLE, input-major)")
 
     def drop(self):
-        del self.data, self.parity
+        del self.data, self.parity, self.obj
 
 
 class Reconstruct:
@@ -611,7 +620,10 @@ def probe_lib():
                      ("mxprobe_read", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
                      ("mxprobe_write", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
                      ("mxprobe_rs_pattern", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
-                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p])):
+                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
+                     ("mxprobe_rs_pattern_strided", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                     ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p])):
         getattr(lib, fn).argtypes = args
         getattr(lib, fn).restype = ctypes.c_int
     return lib
@@ -658,17 +670,21 @@ def calibrate(torch, dev, stream) -> dict:
     torch.cuda.empty_cache()
     # The RS kernel's own access pattern (same tile, same loads in flight,
     # 32 WG per CU) with XOR for the GF math, at the two encode shapes.
-    for k, m, S, n in ((4, 2, 10 << 20, 64), (8, 4, 1 << 20, 512)):
-        d = torch.empty((n, k, S), dtype=torch.uint8, device=dev)
-        d.random_(0, 256)
-        p = torch.empty((n, m, S), dtype=torch.uint8, device=dev)
-        ms = event_ms(torch, stream, lambda: run(lib.mxprobe_rs_pattern(d.data_ptr(), p.data_ptr(), k, m, S, n, sh)), 5)
+    # In the bench's object-major layout ([n][k+m][S], Encode), 15 / 24 GiB:
+    # a few GiB measured low (launch ramp and tail on a ~1 ms launch).
+    for k, m, S, n in ((4, 2, 10 << 20, 256), (8, 4, 1 << 20, 2048)):
+        whole = torch.empty((n, k + m, S), dtype=torch.uint8, device=dev)
+        whole.random_(0, 256)
+        st = (k + m) * S
+        ms = event_ms(torch, stream, lambda: run(lib.mxprobe_rs_pattern_strided(
+            whole.data_ptr(), whole[:, k:].data_ptr(), k, m, S, n, st, st, sh)), 5)
         out[f"rs_pattern_k{k}m{m}_GBps"] = round(n * (k + m) * S / (ms * 1e-3) / 1e9, 1)
-        del d, p
+        del whole
     out["what"] = ("libmaxio_probe.so streams, HIP-event timed, 5 launches each: copy / read2_write1 / read over 2 GiB "
                    "buffers (nontemporal global_load_dwordx4, 4 loads in flight per lane, nontemporal stores, 16 WG "
                    "x 256 lanes per CU); rs_pattern_kXmY = the RS kernel's tile and load schedule with XOR for the "
-                   "GF math, 32 WG per CU, over 3.75 GiB (k=4 m=2, 10 MiB) / 6 GiB (k=8 m=4, 1 MiB)")
+                   "GF math, 32 WG per CU, over 15 GiB (k=4 m=2, 10 MiB) / 24 GiB (k=8 m=4, 1 MiB) in the "
+                   "object-major [n][k+m][S] layout the Encode workloads use")
     torch.cuda.empty_cache()
     return out
 
@@ -818,7 +834,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     kk, mm, SS, nn = w.k, w.m, w.S, w.n
     dig = torch.empty((nn, kk + mm, 32), dtype=torch.uint8, device=dev)
     ms = event_ms(torch, stream, lambda: ctx.encode_strided_device(
-        kk, mm, SS, nn, w.data.data_ptr(), kk * SS, SS, w.parity.data_ptr(), mm * SS, SS,
+        kk, mm, SS, nn, w.data.data_ptr(), w.stride, SS, w.parity.data_ptr(), w.stride, SS,
         digests_ptr=dig.data_ptr(), stream=sh), 2)
     out["put_path_encode_plus_sha256"] = {
         "GiBps_payload": round(nn * kk * SS / GIB / (ms * 1e-3), 3), "ms": round(ms, 2),

@@ -28,6 +28,10 @@ def main() -> int:
     ap.add_argument("--alloc", default="torch", choices=["torch", "contiguous"],
                     help="torch: the caching allocator (hipMalloc); contiguous: "
                          "hipExtMallocWithFlags(hipDeviceMallocContiguous)")
+    ap.add_argument("--layout", default="separate", choices=["separate", "parity_first", "object_major"],
+                    help="separate: data [n][k][S] then parity [n][m][S] (the bench); parity_first: the "
+                         "same, parity allocated first; object_major: one [n][k+m][S] tensor, each object's "
+                         "parity after its data")
     a = ap.parse_args()
     import torch
 
@@ -82,13 +86,25 @@ def main() -> int:
 
     with maxio_amd.Context(device_mask=1, streams_per_device=2) as ctx:
         for i in range(a.allocs):
-            data, rdat = alloc((n, k, S))
-            data.random_(0, 256)
-            parity, rp = alloc((n, m, S))
+            rdat = rp = None
+            if a.layout == "object_major":
+                whole, rdat = alloc((n, k + m, S))
+                whole.random_(0, 256)
+                data, parity = whole[:, :k], whole[:, k:]
+                dstride = pstride = (k + m) * S
+            else:
+                if a.layout == "parity_first":
+                    parity, rp = alloc((n, m, S))
+                    data, rdat = alloc((n, k, S))
+                else:
+                    data, rdat = alloc((n, k, S))
+                    parity, rp = alloc((n, m, S))
+                data.random_(0, 256)
+                dstride, pstride = k * S, m * S
             torch.cuda.synchronize()
 
             def step():
-                ctx.encode_strided_device(k, m, S, n, data.data_ptr(), k * S, S, parity.data_ptr(), m * S, S,
+                ctx.encode_strided_device(k, m, S, n, data.data_ptr(), dstride, S, parity.data_ptr(), pstride, S,
                                           stream=st.cuda_stream)
 
             ms = timed(step, a.reps)
@@ -96,6 +112,14 @@ def main() -> int:
             # the same buffers under the probe streams: the RS pattern with XOR,
             # a read of the data, a copy of the parity-sized front of the data
             # into the parity (write side)
+            if a.layout == "object_major":
+                print(json.dumps({"alloc": i, "layout": a.layout, "ms": [round(x, 3) for x in ms],
+                                  "rs_TBps": round(alg / (sum(ms) / len(ms) * 1e-3) / 1e12, 3)}), flush=True)
+                del data, parity, whole
+                if rdat is not None:
+                    rdat.free()
+                torch.cuda.empty_cache()
+                continue
             pat = timed(lambda: probe.mxprobe_rs_pattern(data.data_ptr(), parity.data_ptr(), k, m, S, n,
                                                          st.cuda_stream), 3)
             rd = timed(lambda: probe.mxprobe_read(data.data_ptr(), n * k * S, sink.data_ptr(), st.cuda_stream), 3)
@@ -104,7 +128,7 @@ def main() -> int:
             wpl = timed(lambda: probe.mxprobe_write(parity.data_ptr(), n * m * S, 1, st.cuda_stream), 3)
             wdn = timed(lambda: probe.mxprobe_write(data.data_ptr(), n * m * S, 0, st.cuda_stream), 3)
             avg = lambda v: sum(v) / len(v)
-            print(json.dumps({"alloc": i, "how": a.alloc, "ms": [round(x, 3) for x in ms],
+            print(json.dumps({"alloc": i, "how": a.alloc, "layout": a.layout, "ms": [round(x, 3) for x in ms],
                               "rs_TBps": round(alg / (avg(ms) * 1e-3) / 1e12, 3),
                               "pattern_TBps": round(alg / (avg(pat) * 1e-3) / 1e12, 3),
                               "read_data_TBps": round(n * k * S / (avg(rd) * 1e-3) / 1e12, 3),
