@@ -201,3 +201,70 @@ def test_oracle_under_sanitizers(tools):
     _, oc, _ = tools
     r = subprocess.run([oc], capture_output=True, text=True, env=ENV, timeout=300)
     assert r.returncode == 0 and "oracle_check ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+def _python_verdict(text: bytes):
+    """Syntax per Python's json (RFC 8259 plus NaN / Infinity, which the
+    reader rejects): True accepted, False rejected, None no verdict."""
+    try:
+        s = text.decode("utf-8")
+    except UnicodeDecodeError:
+        return None
+    if "NaN" in s or "Infinity" in s:
+        return None
+    try:
+        json.loads(s)
+        return True
+    except RecursionError:
+        return None
+    except ValueError:
+        return False
+
+
+KNOWN = ("version", "total_size", "chunk_size", "chunk_count", "parity_shards", "shard_size", "plaintext_size")
+
+
+def test_fuzzed_manifests_no_crash_and_consistent_with_json(tools):
+    """3 000 mutants of the CASES (byte flips, deletions, insertions of JSON
+    punctuation, truncations) through the sanitized reader: no sanitizer
+    report, one verdict per input, every input Python's json rejects as JSON
+    is rejected too, and every accepted input is valid JSON whose fields are
+    the reader's values (map form)."""
+    import random
+
+    mc, _, d = tools
+    rnd = random.Random(0x6D6178)
+    seeds = [c[1].encode() if isinstance(c[1], str) else c[1] for c in CASES if len(c[1]) < 4000]
+    tokens = [b"{", b"}", b"[", b"]", b",", b":", b'"', b"\\", b"0", b"-", b"e", b"null", b"true", b"1.5",
+              b'"kind"', b'"parity"', b"\\u00", b" ", b"\n", b"\x00", b"\xff"]
+    cases = []
+    for i in range(3000):
+        t = bytearray(rnd.choice(seeds))
+        for _ in range(rnd.randint(1, 4)):
+            op = rnd.randrange(4)
+            pos = rnd.randrange(len(t) + 1)
+            if op == 0 and t:
+                t[min(pos, len(t) - 1)] ^= 1 << rnd.randrange(8)
+            elif op == 1 and t:
+                del t[min(pos, len(t) - 1): min(pos, len(t) - 1) + rnd.randint(1, 8)]
+            elif op == 2:
+                t[pos:pos] = rnd.choice(tokens)
+            else:
+                t = t[:pos]
+        cases.append((f"fz{i}", bytes(t), None))
+    out = run_cases(mc, d, cases)
+    assert len(out) == len(cases)
+    accepted = 0
+    for (name, raw, _), got in zip(cases, out):
+        verdict = _python_verdict(raw)
+        if verdict is False:
+            assert not got["ok"], (name, raw[:200], got)
+        if got["ok"]:
+            accepted += 1
+            assert verdict is not False, (name, raw[:200])
+            v = json.loads(raw.decode())
+            if isinstance(v, dict):
+                for f in KNOWN:
+                    if f in got and f in v:
+                        assert got[f] == v[f], (name, f, got[f], v[f])
+    assert accepted > 50  # the mutants do exercise the accepting paths
