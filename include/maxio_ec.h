@@ -241,7 +241,10 @@ int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs,
  * present (host, n_obj*(k+m)) in/out as in mxec_reconstruct.
  * expected_sha_dev (device, n_obj*(k+m)*32) or NULL to skip verification.
  * status_out (host, n_obj, may be NULL): 0 or MXEC_E_TOO_FEW_SHARDS_PRESENT
- * per object; the call returns the first non-zero status. */
+ * per object; the call returns the first non-zero status.  With verification
+ * the rebuild from the mask as given runs beside the hash (objects with a
+ * digest mismatch are rebuilt again), so an object that fails may have had
+ * its missing shards written. */
 int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream,
                                     int k, int m, uint64_t shard_size,
                                     uint64_t n_obj, uint8_t* shards,
@@ -249,6 +252,18 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream,
                                     const uint64_t* shard_len, uint8_t* present,
                                     const uint8_t* expected_sha_dev,
                                     uint32_t flags, int32_t* status_out);
+
+/* The completion-handle form (see mxec_ticket above): shard_len is copied at
+ * submission; present and status_out must stay valid until the ticket
+ * completes, and the shards are the caller's until then. */
+int mxec_reconstruct_strided_device_async(mxec_ctx* ctx, int dev, void* stream,
+                                          int k, int m, uint64_t shard_size,
+                                          uint64_t n_obj, uint8_t* shards,
+                                          uint64_t obj_stride, uint64_t shard_stride,
+                                          const uint64_t* shard_len, uint8_t* present,
+                                          const uint8_t* expected_sha_dev,
+                                          uint32_t flags, int32_t* status_out,
+                                          mxec_ticket** ticket);
 
 /* SHA-256 of n device buffers (host arrays of device pointers and lengths)
  * into digests_dev (device, n*32). */

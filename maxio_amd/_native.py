@@ -154,6 +154,9 @@ _SIGS = {
                                             ctypes.POINTER(ctypes.c_void_p)]),
     "mxec_get_object_chunked_async": (INT, [P, ctypes.c_char_p, U64, U64, P, U64, U64P,
                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "mxec_reconstruct_strided_device_async": (
+        INT, [P, INT, P, INT, INT, U64, U64, P, U64, U64, U64P, U8P, P, ctypes.c_uint32, I32P,
+              ctypes.POINTER(ctypes.c_void_p)]),
 }
 
 

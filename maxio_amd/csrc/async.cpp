@@ -231,6 +231,25 @@ int mxec_reconstruct_async(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8
     });
 }
 
+int mxec_reconstruct_strided_device_async(mxec_ctx* ctx, int dev, void* stream, int k, int m, uint64_t shard_size,
+                                          uint64_t n_obj, uint8_t* shards, uint64_t obj_stride, uint64_t shard_stride,
+                                          const uint64_t* shard_len, uint8_t* present,
+                                          const uint8_t* expected_sha_dev, uint32_t flags, int32_t* status_out,
+                                          mxec_ticket** ticket) {
+    return guarded([&] {
+        if (int rc = mxec_rs_check(k, m)) return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
+        if (shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+        if (n_obj && (!shards || !present)) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        auto sl = copy_n(shard_len, size_t(k + m));
+        const bool has_sl = shard_len != nullptr;
+        return submit(ctx, ticket, [=] {
+            return mxec_reconstruct_strided_device(ctx, dev, stream, k, m, shard_size, n_obj, shards, obj_stride,
+                                                   shard_stride, has_sl ? sl.data() : nullptr, present,
+                                                   expected_sha_dev, flags, status_out);
+        });
+    });
+}
+
 int mxec_put_object_chunked_async(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
                                   const uint8_t* body, size_t len, mxec_ticket** ticket) {
     return guarded([&] {

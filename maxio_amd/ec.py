@@ -353,6 +353,21 @@ class Context:
             expected_ptr, DATA_ONLY if data_only else 0, status.ctypes.data_as(N.I32P))
         return rc, status[:n_obj]
 
+    def reconstruct_strided_device_async(self, k, m, shard_size, n_obj, shards_ptr, obj_stride,
+                                         shard_stride, present: np.ndarray, shard_len=None,
+                                         expected_ptr=None, data_only=False, dev=0,
+                                         stream=None) -> "Ticket":
+        """The completion-handle form: `present` is updated in place when the
+        ticket completes; wait() returns the per-object status array."""
+        assert present.dtype == np.uint8 and present.size == n_obj * (k + m)
+        status = np.zeros(max(1, n_obj), np.int32)
+        sl = _u64p(shard_len) if shard_len is not None else None
+        args = (self._h, dev, stream, k, m, shard_size, n_obj, shards_ptr, obj_stride, shard_stride, sl,
+                present.ctypes.data_as(N.U8P), expected_ptr, DATA_ONLY if data_only else 0,
+                status.ctypes.data_as(N.I32P))
+        return self._submit(self._lib.mxec_reconstruct_strided_device_async, args, (present, status, sl),
+                            lambda: status[:n_obj])
+
     def sha256_batch_device(self, ptrs, lens, digests_ptr, dev=0, stream=None):
         _check(self._lib.mxec_sha256_batch_device(
             self._h, dev, stream, _pp(ptrs), _u64p(lens), len(ptrs), digests_ptr))

@@ -130,3 +130,39 @@ def test_async_storage_errors_and_ticket_lifecycle(ctx, tmp_path):
     assert t.wait() == [hashlib.sha256(b).digest() for b in bufs]
     t2 = ctx.sha256_async(bufs)
     t2.close()  # frees only after the call finished; no crash, no leak of the fd
+
+
+def test_reconstruct_strided_device_async_matches_blocking(ctx):
+    """mxec_reconstruct_strided_device_async (the device verify + rebuild a
+    GPU-direct GET stream calls, chunk_reader.rs:176-211) gives the blocking
+    call's present flags, statuses and rebuilt bytes; its argument errors
+    answer before queueing."""
+    import torch
+
+    k, m, S, n = 8, 4, 65536, 96
+    total = k + m
+    g = torch.Generator(device="cuda").manual_seed(97)
+    obj = torch.randint(0, 256, (n, total, S), dtype=torch.uint8, device="cuda", generator=g)
+    dig = torch.zeros((n, total, 32), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    ctx.encode_strided_device(k, m, S, n, obj.data_ptr(), total * S, S, obj[:, k:].data_ptr(), total * S, S,
+                              digests_ptr=dig.data_ptr())
+    torch.cuda.synchronize()
+    ref = obj.clone()
+    rng = np.random.default_rng(98)
+    present = np.ones(n * total, np.uint8)
+    for o in range(n):
+        for i in rng.choice(total, 3, replace=False):
+            present[o * total + i] = 0
+            obj[o, i].zero_()
+        obj[o, int(rng.integers(0, total)), 9] ^= 1  # may hit an erased shard: harmless
+    torch.cuda.synchronize()
+    t = ctx.reconstruct_strided_device_async(k, m, S, n, obj.data_ptr(), total * S, S, present,
+                                             expected_ptr=dig.data_ptr())
+    status = t.wait()
+    torch.cuda.synchronize()
+    assert (status == 0).all() and present.all()
+    assert torch.equal(obj, ref)
+    with pytest.raises(maxio_amd.RSError) as ei:
+        ctx.reconstruct_strided_device_async(0, 2, S, 1, obj.data_ptr(), total * S, S, np.ones(2, np.uint8))
+    assert ei.value.code == -3  # TooFewDataShards from the crate's guard, no ticket
