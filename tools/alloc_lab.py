@@ -32,6 +32,8 @@ def main() -> int:
                     help="separate: data [n][k][S] then parity [n][m][S] (the bench); parity_first: the "
                          "same, parity allocated first; object_major: one [n][k+m][S] tensor, each object's "
                          "parity after its data")
+    ap.add_argument("--pad", type=int, default=0,
+                    help="object_major only: bytes of padding after each shard (shard stride S + pad)")
     a = ap.parse_args()
     import torch
 
@@ -87,11 +89,13 @@ def main() -> int:
     with maxio_amd.Context(device_mask=1, streams_per_device=2) as ctx:
         for i in range(a.allocs):
             rdat = rp = None
+            sstride = S
             if a.layout == "object_major":
-                whole, rdat = alloc((n, k + m, S))
+                sstride = S + a.pad
+                whole, rdat = alloc((n, k + m, sstride))
                 whole.random_(0, 256)
                 data, parity = whole[:, :k], whole[:, k:]
-                dstride = pstride = (k + m) * S
+                dstride = pstride = (k + m) * sstride
             else:
                 if a.layout == "parity_first":
                     parity, rp = alloc((n, m, S))
@@ -104,8 +108,8 @@ def main() -> int:
             torch.cuda.synchronize()
 
             def step():
-                ctx.encode_strided_device(k, m, S, n, data.data_ptr(), dstride, S, parity.data_ptr(), pstride, S,
-                                          stream=st.cuda_stream)
+                ctx.encode_strided_device(k, m, S, n, data.data_ptr(), dstride, sstride, parity.data_ptr(), pstride,
+                                          sstride, stream=st.cuda_stream)
 
             ms = timed(step, a.reps)
             alg = n * (k + m) * S
@@ -113,7 +117,7 @@ def main() -> int:
             # a read of the data, a copy of the parity-sized front of the data
             # into the parity (write side)
             if a.layout == "object_major":
-                print(json.dumps({"alloc": i, "layout": a.layout, "ms": [round(x, 3) for x in ms],
+                print(json.dumps({"alloc": i, "layout": a.layout, "pad": a.pad, "ms": [round(x, 3) for x in ms],
                                   "rs_TBps": round(alg / (sum(ms) / len(ms) * 1e-3) / 1e12, 3)}), flush=True)
                 del data, parity, whole
                 if rdat is not None:
