@@ -141,12 +141,19 @@ class Encode:
         # placement (5.25-6.29 TB/s from one allocation to the next); parity
         # interleaved with data measured 5.85-6.08 (tools/alloc_lab.py,
         # profiles/r2_cfg2_allocation_spread.txt).
-        self.obj = torch.empty((n, k + m, S), dtype=torch.uint8, device=dev)
+        # Multi-MiB shard slots are padded by 2 MiB + 64 KiB, so an object's
+        # slots start at different offsets modulo 2 MiB: on one box the
+        # unpadded layout fell to 5.2 TB/s on 2 of 8 allocations and the
+        # padded one on none; elsewhere the pad measured +1 %
+        # (profiles/r2_shard_pad_spread.txt).
+        self.pad = (2 << 20) + (64 << 10) if S >= (4 << 20) else 0
+        self.sstride = S + self.pad
+        self.obj = torch.empty((n, k + m, self.sstride), dtype=torch.uint8, device=dev)
         for o in range(n):  # per object keeps the randint temporary small
-            self.obj[o, :k].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
+            self.obj[o, :k, :S].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
         self.obj[:, k:].zero_()
-        self.data, self.parity = self.obj[:, :k], self.obj[:, k:]
-        self.stride = (k + m) * S
+        self.data, self.parity = self.obj[:, :k, :S], self.obj[:, k:, :S]
+        self.stride = (k + m) * self.sstride
         self.payload = n * k * S
         self.alg_bytes = n * (k + m) * S
         r = min(m, 8)
@@ -156,16 +163,17 @@ class Encode:
     def step(self):
         k, m, S = self.k, self.m, self.S
         if len(self.streams) == 1:
-            self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), self.stride, S,
-                                           self.parity.data_ptr(), self.stride, S, stream=self.sh)
+            self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), self.stride, self.sstride,
+                                           self.parity.data_ptr(), self.stride, self.sstride, stream=self.sh)
             return
         ns = len(self.streams)
         for st in self.streams:
             st.wait_stream(self.main)
         for i, st in enumerate(self.streams):
             a, b = self.n * i // ns, self.n * (i + 1) // ns
-            self.ctx.encode_strided_device(k, m, S, b - a, self.data[a].data_ptr(), self.stride, S,
-                                           self.parity[a].data_ptr(), self.stride, S, stream=st.cuda_stream)
+            self.ctx.encode_strided_device(k, m, S, b - a, self.data[a].data_ptr(), self.stride, self.sstride,
+                                           self.parity[a].data_ptr(), self.stride, self.sstride,
+                                           stream=st.cuda_stream)
         for st in self.streams:
             self.main.wait_stream(st)
 
@@ -623,7 +631,8 @@ def probe_lib():
                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
                      ("mxprobe_rs_pattern_strided", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
-                                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p])):
+                                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                     ctypes.c_void_p])):
         getattr(lib, fn).argtypes = args
         getattr(lib, fn).restype = ctypes.c_int
     return lib
@@ -677,7 +686,7 @@ def calibrate(torch, dev, stream) -> dict:
         whole.random_(0, 256)
         st = (k + m) * S
         ms = event_ms(torch, stream, lambda: run(lib.mxprobe_rs_pattern_strided(
-            whole.data_ptr(), whole[:, k:].data_ptr(), k, m, S, n, st, st, sh)), 5)
+            whole.data_ptr(), whole[:, k:].data_ptr(), k, m, S, n, st, st, S, sh)), 5)
         out[f"rs_pattern_k{k}m{m}_GBps"] = round(n * (k + m) * S / (ms * 1e-3) / 1e9, 1)
         del whole
     out["what"] = ("libmaxio_probe.so streams, HIP-event timed, 5 launches each: copy / read2_write1 / read over 2 GiB "
@@ -700,7 +709,7 @@ def pattern_on_buffers(torch, stream, w) -> float:
     if k % 4 or m not in (1, 2, 4) or S % 16384:
         return None
     ms = event_ms(torch, stream, lambda: lib.mxprobe_rs_pattern_strided(
-        w.data.data_ptr(), w.parity.data_ptr(), k, m, S, n, w.stride, w.stride, stream.cuda_stream), 5)
+        w.data.data_ptr(), w.parity.data_ptr(), k, m, S, n, w.stride, w.stride, w.sstride, stream.cuda_stream), 5)
     return round(n * (k + m) * S / (ms * 1e-3) / 1e9, 1)
 
 
@@ -852,7 +861,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     kk, mm, SS, nn = w.k, w.m, w.S, w.n
     dig = torch.empty((nn, kk + mm, 32), dtype=torch.uint8, device=dev)
     ms = event_ms(torch, stream, lambda: ctx.encode_strided_device(
-        kk, mm, SS, nn, w.data.data_ptr(), w.stride, SS, w.parity.data_ptr(), w.stride, SS,
+        kk, mm, SS, nn, w.data.data_ptr(), w.stride, w.sstride, w.parity.data_ptr(), w.stride, w.sstride,
         digests_ptr=dig.data_ptr(), stream=sh), 2)
     out["put_path_encode_plus_sha256"] = {
         "GiBps_payload": round(nn * kk * SS / GIB / (ms * 1e-3), 3), "ms": round(ms, 2),

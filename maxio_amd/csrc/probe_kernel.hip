@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void probe_write(u32x4* __restrict__ d, uint64
 template <int R>
 __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
                                                      uint32_t k, uint64_t S, uint64_t n_obj, uint64_t dstride,
-                                                     uint64_t pstride) {
+                                                     uint64_t pstride, uint64_t sstride) {
     constexpr uint64_t kTile = 256 * 16 * 4;
     const uint64_t tpo = S / kTile, n_tiles = tpo * n_obj;
     for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__
 #pragma unroll
                 for (int v = 0; v < 4; ++v)
                     x[jj][v] = __builtin_nontemporal_load(
-                        reinterpret_cast<const u32x4*>(data + o * dstride + (j + jj) * S + base + v * 4096));
+                        reinterpret_cast<const u32x4*>(data + o * dstride + (j + jj) * sstride + base + v * 4096));
 #pragma unroll
             for (int v = 0; v < 4; ++v)
 #pragma unroll
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__
         for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int v = 0; v < 4; ++v)
-                __builtin_nontemporal_store(acc[v][i], reinterpret_cast<u32x4*>(par + o * pstride + i * S + base + v * 4096));
+                __builtin_nontemporal_store(acc[v][i], reinterpret_cast<u32x4*>(par + o * pstride + i * sstride + base + v * 4096));
     }
 }
 
@@ -160,12 +160,12 @@ extern "C" int mxprobe_write(void* dst, uint64_t bytes, int policy, void* stream
 }
 
 // k a multiple of 4, m in {1, 2, 4}, S a multiple of 16 KiB; object o's
-// shards at data + o * data_obj_stride (+ j * S) and parity + o *
-// parity_obj_stride (+ i * S): [n][k][S] / [n][m][S] with strides k*S / m*S,
-// or one object-major [n][k+m][S] buffer with both strides (k+m)*S.
+// shard j at data + o * data_obj_stride + j * shard_stride (parity likewise):
+// [n][k][S] / [n][m][S] with strides k*S / m*S and S, or one object-major
+// [n][k+m][shard_stride] buffer with both object strides (k+m)*shard_stride.
 extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32_t k, uint32_t m, uint64_t S,
                                           uint64_t n_obj, uint64_t data_obj_stride, uint64_t parity_obj_stride,
-                                          void* stream) {
+                                          uint64_t shard_stride, void* stream) {
     if (k == 0 || (k & 3) || S == 0 || (S % 16384) ||
         ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
         return int(hipErrorInvalidValue);
@@ -173,15 +173,15 @@ extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32
     const auto* in = static_cast<const uint8_t*>(data);
     auto* out = static_cast<uint8_t*>(parity);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const uint64_t ds = data_obj_stride, ps = parity_obj_stride;
-    if (m == 1) hipLaunchKernelGGL(probe_pattern<1>, g, b, 0, s, in, out, k, S, n_obj, ds, ps);
-    else if (m == 2) hipLaunchKernelGGL(probe_pattern<2>, g, b, 0, s, in, out, k, S, n_obj, ds, ps);
-    else if (m == 4) hipLaunchKernelGGL(probe_pattern<4>, g, b, 0, s, in, out, k, S, n_obj, ds, ps);
+    const uint64_t ds = data_obj_stride, ps = parity_obj_stride, ss = shard_stride;
+    if (m == 1) hipLaunchKernelGGL(probe_pattern<1>, g, b, 0, s, in, out, k, S, n_obj, ds, ps, ss);
+    else if (m == 2) hipLaunchKernelGGL(probe_pattern<2>, g, b, 0, s, in, out, k, S, n_obj, ds, ps, ss);
+    else if (m == 4) hipLaunchKernelGGL(probe_pattern<4>, g, b, 0, s, in, out, k, S, n_obj, ds, ps, ss);
     else return int(hipErrorInvalidValue);
     return int(hipGetLastError());
 }
 
 extern "C" int mxprobe_rs_pattern(const void* data, void* parity, uint32_t k, uint32_t m, uint64_t S, uint64_t n_obj,
                                   void* stream) {
-    return mxprobe_rs_pattern_strided(data, parity, k, m, S, n_obj, uint64_t(k) * S, uint64_t(m) * S, stream);
+    return mxprobe_rs_pattern_strided(data, parity, k, m, S, n_obj, uint64_t(k) * S, uint64_t(m) * S, S, stream);
 }
