@@ -841,10 +841,11 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     # -- config 3c: 8 concurrent batches -----------------------------------
     rs = ReconstructStream(torch, ctx, dev, sh, 1024, 8, SEED)
     torch.cuda.synchronize()
-    rs.step()
+    for _ in range(2):  # the first steps gather and place unevenly
+        rs.step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    reps = 3
+    reps = 6
     for _ in range(reps):
         rs.step()
     torch.cuda.synchronize()
