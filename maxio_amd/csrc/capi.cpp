@@ -558,7 +558,14 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 const std::function<int()> spec = [&] { return rebuild(all); };
                 rebuilt = true;
                 std::vector<uint8_t> dig(ptrs.size() * 32);
-                MXEC_TRY(sha256_combined(*ds.d, slot, s, ptrs, lens, dig.data(), slot.ready_ev, &spec));
+                if (int hrc = sha256_combined(*ds.d, slot, s, ptrs, lens, dig.data(), slot.ready_ev, &spec)) {
+                    // No verdict: the mask goes back as it came (the speculative
+                    // rebuild may already have marked shards present).
+                    const std::string msg = last_error();
+                    std::memcpy(present, orig.data(), orig.size());
+                    (void)slot_wait(*ds.slot, s);  // the speculative decode, if queued
+                    return set_error(hrc, msg);
+                }
                 MXEC_TRY(slot_wait(*ds.slot, s));  // the digest copy (long done), the speculative decode
                 const auto* exph = static_cast<const uint8_t*>(slot.hdig.p);
                 std::vector<uint64_t> redo;
