@@ -352,12 +352,21 @@ class Mixed:
                 last = int(rng.integers(1, S))  # short last chunk, zero padded
                 dl = [S] * (k - 1) + [last]
                 pres = np.ones(n * (k + m), np.uint8)
+                lens = dl + [S] * m
+                # Algorithmic bytes, exactly: the encode reads the k data
+                # chunks (the last one short) and writes m parity; the
+                # reconstruct reads the first k present shards and writes the
+                # e missing ones (1 <= e <= m).
+                alg += n * (sum(dl) + m * S)
                 for o in range(n):
-                    for i in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False):
+                    miss = rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False)
+                    for i in miss:
                         pres[o * (k + m) + i] = 0
+                    row = pres[o * (k + m): (o + 1) * (k + m)]
+                    used = [i for i in range(k + m) if row[i]][:k]
+                    alg += sum(lens[i] for i in used) + sum(lens[i] for i in miss)
                 self.classes.append((k, m, S, n, t, dl, pres))
                 payload += n * ((k - 1) * S + last) * 2  # encoded + decoded
-                alg += n * (k + m) * S * 2
         self.payload, self.alg_bytes = payload, alg
         self.kernel = "rs_apply_fast (mixed R) + edge tiles"
         self.name = ("mixed 4+2 / 8+4 / 10+4 at 64 KiB-10 MiB chunks, short last chunks: encode then "
