@@ -22,8 +22,8 @@ struct RsArgs {
     const uint64_t* out_len;        // [n_obj][r_total]
     const uint32_t* coef;           // tables, [j][i][8] per matrix (gf256.hpp)
     const uint32_t* coef_off;       // [n_obj] dword offset of object's table
-    const uint64_t* edge_list;      // [n_edge] object << 32 | tile: tiles a
-                                    //   length boundary or the shard end cuts
+    const uint64_t* edge_list;      // [n_edge] object << 32 | tile: every tile
+                                    //   of an unaligned launch (edge kernel)
     uint64_t n_edge;
     uint64_t edge_tile_bytes;       // tile size the list was built for
     uint64_t shard_size;

@@ -92,8 +92,6 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     if (objs.empty() || r == 0) return MXEC_OK;
     const size_t n = objs.size();
     DescWriter w(slot, arena);
-    // Tiles a length boundary or the shard end cuts (or all tiles when a
-    // pointer is unaligned) go to the byte-exact edge kernel.
     const uint64_t tile = rs_tile_bytes(rs_default_variant(uint32_t(r)));
     const uint64_t tiles_per_obj = (shard_size + tile - 1) / tile;
     bool aligned = true;
@@ -101,27 +99,12 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
         for (int j = 0; j < k; ++j) aligned &= (reinterpret_cast<uintptr_t>(objs[o].in[j]) & 15) == 0;
         for (int i = 0; i < r; ++i) aligned &= (reinterpret_cast<uintptr_t>(objs[o].out[i]) & 15) == 0;
     }
+    // Aligned launches handle length boundaries inside the fast kernel; an
+    // unaligned pointer sends every tile to the byte-exact edge kernel.
     std::vector<uint64_t> edges;
-    std::vector<uint64_t> cut;
-    for (size_t o = 0; o < n; ++o) {
-        if (!aligned) {
+    if (!aligned)
+        for (size_t o = 0; o < n; ++o)
             for (uint64_t t = 0; t < tiles_per_obj; ++t) edges.push_back(uint64_t(o) << 32 | t);
-            continue;
-        }
-        // Boundaries at a tile multiple (or at the shard end) cut nothing.
-        cut.clear();
-        auto mark = [&](uint64_t len) {
-            if (len < shard_size && len % tile) cut.push_back(len / tile);
-        };
-        if (shard_size % tile) cut.push_back(shard_size / tile);
-        for (int j = 0; j < k; ++j) mark(objs[o].in_len[j]);
-        for (int i = 0; i < r; ++i) mark(objs[o].out_len[i]);
-        if (cut.size() > 1) {
-            std::sort(cut.begin(), cut.end());
-            cut.erase(std::unique(cut.begin(), cut.end()), cut.end());
-        }
-        for (uint64_t t : cut) edges.push_back(uint64_t(o) << 32 | t);
-    }
     const size_t o_in = w.add(sizeof(void*) * n * k);
     const size_t o_out = w.add(sizeof(void*) * n * r);
     const size_t o_inlen = w.add(8 * n * k);

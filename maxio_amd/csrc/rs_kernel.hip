@@ -21,11 +21,11 @@
 //    nontemporal hint (every byte is touched once).
 //  * Zero padding (the crate pads the short last chunk, filesystem.rs:1111)
 //    is never materialised: in the fast kernel an input whose length ends at
-//    or before a tile contributes zero and is not loaded; only the few tiles
-//    that a length boundary cuts through take the byte-exact edge path, from
-//    a per-launch list built by the host (run_rs) -- as the first items of
-//    the same grid-stride launch when every pointer is aligned, as a launch
-//    of their own otherwise.
+//    or before a tile contributes zero and is not loaded; a tile that a
+//    length boundary cuts through masks that shard's vectors at the boundary
+//    in the same pass.  Launches with an unaligned pointer run the
+//    byte-exact edge kernel over every tile instead (a per-launch tile list
+//    built by the host, run_rs).
 #include "kernels.hpp"
 
 namespace mxec {
@@ -164,9 +164,8 @@ __device__ __forceinline__ void gstore16(gptr p, const uint32_t (&w)[4]) {
     else *q = v;
 }
 
-// Edge tiles: the list entries (object << 32 | fast tile index) are the fast
-// tiles that a length boundary or the shard end cuts through, or every tile
-// when a pointer is unaligned.  Each is walked in kEdgeTile steps with
+// Edge tiles (launches with an unaligned pointer): the list entries
+// (object << 32 | tile index) are every tile of every object.  Each is walked in kEdgeTile steps with
 // byte-exact bounds on every input and output.  One step:
 template <int R>
 __device__ __forceinline__ void edge_step(
@@ -252,43 +251,56 @@ __global__ __launch_bounds__(kThreads) void rs_apply_edge(
                      steps_per_tile, tile_bytes, aligned, step);
 }
 
-// Fast tiles: every tile of every object that no length boundary cuts
-// through (those are in the edge list and skipped here).  An input whose
-// length ends at or before the tile reads as zero without a load; an output
-// whose length ends there is not stored.  All pointers 16-byte aligned.
+// Inputs and outputs that a length boundary cuts inside a tile (the short
+// last data chunk, its decoded copy, a shard end that is not a tile
+// multiple).  `valid` is a lane's count of bytes below the length from the
+// start of its 16-byte vector (<= 0: none, >= 16: all).  A vector with at
+// least one valid byte is loaded whole -- it is 16-byte aligned, so it lies
+// in the page of its first byte -- and the bytes at or past the length are
+// zeroed; a vector with none reads a safe dummy address, so every load
+// stays unconditional and counted.
+__device__ __forceinline__ Vec4 mask_tail(Vec4 x, int32_t valid) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int32_t nb = valid - 4 * w;
+        const uint32_t mk = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * nb)));
+        x.w[w] &= mk;
+    }
+    return x;
+}
+
+template <bool NT>
+__device__ __forceinline__ Vec4 gload16_upto(gcptr p, int32_t valid, gcptr safe) {
+    return mask_tail(gload16<NT>(valid > 0 ? p : safe), valid);
+}
+
+// Every tile of every object, 16-byte aligned pointers.  An input whose
+// length ends at or before the tile reads as zero without a load, an output
+// whose length ends there is not stored; a tile that a length boundary cuts
+// through takes the masked loads / stores above for the cut shard only, in
+// the same pass (config 5's short last chunks put one such tile in every
+// object: a quarter of all tiles at 64 KiB chunks).
 template <int R, int V, bool NT>
 __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
     const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
-    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles,
-    const uint64_t* __restrict__ edge_list, uint64_t n_edge_steps) {
+    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles) {
     constexpr uint32_t kTile = kThreads * 16 * V;
-    // The edge steps come first in the grid-stride order, so they run side
-    // by side with the interior tiles instead of as a launch of their own
-    // (a few hundred latency-bound steps after the interior kernel drained:
-    // ~11 % of config 5's kernel time).
-    uint64_t item = blockIdx.x;
-    for (; item < n_edge_steps; item += gridDim.x)
-        edge_step<R>(in_ptrs, out_ptrs, in_len, out_len, coef, coef_off, shard_size, k, r_total, row0, edge_list,
-                     uint32_t(kTile / kEdgeTile), kTile, 1u, item);
-    for (uint64_t tile = item - n_edge_steps; tile < n_tiles; tile += gridDim.x) {
+    const gcptr safe = (gcptr)(reinterpret_cast<const uint8_t*>(coef));
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const uint32_t obj = uint32_t(tile / tiles_per_obj);
         const uint64_t base = (tile - uint64_t(obj) * tiles_per_obj) * kTile;
         const uint64_t end = base + kTile;
+        // Lengths are clamped to shard_size by the host, so a tile past the
+        // shard end is cut by the same tests.
         const uint64_t* __restrict__ il = in_len + uint64_t(obj) * k;
         const uint64_t* __restrict__ ol = out_len + uint64_t(obj) * r_total + row0;
-        // Wave-uniform: skip tiles cut by a boundary (edge kernel's job).
-        bool cut = end > shard_size;
-        for (uint32_t j = 0; j < k; ++j) cut |= il[j] > base && il[j] < end;
-#pragma unroll
-        for (int i = 0; i < R; ++i) cut |= ol[i] > base && ol[i] < end;
-        if (cut) continue;
-
         const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
         const uint8_t* const* __restrict__ ip = in_ptrs + uint64_t(obj) * k;
         uint8_t* const* __restrict__ op = out_ptrs + uint64_t(obj) * r_total + row0;
         const uint64_t lane = base + threadIdx.x * 16;
+        const int32_t lane_off = int32_t(threadIdx.x * 16);
 
         uint32_t acc[V][4][R];
 #pragma unroll
@@ -298,13 +310,32 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
 #pragma unroll
                 for (int i = 0; i < R; ++i) acc[v][w][i] = 0;
 
+        // Input jj of a group: whole (the common case), zero, or cut.
+        auto load_in = [&](uint32_t jj, Vec4 (&x)[V]) {
+            const uint64_t len = il[jj];
+            gcptr p = ((gcptr)(ip[jj])) + lane;
+            if (len >= end) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) x[v] = gload16<NT>(p + v * kThreads * 16);
+            } else if (len <= base) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) x[v] = Vec4{{0, 0, 0, 0}};
+            } else {
+                const int32_t d = int32_t(len - base) - lane_off;
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    x[v] = gload16_upto<NT>(p + v * kThreads * 16, d - v * int32_t(kThreads * 16), safe);
+            }
+        };
+
         uint32_t j = 0;
         for (; j + 4 <= k; j += 4) {
             Vec4 x[4][V];
             // Wave-uniform: all four inputs reach past this tile (every tile
-            // but the few past a short last chunk).  The common case loads
-            // unconditionally; the per-input select would zero 4V registers
-            // and branch around every load, one VALU per input dword.
+            // but the few at or past a short last chunk).  The common case
+            // loads unconditionally; the per-input select would zero 4V
+            // registers and branch around every load, one VALU per input
+            // dword.
             if (il[j] >= end && il[j + 1] >= end && il[j + 2] >= end && il[j + 3] >= end) {
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {
@@ -314,13 +345,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
                 }
             } else {
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    gcptr p = ((gcptr)(ip[j + jj])) + lane;
-                    const bool live = il[j + jj] >= end;  // else ends at/before base: zero
-#pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        x[jj][v] = live ? gload16<NT>(p + v * kThreads * 16) : Vec4{{0, 0, 0, 0}};
-                }
+                for (int jj = 0; jj < 4; ++jj) load_in(j + jj, x[jj]);
             }
             if constexpr (R >= 3) {
                 mac_column_pair<R, V>(acc, x[0], x[1], tab + (j + 0) * r_total * 8, tab + (j + 1) * r_total * 8);
@@ -331,21 +356,31 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
             }
         }
         for (; j < k; ++j) {
-            if (il[j] < end) continue;  // zero column: contributes nothing
+            if (il[j] <= base) continue;  // zero column: contributes nothing
             Vec4 x[V];
-            gcptr p = ((gcptr)(ip[j])) + lane;
-#pragma unroll
-            for (int v = 0; v < V; ++v) x[v] = gload16<NT>(p + v * kThreads * 16);
+            load_in(j, x);
             mac_column<R, V>(acc, x, tab + j * r_total * 8);
         }
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-            if (ol[i] < end) continue;  // output ends at/before base
+            const uint64_t olen = ol[i];
+            if (olen <= base) continue;  // output ends at/before base
             gptr o = ((gptr)(op[i])) + lane;
+            const int32_t d = olen >= end ? int32_t(kTile) : int32_t(olen - base) - lane_off;
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 uint32_t ov[4] = {acc[v][0][i], acc[v][1][i], acc[v][2][i], acc[v][3][i]};
-                gstore16<NT>(o + v * kThreads * 16, ov);
+                if (olen >= end) {
+                    gstore16<NT>(o + v * kThreads * 16, ov);
+                } else {
+                    const int32_t valid = d - v * int32_t(kThreads * 16);
+                    if (valid >= 16) {
+                        gstore16<NT>(o + v * kThreads * 16, ov);
+                    } else if (valid > 0) {  // the one straddling lane
+                        for (int b = 0; b < valid; ++b)
+                            o[v * kThreads * 16 + b] = uint8_t(ov[b >> 2] >> (8 * (b & 3)));
+                    }
+                }
             }
         }
     }
@@ -354,23 +389,20 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
 template <int R, int V, bool NT>
 hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
-    const uint64_t n_edge_steps = a.n_edge * (uint64_t(kThreads) * 16 * V / kEdgeTile);
     hipLaunchKernelGGL((rs_apply_fast<R, V, NT>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                        a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.shard_size,
-                       a.k, a.r_total, a.row0, tiles_per_obj, n_tiles, a.edge_list, n_edge_steps);
+                       a.k, a.r_total, a.row0, tiles_per_obj, n_tiles);
     return hipGetLastError();
 }
 
 template <int R>
 hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& var) {
     const uint64_t tile = rs_tile_bytes(var);
-    if (a.n_edge && a.edge_tile_bytes != tile) return hipErrorInvalidValue;  // list built for another tile
-    if (a.aligned) {
+    if (a.aligned) {  // cut tiles run inside the fast kernel; no edge list
         const uint32_t tiles_per_obj = uint32_t((a.shard_size + tile - 1) / tile);
         const uint64_t n_tiles = uint64_t(tiles_per_obj) * a.n_obj;
-        const uint64_t n_items = n_tiles + a.n_edge * (tile / kEdgeTile);
         uint64_t blocks = uint64_t(n_cus) * uint64_t(var.blocks_per_cu);
-        if (blocks > n_items) blocks = n_items;
+        if (blocks > n_tiles) blocks = n_tiles;
         hipError_t e = hipErrorInvalidValue;
         if (var.vecs == 1) e = var.nt ? launch_fast<R, 1, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                       : launch_fast<R, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
@@ -378,8 +410,9 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
                                            : launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                            : launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
-        return e;  // edge steps ran inside the fast launch
+        return e;
     }
+    if (a.n_edge && a.edge_tile_bytes != tile) return hipErrorInvalidValue;  // list built for another tile
     if (a.n_edge) {
         const uint32_t steps = uint32_t(tile / kEdgeTile);
         const uint64_t n_steps = a.n_edge * steps;
