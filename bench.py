@@ -21,6 +21,8 @@ Other BASELINE configs (same JSON line, for DESIGN.md / profiles):
   4b  encode k=64 m=4, 1 MiB chunks (literal 64 MiB objects), 640 per GPU
   5   mixed 4+2 / 8+4 / 10+4 at 64 KiB..10 MiB chunks with short last chunks:
       encode the batch, then reconstruct it with seeded erasures, per step
+      (one mixed-shape batch call each way; BENCH_MIXED_MODE=streams: the
+      classes as separate calls on four streams)
 
 One process per GPU; objects are partitioned per GPU (weak scaling, no
 collective on the data path; only the timing barrier / max-reduce).  Rank 0
@@ -333,12 +335,16 @@ class Mixed:
 
     bound = "hbm"
 
-    def __init__(self, torch, ctx, dev, sh, budget, seed, streams=4):
+    def __init__(self, torch, ctx, dev, sh, budget, seed, streams=4, mode="streams"):
+        import ctypes
+
         import numpy as np
 
         self.torch, self.ctx, self.sh = torch, ctx, sh
+        self.mode = mode
         self.main = torch.cuda.ExternalStream(sh, device=dev)
-        self.streams = [self.main] if streams <= 1 else [torch.cuda.Stream(device=dev) for _ in range(streams)]
+        self.streams = [self.main] if streams <= 1 or mode == "batch" else \
+            [torch.cuda.Stream(device=dev) for _ in range(streams)]
         rng = np.random.default_rng(seed)
         kms = [(4, 2), (8, 4), (10, 4)]
         sizes = [64 << 10, 256 << 10, 1 << 20, 4 << 20, 10 << 20]
@@ -372,8 +378,42 @@ class Mixed:
         self.name = ("mixed 4+2 / 8+4 / 10+4 at 64 KiB-10 MiB chunks, short last chunks: encode then "
                      f"reconstruct (1..m erasures), {sum(c[3] for c in self.classes)} objects per GPU "
                      "(BASELINE configs[4], per GPU)")
+        if mode == "batch":
+            # Every object of every class in ONE mxec_encode_batch_device and
+            # ONE mxec_reconstruct_batch_device call per step (grouped launches:
+            # one per m, one per erasure count), arrays built once.
+            from maxio_amd import _native as N
+
+            objs, dptr, pptr, dlen, sptr, slen, pres = [], [], [], [], [], [], []
+            for (k, m, S, n, t, dl, pr) in self.classes:
+                base, ss, os_ = t.data_ptr(), S, (k + m) * S
+                for o in range(n):
+                    objs.append(N.Object(k, m, S))
+                    dptr += [base + o * os_ + j * ss for j in range(k)]
+                    pptr += [base + o * os_ + (k + i) * ss for i in range(m)]
+                    dlen += dl
+                    sptr += [base + o * os_ + i * ss for i in range(k + m)]
+                    slen += dl + [S] * m
+                pres.append(pr)
+            self.b_objs = (N.Object * len(objs))(*objs)
+            self.b_dptr = (ctypes.c_void_p * len(dptr))(*dptr)
+            self.b_pptr = (ctypes.c_void_p * len(pptr))(*pptr)
+            self.b_dlen = (ctypes.c_uint64 * len(dlen))(*dlen)
+            self.b_sptr = (ctypes.c_void_p * len(sptr))(*sptr)
+            self.b_slen = (ctypes.c_uint64 * len(slen))(*slen)
+            self.b_pres = np.concatenate(pres)
+            self.kernel = "rs_apply_fast grouped (one launch per m, one per erasure count)"
+            self.name += "; one encode + one reconstruct call per step (mixed-shape batches)"
 
     def step(self):
+        if self.mode == "batch":
+            self.ctx.encode_batch_device(self.b_objs, self.b_dptr, self.b_pptr, data_len=self.b_dlen,
+                                         stream=self.sh)
+            pr = self.b_pres.copy()
+            rc, _ = self.ctx.reconstruct_batch_device(self.b_objs, self.b_sptr, pr, shard_len=self.b_slen,
+                                                      stream=self.sh)
+            assert rc == 0
+            return
         ns = len(self.streams)
         for st in self.streams:
             if st is not self.main:
@@ -599,7 +639,8 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank, workers=8):
                       f"RS encode k=64 m=4, chunk_size=1 MiB (literal 64 MiB objects), {n} objects per "
                       "GPU (BASELINE configs[3], literal reading)", seed)
     if cfg == "5":
-        return Mixed(torch, ctx, dev, sh, 24 << 30, seed, int(os.environ.get("BENCH_MIXED_STREAMS", "4")))
+        return Mixed(torch, ctx, dev, sh, 24 << 30, seed, int(os.environ.get("BENCH_MIXED_STREAMS", "4")),
+                     os.environ.get("BENCH_MIXED_MODE", "batch"))
     if cfg == "sums":
         return BodySums(torch, ctx, dev, sh, n_objects or 1024, 40 << 20, seed)
     if cfg == "frames":

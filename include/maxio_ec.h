@@ -189,8 +189,9 @@ int mxec_get_object_chunked_async(mxec_ctx* ctx, const char* ec_dir, uint64_t of
  * NULL is the HIP null (default) stream, as in other HIP libraries, so work
  * the caller queued there is ordered before ours.  Calls return after
  * enqueueing, except
- * mxec_reconstruct_strided_device which synchronises once to read the
- * verification result (the erasure pattern picks the decode matrix). */
+ * mxec_reconstruct_strided_device and mxec_reconstruct_batch_device with
+ * verification, which synchronise once to read the verdicts (the erasure
+ * pattern picks the decode matrix). */
 
 /* Uniform batch of n_obj objects, each k data + m parity shards of
  * shard_size bytes.  Object o, data shard j lives at
@@ -210,7 +211,10 @@ int mxec_encode_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
 /* General batch: object o has k[o] data and m[o] parity shards of
  * shard_size[o] bytes; the pointer arrays are host arrays of device pointers,
  * concatenated over objects (sum k, sum m entries); data_len likewise (NULL =
- * full shards).  digests_dev: sum(k+m)*32 bytes, object-major, or NULL. */
+ * full shards).  digests_dev: sum(k+m)*32 bytes, object-major, or NULL.
+ * Objects with the same m share one kernel launch whatever their k and
+ * shard size (16-byte aligned pointers, m <= 8; otherwise one launch per
+ * (k, m, shard_size)). */
 typedef struct mxec_object {
     int32_t k;
     int32_t m;
@@ -264,6 +268,24 @@ int mxec_reconstruct_strided_device_async(mxec_ctx* ctx, int dev, void* stream,
                                           const uint8_t* expected_sha_dev,
                                           uint32_t flags, int32_t* status_out,
                                           mxec_ticket** ticket);
+
+/* Mixed reconstruct batch — the counterpart of mxec_encode_batch_device for
+ * a stream of objects of different (k, m) and shard sizes (BASELINE
+ * configs[4]; try_reconstruct_data_chunk, chunk_reader.rs:157-226, per
+ * object).  shards (host array of device pointers, sum(k+m) entries,
+ * object-major), shard_len (host, sum(k+m), NULL = shard_size) and present
+ * (host, sum(k+m), in/out as in mxec_reconstruct) are concatenated over
+ * objects; expected_sha_dev (device, sum(k+m)*32) or NULL to skip
+ * verification; status_out (host, n_obj, may be NULL) as in
+ * mxec_reconstruct_strided_device.  With verification the call synchronises
+ * once to read the verdicts.  Objects of every shape that rebuild the same
+ * number of shards share one kernel launch. */
+int mxec_reconstruct_batch_device(mxec_ctx* ctx, int dev, void* stream,
+                                  const mxec_object* objs, uint64_t n_obj,
+                                  uint8_t* const* shards,
+                                  const uint64_t* shard_len, uint8_t* present,
+                                  const uint8_t* expected_sha_dev,
+                                  uint32_t flags, int32_t* status_out);
 
 /* SHA-256 of n device buffers (host arrays of device pointers and lengths)
  * into digests_dev (device, n*32). */

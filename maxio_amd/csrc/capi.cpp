@@ -23,6 +23,87 @@ std::string too_few_msg(int present, int k, int total) {
            " missing)";
 }
 
+// Runs `collect` (which takes coefficient-table offsets for a batch's
+// launches) until no arena recycle happened during it: a recycle
+// (runtime.cpp coef_offset) drops every offset handed out before it.
+template <class F>
+int with_stable_coef(Device& d, F&& collect) {
+    auto epoch = [&] {
+        std::lock_guard<std::mutex> g(d.coef_mu);
+        return d.coef_epoch;
+    };
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        const uint64_t e0 = epoch();
+        MXEC_TRY(collect());
+        if (epoch() == e0) return MXEC_OK;
+    }
+    return set_error(MXEC_E_INVALID_ARG, "the coefficient tables of one batch exceed the device's table arena");
+}
+
+// One object of a device-resident reconstruct batch (device shard pointers).
+struct BatchObj {
+    int k, m;
+    uint64_t shard_size;
+    uint8_t* const* shards;  // k + m
+    const uint64_t* len;     // k + m, clamped to shard_size
+    uint8_t* present;        // k + m, host
+};
+
+// Rebuilds objects `which` of a batch from their present masks as they stand
+// (chunk_reader.rs:190-211 per object): one decode plan per object, one launch
+// per number of shards to rebuild, shared by objects of every (k, m) and
+// shard size (run_rs_mixed).  Rebuilt shards become present; an object short
+// of k shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT in st.
+int rebuild_batch(Device& d, Slot& slot, hipStream_t s, bool data_only, const std::vector<BatchObj>& all,
+                  const std::vector<uint64_t>& which, std::vector<int32_t>& st) {
+    std::vector<std::shared_ptr<const DecodePlan>> plans(which.size());
+    std::vector<uint32_t> offs(which.size());
+    MXEC_TRY(with_stable_coef(d, [&]() -> int {
+        for (size_t t = 0; t < which.size(); ++t) {
+            const BatchObj& b = all[which[t]];
+            MXEC_TRY(decode_plan(d, b.k, b.m, b.present, data_only, &plans[t], &offs[t]));
+        }
+        return MXEC_OK;
+    }));
+    // Pointer and length tables of every rebuilt object, sized up front (the
+    // RsObjects point into them).
+    size_t n_in = 0, n_out = 0;
+    for (size_t t = 0; t < which.size(); ++t) {
+        st[which[t]] = plans[t] ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
+        if (plans[t] && !plans[t]->missing.empty()) {
+            n_in += size_t(all[which[t]].k);
+            n_out += plans[t]->missing.size();
+        }
+    }
+    std::vector<const uint8_t*> in(n_in);
+    std::vector<uint8_t*> out(n_out);
+    std::vector<uint64_t> il(n_in), ol(n_out);
+    std::map<int, std::vector<RsMixedObject>> groups;
+    size_t pi = 0, po = 0;
+    for (size_t t = 0; t < which.size(); ++t) {
+        if (!plans[t] || plans[t]->missing.empty()) continue;
+        const BatchObj& b = all[which[t]];
+        const DecodePlan& p = *plans[t];
+        const int r = int(p.missing.size());
+        for (int v = 0; v < b.k; ++v) {
+            in[pi + v] = b.shards[p.valid[size_t(v)]];
+            il[pi + v] = b.len[p.valid[size_t(v)]];
+        }
+        for (int e = 0; e < r; ++e) {
+            out[po + e] = b.shards[p.missing[size_t(e)]];
+            ol[po + e] = b.len[p.missing[size_t(e)]];
+        }
+        groups[r].push_back(RsMixedObject{b.k, b.shard_size, RsObject{&in[pi], &il[pi], &out[po], &ol[po], offs[t]}});
+        pi += size_t(b.k);
+        po += size_t(r);
+    }
+    MXEC_TRY(run_rs_mixed(d, slot, s, groups));
+    for (size_t t = 0; t < which.size(); ++t)
+        if (plans[t])
+            for (int e : plans[t]->missing) all[which[t]].present[e] = 1;
+    return MXEC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -403,19 +484,27 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_ob
             }
             for (int i = 0; i < objs[o].m; ++i) pl[pofs[o] + uint64_t(i)] = objs[o].shard_size;
         }
-        // One launch per homogeneous (k, m, shard_size) group.
-        std::map<std::tuple<int, int, uint64_t>, std::vector<uint64_t>> groups;
-        for (uint64_t o = 0; o < n_obj; ++o) groups[{objs[o].k, objs[o].m, objs[o].shard_size}].push_back(o);
-        for (auto& g : groups) {
-            const int k = std::get<0>(g.first), m = std::get<1>(g.first);
-            uint32_t off = 0;
-            MXEC_TRY(encode_coef(*ds.d, k, m, &off));
-            std::vector<RsObject> ro;
-            ro.reserve(g.second.size());
-            for (uint64_t o : g.second)
-                ro.push_back(RsObject{data + dofs[o], &dl[dofs[o]], parity + pofs[o], &pl[pofs[o]], off});
-            MXEC_TRY(run_rs(*ds.d, *ds.slot, s, std::get<2>(g.first), k, m, ro));
-        }
+        // One launch per parity count m: objects of every k and shard size
+        // share it (run_rs_mixed; unaligned or m > 8: per (k, shard_size)).
+        std::map<int, std::vector<RsMixedObject>> groups;
+        MXEC_TRY(with_stable_coef(*ds.d, [&]() -> int {
+            groups.clear();
+            std::map<std::pair<int, int>, uint32_t> offs;
+            for (uint64_t o = 0; o < n_obj; ++o) {
+                const int k = objs[o].k, m = objs[o].m;
+                auto it = offs.find({k, m});
+                if (it == offs.end()) {
+                    uint32_t off = 0;
+                    MXEC_TRY(encode_coef(*ds.d, k, m, &off));
+                    it = offs.emplace(std::make_pair(k, m), off).first;
+                }
+                groups[m].push_back(RsMixedObject{k, objs[o].shard_size,
+                                                  RsObject{data + dofs[o], &dl[dofs[o]], parity + pofs[o],
+                                                           &pl[pofs[o]], it->second}});
+            }
+            return MXEC_OK;
+        }));
+        MXEC_TRY(run_rs_mixed(*ds.d, *ds.slot, s, groups));
         if (digests_dev) {
             std::vector<const uint8_t*> ptrs;
             std::vector<uint64_t> lens;
@@ -452,46 +541,15 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
         auto shard_ptr = [&](uint64_t o, int i) { return shards + o * obj_stride + uint64_t(i) * shard_stride; };
         const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
         std::vector<int32_t> st(static_cast<size_t>(n_obj), MXEC_OK);
-        // Rebuild `objs` from the present mask as it stands: one decode plan
-        // per object, one launch per number of shards to rebuild; rebuilt
-        // shards become present, an object short of k shards gets
-        // MXEC_E_TOO_FEW_SHARDS_PRESENT in st.
+        std::vector<uint8_t*> sp(static_cast<size_t>(n_obj * total));
+        std::vector<BatchObj> bo(static_cast<size_t>(n_obj));
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            for (int i = 0; i < total; ++i) sp[o * total + i] = shard_ptr(o, i);
+            bo[o] = BatchObj{k, m, shard_size, &sp[o * total], len.data(), present + o * total};
+        }
+        // Rebuild `objs` from the present mask as it stands (rebuild_batch).
         auto rebuild = [&](const std::vector<uint64_t>& objs) -> int {
-            std::map<int, std::vector<uint64_t>> groups;
-            std::vector<std::shared_ptr<const DecodePlan>> plans(objs.size());
-            std::vector<uint32_t> offs(objs.size());
-            for (size_t t = 0; t < objs.size(); ++t) {
-                const uint64_t o = objs[t];
-                MXEC_TRY(decode_plan(*ds.d, k, m, present + o * total, data_only, &plans[t], &offs[t]));
-                st[o] = plans[t] ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
-                if (plans[t] && !plans[t]->missing.empty()) groups[int(plans[t]->missing.size())].push_back(t);
-            }
-            for (auto& g : groups) {
-                const int r = g.first;
-                const size_t n = g.second.size();
-                std::vector<const uint8_t*> in(n * k);
-                std::vector<uint64_t> il(n * k), ol(n * r);
-                std::vector<uint8_t*> out(n * r);
-                std::vector<RsObject> ro(n);
-                for (size_t u = 0; u < n; ++u) {
-                    const size_t t = g.second[u];
-                    const uint64_t o = objs[t];
-                    const DecodePlan& p = *plans[t];
-                    for (int v = 0; v < k; ++v) {
-                        in[u * k + v] = shard_ptr(o, p.valid[size_t(v)]);
-                        il[u * k + v] = len[size_t(p.valid[size_t(v)])];
-                    }
-                    for (int e = 0; e < r; ++e) {
-                        out[u * r + e] = shard_ptr(o, p.missing[size_t(e)]);
-                        ol[u * r + e] = len[size_t(p.missing[size_t(e)])];
-                    }
-                    ro[u] = RsObject{&in[u * k], &il[u * k], &out[u * r], &ol[u * r], offs[t]};
-                }
-                MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, r, ro));
-                for (size_t t : g.second)
-                    for (int e : plans[t]->missing) present[objs[t] * total + e] = 1;
-            }
-            return MXEC_OK;
+            return rebuild_batch(*ds.d, slot, s, data_only, bo, objs, st);
         };
         std::vector<uint64_t> all(static_cast<size_t>(n_obj));
         for (uint64_t o = 0; o < n_obj; ++o) all[o] = o;
@@ -591,6 +649,87 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 for (int i = 0; i < total; ++i) np += present[o * total + i] != 0;
                 first_err = st[o];
                 set_error(first_err, too_few_msg(np, k, total));
+            }
+        }
+        return first_err;
+    });
+}
+
+int mxec_reconstruct_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_object* objs,
+                                  uint64_t n_obj, uint8_t* const* shards, const uint64_t* shard_len,
+                                  uint8_t* present, const uint8_t* expected_sha_dev, uint32_t flags,
+                                  int32_t* status_out) {
+    return guarded([&] {
+        if (n_obj == 0) return MXEC_OK;
+        if (!objs || !shards || !present) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        std::vector<uint64_t> first(static_cast<size_t>(n_obj));
+        uint64_t sum = 0;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            if (int rc = rs_check(objs[o].k, objs[o].m))
+                return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
+            if (objs[o].shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+            first[o] = sum;
+            sum += uint64_t(objs[o].k + objs[o].m);
+        }
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, dev));
+        Slot& slot = *ds.slot;
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
+        std::vector<uint64_t> len(static_cast<size_t>(sum));
+        std::vector<BatchObj> bo(static_cast<size_t>(n_obj));
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            const uint64_t S = objs[o].shard_size;
+            for (int i = 0; i < objs[o].k + objs[o].m; ++i) {
+                const uint64_t g = first[o] + uint64_t(i);
+                len[g] = shard_len ? std::min<uint64_t>(shard_len[g], S) : S;
+            }
+            bo[o] = BatchObj{objs[o].k, objs[o].m, S, shards + first[o], &len[first[o]], present + first[o]};
+        }
+        if (expected_sha_dev) {
+            // Verify every present shard in one launch on `stream` (digests
+            // compared on the device against expected[global shard index]),
+            // read the flags back; a mismatch is an erasure
+            // (chunk_reader.rs:176-196).
+            std::vector<const uint8_t*> ptrs;
+            std::vector<uint64_t> lens, idx;
+            for (uint64_t g = 0; g < sum; ++g)
+                if (present[g]) {
+                    ptrs.push_back(shards[g]);
+                    lens.push_back(len[g]);
+                    idx.push_back(g);
+                }
+            if (!ptrs.empty()) {
+                MXEC_TRY(slot.digests.ensure(ptrs.size()));
+                auto* ok = static_cast<uint8_t*>(slot.digests.p);
+                const uint32_t* tmo = nullptr;
+                MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx, nullptr, 0, &tmo));
+                const size_t fo = (ptrs.size() + 15) & ~size_t(15);
+                MXEC_TRY(slot.hdig.ensure(fo + 16));
+                auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + fo);
+                *hflag = 0;
+                MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok, ptrs.size(), hipMemcpyDeviceToHost, s));
+                if (tmo) MXEC_HIP(hipMemcpyAsync(hflag, tmo, 4, hipMemcpyDeviceToHost, s));
+                MXEC_TRY(slot_wait(slot, s));
+                if (*hflag != 0)
+                    return set_error(MXEC_E_DEVICE, "SHA-256 stream kernel: a wave timed out waiting for its predecessor segment");
+                const auto* okh = static_cast<const uint8_t*>(slot.hdig.p);
+                for (size_t t = 0; t < idx.size(); ++t)
+                    if (!okh[t]) present[idx[t]] = 0;
+            }
+        }
+        std::vector<int32_t> st(static_cast<size_t>(n_obj), MXEC_OK);
+        std::vector<uint64_t> all(static_cast<size_t>(n_obj));
+        for (uint64_t o = 0; o < n_obj; ++o) all[o] = o;
+        MXEC_TRY(rebuild_batch(*ds.d, slot, s, (flags & MXEC_F_DATA_ONLY) != 0, bo, all, st));
+        int first_err = MXEC_OK;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            if (status_out) status_out[o] = st[o];
+            if (st[o] != MXEC_OK && first_err == MXEC_OK) {
+                const int total = objs[o].k + objs[o].m;
+                int np = 0;
+                for (int i = 0; i < total; ++i) np += present[first[o] + uint64_t(i)] != 0;
+                first_err = st[o];
+                set_error(first_err, too_few_msg(np, objs[o].k, total));
             }
         }
         return first_err;

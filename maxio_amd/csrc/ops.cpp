@@ -5,7 +5,9 @@
 #include "ops.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
+#include <map>
 
 #include "kernels.hpp"
 
@@ -150,6 +152,114 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     for (int row0 = 0; row0 < r; row0 += 8) {
         a.row0 = uint32_t(row0);
         a.r = uint32_t(std::min(8, r - row0));
+        MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
+    }
+    return w.finish(s);
+}
+
+int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups) {
+    // Which groups take the grouped kernel: every pointer 16-byte aligned,
+    // r <= 8, index ranges that fit its 32-bit fields.  A call that is one
+    // uniform group keeps the uniform kernel (no tile table).
+    struct Plan {
+        int r;
+        const std::vector<RsMixedObject>* objs;
+        uint64_t sum_k = 0, n_tiles = 0, tile = 0;
+        size_t o_in = 0, o_out = 0, o_inlen = 0, o_outlen = 0, o_coef = 0, o_grp = 0, o_tobj = 0;
+    };
+    std::vector<Plan> grouped;
+    std::vector<std::pair<int, const std::vector<RsMixedObject>*>> rest;
+    for (const auto& g : groups) {
+        const int r = g.first;
+        const auto& objs = g.second;
+        if (objs.empty() || r == 0) continue;
+        bool uniform = true, aligned = r <= 8;
+        Plan p{r, &objs};
+        p.tile = rs_tile_bytes(rs_default_variant(uint32_t(r)));
+        for (const RsMixedObject& ob : objs) {
+            uniform &= ob.k == objs[0].k && ob.shard_size == objs[0].shard_size;
+            p.sum_k += uint64_t(ob.k);
+            p.n_tiles += (ob.shard_size + p.tile - 1) / p.tile;
+            for (int j = 0; j < ob.k && aligned; ++j) aligned &= (reinterpret_cast<uintptr_t>(ob.o.in[j]) & 15) == 0;
+            for (int i = 0; i < r && aligned; ++i) aligned &= (reinterpret_cast<uintptr_t>(ob.o.out[i]) & 15) == 0;
+        }
+        const bool fits = objs.size() <= UINT32_MAX && p.sum_k <= UINT32_MAX && p.n_tiles <= (uint64_t(1) << 32);
+        if (aligned && fits && !(uniform && groups.size() == 1)) grouped.push_back(p);
+        else rest.emplace_back(r, &objs);
+    }
+    for (const auto& g : rest) {
+        // One launch per (k, shard_size), in order of first appearance.
+        std::map<std::pair<int, uint64_t>, std::vector<RsObject>> by;
+        std::vector<std::pair<int, uint64_t>> order;
+        for (const RsMixedObject& ob : *g.second) {
+            auto key = std::make_pair(ob.k, ob.shard_size);
+            auto& v = by[key];
+            if (v.empty()) order.push_back(key);
+            v.push_back(ob.o);
+        }
+        for (const auto& key : order) MXEC_TRY(run_rs(dev, slot, s, key.second, key.first, g.first, by[key]));
+    }
+    if (grouped.empty()) return MXEC_OK;
+    // Every grouped launch's tables in one upload: one host-to-device copy
+    // ahead of the launches instead of one between each pair of them (a
+    // copy in the stream costs ~25-50 us of idle GPU at that point).
+    DescWriter w(slot);
+    for (Plan& p : grouped) {
+        const size_t n = p.objs->size();
+        p.o_in = w.add(sizeof(void*) * p.sum_k);
+        p.o_out = w.add(sizeof(void*) * n * p.r);
+        p.o_inlen = w.add(8 * p.sum_k);
+        p.o_outlen = w.add(8 * n * p.r);
+        p.o_coef = w.add(4 * n);
+        p.o_grp = w.add(sizeof(RsGroupObj) * n);
+        p.o_tobj = w.add(4 * p.n_tiles);
+    }
+    char* hb = w.data();
+    for (const Plan& p : grouped) {
+        const int r = p.r;
+        auto** ip = reinterpret_cast<const uint8_t**>(hb + p.o_in);
+        auto** op = reinterpret_cast<uint8_t**>(hb + p.o_out);
+        auto* il = reinterpret_cast<uint64_t*>(hb + p.o_inlen);
+        auto* ol = reinterpret_cast<uint64_t*>(hb + p.o_outlen);
+        auto* co = reinterpret_cast<uint32_t*>(hb + p.o_coef);
+        auto* gr = reinterpret_cast<RsGroupObj*>(hb + p.o_grp);
+        auto* to = reinterpret_cast<uint32_t*>(hb + p.o_tobj);
+        uint64_t in0 = 0, t0 = 0;
+        for (size_t o = 0; o < p.objs->size(); ++o) {
+            const RsMixedObject& ob = (*p.objs)[o];
+            for (int j = 0; j < ob.k; ++j) {
+                ip[in0 + j] = ob.o.in[j];
+                il[in0 + j] = std::min<uint64_t>(ob.o.in_len[j], ob.shard_size);
+            }
+            for (int i = 0; i < r; ++i) {
+                op[o * r + i] = ob.o.out[i];
+                ol[o * r + i] = std::min<uint64_t>(ob.o.out_len[i], ob.shard_size);
+            }
+            co[o] = ob.o.coef_off;
+            const uint64_t nt = (ob.shard_size + p.tile - 1) / p.tile;
+            gr[o] = RsGroupObj{t0, uint32_t(in0), uint32_t(ob.k)};
+            std::fill(to + t0, to + t0 + nt, uint32_t(o));
+            in0 += uint64_t(ob.k);
+            t0 += nt;
+        }
+    }
+    char* db = nullptr;
+    MXEC_TRY(w.commit(s, &db));
+    for (const Plan& p : grouped) {
+        RsArgs a{};
+        a.in_ptrs = reinterpret_cast<const uint8_t* const*>(db + p.o_in);
+        a.out_ptrs = reinterpret_cast<uint8_t* const*>(db + p.o_out);
+        a.in_len = reinterpret_cast<const uint64_t*>(db + p.o_inlen);
+        a.out_len = reinterpret_cast<const uint64_t*>(db + p.o_outlen);
+        a.coef = static_cast<const uint32_t*>(dev.coef.p);
+        a.coef_off = reinterpret_cast<const uint32_t*>(db + p.o_coef);
+        a.n_obj = uint32_t(p.objs->size());
+        a.r = a.r_total = uint32_t(p.r);
+        a.row0 = 0;
+        a.aligned = 1;
+        a.group = reinterpret_cast<const RsGroupObj*>(db + p.o_grp);
+        a.tile_obj = reinterpret_cast<const uint32_t*>(db + p.o_tobj);
+        a.n_tiles = p.n_tiles;
         MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
     }
     return w.finish(s);

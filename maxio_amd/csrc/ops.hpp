@@ -6,6 +6,7 @@
 #include <mutex>
 #include <new>
 #include <functional>
+#include <map>
 #include <vector>
 
 #include "gf256.hpp"
@@ -28,6 +29,18 @@ struct RsObject {
 // launches in flight, see pipeline.cpp).
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
            const std::vector<RsObject>& objs, DescArena* arena = nullptr);
+
+// An object of a mixed batch: its own k and shard size.
+struct RsMixedObject {
+    int k;
+    uint64_t shard_size;
+    RsObject o;
+};
+// Applies each object's matrix, objects grouped by r (map key).  One grouped
+// launch (rs_apply_fast<GRP>) per r whose pointers are all 16-byte aligned
+// (r <= 8), their tables in one upload; otherwise one run_rs per
+// (k, shard_size).  A lone uniform group runs the uniform kernel.
+int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups);
 
 // SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be
 // null (see ShaArgs).

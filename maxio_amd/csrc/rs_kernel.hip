@@ -280,24 +280,42 @@ __device__ __forceinline__ Vec4 gload16_upto(gcptr p, int32_t valid, gcptr safe)
 // through takes the masked loads / stores above for the cut shard only, in
 // the same pass (config 5's short last chunks put one such tile in every
 // object: a quarter of all tiles at 64 KiB chunks).
-template <int R, int V, bool NT>
+//
+// GRP: a grouped launch — objects of different k and shard size that share
+// r (config 5's mixed classes, a server's batch of mixed requests) in one
+// grid: the tile's object comes from tile_obj, its k and input offset from
+// group[obj] (wave-uniform scalar loads, one 16-byte record per tile).
+template <int R, int V, bool NT, bool GRP>
 __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
-    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t shard_size,
-    uint32_t k, uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles) {
+    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint32_t k_uniform,
+    uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles,
+    const RsGroupObj* __restrict__ group, const uint32_t* __restrict__ tile_obj) {
     constexpr uint32_t kTile = kThreads * 16 * V;
     const gcptr safe = (gcptr)(reinterpret_cast<const uint8_t*>(coef));
     for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const uint32_t obj = uint32_t(tile / tiles_per_obj);
-        const uint64_t base = (tile - uint64_t(obj) * tiles_per_obj) * kTile;
+        uint32_t obj, k;
+        uint64_t base, in0;
+        if constexpr (GRP) {
+            obj = tile_obj[tile];
+            const RsGroupObj g = group[obj];
+            base = (tile - g.tile0) * kTile;
+            k = g.k;
+            in0 = g.in0;
+        } else {
+            obj = uint32_t(tile / tiles_per_obj);
+            base = (tile - uint64_t(obj) * tiles_per_obj) * kTile;
+            k = k_uniform;
+            in0 = uint64_t(obj) * k;
+        }
         const uint64_t end = base + kTile;
-        // Lengths are clamped to shard_size by the host, so a tile past the
-        // shard end is cut by the same tests.
-        const uint64_t* __restrict__ il = in_len + uint64_t(obj) * k;
+        // Lengths are clamped to the shard size by the host, so a tile past
+        // the shard end is cut by the same tests.
+        const uint64_t* __restrict__ il = in_len + in0;
         const uint64_t* __restrict__ ol = out_len + uint64_t(obj) * r_total + row0;
         const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
-        const uint8_t* const* __restrict__ ip = in_ptrs + uint64_t(obj) * k;
+        const uint8_t* const* __restrict__ ip = in_ptrs + in0;
         uint8_t* const* __restrict__ op = out_ptrs + uint64_t(obj) * r_total + row0;
         const uint64_t lane = base + threadIdx.x * 16;
         const int32_t lane_off = int32_t(threadIdx.x * 16);
@@ -386,13 +404,22 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     }
 }
 
-template <int R, int V, bool NT>
+template <int R, int V, bool NT, bool GRP = false>
 hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
-    hipLaunchKernelGGL((rs_apply_fast<R, V, NT>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
-                       a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.shard_size,
-                       a.k, a.r_total, a.row0, tiles_per_obj, n_tiles);
+    hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
+                       a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.k, a.r_total,
+                       a.row0, tiles_per_obj, n_tiles, a.group, a.tile_obj);
     return hipGetLastError();
+}
+
+// Grouped launches run the default geometry only (rs_default_variant).
+template <int R>
+hipError_t launch_grouped(const RsArgs& a, int n_cus, hipStream_t s) {
+    constexpr int V = R <= 4 ? 4 : 2;
+    uint64_t blocks = uint64_t(n_cus) * 32;
+    if (blocks > a.n_tiles) blocks = a.n_tiles;
+    return launch_fast<R, V, true, true>(a, 0, a.n_tiles, blocks, s);
 }
 
 template <int R>
@@ -462,6 +489,21 @@ hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, co
 }
 
 hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
+    if (a.group) {
+        if (!a.aligned || !a.tile_obj || a.row0 != 0 || a.r != a.r_total) return hipErrorInvalidValue;
+        if (a.n_tiles == 0) return hipSuccess;
+        switch (a.r) {
+            case 1: return launch_grouped<1>(a, n_cus, s);
+            case 2: return launch_grouped<2>(a, n_cus, s);
+            case 3: return launch_grouped<3>(a, n_cus, s);
+            case 4: return launch_grouped<4>(a, n_cus, s);
+            case 5: return launch_grouped<5>(a, n_cus, s);
+            case 6: return launch_grouped<6>(a, n_cus, s);
+            case 7: return launch_grouped<7>(a, n_cus, s);
+            case 8: return launch_grouped<8>(a, n_cus, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     return launch_rs_apply_variant(a, n_cus, s, rs_default_variant(a.r_total));
 }
 

@@ -62,8 +62,12 @@ int slot_wait(Slot& slot, hipStream_t s) {
 }
 
 void slot_destroy(Slot& slot) {
-    for (auto& rb : slot.ring)
+    for (auto& rb : slot.ring) {
         if (rb.done) (void)hipEventDestroy(rb.done);
+        if (rb.uploaded) (void)hipEventDestroy(rb.uploaded);
+    }
+    if (slot.upload) (void)hipStreamDestroy(slot.upload);
+    slot.upload = nullptr;
     for (auto& e : slot.stage_done)
         if (e) (void)hipEventDestroy(e);
     if (slot.sync_ev) (void)hipEventDestroy(slot.sync_ev);
@@ -255,7 +259,25 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
     MXEC_TRY(buf_->host.ensure(n));
     MXEC_TRY(buf_->dev.ensure(n));
     std::memcpy(buf_->host.p, tmp_.data(), tmp_.size());
-    MXEC_HIP(hipMemcpyAsync(buf_->dev.p, buf_->host.p, n, hipMemcpyHostToDevice, stream));
+    // Large tables (a mixed batch's: MiBs) go on the side stream; small ones
+    // stay in the launch stream, where the extra cross-stream wait measured
+    // no better (config 3c's per-call decodes, profiles/r2_desc_upload_ab.txt).
+    static const int mode = [] {
+        const char* e = getenv("MXEC_DESC_UPLOAD");
+        return e && !strcmp(e, "inline") ? 0 : e && !strcmp(e, "stream") ? 2 : 1;
+    }();
+    if (mode == 0 || (mode == 1 && n < (size_t(256) << 10))) {
+        MXEC_HIP(hipMemcpyAsync(buf_->dev.p, buf_->host.p, n, hipMemcpyHostToDevice, stream));
+    } else {
+        // The entry's previous launches are done (waited above), so the copy
+        // needs no ordering against `stream`; only the launches that follow
+        // wait for it.
+        if (!slot_.upload) MXEC_HIP(hipStreamCreateWithFlags(&slot_.upload, hipStreamNonBlocking));
+        if (!buf_->uploaded) MXEC_HIP(hipEventCreateWithFlags(&buf_->uploaded, hipEventDisableTiming));
+        MXEC_HIP(hipMemcpyAsync(buf_->dev.p, buf_->host.p, n, hipMemcpyHostToDevice, slot_.upload));
+        MXEC_HIP(hipEventRecord(buf_->uploaded, slot_.upload));
+        MXEC_HIP(hipStreamWaitEvent(stream, buf_->uploaded, 0));
+    }
     *dev_base = static_cast<char*>(buf_->dev.p);
     return MXEC_OK;
 }

@@ -58,6 +58,7 @@ struct DescBuf {
     DevBuf dev;
     DevBuf scratch;  // per-launch device scratch (DescWriter::scratch), same lifetime
     hipEvent_t done = nullptr;
+    hipEvent_t uploaded = nullptr;  // the tables' copy on Slot::upload finished
     bool pending = false;
 };
 
@@ -70,6 +71,12 @@ struct Slot {
     static constexpr int kRing = 4;
     DescBuf ring[kRing];
     int ring_next = 0;
+    // Descriptor tables of 256 KiB and more are copied on this stream of
+    // their own and the launch stream waits for the copy's event: the copy
+    // then runs while earlier kernels still execute, where an in-stream copy
+    // left the GPU idle for ~60-70 us between two kernels (19-21 us with the
+    // event wait; MXEC_DESC_UPLOAD=inline / stream force one way).
+    hipStream_t upload = nullptr;
     // Host-API uploads go through this pinned pair (pieces of kStagePiece,
     // double-buffered): one DMA per piece instead of HIP's pageable staging.
     PinnedBuf stage[2];

@@ -317,10 +317,13 @@ class Context:
 
     def encode_batch_device(self, objs: Sequence[tuple], data_ptrs, parity_ptrs, data_len=None,
                             digests_ptr=None, dev=0, stream=None):
-        arr = (N.Object * len(objs))(*[N.Object(k, m, s) for (k, m, s) in objs])
-        _check(self._lib.mxec_encode_batch_device(
-            self._h, dev, stream, arr, len(objs), _pp(data_ptrs),
-            _u64p(data_len) if data_len is not None else None, _pp(parity_ptrs), digests_ptr))
+        """Objects of mixed (k, m, shard_size); one launch per m (ctypes
+        arrays for objs / pointers / lengths pass through as built)."""
+        arr = objs if isinstance(objs, ctypes.Array) else (N.Object * len(objs))(*[N.Object(k, m, s) for (k, m, s) in objs])
+        dp = data_ptrs if isinstance(data_ptrs, ctypes.Array) else _pp(data_ptrs)
+        pp = parity_ptrs if isinstance(parity_ptrs, ctypes.Array) else _pp(parity_ptrs)
+        dl = None if data_len is None else (data_len if isinstance(data_len, ctypes.Array) else _u64p(data_len))
+        _check(self._lib.mxec_encode_batch_device(self._h, dev, stream, arr, len(objs), dp, dl, pp, digests_ptr))
 
     def encode_batch_host(self, objs: Sequence[tuple], data_ptrs, parity_ptrs, data_len=None,
                           digests: Optional[np.ndarray] = None, return_rc: bool = False):
@@ -367,6 +370,23 @@ class Context:
                 status.ctypes.data_as(N.I32P))
         return self._submit(self._lib.mxec_reconstruct_strided_device_async, args, (present, status, sl),
                             lambda: status[:n_obj])
+
+    def reconstruct_batch_device(self, objs, shard_ptrs, present: np.ndarray, shard_len=None,
+                                 expected_ptr=None, data_only=False, dev=0, stream=None):
+        """mxec_reconstruct_batch_device: objects of mixed (k, m, shard_size);
+        shard_ptrs / shard_len / present concatenated over objects (sum(k+m)
+        each; ctypes arrays pass through as built).  present (uint8) is updated
+        in place.  Returns (rc, per-object status array)."""
+        n = len(objs)
+        arr = objs if isinstance(objs, ctypes.Array) else (N.Object * n)(*[N.Object(k, m, s) for (k, m, s) in objs])
+        assert present.dtype == np.uint8
+        status = np.zeros(max(1, n), np.int32)
+        sp = shard_ptrs if isinstance(shard_ptrs, ctypes.Array) else _pp(shard_ptrs)
+        sl = None if shard_len is None else (shard_len if isinstance(shard_len, ctypes.Array) else _u64p(shard_len))
+        rc = self._lib.mxec_reconstruct_batch_device(
+            self._h, dev, stream, arr, n, sp, sl, present.ctypes.data_as(N.U8P), expected_ptr,
+            DATA_ONLY if data_only else 0, status.ctypes.data_as(N.I32P))
+        return rc, status[:n]
 
     def sha256_batch_device(self, ptrs, lens, digests_ptr, dev=0, stream=None):
         _check(self._lib.mxec_sha256_batch_device(

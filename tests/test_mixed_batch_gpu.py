@@ -1,0 +1,234 @@
+"""GPU: mixed-shape device batches — objects of different (k, m) and chunk
+sizes in ONE call each way (BASELINE configs[4]'s continuous encode + decode
+stream): `mxec_encode_batch_device` (one grouped launch per m) and
+`mxec_reconstruct_batch_device` (one grouped launch per number of shards to
+rebuild), checked object by object against the oracle.
+
+Reference: filesystem.rs:1084-1145 (encode of each object),
+chunk_reader.rs:157-226 (verify -> erasure -> reconstruct of each object)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x6D6178696F
+DATA_ONLY = 1
+E_TOO_FEW_PRESENT = -10
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _classes(rng, sizes=(64 << 10, 256 << 10, 1 << 20), kms=((4, 2), (8, 4), (10, 4)), n=2):
+    out = []
+    for (k, m) in kms:
+        for S in sizes:
+            out.append((k, m, S, n, [S] * (k - 1) + [int(rng.integers(1, S))]))
+    return out
+
+
+class Batch:
+    """Object-major tensors per class ([n][k+m][S]); the flat per-object
+    arrays the mixed entry points take."""
+
+    def __init__(self, torch, classes):
+        self.classes = []
+        self.objs, self.dptr, self.pptr, self.dlen, self.sptr, self.slen = [], [], [], [], [], []
+        for (k, m, S, n, dl) in classes:
+            t = torch.randint(0, 256, (n, k + m, S), dtype=torch.uint8, device="cuda")
+            t[:, k - 1, dl[-1]:] = 0  # bytes past the short chunk are not part of it
+            self.classes.append((k, m, S, n, dl, t))
+            for o in range(n):
+                self.objs.append((k, m, S))
+                self.dptr += [t[o, j].data_ptr() for j in range(k)]
+                self.pptr += [t[o, k + i].data_ptr() for i in range(m)]
+                self.dlen += dl
+                self.sptr += [t[o, i].data_ptr() for i in range(k + m)]
+                self.slen += dl + [S] * m
+        self.total = len(self.sptr)
+
+    def check_parity(self):
+        for (k, m, S, n, dl, t) in self.classes:
+            h = t.cpu().numpy()
+            for o in range(n):
+                want = oracle.encode([h[o][j][:dl[j]] for j in range(k)], m, S)
+                for i in range(m):
+                    assert np.array_equal(h[o][k + i], want[i]), (k, m, S, o, i)
+
+
+def test_mixed_encode_then_reconstruct_one_call_each(ctx):
+    """Encode every class in one call (digests too), erase 1..m seeded
+    shards per object (data and parity) and silently corrupt a present shard
+    of every third object, then one verified reconstruct call: every object
+    equals its encoded state, the corrupted shards were caught."""
+    torch = _torch()
+    rng = np.random.default_rng(SEED)
+    b = Batch(torch, _classes(rng) + [(4, 2, 10 << 20, 1, [10 << 20] * 3 + [777])])
+    dig = torch.zeros((b.total, 32), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(b.objs, b.dptr, b.pptr, data_len=b.dlen, digests_ptr=dig.data_ptr(),
+                            stream=st.cuda_stream)
+    st.synchronize()
+    b.check_parity()
+    refs = [c[5].clone() for c in b.classes]
+    present = np.ones(b.total, np.uint8)
+    corrupted = []
+    g = 0
+    ob = 0
+    for (k, m, S, n, dl, t) in b.classes:
+        for o in range(n):
+            e = int(rng.integers(1, m + 1))
+            if ob % 3 == 0:
+                e = min(e, m - 1)
+            miss = rng.choice(k + m, e, replace=False)
+            for i in miss:
+                present[g + i] = 0
+                t[o, i].fill_(0xA5)
+            if ob % 3 == 0:
+                keep = [i for i in range(k + m) if i not in miss]
+                c = int(rng.choice(keep))
+                t[o, c, 0] ^= 0x01
+                corrupted.append(g + c)
+            g += k + m
+            ob += 1
+    torch.cuda.synchronize()
+    p = present.copy()
+    rc, status = ctx.reconstruct_batch_device(b.objs, b.sptr, p, shard_len=b.slen, expected_ptr=dig.data_ptr(),
+                                              stream=st.cuda_stream)
+    st.synchronize()
+    assert rc == 0 and not status.any() and p.all()
+    for (k, m, S, n, dl, t), ref in zip(b.classes, refs):
+        t[:, k - 1, dl[-1]:] = 0  # a rebuilt short chunk is written at its length
+        assert torch.equal(t, ref), (k, m, S)
+    assert corrupted
+
+
+def test_mixed_reconstruct_without_verify_and_data_only(ctx):
+    """No expected digests: the masks as given; with MXEC_F_DATA_ONLY only the
+    missing data shards are rebuilt (crate reconstruct_data) and missing
+    parity stays missing."""
+    torch = _torch()
+    rng = np.random.default_rng(SEED + 1)
+    b = Batch(torch, _classes(rng, sizes=(64 << 10, 1 << 20)))
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(b.objs, b.dptr, b.pptr, data_len=b.dlen)
+    torch.cuda.synchronize()
+    refs = [c[5].clone() for c in b.classes]
+    present = np.ones(b.total, np.uint8)
+    g = 0
+    for (k, m, S, n, dl, t) in b.classes:
+        for o in range(n):
+            # one data shard and one parity shard missing
+            for i in (int(rng.integers(0, k)), k + int(rng.integers(0, m))):
+                present[g + i] = 0
+                t[o, i].fill_(0x5A)
+            g += k + m
+    torch.cuda.synchronize()
+    p = present.copy()
+    rc, status = ctx.reconstruct_batch_device(b.objs, b.sptr, p, shard_len=b.slen, data_only=True)
+    torch.cuda.synchronize()
+    assert rc == 0 and not status.any()
+    g = 0
+    for (k, m, S, n, dl, t), ref in zip(b.classes, refs):
+        t[:, k - 1, dl[-1]:] = 0
+        for o in range(n):
+            for i in range(k + m):
+                if i < k:
+                    assert p[g + i] == 1
+                    assert torch.equal(t[o, i], ref[o, i]), (k, m, S, o, i)
+                else:
+                    assert p[g + i] == present[g + i]
+            g += k + m
+    # now the parity too
+    rc, status = ctx.reconstruct_batch_device(b.objs, b.sptr, p, shard_len=b.slen)
+    torch.cuda.synchronize()
+    assert rc == 0 and p.all()
+    for (k, m, S, n, dl, t), ref in zip(b.classes, refs):
+        assert torch.equal(t, ref), (k, m, S)
+
+
+def test_mixed_reconstruct_too_few_shards(ctx):
+    """An object missing m+1 shards fails alone (status -10, the reference's
+    message); the others of the batch are rebuilt."""
+    torch = _torch()
+    rng = np.random.default_rng(SEED + 2)
+    b = Batch(torch, _classes(rng, sizes=(64 << 10,), n=3))
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(b.objs, b.dptr, b.pptr, data_len=b.dlen)
+    torch.cuda.synchronize()
+    refs = [c[5].clone() for c in b.classes]
+    present = np.ones(b.total, np.uint8)
+    bad = 4  # object index in batch order
+    g = 0
+    ob = 0
+    for (k, m, S, n, dl, t) in b.classes:
+        for o in range(n):
+            e = m + 1 if ob == bad else 1
+            for i in rng.choice(k + m, e, replace=False):
+                present[g + i] = 0
+                if ob != bad:
+                    t[o, i].fill_(0x33)
+            g += k + m
+            ob += 1
+    torch.cuda.synchronize()
+    p = present.copy()
+    rc, status = ctx.reconstruct_batch_device(b.objs, b.sptr, p, shard_len=b.slen)
+    torch.cuda.synchronize()
+    assert rc == E_TOO_FEW_PRESENT
+    assert [i for i, s in enumerate(status) if s] == [bad] and status[bad] == E_TOO_FEW_PRESENT
+    for (k, m, S, n, dl, t), ref in zip(b.classes, refs):
+        t[:, k - 1, dl[-1]:] = 0
+        assert torch.equal(t, ref), (k, m, S)
+
+
+def test_mixed_batches_unaligned_and_wide(ctx):
+    """Shapes the grouped launch does not take fall back per (k, S) inside the
+    same calls: a shard size that is not a multiple of 16 (unaligned shard
+    pointers), m > 8 (row groups), beside aligned objects of the same m."""
+    torch = _torch()
+    rng = np.random.default_rng(SEED + 3)
+    classes = [(3, 2, 5000, 2, [5000, 5000, 1234]), (4, 2, 64 << 10, 2, [64 << 10] * 3 + [100]),
+               (20, 10, 4096, 2, [4096] * 19 + [4000]), (6, 10, 8192, 1, [8192] * 6)]
+    b = Batch(torch, classes)
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(b.objs, b.dptr, b.pptr, data_len=b.dlen)
+    torch.cuda.synchronize()
+    b.check_parity()
+    refs = [c[5].clone() for c in b.classes]
+    present = np.ones(b.total, np.uint8)
+    g = 0
+    for (k, m, S, n, dl, t) in b.classes:
+        for o in range(n):
+            for i in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False):
+                present[g + i] = 0
+                t[o, i].fill_(0x77)
+            g += k + m
+    torch.cuda.synchronize()
+    p = present.copy()
+    rc, status = ctx.reconstruct_batch_device(b.objs, b.sptr, p, shard_len=b.slen)
+    torch.cuda.synchronize()
+    assert rc == 0 and p.all() and not status.any()
+    for (k, m, S, n, dl, t), ref in zip(b.classes, refs):
+        t[:, k - 1, dl[-1]:] = 0
+        assert torch.equal(t, ref), (k, m, S)
+
+
+def test_mixed_batch_argument_errors(ctx):
+    """Crate argument errors answer before any work (k = 0, k + m > 256, a
+    zero shard size)."""
+    import maxio_amd
+
+    present = np.ones(8, np.uint8)
+    for objs, code in (([(0, 2, 64)], -3), ([(250, 10, 64)], -2), ([(4, 2, 0)], -11)):
+        rc, _ = ctx.reconstruct_batch_device(objs, [0] * 8, present)
+        assert rc == code, (objs, rc)
+    with pytest.raises(maxio_amd.RSError):
+        ctx.encode_batch_device([(0, 2, 64)], [0], [0, 0])
