@@ -58,6 +58,8 @@ hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s);
 hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& v);
 // Geometry the default launch uses for a given total row count, and its tile.
 RsVariant rs_default_variant(uint32_t r_total);
+// Geometry of grouped launches (a.group set) for r rows.
+RsVariant rs_group_variant(uint32_t r);
 uint64_t rs_tile_bytes(const RsVariant& v);
 
 // SHA-256 over n messages, one lane per message.  If `expected` is set the

@@ -175,7 +175,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         if (objs.empty() || r == 0) continue;
         bool uniform = true, aligned = r <= 8;
         Plan p{r, &objs};
-        p.tile = rs_tile_bytes(rs_default_variant(uint32_t(r)));
+        p.tile = rs_tile_bytes(rs_group_variant(uint32_t(r)));
         for (const RsMixedObject& ob : objs) {
             uniform &= ob.k == objs[0].k && ob.shard_size == objs[0].shard_size;
             p.sum_k += uint64_t(ob.k);

@@ -28,6 +28,8 @@
 //    built by the host, run_rs).
 #include "kernels.hpp"
 
+#include <cstdlib>
+
 namespace mxec {
 namespace {
 
@@ -413,13 +415,16 @@ hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles
     return hipGetLastError();
 }
 
-// Grouped launches run the default geometry only (rs_default_variant).
+// Grouped launches: rs_group_variant's geometry (nontemporal, V = 4 or 2).
 template <int R>
 hipError_t launch_grouped(const RsArgs& a, int n_cus, hipStream_t s) {
-    constexpr int V = R <= 4 ? 4 : 2;
-    uint64_t blocks = uint64_t(n_cus) * 32;
+    const RsVariant v = rs_group_variant(uint32_t(R));
+    uint64_t blocks = uint64_t(n_cus) * uint64_t(v.blocks_per_cu);
     if (blocks > a.n_tiles) blocks = a.n_tiles;
-    return launch_fast<R, V, true, true>(a, 0, a.n_tiles, blocks, s);
+    if constexpr (R <= 4) {
+        if (v.vecs == 4) return launch_fast<R, 4, true, true>(a, 0, a.n_tiles, blocks, s);
+    }
+    return launch_fast<R, 2, true, true>(a, 0, a.n_tiles, blocks, s);
 }
 
 template <int R>
@@ -471,6 +476,27 @@ RsVariant rs_default_variant(uint32_t r_total) {
     v.vecs = r_total <= 4 ? 4 : 2;
     v.nt = true;
     v.blocks_per_cu = 32;
+    return v;
+}
+
+// Grouped launches (mixed batches: many objects of a few tiles each) take the
+// default geometry with 64 workgroups per CU of grid-stride: config 5 measured
+// 32 / 48 / 64 / 128 / one tile per workgroup within ~1 %, 64 at the top
+// with 128, V = 2 3-4 % slower (profiles/r2_rs_group_geometry.txt).
+// MXEC_RS_GROUP_VECS (2 | 4) and MXEC_RS_GROUP_BPC override it for labs.
+RsVariant rs_group_variant(uint32_t r) {
+    static const int env_v = [] {
+        const char* e = getenv("MXEC_RS_GROUP_VECS");
+        return e ? atoi(e) : 0;
+    }();
+    static const int env_b = [] {
+        const char* e = getenv("MXEC_RS_GROUP_BPC");
+        return e ? atoi(e) : 0;
+    }();
+    RsVariant v = rs_default_variant(r);
+    v.blocks_per_cu = 64;
+    if (r <= 4 && (env_v == 2 || env_v == 4)) v.vecs = env_v;
+    if (env_b > 0 && env_b <= 4096) v.blocks_per_cu = env_b;
     return v;
 }
 
