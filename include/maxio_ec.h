@@ -287,6 +287,18 @@ int mxec_reconstruct_batch_device(mxec_ctx* ctx, int dev, void* stream,
                                   const uint8_t* expected_sha_dev,
                                   uint32_t flags, int32_t* status_out);
 
+/* The completion-handle form: objs, shards and shard_len are copied at
+ * submission; present and status_out must stay valid until the ticket
+ * completes, and the shards are the caller's until then. */
+int mxec_reconstruct_batch_device_async(mxec_ctx* ctx, int dev, void* stream,
+                                        const mxec_object* objs, uint64_t n_obj,
+                                        uint8_t* const* shards,
+                                        const uint64_t* shard_len,
+                                        uint8_t* present,
+                                        const uint8_t* expected_sha_dev,
+                                        uint32_t flags, int32_t* status_out,
+                                        mxec_ticket** ticket);
+
 /* SHA-256 of n device buffers (host arrays of device pointers and lengths)
  * into digests_dev (device, n*32). */
 int mxec_sha256_batch_device(mxec_ctx* ctx, int dev, void* stream,

@@ -114,6 +114,9 @@ _SIGS = {
         INT, [P, INT, P, INT, INT, U64, U64, P, U64, U64, U64P, U8P, P, ctypes.c_uint32, I32P]),
     "mxec_reconstruct_batch_device": (
         INT, [P, INT, P, ctypes.POINTER(Object), U64, PP, U64P, U8P, P, ctypes.c_uint32, I32P]),
+    "mxec_reconstruct_batch_device_async": (
+        INT, [P, INT, P, ctypes.POINTER(Object), U64, PP, U64P, U8P, P, ctypes.c_uint32, I32P,
+              ctypes.POINTER(ctypes.c_void_p)]),
     "mxec_sha256_batch_device": (INT, [P, INT, P, PP, U64P, U64, P]),
     "mxec_write_chunk": (INT, [P, ctypes.c_char_p, ctypes.c_uint32, P, SZ, ctypes.POINTER(ChunkInfo)]),
     "mxec_compute_and_write_parity": (

@@ -250,6 +250,33 @@ int mxec_reconstruct_strided_device_async(mxec_ctx* ctx, int dev, void* stream, 
     });
 }
 
+int mxec_reconstruct_batch_device_async(mxec_ctx* ctx, int dev, void* stream, const mxec_object* objs,
+                                        uint64_t n_obj, uint8_t* const* shards, const uint64_t* shard_len,
+                                        uint8_t* present, const uint8_t* expected_sha_dev, uint32_t flags,
+                                        int32_t* status_out, mxec_ticket** ticket) {
+    return guarded([&] {
+        if (n_obj && (!objs || !shards || !present)) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        uint64_t sum = 0;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            if (int rc = mxec_rs_check(objs[o].k, objs[o].m))
+                return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
+            if (objs[o].shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+            sum += uint64_t(objs[o].k + objs[o].m);
+        }
+        // The object list, pointer and length arrays are copied here; present,
+        // status_out and the shards stay the caller's until completion.
+        auto ob = copy_n(objs, size_t(n_obj));
+        auto sp = copy_n(shards, size_t(sum));
+        auto sl = copy_n(shard_len, size_t(sum));
+        const bool has_sl = shard_len != nullptr;
+        return submit(ctx, ticket, [=] {
+            return mxec_reconstruct_batch_device(ctx, dev, stream, ob.data(), n_obj, sp.data(),
+                                                 has_sl ? sl.data() : nullptr, present, expected_sha_dev, flags,
+                                                 status_out);
+        });
+    });
+}
+
 int mxec_put_object_chunked_async(mxec_ctx* ctx, const char* ec_dir, uint64_t chunk_size, uint32_t parity_shards,
                                   const uint8_t* body, size_t len, mxec_ticket** ticket) {
     return guarded([&] {

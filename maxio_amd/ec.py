@@ -388,6 +388,22 @@ class Context:
             DATA_ONLY if data_only else 0, status.ctypes.data_as(N.I32P))
         return rc, status[:n]
 
+    def reconstruct_batch_device_async(self, objs, shard_ptrs, present: np.ndarray, shard_len=None,
+                                       expected_ptr=None, data_only=False, dev=0, stream=None) -> "Ticket":
+        """The completion-handle form of reconstruct_batch_device: `present`
+        is updated in place when the ticket completes; wait() returns the
+        per-object status array."""
+        n = len(objs)
+        arr = objs if isinstance(objs, ctypes.Array) else (N.Object * n)(*[N.Object(k, m, s) for (k, m, s) in objs])
+        assert present.dtype == np.uint8
+        status = np.zeros(max(1, n), np.int32)
+        sp = shard_ptrs if isinstance(shard_ptrs, ctypes.Array) else _pp(shard_ptrs)
+        sl = None if shard_len is None else (shard_len if isinstance(shard_len, ctypes.Array) else _u64p(shard_len))
+        args = (self._h, dev, stream, arr, n, sp, sl, present.ctypes.data_as(N.U8P), expected_ptr,
+                DATA_ONLY if data_only else 0, status.ctypes.data_as(N.I32P))
+        return self._submit(self._lib.mxec_reconstruct_batch_device_async, args, (present, status),
+                            lambda: status[:n])
+
     def sha256_batch_device(self, ptrs, lens, digests_ptr, dev=0, stream=None):
         _check(self._lib.mxec_sha256_batch_device(
             self._h, dev, stream, _pp(ptrs), _u64p(lens), len(ptrs), digests_ptr))

@@ -157,6 +157,7 @@ extern "C" {
     pub fn mxec_encode_batch_host(ctx: *mut MxecCtx, objs: *const MxecObject, n_obj: u64, data: *const *const u8, data_len: *const u64, parity: *const *mut u8, digests: *mut [u8; 32], status_out: *mut i32) -> c_int;
     pub fn mxec_reconstruct_strided_device(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, k: c_int, m: c_int, shard_size: u64, n_obj: u64, shards: *mut u8, obj_stride: u64, shard_stride: u64, shard_len: *const u64, present: *mut u8, expected_sha_dev: *const u8, flags: u32, status_out: *mut i32) -> c_int;
     pub fn mxec_reconstruct_batch_device(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, objs: *const MxecObject, n_obj: u64, shards: *const *mut u8, shard_len: *const u64, present: *mut u8, expected_sha_dev: *const u8, flags: u32, status_out: *mut i32) -> c_int;
+    pub fn mxec_reconstruct_batch_device_async(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, objs: *const MxecObject, n_obj: u64, shards: *const *mut u8, shard_len: *const u64, present: *mut u8, expected_sha_dev: *const u8, flags: u32, status_out: *mut i32, ticket: *mut *mut MxecTicket) -> c_int;
     pub fn mxec_reconstruct_strided_device_async(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, k: c_int, m: c_int, shard_size: u64, n_obj: u64, shards: *mut u8, obj_stride: u64, shard_stride: u64, shard_len: *const u64, present: *mut u8, expected_sha_dev: *const u8, flags: u32, status_out: *mut i32, ticket: *mut *mut MxecTicket) -> c_int;
     pub fn mxec_sha256_batch_device(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, bufs: *const *const u8, lens: *const u64, n: u64, digests_dev: *mut u8) -> c_int;
     pub fn mxec_write_chunk(ctx: *mut MxecCtx, ec_dir: *const c_char, index: u32, data: *const u8, len: usize, out: *mut MxecChunkInfo) -> c_int;

@@ -221,6 +221,40 @@ def test_mixed_batches_unaligned_and_wide(ctx):
         assert torch.equal(t, ref), (k, m, S)
 
 
+def test_mixed_reconstruct_async_matches(ctx):
+    """mxec_reconstruct_batch_device_async (ticket + eventfd): the same
+    rebuild as the blocking call, the pointer arrays copied at submission
+    (the caller's lists are dropped before the ticket completes)."""
+    torch = _torch()
+    rng = np.random.default_rng(SEED + 4)
+    b = Batch(torch, _classes(rng, sizes=(64 << 10, 1 << 20)))
+    dig = torch.zeros((b.total, 32), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(b.objs, b.dptr, b.pptr, data_len=b.dlen, digests_ptr=dig.data_ptr())
+    torch.cuda.synchronize()
+    refs = [c[5].clone() for c in b.classes]
+    present = np.ones(b.total, np.uint8)
+    g = 0
+    for (k, m, S, n, dl, t) in b.classes:
+        for o in range(n):
+            for i in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False):
+                present[g + i] = 0
+                t[o, i].fill_(0x11)
+            g += k + m
+    torch.cuda.synchronize()
+    p = present.copy()
+    sptr, slen = list(b.sptr), list(b.slen)
+    tk = ctx.reconstruct_batch_device_async(b.objs, sptr, p, shard_len=slen, expected_ptr=dig.data_ptr())
+    del sptr, slen
+    status = tk.wait()
+    tk.close()
+    torch.cuda.synchronize()
+    assert not status.any() and p.all()
+    for (k, m, S, n, dl, t), ref in zip(b.classes, refs):
+        t[:, k - 1, dl[-1]:] = 0
+        assert torch.equal(t, ref), (k, m, S)
+
+
 def test_mixed_batch_argument_errors(ctx):
     """Crate argument errors answer before any work (k = 0, k + m > 256, a
     zero shard size)."""
