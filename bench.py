@@ -928,7 +928,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="2", choices=["2", "3", "3c", "ns", "4a", "4b", "5", "sums", "frames"])
     ap.add_argument("--workers", type=int, default=8, help="config 3c: concurrent batches")
@@ -1053,6 +1053,8 @@ def main() -> int:
 
     if rank == 0:
         tag = {"2": "k4m2", "ns": "k8m4", "sums": "crc_tiles", "frames": "gcm_frames"}.get(args.config)
+        if args.config == "5" and getattr(w, "mode", "") == "batch":
+            tag = "cfg5_grouped"
         traffic, tsrc = pmc_traffic(tag, w.alg_bytes) if tag else (None, None)
         line = {
             "metric": METRIC,
