@@ -66,17 +66,29 @@ __global__ __launch_bounds__(256) void probe_read(const u32x4* __restrict__ s, u
     if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) sink[0] = acc;  // keeps the loads; never true for the probe's data
 }
 
-template <bool NT>
+// Store policies of the write probes (gfx950 cache-policy bits on a vector
+// global_store_dwordx4): 0 nt, 1 plain, 2 sc1, 3 sc0 sc1, 4 sc1 nt.  Plain /
+// nt keep the line in the XCD's L2, sc1 / sc0 sc1 drop it
+// (MI355X_MICROARCH.md, memory-model table).
+typedef u32x4 __attribute__((address_space(1)))* g4ptr;
+template <int P>
+__device__ __forceinline__ void store_p(u32x4* d, u32x4 v) {
+    g4ptr g = (g4ptr)(d);
+    if constexpr (P == 0) __builtin_nontemporal_store(v, g);
+    else if constexpr (P == 1) *g = v;
+    else if constexpr (P == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(g), "v"(v) : "memory");
+    else if constexpr (P == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(g), "v"(v) : "memory");
+    else asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(g), "v"(v) : "memory");
+}
+
+template <int P>
 __global__ __launch_bounds__(256) void probe_write(u32x4* __restrict__ d, uint64_t n) {
     const uint64_t stride = uint64_t(gridDim.x) * 256;
     const u32x4 v = {blockIdx.x, threadIdx.x, 0x5A5A5A5Au, 0xA5A5A5A5u};
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += stride) {
-        if (NT) __builtin_nontemporal_store(v, d + i);
-        else d[i] = v;
-    }
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += stride) store_p<P>(d + i, v);
 }
 
-template <int R>
+template <int R, int P = 0>
 __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
                                                      uint32_t k, uint64_t S, uint64_t n_obj, uint64_t dstride,
                                                      uint64_t pstride, uint64_t sstride) {
@@ -106,7 +118,7 @@ __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__
         for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int v = 0; v < 4; ++v)
-                __builtin_nontemporal_store(acc[v][i], reinterpret_cast<u32x4*>(par + o * pstride + i * sstride + base + v * 4096));
+                store_p<P>(reinterpret_cast<u32x4*>(par + o * pstride + i * sstride + base + v * 4096), acc[v][i]);
     }
 }
 
@@ -148,14 +160,17 @@ extern "C" int mxprobe_read(const void* src, uint64_t bytes, void* sink16, void*
 }
 
 extern "C" int mxprobe_write(void* dst, uint64_t bytes, int policy, void* stream) {
-    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || policy < 0 || policy > 1)
+    if ((bytes & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) || policy < 0 || policy > 4)
         return int(hipErrorInvalidValue);
-    if (policy == 0)
-        hipLaunchKernelGGL(probe_write<true>, dim3(grid()), dim3(256), 0, static_cast<hipStream_t>(stream),
-                           static_cast<u32x4*>(dst), bytes / 16);
-    else
-        hipLaunchKernelGGL(probe_write<false>, dim3(grid()), dim3(256), 0, static_cast<hipStream_t>(stream),
-                           static_cast<u32x4*>(dst), bytes / 16);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    u32x4* d = static_cast<u32x4*>(dst);
+    switch (policy) {
+        case 0: hipLaunchKernelGGL(probe_write<0>, dim3(grid()), dim3(256), 0, s, d, bytes / 16); break;
+        case 1: hipLaunchKernelGGL(probe_write<1>, dim3(grid()), dim3(256), 0, s, d, bytes / 16); break;
+        case 2: hipLaunchKernelGGL(probe_write<2>, dim3(grid()), dim3(256), 0, s, d, bytes / 16); break;
+        case 3: hipLaunchKernelGGL(probe_write<3>, dim3(grid()), dim3(256), 0, s, d, bytes / 16); break;
+        default: hipLaunchKernelGGL(probe_write<4>, dim3(grid()), dim3(256), 0, s, d, bytes / 16); break;
+    }
     return int(hipGetLastError());
 }
 
@@ -184,4 +199,27 @@ extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32
 extern "C" int mxprobe_rs_pattern(const void* data, void* parity, uint32_t k, uint32_t m, uint64_t S, uint64_t n_obj,
                                   void* stream) {
     return mxprobe_rs_pattern_strided(data, parity, k, m, S, n_obj, uint64_t(k) * S, uint64_t(m) * S, S, stream);
+}
+
+// The RS pattern at m = 2 with store policy `policy` (store_p above), for the
+// write-policy lab (tools/region_lab.py --policies); same geometry as
+// mxprobe_rs_pattern_strided.
+extern "C" int mxprobe_rs_pattern_policy(const void* data, void* parity, uint32_t k, uint64_t S, uint64_t n_obj,
+                                         uint64_t obj_stride, uint64_t shard_stride, int policy, void* stream) {
+    if (k == 0 || (k & 3) || S == 0 || (S % 16384) || policy < 0 || policy > 4 ||
+        ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
+        return int(hipErrorInvalidValue);
+    const dim3 g(uint32_t(grid() * 2)), b(256);
+    const auto* in = static_cast<const uint8_t*>(data);
+    auto* out = static_cast<uint8_t*>(parity);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t os = obj_stride, ss = shard_stride;
+    switch (policy) {
+        case 0: hipLaunchKernelGGL((probe_pattern<2, 0>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
+        case 1: hipLaunchKernelGGL((probe_pattern<2, 1>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
+        case 2: hipLaunchKernelGGL((probe_pattern<2, 2>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
+        case 3: hipLaunchKernelGGL((probe_pattern<2, 3>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
+        default: hipLaunchKernelGGL((probe_pattern<2, 4>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
+    }
+    return int(hipGetLastError());
 }

@@ -26,6 +26,9 @@ def main() -> int:
     ap.add_argument("--gib", type=int, default=8)
     ap.add_argument("--chunks", type=int, default=30)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--policies", action="store_true",
+                    help="per chunk: write streams and the RS access pattern (k=4 m=2, 1 MiB shards, "
+                         "object-major) under each store policy: 0 nt, 1 plain, 2 sc1, 3 sc0 sc1, 4 sc1 nt")
     a = ap.parse_args()
     import torch
 
@@ -59,6 +62,25 @@ def main() -> int:
     print(json.dumps({"chunks": len(bufs), "gib_each": a.gib, "free_GiB": round(free / 2**30, 1),
                       "total_GiB": round(total / 2**30, 1)}), flush=True)
     half = n // 2
+    if a.policies:
+        import ctypes
+
+        probe.mxprobe_rs_pattern_policy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                    ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        probe.mxprobe_rs_pattern_policy.restype = ctypes.c_int
+        k, m, S = 4, 2, 1 << 20
+        nobj = n // ((k + m) * S)
+        for i, b in enumerate(bufs):
+            row = {"chunk": i}
+            for pol, name in enumerate(("nt", "plain", "sc1", "sc0sc1", "sc1nt")):
+                w = timed(lambda: probe.mxprobe_write(b.data_ptr(), n, pol, sh))
+                pt = timed(lambda: probe.mxprobe_rs_pattern_policy(b.data_ptr(), b.data_ptr() + k * S, k, S, nobj,
+                                                                   (k + m) * S, S, pol, sh))
+                row[f"write_{name}"] = round(n / w / 1e9, 3)
+                row[f"rs_{name}"] = round(nobj * (k + m) * S / pt / 1e9, 3)
+            print(json.dumps(row), flush=True)
+        return 0
     for i, b in enumerate(bufs):
         w = timed(lambda: probe.mxprobe_write(b.data_ptr(), n, 0, sh))
         wp = timed(lambda: probe.mxprobe_write(b.data_ptr(), n, 1, sh))
