@@ -255,6 +255,105 @@ def test_mixed_reconstruct_async_matches(ctx):
         assert torch.equal(t, ref), (k, m, S)
 
 
+@pytest.fixture()
+def ctx8(monkeypatch):
+    import maxio_amd
+
+    monkeypatch.setenv("MXEC_LOGICAL_DEVICES", "8")
+    c = maxio_amd.Context(device_mask=1, streams_per_device=1)
+    monkeypatch.delenv("MXEC_LOGICAL_DEVICES")
+    assert c.device_ids() == [0] * 8
+    yield c
+    c.close()
+
+
+def test_mixed_batches_over_eight_devices(ctx8):
+    """configs[4] as eight GPUs would run it: the mixed objects dealt object
+    i -> device i mod 8; each device's share is one encode and
+    then one verified reconstruct batch call from its own host thread on its
+    own stream (per-device slots, descriptor rings, coefficient arenas).
+    Every parity equals the oracle's and every object its encoded state."""
+    import threading
+
+    torch = _torch()
+    rng = np.random.default_rng(SEED + 5)
+    b = Batch(torch, _classes(rng, sizes=(64 << 10, 256 << 10, 1 << 20), n=3))
+    where, spans, g = [], [], 0  # object -> (class tensor, index in class), (first global shard, k, m)
+    for (k, m, S, n, dl, t) in b.classes:
+        for o in range(n):
+            where.append((t, o))
+            spans.append((g, k, m))
+            g += k + m
+    D = 8
+    mine = [[o for o in range(len(b.objs)) if o % D == d] for d in range(D)]
+    streams = [torch.cuda.Stream() for _ in range(D)]
+    dig = torch.zeros((b.total, 32), dtype=torch.uint8, device="cuda")
+    errors = []
+
+    def arrays(d):
+        gi = [gg for o in mine[d] for gg in range(spans[o][0], spans[o][0] + spans[o][1] + spans[o][2])]
+        return [b.objs[o] for o in mine[d]], gi
+
+    def encode(d):
+        try:
+            oo, gi = arrays(d)
+            dp = [b.sptr[spans[o][0] + j] for o in mine[d] for j in range(spans[o][1])]
+            pp = [b.sptr[spans[o][0] + spans[o][1] + i] for o in mine[d] for i in range(spans[o][2])]
+            dl = [b.slen[spans[o][0] + j] for o in mine[d] for j in range(spans[o][1])]
+            # this device's digests: rows gi of `dig`, contiguous per object in batch order
+            dg = torch.zeros((len(gi), 32), dtype=torch.uint8, device="cuda")
+            ctx8.encode_batch_device(oo, dp, pp, data_len=dl, digests_ptr=dg.data_ptr(), dev=d,
+                                     stream=streams[d].cuda_stream)
+            streams[d].synchronize()
+            dig[gi] = dg
+        except Exception as e:  # noqa: BLE001
+            errors.append(("encode", d, repr(e)))
+
+    def reconstruct(d, present):
+        try:
+            oo, gi = arrays(d)
+            pr = present[gi].copy()
+            dg = dig[gi].contiguous()
+            torch.cuda.synchronize()
+            rc, status = ctx8.reconstruct_batch_device(oo, [b.sptr[x] for x in gi], pr,
+                                                       shard_len=[b.slen[x] for x in gi],
+                                                       expected_ptr=dg.data_ptr(), dev=d,
+                                                       stream=streams[d].cuda_stream)
+            streams[d].synchronize()
+            if rc != 0 or status.any() or not pr.all():
+                errors.append(("reconstruct", d, rc, status.tolist()))
+        except Exception as e:  # noqa: BLE001
+            errors.append(("reconstruct", d, repr(e)))
+
+    torch.cuda.synchronize()
+    ths = [threading.Thread(target=encode, args=(d,)) for d in range(D)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    b.check_parity()
+    refs = [c[5].clone() for c in b.classes]
+    present = np.ones(b.total, np.uint8)
+    for o, (g0, k, m) in enumerate(spans):
+        t, oi = where[o]
+        for i in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False):
+            present[g0 + int(i)] = 0
+            t[oi, int(i)].fill_(0xC3)
+    torch.cuda.synchronize()
+    ths = [threading.Thread(target=reconstruct, args=(d, present)) for d in range(D)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for (k, m, S, n, dl, t), ref in zip(b.classes, refs):
+        t[:, k - 1, dl[-1]:] = 0
+        assert torch.equal(t, ref), (k, m, S)
+
+
 def test_mixed_batch_argument_errors(ctx):
     """Crate argument errors answer before any work (k = 0, k + m > 256, a
     zero shard size)."""
