@@ -823,9 +823,9 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     """Driver-timed secondary measurements beside the headline (VERDICT r1
     item 1), each with its own roofline block: the north-star shape (encode
     k=8 m=4, 1 MiB chunks), config 3 (verify + rebuild) with the SHA kernel
-    timed alone against the INT32-VALU bound, config 3c (8 concurrent
-    batches), and the reference-equivalent PUT compute (encode + SHA-256 of
-    all k+m chunks)."""
+    timed alone against the INT32-VALU bound, config 5 (the mixed
+    encode + reconstruct stream), config 3c (8 concurrent batches), and the
+    reference-equivalent PUT compute (encode + SHA-256 of all k+m chunks)."""
     sh = stream.cuda_stream
     n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     out = {}
@@ -869,6 +869,12 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
         rc, _ = ctx.reconstruct_strided_device(k, m, S, n, r.obj.data_ptr(), (k + m) * S, S, pr, stream=sh)
         assert rc == 0
     ms_rs = event_ms(torch, stream, decode_only, 3)
+    # its denominator: the RS pattern on the same buffers, 8 shards read and
+    # 2 written per object (shards 0-7 -> 10-11; after the spot check)
+    lib = probe_lib()
+    ms_pat = event_ms(torch, stream, lambda: lib.mxprobe_rs_pattern_strided(
+        r.obj.data_ptr(), r.obj[:, k + 2:].data_ptr(), k, 2, S, n, (k + m) * S, (k + m) * S, S, sh), 3)
+    cal3 = dict(cal or {}, rs_pattern_same_buffers_GBps=round(n * (k + 2) * S / (ms_pat * 1e-3) / 1e9, 1))
     out["config3"] = {
         "workload": r.name, "GiBps_payload": round(r.payload / GIB / (ms_call * 1e-3), 3),
         "ms_per_call": round(ms_call, 3), "spot_check_vs_original": ok,
@@ -882,11 +888,25 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                      "note": ("10 240 messages fill 160 of 1024 SIMDs: this launch is bound by the serial "
                               "chain of one 1 MiB message (16 384 blocks), not by chip-wide VALU issue")},
         "rs_decode": hbm_block(float(n) * (k + 2) * S, ms_rs, "rs_apply_fast<R=2> (decode 8 -> 2, no verify)",
-                               cal, "copy_GBps"),
+                               cal3, "rs_pattern_same_buffers_GBps"),
     }
     del dig
     r.drop()
     del r
+    torch.cuda.empty_cache()
+    # -- config 5: the mixed 4+2 / 8+4 / 10+4 stream, encode + reconstruct --
+    w5 = make_workload("5", torch, ctx, dev, sh, 0, 0)
+    torch.cuda.synchronize()
+    ms5 = event_ms(torch, stream, w5.step, max(5, steps // 6))
+    ok5 = w5.spot_check()
+    out["config5"] = {"workload": w5.name, "GiBps_payload": round(w5.payload / GIB / (ms5 * 1e-3), 3),
+                      "ms_per_step": round(ms5, 3), "spot_check_vs_oracle": ok5,
+                      "roofline": hbm_block(w5.alg_bytes, ms5, w5.kernel + ", whole step", cal,
+                                            "rs_pattern_k4m2_GBps")}
+    tr, src = pmc_traffic("cfg5_grouped", w5.alg_bytes)
+    out["config5"]["roofline"]["traffic"], out["config5"]["roofline"]["traffic_source"] = tr, src
+    w5.drop()
+    del w5
     torch.cuda.empty_cache()
     # -- config 3c: 8 concurrent batches -----------------------------------
     rs = ReconstructStream(torch, ctx, dev, sh, 1024, 8, SEED)
