@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <deque>
 #include <cstring>
 #include <map>
 
@@ -169,23 +170,33 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
     };
     std::vector<Plan> grouped;
     std::vector<std::pair<int, const std::vector<RsMixedObject>*>> rest;
+    // Per r: the aligned objects (grouped launch) and the others (per (k, S)
+    // launches through run_rs, whose edge kernel takes unaligned pointers).
+    std::deque<std::vector<RsMixedObject>> parts;
     for (const auto& g : groups) {
         const int r = g.first;
-        const auto& objs = g.second;
-        if (objs.empty() || r == 0) continue;
-        bool uniform = true, aligned = r <= 8;
-        Plan p{r, &objs};
-        p.tile = rs_tile_bytes(rs_group_variant(uint32_t(r)));
-        for (const RsMixedObject& ob : objs) {
-            uniform &= ob.k == objs[0].k && ob.shard_size == objs[0].shard_size;
-            p.sum_k += uint64_t(ob.k);
-            p.n_tiles += (ob.shard_size + p.tile - 1) / p.tile;
+        if (g.second.empty() || r == 0) continue;
+        auto& al = parts.emplace_back();
+        auto& un = parts.emplace_back();
+        for (const RsMixedObject& ob : g.second) {
+            bool aligned = r <= 8;
             for (int j = 0; j < ob.k && aligned; ++j) aligned &= (reinterpret_cast<uintptr_t>(ob.o.in[j]) & 15) == 0;
             for (int i = 0; i < r && aligned; ++i) aligned &= (reinterpret_cast<uintptr_t>(ob.o.out[i]) & 15) == 0;
+            (aligned ? al : un).push_back(ob);
         }
-        const bool fits = objs.size() <= UINT32_MAX && p.sum_k <= UINT32_MAX && p.n_tiles <= (uint64_t(1) << 32);
-        if (aligned && fits && !(uniform && groups.size() == 1)) grouped.push_back(p);
-        else rest.emplace_back(r, &objs);
+        if (!un.empty()) rest.emplace_back(r, &un);
+        if (al.empty()) continue;
+        bool uniform = true;
+        Plan p{r, &al};
+        p.tile = rs_tile_bytes(rs_group_variant(uint32_t(r)));
+        for (const RsMixedObject& ob : al) {
+            uniform &= ob.k == al[0].k && ob.shard_size == al[0].shard_size;
+            p.sum_k += uint64_t(ob.k);
+            p.n_tiles += (ob.shard_size + p.tile - 1) / p.tile;
+        }
+        const bool fits = al.size() <= UINT32_MAX && p.sum_k <= UINT32_MAX && p.n_tiles <= (uint64_t(1) << 32);
+        if (fits && !(uniform && groups.size() == 1 && un.empty())) grouped.push_back(p);
+        else rest.emplace_back(r, &al);
     }
     for (const auto& g : rest) {
         // One launch per (k, shard_size), in order of first appearance.

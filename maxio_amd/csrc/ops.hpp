@@ -36,10 +36,11 @@ struct RsMixedObject {
     uint64_t shard_size;
     RsObject o;
 };
-// Applies each object's matrix, objects grouped by r (map key).  One grouped
-// launch (rs_apply_fast<GRP>) per r whose pointers are all 16-byte aligned
-// (r <= 8), their tables in one upload; otherwise one run_rs per
-// (k, shard_size).  A lone uniform group runs the uniform kernel.
+// Applies each object's matrix, objects grouped by r (map key).  Per r, the
+// objects whose pointers are all 16-byte aligned (r <= 8) share one grouped
+// launch (rs_apply_fast<GRP>), every grouped launch's tables in one upload;
+// the others run one run_rs per (k, shard_size).  A lone uniform group runs
+// the uniform kernel.
 int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups);
 
 // SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be

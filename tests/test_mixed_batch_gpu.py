@@ -354,6 +354,62 @@ def test_mixed_batches_over_eight_devices(ctx8):
         assert torch.equal(t, ref), (k, m, S)
 
 
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_mixed_random_shapes(ctx, seed):
+    """60 objects of random k (1-24), m (1-10) and shard size (16 B-320 KiB,
+    a few not a multiple of 16), ragged last chunks, in one encode and one
+    reconstruct call (grouped launches and the per-(k, S) fallbacks mixed):
+    every parity equals the oracle's, every object with <= m erasures comes
+    back bit-exact, every object with more fails alone."""
+    torch = _torch()
+    rng = np.random.default_rng(seed)
+    objs, tens, dls = [], [], []
+    for _ in range(60):
+        k, m = int(rng.integers(1, 25)), int(rng.integers(1, 11))
+        S = int(rng.integers(1, 20001)) * 16 if rng.random() < 0.85 else int(rng.integers(1, 4000)) * 16 + 7
+        dl = [S] * (k - 1) + [int(rng.integers(1, S + 1))]
+        t = torch.randint(0, 256, (k + m, S), dtype=torch.uint8, device="cuda")
+        t[k - 1, dl[-1]:] = 0
+        objs.append((k, m, S))
+        tens.append(t)
+        dls.append(dl)
+    dptr = [t[j].data_ptr() for (k, m, S), t in zip(objs, tens) for j in range(k)]
+    pptr = [t[k + i].data_ptr() for (k, m, S), t in zip(objs, tens) for i in range(m)]
+    dlen = [x for dl in dls for x in dl]
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(objs, dptr, pptr, data_len=dlen)
+    torch.cuda.synchronize()
+    for (k, m, S), t, dl in zip(objs, tens, dls):
+        h = t.cpu().numpy()
+        want = oracle.encode([h[j][:dl[j]] for j in range(k)], m, S)
+        for i in range(m):
+            assert np.array_equal(h[k + i], want[i]), (k, m, S, i)
+    refs = [t.clone() for t in tens]
+    present, sptr, slen, fail = [], [], [], []
+    for o, ((k, m, S), t, dl) in enumerate(zip(objs, tens, dls)):
+        e = int(rng.integers(1, m + 1)) if o % 7 else min(k + m, m + 1)
+        p = np.ones(k + m, np.uint8)
+        for i in rng.choice(k + m, e, replace=False):
+            p[i] = 0
+            t[int(i)].fill_(0x99)
+        if e > m:
+            fail.append(o)
+        present.append(p)
+        sptr += [t[i].data_ptr() for i in range(k + m)]
+        slen += dl + [S] * m
+    pres = np.concatenate(present)
+    torch.cuda.synchronize()
+    rc, status = ctx.reconstruct_batch_device(objs, sptr, pres, shard_len=slen)
+    torch.cuda.synchronize()
+    assert [o for o, st in enumerate(status) if st] == fail
+    assert rc == (E_TOO_FEW_PRESENT if fail else 0)
+    for o, ((k, m, S), t, dl, ref) in enumerate(zip(objs, tens, dls, refs)):
+        if o in fail:
+            continue
+        t[k - 1, dl[-1]:] = 0
+        assert torch.equal(t, ref), (o, k, m, S)
+
+
 def test_mixed_batch_argument_errors(ctx):
     """Crate argument errors answer before any work (k = 0, k + m > 256, a
     zero shard size)."""
