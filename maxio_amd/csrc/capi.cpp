@@ -476,6 +476,8 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_ob
             dsum += uint64_t(objs[o].k);
             psum += uint64_t(objs[o].m);
         }
+        for (uint64_t i = 0; i < psum; ++i)
+            if (!parity[i]) return set_error(MXEC_E_INVALID_ARG, "null parity pointer " + std::to_string(i));
         std::vector<uint64_t> dl(static_cast<size_t>(dsum)), pl(static_cast<size_t>(psum));
         for (uint64_t o = 0; o < n_obj; ++o) {
             for (int j = 0; j < objs[o].k; ++j) {
@@ -484,6 +486,8 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_ob
             }
             for (int i = 0; i < objs[o].m; ++i) pl[pofs[o] + uint64_t(i)] = objs[o].shard_size;
         }
+        for (uint64_t j = 0; j < dsum; ++j)
+            if (!data[j] && dl[j]) return set_error(MXEC_E_INVALID_ARG, "null data pointer " + std::to_string(j));
         // One launch per parity count m: objects of every k and shard size
         // share it (run_rs_mixed; unaligned or m > 8: per (k, shard_size)).
         std::map<int, std::vector<RsMixedObject>> groups;
@@ -675,6 +679,10 @@ int mxec_reconstruct_batch_device(mxec_ctx* ctx, int dev, void* stream, const mx
         MXEC_TRY(ds.open(ctx, dev));
         Slot& slot = *ds.slot;
         hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
+        // Every shard pointer is needed: present ones are read, missing ones
+        // are where the rebuilt bytes go (a NULL would fault the device).
+        for (uint64_t g = 0; g < sum; ++g)
+            if (!shards[g]) return set_error(MXEC_E_INVALID_ARG, "null shard pointer " + std::to_string(g));
         std::vector<uint64_t> len(static_cast<size_t>(sum));
         std::vector<BatchObj> bo(static_cast<size_t>(n_obj));
         for (uint64_t o = 0; o < n_obj; ++o) {

@@ -421,3 +421,8 @@ def test_mixed_batch_argument_errors(ctx):
         assert rc == code, (objs, rc)
     with pytest.raises(maxio_amd.RSError):
         ctx.encode_batch_device([(0, 2, 64)], [0], [0, 0])
+    # a NULL output (a missing shard's buffer, a parity buffer) is refused, not written
+    rc, _ = ctx.reconstruct_batch_device([(2, 1, 64)], [0, 0, 0], np.array([1, 0, 1], np.uint8))
+    assert rc == -21
+    with pytest.raises(maxio_amd.RSError):
+        ctx.encode_batch_device([(2, 1, 64)], [0, 0], [0])
