@@ -749,6 +749,8 @@ int mxec_sha256_batch_device(mxec_ctx* ctx, int dev, void* stream, const uint8_t
     return guarded([&] {
         if (n == 0) return MXEC_OK;
         if (!bufs || !lens || !digests_dev) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        for (uint64_t i = 0; i < n; ++i)
+            if (!bufs[i]) return set_error(MXEC_E_INVALID_ARG, "null message pointer " + std::to_string(i));
         DevScope ds;
         MXEC_TRY(ds.open(ctx, dev));
         hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream

@@ -193,6 +193,8 @@ int mxec_body_sums_batch_device(mxec_ctx* ctx, int dev, void* stream, const uint
         if (n == 0 || which == 0) return MXEC_OK;
         if (!bodies_dev || !lens || !out_dev) return set_error(MXEC_E_INVALID_ARG, "null argument");
         if (which & ~uint32_t(0x1F)) return set_error(MXEC_E_INVALID_ARG, "unknown digest flag");
+        for (uint64_t i = 0; i < n; ++i)
+            if (!bodies_dev[i]) return set_error(MXEC_E_INVALID_ARG, "null body pointer " + std::to_string(i));
         DevScope ds;
         MXEC_TRY(ds.open(ctx, dev));
         std::vector<const uint8_t*> p(bodies_dev, bodies_dev + n);
