@@ -14,10 +14,11 @@ namespace mxec {
 // Bytes of input j at or beyond in_len[o][j] read as zero (the crate's
 // zero padding, filesystem.rs:1111 / chunk_reader.rs:192); output i is written
 // for b < out_len[o][i] only.
-struct alignas(16) RsGroupObj {  // one object of a grouped launch (below)
-    uint64_t tile0;  // its first tile in the launch's tile space
-    uint32_t in0;    // its first entry in in_ptrs / in_len
-    uint32_t k;      // its input count
+struct alignas(16) RsTileRec {  // one tile of a grouped launch (below)
+    uint32_t obj;    // its object
+    uint32_t k;      // the object's input count
+    uint32_t in0;    // the object's first entry in in_ptrs / in_len
+    uint32_t local;  // the tile's index within the object
 };
 struct RsArgs {
     const uint8_t* const* in_ptrs;  // [n_obj][k]
@@ -36,13 +37,11 @@ struct RsArgs {
     uint32_t aligned;               // all pointers 16-byte aligned (else every
                                     //   tile is in the edge list)
     // Grouped launch (objects of different k and shard size sharing r, every
-    // pointer aligned, r_total == r <= 8): when `group` is set, object o's
-    // inputs start at in_ptrs / in_len + group[o].in0, it has group[o].k of
-    // them and its tiles are [group[o].tile0, next object's tile0);
-    // tile_obj[t] names the object of launch tile t.  k and shard_size above
-    // are then unused.
-    const RsGroupObj* group = nullptr;
-    const uint32_t* tile_obj = nullptr;
+    // pointer aligned, r_total == r <= 8): when `tiles` is set, launch tile t
+    // is tiles[t] — its object, that object's k and first input entry, and
+    // the tile's index within the object.  k and shard_size above are then
+    // unused.
+    const RsTileRec* tiles = nullptr;
     uint64_t n_tiles = 0;
 };
 
@@ -53,12 +52,12 @@ struct RsVariant {
     int blocks_per_cu = 8;  // grid = n_cus * blocks_per_cu (grid-stride)
 };
 
-// Uniform launches, or grouped ones (a.group set: default variant, aligned).
+// Uniform launches, or grouped ones (a.tiles set: rs_group_variant, aligned).
 hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s);
 hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& v);
 // Geometry the default launch uses for a given total row count, and its tile.
 RsVariant rs_default_variant(uint32_t r_total);
-// Geometry of grouped launches (a.group set) for r rows.
+// Geometry of grouped launches (a.tiles set) for r rows.
 RsVariant rs_group_variant(uint32_t r);
 uint64_t rs_tile_bytes(const RsVariant& v);
 

@@ -166,7 +166,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         int r;
         const std::vector<RsMixedObject>* objs;
         uint64_t sum_k = 0, n_tiles = 0, tile = 0;
-        size_t o_in = 0, o_out = 0, o_inlen = 0, o_outlen = 0, o_coef = 0, o_grp = 0, o_tobj = 0;
+        size_t o_in = 0, o_out = 0, o_inlen = 0, o_outlen = 0, o_coef = 0, o_tiles = 0;
     };
     std::vector<Plan> grouped;
     std::vector<std::pair<int, const std::vector<RsMixedObject>*>> rest;
@@ -222,8 +222,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         p.o_inlen = w.add(8 * p.sum_k);
         p.o_outlen = w.add(8 * n * p.r);
         p.o_coef = w.add(4 * n);
-        p.o_grp = w.add(sizeof(RsGroupObj) * n);
-        p.o_tobj = w.add(4 * p.n_tiles);
+        p.o_tiles = w.add(sizeof(RsTileRec) * p.n_tiles);
     }
     char* hb = w.data();
     for (const Plan& p : grouped) {
@@ -233,8 +232,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         auto* il = reinterpret_cast<uint64_t*>(hb + p.o_inlen);
         auto* ol = reinterpret_cast<uint64_t*>(hb + p.o_outlen);
         auto* co = reinterpret_cast<uint32_t*>(hb + p.o_coef);
-        auto* gr = reinterpret_cast<RsGroupObj*>(hb + p.o_grp);
-        auto* to = reinterpret_cast<uint32_t*>(hb + p.o_tobj);
+        auto* tr = reinterpret_cast<RsTileRec*>(hb + p.o_tiles);
         uint64_t in0 = 0, t0 = 0;
         for (size_t o = 0; o < p.objs->size(); ++o) {
             const RsMixedObject& ob = (*p.objs)[o];
@@ -248,8 +246,8 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
             }
             co[o] = ob.o.coef_off;
             const uint64_t nt = (ob.shard_size + p.tile - 1) / p.tile;
-            gr[o] = RsGroupObj{t0, uint32_t(in0), uint32_t(ob.k)};
-            std::fill(to + t0, to + t0 + nt, uint32_t(o));
+            for (uint64_t t = 0; t < nt; ++t)
+                tr[t0 + t] = RsTileRec{uint32_t(o), uint32_t(ob.k), uint32_t(in0), uint32_t(t)};
             in0 += uint64_t(ob.k);
             t0 += nt;
         }
@@ -268,8 +266,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         a.r = a.r_total = uint32_t(p.r);
         a.row0 = 0;
         a.aligned = 1;
-        a.group = reinterpret_cast<const RsGroupObj*>(db + p.o_grp);
-        a.tile_obj = reinterpret_cast<const uint32_t*>(db + p.o_tobj);
+        a.tiles = reinterpret_cast<const RsTileRec*>(db + p.o_tiles);
         a.n_tiles = p.n_tiles;
         MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
     }

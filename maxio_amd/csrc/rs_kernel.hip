@@ -285,26 +285,31 @@ __device__ __forceinline__ Vec4 gload16_upto(gcptr p, int32_t valid, gcptr safe)
 //
 // GRP: a grouped launch — objects of different k and shard size that share
 // r (config 5's mixed classes, a server's batch of mixed requests) in one
-// grid: the tile's object comes from tile_obj, its k and input offset from
-// group[obj] (wave-uniform scalar loads, one 16-byte record per tile).
+// grid: a 16-byte record per tile (object, k, first input entry, tile within
+// the object), one wave-uniform scalar load, fetched one tile ahead so it
+// is in SGPRs when the tile starts (the uniform kernel computes the same
+// from the tile index).
 template <int R, int V, bool NT, bool GRP>
 __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
     const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint32_t k_uniform,
     uint32_t r_total, uint32_t row0, uint32_t tiles_per_obj, uint64_t n_tiles,
-    const RsGroupObj* __restrict__ group, const uint32_t* __restrict__ tile_obj) {
+    const RsTileRec* __restrict__ tiles) {
     constexpr uint32_t kTile = kThreads * 16 * V;
     const gcptr safe = (gcptr)(reinterpret_cast<const uint8_t*>(coef));
+    RsTileRec next{};
+    if constexpr (GRP) next = tiles[blockIdx.x];  // the grid never exceeds n_tiles
     for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         uint32_t obj, k;
         uint64_t base, in0;
         if constexpr (GRP) {
-            obj = tile_obj[tile];
-            const RsGroupObj g = group[obj];
-            base = (tile - g.tile0) * kTile;
-            k = g.k;
-            in0 = g.in0;
+            const RsTileRec cur = next;
+            if (tile + gridDim.x < n_tiles) next = tiles[tile + gridDim.x];
+            obj = cur.obj;
+            k = cur.k;
+            in0 = cur.in0;
+            base = uint64_t(cur.local) * kTile;
         } else {
             obj = uint32_t(tile / tiles_per_obj);
             base = (tile - uint64_t(obj) * tiles_per_obj) * kTile;
@@ -411,7 +416,7 @@ hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles
                        hipStream_t s) {
     hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                        a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.k, a.r_total,
-                       a.row0, tiles_per_obj, n_tiles, a.group, a.tile_obj);
+                       a.row0, tiles_per_obj, n_tiles, a.tiles);
     return hipGetLastError();
 }
 
@@ -515,8 +520,8 @@ hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, co
 }
 
 hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
-    if (a.group) {
-        if (!a.aligned || !a.tile_obj || a.row0 != 0 || a.r != a.r_total) return hipErrorInvalidValue;
+    if (a.tiles) {
+        if (!a.aligned || a.row0 != 0 || a.r != a.r_total) return hipErrorInvalidValue;
         if (a.n_tiles == 0) return hipSuccess;
         switch (a.r) {
             case 1: return launch_grouped<1>(a, n_cus, s);

@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT}"
 O=gpurun_out/ab; mkdir -p $O
-for r in 1 2; do
+for r in ${ROUNDS:-1 2}; do
  for v in prev new; do
   if [ $v = prev ]; then export MXEC_LIB=$PWD/build_ab/libmaxio_ec_prev.so; else unset MXEC_LIB; fi
   for c in ${CONFIGS:-3c}; do
