@@ -50,6 +50,7 @@ struct RsVariant {
     int vecs = 2;           // 16-byte column vectors per lane per tile (1, 2, 4)
     bool nt = false;        // nontemporal loads / stores
     int blocks_per_cu = 8;  // grid = n_cus * blocks_per_cu (grid-stride)
+    int min_waves = 0;      // 3: compile for >= 3 waves per SIMD (<= 168 VGPRs; V = 4, nt)
 };
 
 // Uniform launches, or grouped ones (a.tiles set: rs_group_variant, aligned).

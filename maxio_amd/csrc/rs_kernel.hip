@@ -289,8 +289,8 @@ __device__ __forceinline__ Vec4 gload16_upto(gcptr p, int32_t valid, gcptr safe)
 // the object), one wave-uniform scalar load, fetched one tile ahead so it
 // is in SGPRs when the tile starts (the uniform kernel computes the same
 // from the tile index).
-template <int R, int V, bool NT, bool GRP>
-__global__ __launch_bounds__(kThreads) void rs_apply_fast(
+template <int R, int V, bool NT, bool GRP, int OCC = 1>
+__global__ __launch_bounds__(kThreads, OCC) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
     const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint32_t k_uniform,
@@ -411,10 +411,10 @@ __global__ __launch_bounds__(kThreads) void rs_apply_fast(
     }
 }
 
-template <int R, int V, bool NT, bool GRP = false>
+template <int R, int V, bool NT, bool GRP = false, int OCC = 1>
 hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
-    hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP, OCC>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                        a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.k, a.r_total,
                        a.row0, tiles_per_obj, n_tiles, a.tiles);
     return hipGetLastError();
@@ -445,6 +445,8 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
                                       : launch_fast<R, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (var.vecs == 2) e = var.nt ? launch_fast<R, 2, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                            : launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (R == 4 && var.vecs == 4 && var.nt && var.min_waves == 3)
+            e = launch_fast<R, 4, true, false, R == 4 ? 3 : 1>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                            : launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
         return e;
@@ -470,24 +472,31 @@ uint64_t rs_tile_bytes(const RsVariant& v) { return uint64_t(kThreads) * 16 * ui
 
 // Default geometry, from tools/kernel_lab sweeps on MI355X (profiles/): four
 // 16-byte vectors per lane with nontemporal loads/stores while the
-// accumulators fit (R <= 4: <= 158 VGPRs), two beyond that; 32 workgroups per
-// CU of grid-stride (16 beat 8 and 4 on every shape swept; 32 gained another
-// 0.8-0.9 % on one box and was level on another,
-// profiles/r1_lab_copy_pattern_ceilings.jsonl).  Chosen by the
+// accumulators fit (R <= 4: <= 173 VGPRs, two waves per SIMD; compiled for
+// three, 164 VGPRs, measured 1.2-1.6 % slower), two beyond that; 256
+// workgroups per CU of grid-stride.  Round 1 swept 4-64 (16 beat 8 and 4,
+// 32 level or +0.9 %); round 2 swept 32-4096 in one process per box: 256
+// over 32 gains 1.5-4 % in the bench's object-major layout (north star
+// +3.1 %, cfg 4 +2.3 %, cfg 2 +1.5 %, cfg 3 decode +4.1 %) and 3-5 % with
+// data and parity apart, where 1024-2048 gain more (5-12 %) but lose again
+// in the object-major layout (profiles/r2_lab_rs_grid_*.jsonl).  Fewer tiles
+// per workgroup keep the tiles in flight closer together: with few large
+// grid-stride workgroups, resident ones run different iterations and the
+// chip's active tiles spread over many windows of memory.  Chosen by the
 // launch's total row count so every row group of a launch shares one tile
 // size (and one edge list).
 RsVariant rs_default_variant(uint32_t r_total) {
     RsVariant v;
     v.vecs = r_total <= 4 ? 4 : 2;
     v.nt = true;
-    v.blocks_per_cu = 32;
+    v.blocks_per_cu = 256;
     return v;
 }
 
 // Grouped launches (mixed batches: many objects of a few tiles each) take the
-// default geometry with 64 workgroups per CU of grid-stride: config 5 measured
-// 32 / 48 / 64 / 128 / one tile per workgroup within ~1 %, 64 at the top
-// with 128, V = 2 3-4 % slower (profiles/r2_rs_group_geometry.txt).
+// default geometry: config 5 measured 32 / 48 / 64 / 128 / 256 / 2048 /
+// one tile per workgroup within ~1 %, V = 2 3-4 % slower
+// (profiles/r2_rs_group_geometry.txt, r2_rs_grid_bench_ab.txt).
 // MXEC_RS_GROUP_VECS (2 | 4) and MXEC_RS_GROUP_BPC override it for labs.
 RsVariant rs_group_variant(uint32_t r) {
     static const int env_v = [] {
@@ -499,7 +508,7 @@ RsVariant rs_group_variant(uint32_t r) {
         return e ? atoi(e) : 0;
     }();
     RsVariant v = rs_default_variant(r);
-    v.blocks_per_cu = 64;
+    v.blocks_per_cu = 256;
     if (r <= 4 && (env_v == 2 || env_v == 4)) v.vecs = env_v;
     if (env_b > 0 && env_b <= 4096) v.blocks_per_cu = env_b;
     return v;

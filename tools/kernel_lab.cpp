@@ -212,9 +212,17 @@ struct Batch {
         std::vector<uint8_t*> op(sh.n * sh.r);
         std::vector<uint64_t> il(sh.n * sh.k, sh.S), ol(sh.n * sh.r, sh.S);
         std::vector<uint32_t> co(sh.n, 0);
+        // MXEC_LAB_OM=1: the bench's object-major layout ([n][k+r][S + pad],
+        // pad 2 MiB + 64 KiB for multi-MiB shards) from `data`; else data
+        // [n][k][S] and parity [n][r][S] apart.
+        const bool om = getenv("MXEC_LAB_OM") != nullptr;
+        const uint64_t ss = sh.S + (sh.S >= (4u << 20) ? (2u << 20) + (64u << 10) : 0);
         for (uint64_t o = 0; o < sh.n; ++o) {
-            for (int j = 0; j < sh.k; ++j) ip[o * sh.k + j] = data + (o * sh.k + j) * sh.S;
-            for (int i = 0; i < sh.r; ++i) op[o * sh.r + i] = par + (o * sh.r + i) * sh.S;
+            for (int j = 0; j < sh.k; ++j)
+                ip[o * sh.k + j] = om ? data + (o * (sh.k + sh.r) + j) * ss : data + (o * sh.k + j) * sh.S;
+            for (int i = 0; i < sh.r; ++i)
+                op[o * sh.r + i] = om ? const_cast<uint8_t*>(data) + (o * (sh.k + sh.r) + sh.k + i) * ss
+                                      : par + (o * sh.r + i) * sh.S;
         }
         size_t bytes = ip.size() * 8 + op.size() * 8 + il.size() * 8 + ol.size() * 8 + co.size() * 4 + 64;
         CK(hipMalloc(&mem, bytes));
@@ -247,7 +255,8 @@ int main(int argc, char** argv) {
     Timer tm;
     // One pool for everything: config 2 at n2 objects = n2 * 60 MiB.
     const uint64_t S2 = 10ull << 20;
-    const uint64_t pool = n2 * 6 * S2;
+    // (object-major mode: 10 MiB shards padded by 2 MiB + 64 KiB)
+    const uint64_t pool = n2 * 6 * (getenv("MXEC_LAB_OM") ? S2 + (2u << 20) + (64u << 10) : S2);
     uint8_t* buf;
     CK(hipMalloc(&buf, pool));
     CK(hipMemset(buf, 0x5A, pool));
@@ -355,8 +364,16 @@ int main(int argc, char** argv) {
             // profiles/r1_lab_hbm_ceilings_tile_order.jsonl.)
             for (int bpc : {8, 16, 32}) vs.push_back(mxec::RsVariant{4, true, bpc});
         } else if (ns_only) {
-            for (int v : {2, 4})
-                for (int bpc : {8, 16, 32, 64}) vs.push_back(mxec::RsVariant{v, true, bpc});
+            // V = 4: workgroups per CU of grid-stride, alternating, three
+            // rounds; MXEC_LAB_MW=3 adds the R = 4 kernel compiled for 3
+            // waves per SIMD (164 VGPRs against 173: measured 1.2-1.6 %
+            // slower, profiles/r2_lab_ns_occupancy.jsonl)
+            const bool mw = getenv("MXEC_LAB_MW") != nullptr;
+            for (int rep = 0; rep < 3; ++rep)
+                for (int bpc : {32, 256, 1024, 2048, 4096}) {
+                    vs.push_back(mxec::RsVariant{4, true, bpc, 0});
+                    if (mw) vs.push_back(mxec::RsVariant{4, true, bpc, 3});
+                }
         } else if (full) {
             for (int v : {1, 2, 4})
                 for (bool nt : {false, true})
@@ -371,14 +388,15 @@ int main(int argc, char** argv) {
         const uint64_t par_bytes = sh.n * sh.r * sh.S;
         uint8_t* ref = nullptr;
         unsigned long long* bad = nullptr;
-        if (hbm_only) {
+        const bool check = (hbm_only || ns_only) && !getenv("MXEC_LAB_OM");  // OM: parity is inside the data
+        if (check) {
             CK(hipMalloc(&ref, par_bytes));
             CK(hipMalloc(&bad, 8));
             CK(mxec::launch_rs_apply_variant(b.a, cus, 0, mxec::RsVariant{4, true, 16}));
             CK(hipMemcpy(ref, par, par_bytes, hipMemcpyDeviceToDevice));
         }
         for (const auto& v : vs) {
-            if (hbm_only) {
+            if (check) {
                 CK(hipMemset(par, 0, par_bytes));
                 CK(mxec::launch_rs_apply_variant(b.a, cus, 0, v));
                 CK(hipMemset(bad, 0, 8));
@@ -386,11 +404,12 @@ int main(int argc, char** argv) {
                                    reinterpret_cast<const u32x4*>(ref), par_bytes / 16, bad);
                 unsigned long long nb = 0;
                 CK(hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost));
-                std::printf("{\"what\": \"check\", \"v\": %d, \"bpc\": %d, \"bad16\": %llu}\n", v.vecs, v.blocks_per_cu, nb);
+                std::printf("{\"what\": \"check\", \"v\": %d, \"bpc\": %d, \"min_waves\": %d, \"bad16\": %llu}\n",
+                            v.vecs, v.blocks_per_cu, v.min_waves, nb);
             }
             double ms = tm.median_ms([&] { CK(mxec::launch_rs_apply_variant(b.a, cus, 0, v)); });
             char nm[96];
-            std::snprintf(nm, sizeof nm, "rs_v%d_nt%d_bpc%d", v.vecs, int(v.nt), v.blocks_per_cu);
+            std::snprintf(nm, sizeof nm, "rs_v%d_nt%d_bpc%d_mw%d", v.vecs, int(v.nt), v.blocks_per_cu, v.min_waves);
             report(nm, name, ms, bytes);
         }
         (void)hipFree(coef);
@@ -431,10 +450,10 @@ int main(int argc, char** argv) {
         return 0;
     }
     if (ns_only) {
-        for (int rep = 0; rep < 2; ++rep) {
-            sweep(Shape{8, 4, 1ull << 20, n2 * 60 / 12}, "k8m4 S1MiB (north star)", true);
-            sweep(Shape{4, 2, S2, n2}, "k4m2 S10MiB (cfg2)", true);
-        }
+        sweep(Shape{8, 4, 1ull << 20, n2 * 60 / 12}, "k8m4 S1MiB (north star)", true);
+        sweep(Shape{4, 2, S2, n2}, "k4m2 S10MiB (cfg2)", true);
+        sweep(Shape{10, 4, 1ull << 20, n2 * 60 / 14}, "k10m4 S1MiB (cfg4)", true);
+        sweep(Shape{8, 2, 1ull << 20, 1024}, "k8r2 S1MiB x1024 (cfg3 decode)", true);
         CK(hipFree(buf));
         return 0;
     }
