@@ -15,7 +15,7 @@
 //   mxprobe_rs_pattern the RS kernel's own access pattern with the GF math
 //                      replaced by XOR: object-major [n][k][S] in,
 //                      [n][m][S] out, tiles of 256 lanes x 16 B x 4 vectors,
-//                      4 inputs x 4 vectors of loads in flight, 256 WG per CU
+//                      4 inputs x 4 vectors of loads in flight, 512 WG per CU
 //                      (the ceiling the RS kernel is measured against)
 #include <hip/hip_runtime.h>
 
@@ -184,7 +184,7 @@ extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32
     if (k == 0 || (k & 3) || S == 0 || (S % 16384) ||
         ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
         return int(hipErrorInvalidValue);
-    const dim3 g(uint32_t(grid() * 16)), b(256);  // 256 WG per CU, as the RS kernel
+    const dim3 g(uint32_t(grid() * 32)), b(256);  // 512 WG per CU, as the RS kernel
     const auto* in = static_cast<const uint8_t*>(data);
     auto* out = static_cast<uint8_t*>(parity);
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -209,7 +209,7 @@ extern "C" int mxprobe_rs_pattern_policy(const void* data, void* parity, uint32_
     if (k == 0 || (k & 3) || S == 0 || (S % 16384) || policy < 0 || policy > 4 ||
         ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
         return int(hipErrorInvalidValue);
-    const dim3 g(uint32_t(grid() * 16)), b(256);
+    const dim3 g(uint32_t(grid() * 32)), b(256);
     const auto* in = static_cast<const uint8_t*>(data);
     auto* out = static_cast<uint8_t*>(parity);
     hipStream_t s = static_cast<hipStream_t>(stream);

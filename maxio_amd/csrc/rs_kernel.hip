@@ -473,13 +473,14 @@ uint64_t rs_tile_bytes(const RsVariant& v) { return uint64_t(kThreads) * 16 * ui
 // Default geometry, from tools/kernel_lab sweeps on MI355X (profiles/): four
 // 16-byte vectors per lane with nontemporal loads/stores while the
 // accumulators fit (R <= 4: <= 173 VGPRs, two waves per SIMD; compiled for
-// three, 164 VGPRs, measured 1.2-1.6 % slower), two beyond that; 256
+// three, 164 VGPRs, measured 1.2-1.6 % slower), two beyond that; 512
 // workgroups per CU of grid-stride.  Round 1 swept 4-64 (16 beat 8 and 4,
 // 32 level or +0.9 %); round 2 swept 32-4096 in one process per box: 256
 // over 32 gains 1.5-4 % in the bench's object-major layout (north star
 // +3.1 %, cfg 4 +2.3 %, cfg 2 +1.5 %, cfg 3 decode +4.1 %) and 3-5 % with
-// data and parity apart, where 1024-2048 gain more (5-12 %) but lose again
-// in the object-major layout (profiles/r2_lab_rs_grid_*.jsonl).  Fewer tiles
+// data and parity apart, 512 another 0.4-2.1 % / 1-3 %; 1024-2048 gain more
+// with data and parity apart (5-12 % over 32) but lose again in the
+// object-major layout (profiles/r2_lab_rs_grid_*.jsonl).  Fewer tiles
 // per workgroup keep the tiles in flight closer together: with few large
 // grid-stride workgroups, resident ones run different iterations and the
 // chip's active tiles spread over many windows of memory.  Chosen by the
@@ -489,7 +490,7 @@ RsVariant rs_default_variant(uint32_t r_total) {
     RsVariant v;
     v.vecs = r_total <= 4 ? 4 : 2;
     v.nt = true;
-    v.blocks_per_cu = 256;
+    v.blocks_per_cu = 512;
     return v;
 }
 
@@ -508,7 +509,7 @@ RsVariant rs_group_variant(uint32_t r) {
         return e ? atoi(e) : 0;
     }();
     RsVariant v = rs_default_variant(r);
-    v.blocks_per_cu = 256;
+    v.blocks_per_cu = 512;
     if (r <= 4 && (env_v == 2 || env_v == 4)) v.vecs = env_v;
     if (env_b > 0 && env_b <= 4096) v.blocks_per_cu = env_b;
     return v;
