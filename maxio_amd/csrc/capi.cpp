@@ -178,6 +178,18 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
                     ok = false;
                     break;
                 }
+                // Descriptor ring entries at their 1 MiB floor now, so the
+                // first calls on each slot do not allocate (and a later
+                // re-size, which frees and so waits for the device, is rare).
+                for (auto& rb : slot->ring)
+                    if (rb.host.grow(1) || rb.dev.grow(1)) {
+                        ok = false;
+                        break;
+                    }
+                if (!ok) {
+                    slot_destroy(*slot);
+                    break;
+                }
                 dev->slots.push_back(std::move(slot));
             }
             if (ok) ctx->c.devs.push_back(std::move(dev));
@@ -269,7 +281,7 @@ int mxec_sha256_batch(mxec_ctx* ctx, const uint8_t* const* bufs, const size_t* l
             total += round_up(lens[i] ? lens[i] : 1, kSlotAlign);
         }
         MXEC_TRY(slot.shards.ensure(total));
-        MXEC_TRY(slot.digests.ensure(n * 32));
+        MXEC_TRY(slot.digests.grow(n * 32));
         auto* base = static_cast<uint8_t*>(slot.shards.p);
         std::vector<const uint8_t*> ptrs(n);
         std::vector<uint64_t> l(n);
@@ -573,12 +585,12 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 // A batch that fills the chip: its own launch on `stream`,
                 // digests compared on the device (the verify kernel compares
                 // message t against expected[idx[t]]), n flags read back.
-                MXEC_TRY(slot.digests.ensure(ptrs.size()));
+                MXEC_TRY(slot.digests.grow(ptrs.size()));
                 auto* ok = static_cast<uint8_t*>(slot.digests.p);
                 const uint32_t* tmo = nullptr;
                 MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx, nullptr, 0, &tmo));
                 const size_t fo = (ptrs.size() + 15) & ~size_t(15);
-                MXEC_TRY(slot.hdig.ensure(fo + 16));
+                MXEC_TRY(slot.hdig.grow(fo + 16));
                 auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + fo);
                 *hflag = 0;
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok, ptrs.size(), hipMemcpyDeviceToHost, s));
@@ -609,7 +621,7 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                 // ends up short of k shards may have its missing shards
                 // overwritten by the speculative decode.
                 const size_t ne = size_t(n_obj) * size_t(total) * 32;
-                MXEC_TRY(slot.hdig.ensure(ne));
+                MXEC_TRY(slot.hdig.grow(ne));
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, expected_sha_dev, ne, hipMemcpyDeviceToHost, s));
                 if (!slot.ready_ev) MXEC_HIP(hipEventCreateWithFlags(&slot.ready_ev, hipEventDisableTiming));
                 MXEC_HIP(hipEventRecord(slot.ready_ev, s));
@@ -707,12 +719,12 @@ int mxec_reconstruct_batch_device(mxec_ctx* ctx, int dev, void* stream, const mx
                     idx.push_back(g);
                 }
             if (!ptrs.empty()) {
-                MXEC_TRY(slot.digests.ensure(ptrs.size()));
+                MXEC_TRY(slot.digests.grow(ptrs.size()));
                 auto* ok = static_cast<uint8_t*>(slot.digests.p);
                 const uint32_t* tmo = nullptr;
                 MXEC_TRY(run_sha(*ds.d, slot, s, ptrs, lens, nullptr, expected_sha_dev, ok, &idx, nullptr, 0, &tmo));
                 const size_t fo = (ptrs.size() + 15) & ~size_t(15);
-                MXEC_TRY(slot.hdig.ensure(fo + 16));
+                MXEC_TRY(slot.hdig.grow(fo + 16));
                 auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + fo);
                 *hflag = 0;
                 MXEC_HIP(hipMemcpyAsync(slot.hdig.p, ok, ptrs.size(), hipMemcpyDeviceToHost, s));

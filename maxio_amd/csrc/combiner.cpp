@@ -89,7 +89,7 @@ struct ShaCombiner {
         // arrive together (config 3c: the decodes of the previous step).
         for (const Req* r : batch)
             if (r->ready) MXEC_HIP(hipStreamWaitEvent(s, r->ready, 0));
-        MXEC_TRY(slot.digests.ensure(n * 32));
+        MXEC_TRY(slot.digests.grow(n * 32));
         // The split (producer / consumer) form up to 3/4 of a 64-message
         // group per SIMD; beyond, the stream form (segments of every chain
         // dealt to persistent waves) keeps every SIMD busy to the end
@@ -117,7 +117,7 @@ struct ShaCombiner {
             std::fprintf(stderr, "[mxec combine] after-launch work %lld us\n",
                          (long long)std::chrono::duration_cast<std::chrono::microseconds>(
                              std::chrono::steady_clock::now() - ta).count());
-        MXEC_TRY(slot.hdig.ensure(n * 32 + 16));
+        MXEC_TRY(slot.hdig.grow(n * 32 + 16));
         auto* hflag = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(slot.hdig.p) + n * 32);
         *hflag = 0;
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
@@ -240,9 +240,9 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // Opted out by MXEC_COMBINE_BELOW: its own launch on the caller's
         // stream (the kernel picks its form by message count).
         const size_t n = ptrs.size();
-        MXEC_TRY(slot.digests.ensure(n * 32));
+        MXEC_TRY(slot.digests.grow(n * 32));
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr));
-        MXEC_TRY(slot.hdig.ensure(n * 32));
+        MXEC_TRY(slot.hdig.grow(n * 32));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, slot.digests.p, n * 32, hipMemcpyDeviceToHost, s));
         if (after_launch) MXEC_TRY((*after_launch)());  // same stream: after the hash, not beside it
         MXEC_TRY(slot_wait(slot, s));

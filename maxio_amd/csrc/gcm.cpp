@@ -310,7 +310,7 @@ int mxec_frames_decrypt(mxec_ctx* ctx, const uint8_t key[32], uint64_t first_ind
         const uint64_t a_in = round_up(need, kSlotAlign), a_out = round_up(plaintext_size, kSlotAlign);
         const uint64_t a_aad = round_up(uint64_t(aad_len) * nf, kSlotAlign);
         MXEC_TRY(slot.shards.ensure(a_in + a_out + a_aad));
-        MXEC_TRY(slot.digests.ensure(nf * sizeof(int32_t)));
+        MXEC_TRY(slot.digests.grow(nf * sizeof(int32_t)));
         auto* base = static_cast<uint8_t*>(slot.shards.p);
         std::vector<UploadSeg> up{{0, frames, need}};
         if (aad_len) up.push_back({a_in + a_out, aad, uint64_t(aad_len) * nf});
@@ -318,7 +318,7 @@ int mxec_frames_decrypt(mxec_ctx* ctx, const uint8_t key[32], uint64_t first_ind
         Job jb{key, 0, frame_size, first_index, base + a_in + a_out, aad_len, base, plaintext_size, base + a_in};
         auto* st_dev = static_cast<int32_t*>(slot.digests.p);
         MXEC_TRY(run_frames(*ds.d, slot, s, {jb}, true, st_dev));
-        MXEC_TRY(slot.hdig.ensure(nf * sizeof(int32_t)));
+        MXEC_TRY(slot.hdig.grow(nf * sizeof(int32_t)));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, st_dev, nf * sizeof(int32_t), hipMemcpyDeviceToHost, s));
         MXEC_TRY(slot_wait(slot, s));
         MXEC_TRY(frame_error(static_cast<const int32_t*>(slot.hdig.p), nf, first_index, frames, frame_size,
@@ -368,10 +368,10 @@ int mxec_frames_decrypt_device(mxec_ctx* ctx, int dev, void* stream, const mxec_
         Slot& slot = *ds.slot;
         hipStream_t s = static_cast<hipStream_t>(stream);
         const uint64_t nf = first[n_jobs];
-        MXEC_TRY(slot.digests.ensure(std::max<uint64_t>(1, nf) * sizeof(int32_t)));
+        MXEC_TRY(slot.digests.grow(std::max<uint64_t>(1, nf) * sizeof(int32_t)));
         auto* st_dev = static_cast<int32_t*>(slot.digests.p);
         MXEC_TRY(run_frames(*ds.d, slot, s, js, true, st_dev));
-        MXEC_TRY(slot.hdig.ensure(std::max<uint64_t>(1, nf) * sizeof(int32_t)));
+        MXEC_TRY(slot.hdig.grow(std::max<uint64_t>(1, nf) * sizeof(int32_t)));
         if (nf) MXEC_HIP(hipMemcpyAsync(slot.hdig.p, st_dev, nf * sizeof(int32_t), hipMemcpyDeviceToHost, s));
         MXEC_TRY(slot_wait(slot, s));
         const auto* st = static_cast<const int32_t*>(slot.hdig.p);

@@ -256,8 +256,8 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
         buf_->pending = false;
     }
     const size_t n = tmp_.empty() ? 16 : tmp_.size();
-    MXEC_TRY(buf_->host.ensure(n));
-    MXEC_TRY(buf_->dev.ensure(n));
+    MXEC_TRY(buf_->host.grow(n));
+    MXEC_TRY(buf_->dev.grow(n));
     std::memcpy(buf_->host.p, tmp_.data(), tmp_.size());
     // Large tables (a mixed batch's: MiBs) go on the side stream; small ones
     // stay in the launch stream, where the extra cross-stream wait measured
@@ -284,7 +284,7 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
 
 int DescWriter::scratch(size_t bytes, void** dev) {
     if (arena_ || !buf_) return set_error(MXEC_E_INVALID_ARG, "descriptor scratch needs a committed ring entry");
-    MXEC_TRY(buf_->scratch.ensure(bytes));
+    MXEC_TRY(buf_->scratch.grow(bytes));
     *dev = buf_->scratch.p;
     return MXEC_OK;
 }

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <cstdint>
@@ -35,18 +36,26 @@ const char* last_error();
         if (_rc != MXEC_OK) return _rc; \
     } while (0)
 
+// ensure(n): at least n bytes.  grow(n): the same for buffers that are
+// re-sized call after call (descriptor rings, per-launch scratch): at least
+// 1 MiB and at least twice the old capacity, so they reach their working
+// size in a few steps -- a re-size frees the old buffer, and hipFree waits
+// for the whole device (a host-side stall between two kernels).
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
     int ensure(size_t n);
+    int grow(size_t n) { return n <= cap && p ? 0 : ensure(std::max(std::max(n, cap * 2), kGrowFloor)); }
     void release();
     ~DevBuf() { release(); }
+    static constexpr size_t kGrowFloor = size_t(1) << 20;
 };
 
 struct PinnedBuf {
     void* p = nullptr;
     size_t cap = 0;
     int ensure(size_t n);
+    int grow(size_t n) { return n <= cap && p ? 0 : ensure(std::max(std::max(n, cap * 2), DevBuf::kGrowFloor)); }
     void release();
     ~PinnedBuf() { release(); }
 };

@@ -222,7 +222,7 @@ int mxec_body_sums_batch(mxec_ctx* ctx, const uint8_t* const* bodies, const uint
             total += round_up(lens[i], kSlotAlign);
         }
         MXEC_TRY(slot.shards.ensure(std::max<uint64_t>(total, 1)));
-        MXEC_TRY(slot.digests.ensure(n * sizeof(mxec_body_sums)));
+        MXEC_TRY(slot.digests.grow(n * sizeof(mxec_body_sums)));
         auto* base = static_cast<uint8_t*>(slot.shards.p);
         std::vector<const uint8_t*> p(n);
         std::vector<uint64_t> l(lens, lens + n);
@@ -234,7 +234,7 @@ int mxec_body_sums_batch(mxec_ctx* ctx, const uint8_t* const* bodies, const uint
         MXEC_TRY(upload_segments(slot, s, base, up));
         auto* rec = static_cast<uint8_t*>(slot.digests.p);
         MXEC_TRY(run_body_sums(*ds.d, slot, s, p, l, which, rec, sizeof(mxec_body_sums)));
-        MXEC_TRY(slot.hdig.ensure(n * sizeof(mxec_body_sums)));
+        MXEC_TRY(slot.hdig.grow(n * sizeof(mxec_body_sums)));
         MXEC_HIP(hipMemcpyAsync(slot.hdig.p, rec, n * sizeof(mxec_body_sums), hipMemcpyDeviceToHost, s));
         MXEC_TRY(slot_wait(slot, s));
         const auto* h = static_cast<const mxec_body_sums*>(slot.hdig.p);
