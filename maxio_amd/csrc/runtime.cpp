@@ -28,8 +28,21 @@ int DevBuf::ensure(size_t n) {
     return MXEC_OK;
 }
 
+int DevBuf::grow(size_t n) {
+    if (n <= cap && p) return MXEC_OK;
+    const size_t want = std::max(std::max(n, cap * 2), kGrowFloor);
+    void* q = nullptr;
+    MXEC_HIP(hipMalloc(&q, want));
+    if (p) retired.push_back(p);
+    p = q;
+    cap = want;
+    return MXEC_OK;
+}
+
 void DevBuf::release() {
     if (p) (void)hipFree(p);
+    for (void* q : retired) (void)hipFree(q);
+    retired.clear();
     p = nullptr;
     cap = 0;
 }
@@ -223,8 +236,21 @@ int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const 
     return drain(prev, buf ^ 1);
 }
 
+int PinnedBuf::grow(size_t n) {
+    if (n <= cap && p) return MXEC_OK;
+    const size_t want = std::max(std::max(n, cap * 2), DevBuf::kGrowFloor);
+    void* q = nullptr;
+    MXEC_HIP(hipHostMalloc(&q, want, hipHostMallocDefault));
+    if (p) retired.push_back(p);
+    p = q;
+    cap = want;
+    return MXEC_OK;
+}
+
 void PinnedBuf::release() {
     if (p) (void)hipHostFree(p);
+    for (void* q : retired) (void)hipHostFree(q);
+    retired.clear();
     p = nullptr;
     cap = 0;
 }

@@ -36,16 +36,20 @@ const char* last_error();
         if (_rc != MXEC_OK) return _rc; \
     } while (0)
 
-// ensure(n): at least n bytes.  grow(n): the same for buffers that are
-// re-sized call after call (descriptor rings, per-launch scratch): at least
-// 1 MiB and at least twice the old capacity, so they reach their working
-// size in a few steps -- a re-size frees the old buffer, and hipFree waits
-// for the whole device (a host-side stall between two kernels).
+// ensure(n): at least n bytes (a re-size frees the old buffer, and hipFree
+// waits for the whole device).  grow(n): for buffers re-sized call after
+// call while earlier launches may still read them (descriptor rings,
+// per-launch scratch, digest landing zones): at least 1 MiB and at least
+// twice the old capacity, and the old buffer is retired, not freed, until
+// release() -- a free there stalled the host until the device drained,
+// leaving the GPU idle ~0.5-1 ms before the next launch.  Geometric growth
+// keeps the retired bytes below the live ones.
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    std::vector<void*> retired;
     int ensure(size_t n);
-    int grow(size_t n) { return n <= cap && p ? 0 : ensure(std::max(std::max(n, cap * 2), kGrowFloor)); }
+    int grow(size_t n);
     void release();
     ~DevBuf() { release(); }
     static constexpr size_t kGrowFloor = size_t(1) << 20;
@@ -54,8 +58,9 @@ struct DevBuf {
 struct PinnedBuf {
     void* p = nullptr;
     size_t cap = 0;
+    std::vector<void*> retired;
     int ensure(size_t n);
-    int grow(size_t n) { return n <= cap && p ? 0 : ensure(std::max(std::max(n, cap * 2), DevBuf::kGrowFloor)); }
+    int grow(size_t n);
     void release();
     ~PinnedBuf() { release(); }
 };
