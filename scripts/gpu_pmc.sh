@@ -12,7 +12,7 @@ cd /tmp && export TMPDIR=/tmp
 for cfg in ${CONFIGS:-2 ns}; do
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg $c"
-    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast -d "/tmp/pmc/${cfg}_$c" -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --cpu-seconds 0 > "$O/${cfg}_$c.log" 2>&1 || { tail -5 "$O/${cfg}_$c.log"; exit 1; }
+    timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast -d "/tmp/pmc/${cfg}_$c" -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --cpu-seconds 0 --no-extra > "$O/${cfg}_$c.log" 2>&1 || { tail -5 "$O/${cfg}_$c.log"; exit 1; }
     find "/tmp/pmc/${cfg}_$c" -name "*counter_collection.csv" -exec cp {} "$O/${cfg}_$c.csv" \;
   done
 done
