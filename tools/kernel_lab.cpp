@@ -370,8 +370,9 @@ int main(int argc, char** argv) {
             // slower, profiles/r2_lab_ns_occupancy.jsonl)
             const bool mw = getenv("MXEC_LAB_MW") != nullptr;
             for (int rep = 0; rep < 3; ++rep)
-                for (int bpc : {256, 384, 512, 768}) {
+                for (int bpc : {512, 1024}) {
                     vs.push_back(mxec::RsVariant{4, true, bpc, 0});
+                    vs.push_back(mxec::RsVariant{2, true, bpc, 0});
                     if (mw) vs.push_back(mxec::RsVariant{4, true, bpc, 3});
                 }
         } else if (full) {
