@@ -679,6 +679,7 @@ def probe_lib():
                      ("mxprobe_write", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
                      ("mxprobe_rs_pattern", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]),
+                     ("mxprobe_set_stream_wpc", [ctypes.c_int]),
                      ("mxprobe_rs_pattern_strided", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
@@ -725,10 +726,16 @@ def calibrate(torch, dev, stream) -> dict:
     out["read2_write1_GBps"] = round(3 * n / (ms * 1e-3) / 1e9, 1)
     ms = event_ms(torch, stream, lambda: run(lib.mxprobe_read(a.data_ptr(), n, sink.data_ptr(), sh)), 5)
     out["read_GBps"] = round(n / (ms * 1e-3) / 1e9, 1)
+    # the read stream at the RS kernel's 512 WG per CU: the box's read
+    # bandwidth that north_star's ">= 80 % of HBM read bandwidth" refers to
+    run(lib.mxprobe_set_stream_wpc(512))
+    ms = event_ms(torch, stream, lambda: run(lib.mxprobe_read(a.data_ptr(), n, sink.data_ptr(), sh)), 5)
+    run(lib.mxprobe_set_stream_wpc(16))
+    out["read_wpc512_GBps"] = round(n / (ms * 1e-3) / 1e9, 1)
     del a, b, c, sink
     torch.cuda.empty_cache()
     # The RS kernel's own access pattern (same tile, same loads in flight,
-    # 32 WG per CU) with XOR for the GF math, at the two encode shapes.
+    # 512 WG per CU) with XOR for the GF math, at the two encode shapes.
     # In the bench's object-major layout ([n][k+m][S], Encode), 15 / 24 GiB:
     # a few GiB measured low (launch ramp and tail on a ~1 ms launch).
     for k, m, S, n in ((4, 2, 10 << 20, 256), (8, 4, 1 << 20, 2048)):
@@ -741,8 +748,8 @@ def calibrate(torch, dev, stream) -> dict:
         del whole
     out["what"] = ("libmaxio_probe.so streams, HIP-event timed, 5 launches each: copy / read2_write1 / read over 2 GiB "
                    "buffers (nontemporal global_load_dwordx4, 4 loads in flight per lane, nontemporal stores, 16 WG "
-                   "x 256 lanes per CU); rs_pattern_kXmY = the RS kernel's tile and load schedule with XOR for the "
-                   "GF math, 32 WG per CU, over 15 GiB (k=4 m=2, 10 MiB) / 24 GiB (k=8 m=4, 1 MiB) in the "
+                   "x 256 lanes per CU; read_wpc512: the read at 512); rs_pattern_kXmY = the RS kernel's tile and load "
+                   "schedule with XOR for the GF math, 512 WG per CU, over 15 GiB (k=4 m=2, 10 MiB) / 24 GiB (k=8 m=4, 1 MiB) in the "
                    "object-major [n][k+m][S] layout the Encode workloads use")
     torch.cuda.empty_cache()
     return out
@@ -842,6 +849,10 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                                        "rs_pattern_same_buffers_GBps" if same else "rs_pattern_k8m4_GBps")}
     tr, src = pmc_traffic("k8m4", w.alg_bytes)
     out["ns"]["roofline"]["traffic"], out["ns"]["roofline"]["traffic_source"] = tr, src
+    if cal and cal.get("read_wpc512_GBps"):  # north_star: >= 80 % of per-GPU HBM read bandwidth
+        rd = max(cal["read_wpc512_GBps"], cal.get("read_GBps") or 0)
+        out["ns"]["roofline"]["box_read_GBps"] = rd
+        out["ns"]["roofline"]["frac_of_box_read"] = round(out["ns"]["roofline"]["achieved"] / rd, 4)
     w.drop()
     del w
     torch.cuda.empty_cache()

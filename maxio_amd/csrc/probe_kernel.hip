@@ -4,7 +4,8 @@
 // beside the RS kernel's roofline fraction ("what this box's HBM gives a plain
 // stream of the same shape"), measured with the same load / store forms the
 // RS kernel uses — nontemporal global_load_dwordx4 with four 16-byte loads in
-// flight per lane, nontemporal stores, 16 workgroups of 256 lanes per CU,
+// flight per lane, nontemporal stores, 16 workgroups of 256 lanes per CU
+// (mxprobe_set_stream_wpc changes it: the RS kernel's 512 reads faster),
 // grid-stride.
 //
 //   mxprobe_copy       read n bytes, write n bytes             (1:1)
@@ -122,12 +123,15 @@ __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__
     }
 }
 
-int grid() {
-    int dev = 0, cus = 256;
+int g_stream_wpc = 16;  // workgroups per CU of the plain stream probes (mxprobe_set_stream_wpc)
+
+int cus() {
+    int dev = 0, n = 256;
     (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return cus * 16;
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n;
 }
+int grid() { return cus() * g_stream_wpc; }
 
 }  // namespace
 
@@ -184,7 +188,7 @@ extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32
     if (k == 0 || (k & 3) || S == 0 || (S % 16384) ||
         ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
         return int(hipErrorInvalidValue);
-    const dim3 g(uint32_t(grid() * 32)), b(256);  // 512 WG per CU, as the RS kernel
+    const dim3 g(uint32_t(cus() * 512)), b(256);  // 512 WG per CU, as the RS kernel
     const auto* in = static_cast<const uint8_t*>(data);
     auto* out = static_cast<uint8_t*>(parity);
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -209,7 +213,7 @@ extern "C" int mxprobe_rs_pattern_policy(const void* data, void* parity, uint32_
     if (k == 0 || (k & 3) || S == 0 || (S % 16384) || policy < 0 || policy > 4 ||
         ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
         return int(hipErrorInvalidValue);
-    const dim3 g(uint32_t(grid() * 32)), b(256);
+    const dim3 g(uint32_t(cus() * 512)), b(256);
     const auto* in = static_cast<const uint8_t*>(data);
     auto* out = static_cast<uint8_t*>(parity);
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -222,4 +226,11 @@ extern "C" int mxprobe_rs_pattern_policy(const void* data, void* parity, uint32_
         default: hipLaunchKernelGGL((probe_pattern<2, 4>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
     }
     return int(hipGetLastError());
+}
+
+// Workgroups per CU of the copy / read / read2_write1 / write probes (1-4096).
+extern "C" int mxprobe_set_stream_wpc(int wpc) {
+    if (wpc < 1 || wpc > 4096) return int(hipErrorInvalidValue);
+    g_stream_wpc = wpc;
+    return 0;
 }
