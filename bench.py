@@ -704,7 +704,8 @@ def event_ms(torch, stream, fn, reps: int) -> float:
 
 def calibrate(torch, dev, stream) -> dict:
     """This box's HBM rates for plain streams of the RS kernel's load/store
-    forms (nt dwordx4, 4 loads in flight per lane, 16 WG/CU): the second
+    forms (nt dwordx4, 4 loads in flight per lane, 16 WG/CU; the read also at
+    the RS kernel's 512): the second
     denominator of SURVEY §8(d)."""
     lib = probe_lib()
     sh = stream.cuda_stream

@@ -16,9 +16,10 @@
 //    arrive in SGPRs by scalar loads; one of each v_perm's two table dwords must
 //    be a VGPR (gfx950 constant-bus limit 1), the copy is hoisted per column.
 //  * Input shards are loaded in blocks of 4 so each lane keeps 4*V 16-byte
-//    loads in flight; grid-stride over (object, tile) keeps 16 workgroups per
-//    CU busy without one launch per object.  Loads and stores carry the
-//    nontemporal hint (every byte is touched once).
+//    loads in flight; one launch covers every (object, tile) of a batch,
+//    grid-stride over 512 workgroups per CU (a few tiles each, so the tiles
+//    in flight stay together in memory; rs_default_variant).  Loads and
+//    stores carry the nontemporal hint (every byte is touched once).
 //  * Zero padding (the crate pads the short last chunk, filesystem.rs:1111)
 //    is never materialised: in the fast kernel an input whose length ends at
 //    or before a tile contributes zero and is not loaded; a tile that a
