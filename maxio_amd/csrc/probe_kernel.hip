@@ -188,7 +188,7 @@ extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32
     if (k == 0 || (k & 3) || S == 0 || (S % 16384) ||
         ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
         return int(hipErrorInvalidValue);
-    const dim3 g(uint32_t(cus() * 512)), b(256);  // 512 WG per CU, as the RS kernel
+    const dim3 g(uint32_t(cus() * (m <= 2 ? 1024 : 512))), b(256);  // as the RS kernel (rs_default_variant)
     const auto* in = static_cast<const uint8_t*>(data);
     auto* out = static_cast<uint8_t*>(parity);
     hipStream_t s = static_cast<hipStream_t>(stream);
