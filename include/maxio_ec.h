@@ -24,7 +24,8 @@
  *                            (verify :176-196, count :199-208, reconstruct :211,
  *                            truncate :216-222) — minus the file I/O
  *   mxec_*_device            the same two operations over device-resident
- *                            batches (one launch per homogeneous group of objects)
+ *                            batches (objects of any k and chunk size that share
+ *                            the output count share one launch)
  *   mxec_write_chunk,
  *   mxec_compute_and_write_parity,
  *   mxec_try_reconstruct_data_chunk,
