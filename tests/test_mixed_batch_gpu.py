@@ -410,6 +410,49 @@ def test_mixed_random_shapes(ctx, seed):
         assert torch.equal(t, ref), (o, k, m, S)
 
 
+def test_mixed_large_batch_side_stream_tables(ctx):
+    """4 000 objects of 64 KiB shards (4+2 and 8+4) in one call each way: the
+    descriptor tables pass 256 KiB, so they are copied on the slot's side
+    stream the launch waits for (runtime.cpp DescWriter::commit); every
+    object's round trip is exact and a sample's parity equals the oracle's."""
+    torch = _torch()
+    rng = np.random.default_rng(SEED + 6)
+    S = 64 << 10
+    specs = [(4, 2, 2500), (8, 4, 1500)]
+    b = Batch(torch, [(k, m, S, n, [S] * (k - 1) + [int(rng.integers(1, S + 1))]) for (k, m, n) in specs])
+    assert len(b.objs) == 4000
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(b.objs, b.dptr, b.pptr, data_len=b.dlen)
+    torch.cuda.synchronize()
+    for (k, m, S_, n, dl, t) in b.classes:
+        h = t[[0, n // 2, n - 1]].cpu().numpy()
+        for row in h:
+            want = oracle.encode([row[j][:dl[j]] for j in range(k)], m, S_)
+            for i in range(m):
+                assert np.array_equal(row[k + i], want[i]), (k, m, i)
+    refs = [c[5].clone() for c in b.classes]
+    present = np.ones(b.total, np.uint8)
+    g = 0
+    for (k, m, S_, n, dl, t) in b.classes:
+        for o in range(n):
+            for i in rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False):
+                present[g + int(i)] = 0
+            g += k + m
+    g = 0
+    for (k, m, S_, n, dl, t) in b.classes:
+        mask = torch.from_numpy(present[g:g + n * (k + m)].reshape(n, k + m) == 0).cuda()
+        t[mask] = 0x3C
+        g += n * (k + m)
+    torch.cuda.synchronize()
+    p = present.copy()
+    rc, status = ctx.reconstruct_batch_device(b.objs, b.sptr, p, shard_len=b.slen)
+    torch.cuda.synchronize()
+    assert rc == 0 and p.all() and not status.any()
+    for (k, m, S_, n, dl, t), ref in zip(b.classes, refs):
+        t[:, k - 1, dl[-1]:] = 0
+        assert torch.equal(t, ref), (k, m)
+
+
 def test_mixed_batch_argument_errors(ctx):
     """Crate argument errors answer before any work (k = 0, k + m > 256, a
     zero shard size)."""
