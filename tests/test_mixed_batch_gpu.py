@@ -453,6 +453,35 @@ def test_mixed_large_batch_side_stream_tables(ctx):
         assert torch.equal(t, ref), (k, m)
 
 
+def test_mixed_zero_length_and_tile_edge_chunks(ctx):
+    """Data chunks of length 0 (read as all zero, never loaded), lengths
+    that end exactly on a 16 KiB tile edge or one byte past it, and shard
+    sizes that are not a tile multiple, in one grouped launch: parity equals
+    the oracle's zero-padded encode."""
+    torch = _torch()
+    T = 16 << 10
+    cases = [(4, 2, 3 * T, [0, 3 * T, T, T + 1]), (4, 2, 3 * T + 48, [T, 0, 0, 1]),
+             (8, 4, 2 * T, [2 * T] * 6 + [T - 16, 0]), (6, 4, 5 * T + 16, [5 * T + 16, 2 * T, 16, 0, T, 3 * T])]
+    objs, tens = [], []
+    for (k, m, S, dl) in cases:
+        t = torch.randint(0, 256, (k + m, S), dtype=torch.uint8, device="cuda")
+        for j in range(k):
+            t[j, dl[j]:] = 0
+        objs.append((k, m, S))
+        tens.append((t, dl))
+    dptr = [t[j].data_ptr() for (k, m, S), (t, dl) in zip(objs, tens) for j in range(k)]
+    pptr = [t[k + i].data_ptr() for (k, m, S), (t, dl) in zip(objs, tens) for i in range(m)]
+    dlen = [x for (t, dl) in tens for x in dl]
+    torch.cuda.synchronize()
+    ctx.encode_batch_device(objs, dptr, pptr, data_len=dlen)
+    torch.cuda.synchronize()
+    for (k, m, S), (t, dl) in zip(objs, tens):
+        h = t.cpu().numpy()
+        want = oracle.encode([h[j][:dl[j]] for j in range(k)], m, S)
+        for i in range(m):
+            assert np.array_equal(h[k + i], want[i]), (k, m, S, dl, i)
+
+
 def test_mixed_batch_argument_errors(ctx):
     """Crate argument errors answer before any work (k = 0, k + m > 256, a
     zero shard size)."""
