@@ -7,8 +7,20 @@ encode of 1024 objects per GPU, k=4 data + m=2 parity shards of chunk_size =
 inputs resident in HBM, parity written to HBM, through the C ABI
 (mxec_encode_strided_device) on a dedicated HIP stream.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4a|4b|5] [--extra]
+  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4a|4b|5] [--no-extra] [--no-e2e]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+--gpus N in one process opens ONE mxec_ctx over GPUs 0..N-1 (MaxIO's
+production shape): each GPU gets its own objects (object i -> GPU i mod N,
+seeded per GPU), stream, HIP events and host thread; the step is timed over
+all of them (wall clock, after a sync of every device) and the roofline is
+the slowest GPU's kernel, with a per-GPU list.  Under torch.distributed.run
+each rank drives GPU LOCAL_RANK and --gpus must equal WORLD_SIZE.  Fewer
+visible GPUs than --gpus: exit 2 with a message and no JSON line
+(BENCH_REHEARSE_LOGICAL=1: a labelled rehearsal on logical devices of one
+card instead).  The default config-2 run also reports extra.e2e_host: the
+same encode from page-locked host memory through mxec_encode_batch_host
+(PCIe included) over every GPU of the run.
 
 Other BASELINE configs (same JSON line, for DESIGN.md / profiles):
   3   reconstruct k=8 m=4, 2 data erasures + SHA-256 verify of the 10 present
@@ -24,9 +36,9 @@ Other BASELINE configs (same JSON line, for DESIGN.md / profiles):
       (one mixed-shape batch call each way; BENCH_MIXED_MODE=streams: the
       classes as separate calls on four streams)
 
-One process per GPU; objects are partitioned per GPU (weak scaling, no
-collective on the data path; only the timing barrier / max-reduce).  Rank 0
-prints ONE JSON line.  value = payload GiB/s (k * chunk_size bytes per object)
+Objects are partitioned per GPU (weak scaling, no collective on the data
+path; only the timing barrier / max-reduce between ranks).  Rank 0 prints
+ONE JSON line.  value = payload GiB/s (k * chunk_size bytes per object)
 over all GPUs; roofline = the dominant kernel's algorithmic bytes / its
 HIP-event-timed duration vs 8 TB/s; cpu_baseline = oracle/ (C restatement of
 the crate's pure-Rust path) on one host core over a bounded sample, plus the
@@ -648,17 +660,34 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank, workers=8):
     raise SystemExit(f"unknown --config {cfg}")
 
 
-def pmc_traffic(tag: str, alg_bytes: float):
+def rs_blocks_per_cu(r_total: int) -> int:
+    """Workgroups per CU of a uniform RS launch with r_total output rows --
+    mirrors rs_default_variant (maxio_amd/csrc/rs_kernel.hip; a CPU test
+    keeps the two in step)."""
+    return 1024 if r_total <= 2 else 512
+
+
+# Grouped (mixed-batch) launches: rs_group_variant's workgroups per CU.
+RS_GROUP_BLOCKS_PER_CU = 512
+
+
+def pmc_traffic(tag: str, alg_bytes: float, bpc=None):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/*pmc*<tag>*.json, FETCH_SIZE x2 per the gfx950
     correction + WRITE_SIZE; tools/pmc_summary.py): the measured
     traffic / algorithmic ratio applied to this launch's algorithmic bytes
-    (the summary may come from a smaller batch of the same kernel)."""
+    (the summary may come from a smaller batch of the same kernel).  With
+    `bpc` (an RS launch's workgroups per CU) only a summary measured at the
+    timed kernel's grid counts: its blocks_per_cu must equal it, else (older
+    summaries without the field included) traffic is null."""
+    want = bpc
     # newest round first (profiles/rNN_…)
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc*{tag}*.json")), reverse=True):
         try:
             with open(p) as f:
                 d = json.load(f)
+            if want is not None and d.get("blocks_per_cu") != want:
+                continue
             ratio = d["hbm_bytes_per_launch"] / d["algorithmic_bytes_per_launch"]
             return round(ratio * alg_bytes, 0), os.path.relpath(p, ROOT)
         except Exception:
@@ -674,6 +703,7 @@ def probe_lib():
     p = os.path.join(ROOT, "maxio_amd", "lib", "libmaxio_probe.so")
     lib = ctypes.CDLL(p)
     for fn, args in (("mxprobe_copy", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+                     ("mxprobe_copy_float4", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
                      ("mxprobe_read2_write1", [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]),
                      ("mxprobe_read", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
                      ("mxprobe_write", [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
@@ -723,6 +753,9 @@ def calibrate(torch, dev, stream) -> dict:
 
     ms = event_ms(torch, stream, lambda: run(lib.mxprobe_copy(c.data_ptr(), a.data_ptr(), n, sh)), 5)
     out["copy_GBps"] = round(2 * n / (ms * 1e-3) / 1e9, 1)
+    # the guide's float4 copy (MI355X_MICROARCH.md: 6.29 TB/s), same buffers
+    ms = event_ms(torch, stream, lambda: run(lib.mxprobe_copy_float4(c.data_ptr(), a.data_ptr(), n, sh)), 5)
+    out["copy_float4_GBps"] = round(2 * n / (ms * 1e-3) / 1e9, 1)
     ms = event_ms(torch, stream, lambda: run(lib.mxprobe_read2_write1(c.data_ptr(), a.data_ptr(), b.data_ptr(), n, sh)), 5)
     out["read2_write1_GBps"] = round(3 * n / (ms * 1e-3) / 1e9, 1)
     ms = event_ms(torch, stream, lambda: run(lib.mxprobe_read(a.data_ptr(), n, sink.data_ptr(), sh)), 5)
@@ -747,7 +780,8 @@ def calibrate(torch, dev, stream) -> dict:
             whole.data_ptr(), whole[:, k:].data_ptr(), k, m, S, n, st, st, S, sh)), 5)
         out[f"rs_pattern_k{k}m{m}_GBps"] = round(n * (k + m) * S / (ms * 1e-3) / 1e9, 1)
         del whole
-    out["what"] = ("libmaxio_probe.so streams, HIP-event timed, 5 launches each: copy / read2_write1 / read over 2 GiB "
+    out["what"] = ("libmaxio_probe.so streams, HIP-event timed, 5 launches each: copy / copy_float4 (the guide's "
+                   "float4 copy: plain loads and stores, one element per lane) / read2_write1 / read over 2 GiB "
                    "buffers (nontemporal global_load_dwordx4, 4 loads in flight per lane, nontemporal stores, 16 WG "
                    "x 256 lanes per CU; read_wpc512: the read at 512); rs_pattern_kXmY = the RS kernel's tile and load "
                    "schedule with XOR for the GF math, 512 WG per CU, over 15 GiB (k=4 m=2, 10 MiB) / 24 GiB (k=8 m=4, 1 MiB) in the "
@@ -769,6 +803,23 @@ def pattern_on_buffers(torch, stream, w) -> float:
     ms = event_ms(torch, stream, lambda: lib.mxprobe_rs_pattern_strided(
         w.data.data_ptr(), w.parity.data_ptr(), k, m, S, n, w.stride, w.stride, w.sstride, stream.cuda_stream), 5)
     return round(n * (k + m) * S / (ms * 1e-3) / 1e9, 1)
+
+
+def float4_copy_on_buffers(torch, stream, w):
+    """The guide's float4 copy (plain loads and stores, one 16-byte element
+    per lane, MI355X_MICROARCH.md's 6.29 TB/s recipe) over an Encode
+    workload's own allocation: the first half of its object-major buffer
+    copied onto the second half.  A denominator that shares nothing with the
+    RS kernel's schedule.  Overwrites the objects (after the timed steps and
+    the spot check)."""
+    lib = probe_lib()
+    half = (w.obj.numel() // 2) & ~15
+    if half < (1 << 20):
+        return None
+    src = w.obj.data_ptr()
+    dst = src + half
+    ms = event_ms(torch, stream, lambda: lib.mxprobe_copy_float4(dst, src, half, stream.cuda_stream), 5)
+    return round(2 * half / (ms * 1e-3) / 1e9, 1)
 
 
 def valu_bound_GBps(form: str, n_cus: int) -> float:
@@ -848,7 +899,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                  "spot_check_vs_oracle": ok,
                  "roofline": hbm_block(w.alg_bytes, ms, w.kernel, cal_ns,
                                        "rs_pattern_same_buffers_GBps" if same else "rs_pattern_k8m4_GBps")}
-    tr, src = pmc_traffic("k8m4", w.alg_bytes)
+    tr, src = pmc_traffic("k8m4", w.alg_bytes, rs_blocks_per_cu(4))
     out["ns"]["roofline"]["traffic"], out["ns"]["roofline"]["traffic_source"] = tr, src
     if cal and cal.get("read_wpc512_GBps"):  # north_star: >= 80 % of per-GPU HBM read bandwidth
         rd = max(cal["read_wpc512_GBps"], cal.get("read_GBps") or 0)
@@ -915,7 +966,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                       "ms_per_step": round(ms5, 3), "spot_check_vs_oracle": ok5,
                       "roofline": hbm_block(w5.alg_bytes, ms5, w5.kernel + ", whole step", cal,
                                             "rs_pattern_k4m2_GBps")}
-    tr, src = pmc_traffic("cfg5_grouped", w5.alg_bytes)
+    tr, src = pmc_traffic("cfg5_grouped", w5.alg_bytes, RS_GROUP_BLOCKS_PER_CU)
     out["config5"]["roofline"]["traffic"], out["config5"]["roofline"]["traffic_source"] = tr, src
     w5.drop()
     del w5
@@ -957,6 +1008,242 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     return out
 
 
+# ---- device plan ----------------------------------------------------------------
+
+
+class BenchRefusal(Exception):
+    """bench.py cannot measure what was asked (exit status 2, no JSON line)."""
+
+
+class Plan:
+    """Which GPUs this process drives and what the JSON line reports.
+
+    mode  "single"   --gpus 1, one device
+          "devices"  --gpus N > 1 in ONE process: one mxec_ctx over N devices
+                     (MaxIO's production shape), object i -> device i mod N,
+                     each device's launches on its own stream and host thread
+          "ranks"    under torch.distributed.run: WORLD_SIZE ranks, one GPU
+                     each (LOCAL_RANK), --gpus must equal WORLD_SIZE
+          "logical"  BENCH_REHEARSE_LOGICAL=1 and fewer visible GPUs than
+                     --gpus: a labelled rehearsal on N logical devices of one
+                     card (MXEC_TEST_LOGICAL_DEVICES), never an N-GPU number
+    """
+
+    def __init__(self, mode, n_gpus, torch_devs, world=1, rank=0, logical=1, rehearsal=None):
+        self.mode, self.n_gpus, self.torch_devs = mode, n_gpus, list(torch_devs)
+        self.world, self.rank, self.logical, self.rehearsal = world, rank, logical, rehearsal
+
+    @property
+    def local_devices(self) -> int:
+        return len(self.torch_devs)
+
+    @property
+    def device_mask(self) -> int:
+        m = 0
+        for d in self.torch_devs:
+            m |= 1 << d
+        return m
+
+
+def plan_devices(gpus: int, env, visible: int) -> Plan:
+    """The device plan for `bench.py --gpus N`, or BenchRefusal.  A line's
+    n_gpus always equals --gpus; a run that cannot drive that many GPUs exits
+    non-zero instead of printing a smaller measurement."""
+    if gpus < 1:
+        raise BenchRefusal(f"--gpus {gpus}: need at least one GPU")
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world > 1:
+        rank = int(env.get("RANK", "0"))
+        if gpus != world:
+            raise BenchRefusal(f"--gpus {gpus} but WORLD_SIZE={world}: under torch.distributed.run each rank "
+                               "drives one GPU, so --gpus must equal --nproc-per-node")
+        pinned = env.get("BENCH_GPU_OF_RANK")
+        gpu = int(pinned if pinned is not None else env.get("LOCAL_RANK", "0"))
+        if not 0 <= gpu < visible:
+            raise BenchRefusal(f"rank {rank} wants GPU {gpu} but {visible} HIP device(s) are visible")
+        reh = (f"BENCH_GPU_OF_RANK={pinned}: every rank on GPU {pinned} (rehearsal of the rank path, "
+               "not an N-GPU measurement)") if pinned is not None else None
+        return Plan("ranks", world, [gpu], world=world, rank=rank, rehearsal=reh)
+    if gpus <= visible:
+        return Plan("single" if gpus == 1 else "devices", gpus, range(gpus))
+    if env.get("BENCH_REHEARSE_LOGICAL") == "1" and visible >= 1:
+        if gpus > 8:
+            raise BenchRefusal(f"--gpus {gpus}: logical rehearsals go up to 8 devices")
+        return Plan("logical", gpus, [0] * gpus, logical=gpus,
+                    rehearsal=(f"{gpus} logical devices of ONE card (MXEC_TEST_LOGICAL_DEVICES={gpus}): "
+                               "exercises the multi-device path, not an N-GPU measurement"))
+    raise BenchRefusal(f"--gpus {gpus} asks for {gpus} GPUs but {visible} HIP device(s) are visible; run it on a "
+                       f"node with {gpus} GPUs (or set BENCH_REHEARSE_LOGICAL=1 for a labelled rehearsal on "
+                       "logical devices of one card)")
+
+
+class DevView:
+    """The context bound to one of its devices: every *_device call (and
+    combiner_stats) goes to ctx device `di`."""
+
+    _DEV_CALLS = frozenset((
+        "encode_strided_device", "encode_batch_device", "reconstruct_strided_device",
+        "reconstruct_strided_device_async", "reconstruct_batch_device", "reconstruct_batch_device_async",
+        "sha256_batch_device", "body_sums_device", "frames_device", "combiner_stats"))
+
+    def __init__(self, ctx, di: int):
+        self._ctx, self.di = ctx, di
+
+    def __getattr__(self, name):
+        a = getattr(self._ctx, name)
+        if name in self._DEV_CALLS:
+            import functools
+
+            return functools.partial(a, dev=self.di)
+        return a
+
+
+def reduce_sum(value: float) -> float:
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def gather_objects(obj) -> list:
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def sync_all(torch, devs) -> None:
+    for d in sorted(set(devs)):
+        torch.cuda.synchronize(d)
+
+
+def run_steps(torch, lanes, steps: int, events: bool):
+    """`steps` steps of every lane (device): one host thread per device when
+    there are several, so each device's queue is fed independently (every
+    call returns after enqueueing, except the reconstructs that read back
+    verdicts).  Returns per-lane HIP event pairs bracketing each step on the
+    lane's stream."""
+
+    def one(lane):
+        w, stream, tdev = lane
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)] if events else []
+        with torch.cuda.device(tdev):
+            for i in range(steps):
+                if events:
+                    ev[i][0].record(stream)
+                w.step()
+                if events:
+                    ev[i][1].record(stream)
+        return ev
+
+    if len(lanes) == 1:
+        return [one(lanes[0])]
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(len(lanes)) as ex:
+        return list(ex.map(one, lanes))
+
+
+# ---- end-to-end host leg (north_star: PCIe-inclusive rate) -----------------------
+
+
+def _fill_random(buf, seed: int) -> None:
+    """Random bytes without generating gigabytes of randomness: tile a 64 MiB block."""
+    import numpy as np
+
+    blk = np.random.default_rng(seed).integers(0, 256, 64 << 20, dtype=np.uint8)
+    flat = buf.reshape(-1)
+    for o in range(0, flat.size, blk.size):
+        n = min(blk.size, flat.size - o)
+        flat[o:o + n] = blk[:n]
+
+
+def pcie_rates(torch, devs, nbytes: int = 1 << 30) -> dict:
+    """The box's raw copy rates between pinned host memory and the devices:
+    every device at once (one pinned buffer and one stream each), each
+    direction alone, 4 copies per device, wall clock."""
+    hb = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in devs]
+    db = [torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", d)) for d in devs]
+    st = [torch.cuda.Stream(device=torch.device("cuda", d)) for d in devs]
+    out = {}
+    for name in ("h2d", "d2h"):
+        def go(reps):
+            for _ in range(reps):
+                for h, d, s in zip(hb, db, st):
+                    with torch.cuda.stream(s):
+                        (d.copy_(h, non_blocking=True) if name == "h2d" else h.copy_(d, non_blocking=True))
+            sync_all(torch, devs)
+
+        go(1)
+        t0 = time.perf_counter()
+        go(4)
+        out[f"{name}_GBps"] = round(4 * nbytes * len(devs) / (time.perf_counter() - t0) / 1e9, 1)
+    del hb, db
+    return out
+
+
+def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
+    """mxec_encode_batch_host from mxec_host_alloc (page-locked) memory: the
+    PUT path as MaxIO sees it -- request bodies in host memory, parity and
+    digests back in host memory (filesystem.rs:1107-1135) -- over every
+    device of the context, with and without the SHA-256 of every chunk.
+    Payload GiB/s (k * chunk_size per object) over all ranks, next to the
+    box's raw pinned copy rates and the bound they set."""
+    import numpy as np
+
+    k, m, S = 4, 2, 10 << 20
+    D = plan.local_devices
+    n = per_dev * D
+    rates = pcie_rates(torch, plan.torch_devs)
+    data = ctx.host_array(n * k * S).reshape(n, k, S)
+    par = ctx.host_array(n * m * S).reshape(n, m, S)
+    _fill_random(data, 7 + plan.rank)
+    dptr = [data[o, j].ctypes.data for o in range(n) for j in range(k)]
+    pptr = [par[o, i].ctypes.data for o in range(n) for i in range(m)]
+    objs = [(k, m, S)] * n
+    res = {"workload": (f"PUT compute from page-locked host memory: {per_dev} objects per GPU x 4+2 x 10 MiB "
+                        f"(mxec_encode_batch_host over {D} device(s) per process); H2D upload, RS encode, "
+                        "optional SHA-256 of all 6 chunks, D2H of parity and digests, wall clock"),
+           "objects_per_gpu": per_dev, "pcie_all_devices": rates}
+    # H2D and D2H overlap (separate DMA streams): the bound is the slower direction.
+    h2d_s = n * k * S / (rates["h2d_GBps"] * 1e9)
+    d2h_s = n * m * S / (rates["d2h_GBps"] * 1e9)
+    bound_s = max(h2d_s, d2h_s)
+    for sha in (False, True):
+        dig = np.zeros(n * (k + m) * 32, np.uint8) if sha else None
+        ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm: pools, tables
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.encode_batch_host(objs, dptr, pptr, digests=dig)
+        el = reduce_max((time.perf_counter() - t0) / reps)
+        payload = reduce_sum(float(n * k * S))
+        key = "rs_sha256" if sha else "rs_only"
+        res[key] = {"s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
+                    "frac_of_pcie_bound": round(bound_s / el, 4)}
+    res["pcie_bound_s_per_batch"] = round(bound_s, 4)
+    res["bound"] = ("max(upload k*S*n / h2d_GBps, download m*S*n / d2h_GBps), the raw pinned copy rates "
+                    "measured above on the same devices at once")
+    if plan.rank == 0:
+        o = n // 2
+        want = _oracle().encode(list(data[o]), m, S)
+        res["spot_check_vs_oracle"] = all(np.array_equal(par[o, i], want[i]) for i in range(m))
+    del data, par
+    return res
+
+
+# ---- main ------------------------------------------------------------------------
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -969,71 +1256,92 @@ def main() -> int:
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary measurements that the default config-2 run adds "
                          "at N=1 (north-star shape, config 3 / 3c, PUT compute)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host-memory leg")
     args = ap.parse_args()
 
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    try:
+        plan = plan_devices(args.gpus, os.environ, torch.cuda.device_count())
+    except BenchRefusal as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        return 2
+    if plan.logical > 1:
+        os.environ["MXEC_TEST_LOGICAL_DEVICES"] = str(plan.logical)
+    if plan.mode == "ranks":
         import torch.distributed as dist
 
         # BENCH_GPU_OF_RANK=0 pins every rank to GPU 0 and BENCH_DIST_BACKEND=gloo
         # carries the timing collectives on the host: a rehearsal of the
         # multi-rank path on a one-GPU box.  Defaults: GPU = LOCAL_RANK, RCCL.
-        gpu = int(os.environ.get("BENCH_GPU_OF_RANK", local))
+        gpu = plan.torch_devs[0]
         torch.cuda.set_device(gpu)
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
-        local = gpu
     else:
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(plan.torch_devs[0])
+    rank, world = plan.rank, plan.world
 
     import maxio_amd
 
+    D = plan.local_devices
+    one_gpu = plan.n_gpus == 1
     # config 3c (and the default run's extras, which include it) needs one
     # slot per concurrent batch.
-    with_extra = args.config == "2" and world == 1 and not args.no_extra
-    ctx = maxio_amd.Context(device_mask=1 << (local if world > 1 else 0),
+    with_extra = args.config == "2" and one_gpu and not args.no_extra
+    ctx = maxio_amd.Context(device_mask=plan.device_mask,
                             streams_per_device=max(2, args.workers if args.config == "3c" or with_extra else 2))
-    dev = torch.device("cuda", torch.cuda.current_device())
-    # A dedicated stream: the kernels and the HIP events that time them are
-    # on the same queue.
-    stream = torch.cuda.Stream(device=dev)
+    if len(ctx.device_ids()) != D:
+        print(f"bench.py: the context opened {len(ctx.device_ids())} device(s), the plan needs {D}",
+              file=sys.stderr, flush=True)
+        return 3
+    lanes = []  # (workload, stream, torch device) per ctx device
+    for di in range(D):
+        tdev = torch.device("cuda", plan.torch_devs[di])
+        with torch.cuda.device(tdev):
+            # A dedicated stream per device: the kernels and the HIP events
+            # that time them are on the same queue.
+            stream = torch.cuda.Stream(device=tdev)
+            w = make_workload(args.config, torch, DevView(ctx, di), tdev, stream.cuda_stream, args.objects,
+                              rank * D + di, args.workers)
+            torch.cuda.synchronize()
+        lanes.append((w, stream, tdev))
+    w, stream, dev = lanes[0]
     sh = stream.cuda_stream
-    w = make_workload(args.config, torch, ctx, dev, sh, args.objects, rank, args.workers)
-    torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        w.step()
-    torch.cuda.synchronize()
-    spot_ok = w.spot_check() if rank == 0 else None
+    run_steps(torch, lanes, args.warmup, events=False)
+    sync_all(torch, plan.torch_devs)
+    spot_local = all(bool(l[0].spot_check()) for l in lanes)
+    spot_ok = reduce_max(0.0 if spot_local else 1.0) == 0.0
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
     barrier()
-    torch.cuda.synchronize()
+    sync_all(torch, plan.torch_devs)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        w.step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
+    evs = run_steps(torch, lanes, args.steps, events=True)
+    sync_all(torch, plan.torch_devs)
     barrier()
     elapsed = reduce_max(time.perf_counter() - t0)
-    ms_launch = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    ms_dev = [sum(a.elapsed_time(b) for a, b in ev) / len(ev) for ev in evs]
     if getattr(w, "wall_timed", False):  # work on the workers' streams, not `stream`
-        ms_launch = elapsed * 1e3 / args.steps
+        ms_dev = [elapsed * 1e3 / args.steps] * D
 
-    value = float(w.payload) * world * args.steps / GIB / elapsed  # weak scaling: all ranks
+    payload_local = float(sum(l[0].payload for l in lanes))
+    value = reduce_sum(payload_local) * args.steps / GIB / elapsed  # weak scaling: every GPU of every rank
+    per_dev = [{"gpu": plan.torch_devs[i] if plan.mode != "logical" else f"logical {i} of card 0",
+                "rank": rank, "ms_per_launch": round(ms_dev[i], 4),
+                "achieved": round(lanes[i][0].alg_bytes / (ms_dev[i] * 1e-3) / 1e9, 1),
+                "frac": round(lanes[i][0].alg_bytes / (ms_dev[i] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+               for i in range(D)]
+    per_dev = [d for part in gather_objects(per_dev) for d in part]
+    # The headline kernel time: the slowest device's (equal to the one device at N=1).
+    ms_launch = max(d["ms_per_launch"] for d in per_dev)
     achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
 
     # §8(d) second denominator: this box's rates for plain streams of the RS
-    # kernel's own load/store forms (libmaxio_probe.so).
+    # kernel's own load/store forms (libmaxio_probe.so), on rank 0's first device.
     cal = calibrate(torch, dev, stream) if rank == 0 else None
     box_key = {(4, 2): "rs_pattern_k4m2_GBps", (8, 4): "rs_pattern_k8m4_GBps"}.get(
         (getattr(w, "k", 0), getattr(w, "m", 0)), "copy_GBps")
@@ -1044,55 +1352,73 @@ def main() -> int:
         if same:
             cal["rs_pattern_same_buffers_GBps"] = same
             box_key = "rs_pattern_same_buffers_GBps"
+        f4 = float4_copy_on_buffers(torch, stream, w)
+        if f4:
+            cal["float4_copy_same_buffers_GBps"] = f4
     copy_peak = cal.get(box_key) if cal else None
 
-    extra = None
+    extra = {}
     if rank == 0 and hasattr(w, "breakdown"):
-        extra = {"breakdown": w.breakdown()}
-    if extra and "crc32c" in extra["breakdown"]:
+        extra["breakdown"] = w.breakdown()
+    if "crc32c" in extra.get("breakdown", {}):
         crc = extra["breakdown"]["crc32c"]
         # The HBM-bound kernel of this workload is the CRC pass; MD5 is a
         # serial chain per body (us_per_block in the breakdown).
         ms_launch = crc["ms"]
         achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
         w.kernel = "crc_tiles_kernel + crc_finish_kernel (CRC32C alone)"
-    dropped = False
-    if rank == 0 and with_extra:
-        w.drop()  # HBM for the secondary workloads
-        dropped = True
-        torch.cuda.empty_cache()
-        extra = extras(ctx, torch, dev, stream, args.steps, cal)
-        extra["calibration"] = cal
-    cpu = cpu_all = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the CPU leg runs at N=1 only
-        spec = w.cpu_work()
-        if spec is not None:
-            work, per_call, what = spec
-            v, n, el = cpu_leg(work, per_call, args.cpu_seconds, 1)
-            cpu = {"value": round(v, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-                   "sample": f"{n} calls in {el:.1f}s, 1 thread: {what}"}
-            # The GPU box grants 16 host cores (OMP_NUM_THREADS) while
-            # os.cpu_count() shows the whole machine.
-            nc = os.cpu_count() or 1
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(nc, 64)
-            v, n, el = cpu_leg(work, per_call, max(2.0, args.cpu_seconds / 2), threads)
-            cpu_all = {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-                       "sample": f"{n} calls in {el:.1f}s on {threads} threads "
-                                 f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={nc})"}
-    if not dropped:
-        w.drop()
+    cpu_spec = w.cpu_work() if (rank == 0 and one_gpu and args.cpu_seconds > 0) else None
+    alg_bytes, w_name, w_kernel, w_bound, w_payload = w.alg_bytes, w.name, w.kernel, w.bound, w.payload
+    is_stream = isinstance(w, ReconstructStream)
+    stream_dims = (len(w.parts), w.parts[0].n) if is_stream else None
+    mixed_batch = args.config == "5" and getattr(w, "mode", "") == "batch"
+    for l in lanes:
+        l[0].drop()  # HBM for the secondary workloads
+    del w
+    lanes = []
     torch.cuda.empty_cache()
+    if rank == 0 and with_extra:
+        extra.update(extras(ctx, torch, dev, stream, args.steps, cal))
+    if cal is not None:
+        extra["calibration"] = cal
+    if not args.no_e2e and args.config == "2":
+        extra["e2e_host"] = e2e_host_leg(ctx, torch, plan, 128 if D == 1 and world == 1 else 64)
+    cpu = cpu_all = None
+    if cpu_spec is not None:  # the CPU leg runs at N=1 only
+        work, per_call, what = cpu_spec
+        v, n, el = cpu_leg(work, per_call, args.cpu_seconds, 1)
+        cpu = {"value": round(v, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": f"{n} calls in {el:.1f}s, 1 thread: {what}"}
+        # The GPU box grants 16 host cores (OMP_NUM_THREADS) while
+        # os.cpu_count() shows the whole machine.
+        nc = os.cpu_count() or 1
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(nc, 64)
+        v, n, el = cpu_leg(work, per_call, max(2.0, args.cpu_seconds / 2), threads)
+        cpu_all = {"value": round(v, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+                   "sample": f"{n} calls in {el:.1f}s on {threads} threads "
+                             f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={nc})"}
 
     if rank == 0:
-        tag = {"2": "k4m2", "ns": "k8m4", "sums": "crc_tiles", "frames": "gcm_frames"}.get(args.config)
-        if args.config == "5" and getattr(w, "mode", "") == "batch":
-            tag = "cfg5_grouped"
-        traffic, tsrc = pmc_traffic(tag, w.alg_bytes) if tag else (None, None)
+        tag = {"2": ("k4m2", rs_blocks_per_cu(2)), "ns": ("k8m4", rs_blocks_per_cu(4)),
+               "4a": ("k10m4", rs_blocks_per_cu(4)), "sums": ("crc_tiles", None),
+               "frames": ("gcm_frames", None)}.get(args.config)
+        if mixed_batch:
+            tag = ("cfg5_grouped", RS_GROUP_BLOCKS_PER_CU)
+        traffic, tsrc = pmc_traffic(tag[0], alg_bytes, tag[1]) if tag else (None, None)
+        if plan.mode == "devices":
+            par = (f"{plan.n_gpus} GPUs in one process: one mxec_ctx over {plan.n_gpus} devices, each GPU's "
+                   "objects on its own stream and host thread, no collectives")
+        elif plan.mode == "ranks":
+            par = f"{plan.n_gpus} ranks (torch.distributed.run), one GPU each, no data-path collectives"
+        elif plan.mode == "logical":
+            par = f"REHEARSAL: {plan.n_gpus} logical devices of one card, no collectives"
+        else:
+            par = "one GPU, no collectives"
         line = {
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": plan.n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
@@ -1100,22 +1426,22 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: uniform random bytes (torch.randint on device, seeded)",
+            "data": "synthetic: uniform random bytes (torch.randint on device, seeded per GPU)",
             "config": {
-                "workload": w.name,
+                "workload": w_name,
                 "bench_config": args.config,
-                "payload_bytes_per_step_per_gpu": int(w.payload),
-                "parallelism": "objects partitioned per GPU, no collectives",
+                "payload_bytes_per_step_per_gpu": int(w_payload),
+                "parallelism": par,
             },
             "roofline": {
-                "bound": w.bound,
+                "bound": w_bound,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": w.kernel,
-                "bytes_per_launch": float(w.alg_bytes),
+                "kernel": w_kernel,
+                "bytes_per_launch": float(alg_bytes),
                 "ms_per_launch": round(ms_launch, 4),
                 "traffic_source": tsrc,
                 "box_stream": box_key if copy_peak else None,
@@ -1125,15 +1451,23 @@ def main() -> int:
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "spot_check_vs_oracle": spot_ok,
-            "extra": extra,
+            "extra": extra or None,
         }
-        if isinstance(w, ReconstructStream):
+        if cal and cal.get("float4_copy_same_buffers_GBps"):
+            line["roofline"]["float4_copy_GBps"] = cal["float4_copy_same_buffers_GBps"]
+            line["roofline"]["frac_of_float4_copy"] = round(achieved / cal["float4_copy_same_buffers_GBps"], 4)
+        if plan.n_gpus > 1:
+            line["roofline"]["per_gpu"] = per_dev
+            line["config"]["launch"] = plan.mode
+        if plan.rehearsal:
+            line["config"]["rehearsal"] = plan.rehearsal
+        if is_stream:
             n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            line["roofline"] = dict(stream_step_roofline(elapsed * 1e3 / args.steps, len(w.parts), w.parts[0].n, n_cus),
+            line["roofline"] = dict(stream_step_roofline(elapsed * 1e3 / args.steps, *stream_dims, n_cus),
                                     traffic=None)
         print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
+    if plan.mode == "ranks":
         import torch.distributed as dist
 
         dist.destroy_process_group()

@@ -230,10 +230,12 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream,
 /* End-to-end PUT compute for many objects whose chunks are in HOST memory
  * (request bodies) — the batched form of mxec_encode.  Same array layout as
  * mxec_encode_batch_device but host pointers; digests (host, sum(k+m)) and
- * status_out (host, n_obj) may be NULL.  Objects are dealt round-robin over
- * the ctx's devices; per device, uploads (direct from pinned memory, else via
- * a pinned ring), RS + SHA-256 kernels and downloads are pipelined on
- * separate streams with the whole batch resident in HBM.  Blocks until every
+ * status_out (host, n_obj) may be NULL.  Objects are dealt over the ctx's
+ * devices -- object o to device o mod D when every object has the same
+ * (k, m, shard_size), balanced by bytes otherwise; per device, uploads
+ * (direct from pinned memory, else via a pinned ring), RS + SHA-256 kernels
+ * and downloads are pipelined on separate streams with the whole batch
+ * resident in HBM.  Blocks until every
  * parity chunk and digest is in host memory. */
 int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs,
                            uint64_t n_obj, const uint8_t* const* data,

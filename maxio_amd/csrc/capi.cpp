@@ -2,6 +2,7 @@
 // pointer drop-ins, device-resident batches).  No exception crosses the ABI.
 #include <algorithm>
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <unordered_map>
 #include <cstring>
@@ -23,23 +24,6 @@ std::string too_few_msg(int present, int k, int total) {
            " missing)";
 }
 
-// Runs `collect` (which takes coefficient-table offsets for a batch's
-// launches) until no arena recycle happened during it: a recycle
-// (runtime.cpp coef_offset) drops every offset handed out before it.
-template <class F>
-int with_stable_coef(Device& d, F&& collect) {
-    auto epoch = [&] {
-        std::lock_guard<std::mutex> g(d.coef_mu);
-        return d.coef_epoch;
-    };
-    for (int attempt = 0; attempt < 3; ++attempt) {
-        const uint64_t e0 = epoch();
-        MXEC_TRY(collect());
-        if (epoch() == e0) return MXEC_OK;
-    }
-    return set_error(MXEC_E_INVALID_ARG, "the coefficient tables of one batch exceed the device's table arena");
-}
-
 // One object of a device-resident reconstruct batch (device shard pointers).
 struct BatchObj {
     int k, m;
@@ -58,46 +42,54 @@ int rebuild_batch(Device& d, Slot& slot, hipStream_t s, bool data_only, const st
                   const std::vector<uint64_t>& which, std::vector<int32_t>& st) {
     std::vector<std::shared_ptr<const DecodePlan>> plans(which.size());
     std::vector<uint32_t> offs(which.size());
-    MXEC_TRY(with_stable_coef(d, [&]() -> int {
+    std::vector<const uint8_t*> in;
+    std::vector<uint8_t*> out;
+    std::vector<uint64_t> il, ol;
+    std::map<int, std::vector<RsMixedObject>> groups;
+    auto collect = [&]() -> int {
         for (size_t t = 0; t < which.size(); ++t) {
             const BatchObj& b = all[which[t]];
             MXEC_TRY(decode_plan(d, b.k, b.m, b.present, data_only, &plans[t], &offs[t]));
         }
         return MXEC_OK;
-    }));
-    // Pointer and length tables of every rebuilt object, sized up front (the
-    // RsObjects point into them).
-    size_t n_in = 0, n_out = 0;
-    for (size_t t = 0; t < which.size(); ++t) {
-        st[which[t]] = plans[t] ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
-        if (plans[t] && !plans[t]->missing.empty()) {
-            n_in += size_t(all[which[t]].k);
-            n_out += plans[t]->missing.size();
+    };
+    auto launch = [&]() -> int {
+        // Pointer and length tables of every rebuilt object, sized up front
+        // (the RsObjects point into them).
+        size_t n_in = 0, n_out = 0;
+        for (size_t t = 0; t < which.size(); ++t) {
+            st[which[t]] = plans[t] ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
+            if (plans[t] && !plans[t]->missing.empty()) {
+                n_in += size_t(all[which[t]].k);
+                n_out += plans[t]->missing.size();
+            }
         }
-    }
-    std::vector<const uint8_t*> in(n_in);
-    std::vector<uint8_t*> out(n_out);
-    std::vector<uint64_t> il(n_in), ol(n_out);
-    std::map<int, std::vector<RsMixedObject>> groups;
-    size_t pi = 0, po = 0;
-    for (size_t t = 0; t < which.size(); ++t) {
-        if (!plans[t] || plans[t]->missing.empty()) continue;
-        const BatchObj& b = all[which[t]];
-        const DecodePlan& p = *plans[t];
-        const int r = int(p.missing.size());
-        for (int v = 0; v < b.k; ++v) {
-            in[pi + v] = b.shards[p.valid[size_t(v)]];
-            il[pi + v] = b.len[p.valid[size_t(v)]];
+        in.assign(n_in, nullptr);
+        out.assign(n_out, nullptr);
+        il.assign(n_in, 0);
+        ol.assign(n_out, 0);
+        groups.clear();
+        size_t pi = 0, po = 0;
+        for (size_t t = 0; t < which.size(); ++t) {
+            if (!plans[t] || plans[t]->missing.empty()) continue;
+            const BatchObj& b = all[which[t]];
+            const DecodePlan& p = *plans[t];
+            const int r = int(p.missing.size());
+            for (int v = 0; v < b.k; ++v) {
+                in[pi + v] = b.shards[p.valid[size_t(v)]];
+                il[pi + v] = b.len[p.valid[size_t(v)]];
+            }
+            for (int e = 0; e < r; ++e) {
+                out[po + e] = b.shards[p.missing[size_t(e)]];
+                ol[po + e] = b.len[p.missing[size_t(e)]];
+            }
+            groups[r].push_back(RsMixedObject{b.k, b.shard_size, RsObject{&in[pi], &il[pi], &out[po], &ol[po], offs[t]}});
+            pi += size_t(b.k);
+            po += size_t(r);
         }
-        for (int e = 0; e < r; ++e) {
-            out[po + e] = b.shards[p.missing[size_t(e)]];
-            ol[po + e] = b.len[p.missing[size_t(e)]];
-        }
-        groups[r].push_back(RsMixedObject{b.k, b.shard_size, RsObject{&in[pi], &il[pi], &out[po], &ol[po], offs[t]}});
-        pi += size_t(b.k);
-        po += size_t(r);
-    }
-    MXEC_TRY(run_rs_mixed(d, slot, s, groups));
+        return run_rs_mixed(d, slot, s, groups);
+    };
+    MXEC_TRY(with_stable_coef(d, collect, launch));
     for (size_t t = 0; t < which.size(); ++t)
         if (plans[t])
             for (int e : plans[t]->missing) all[which[t]].present[e] = 1;
@@ -155,12 +147,18 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
             return nullptr;
         }
         if (streams_per_device < 1) streams_per_device = 1;
-        // MXEC_LOGICAL_DEVICES=L (tests): open every selected device L times,
-        // each copy with its own slots, streams, arenas, combiner and
-        // pipeline, so the multi-device paths (per-device workers, round
-        // robin, error aggregation) run on a one-GPU box.
+        // MXEC_TEST_LOGICAL_DEVICES=L (tests and bench rehearsals only): open
+        // every selected device L times, each copy with its own slots,
+        // streams, arenas, combiner and pipeline, so the multi-device paths
+        // (per-device workers, round robin, error aggregation) run on a
+        // one-GPU box.  Never meant for production: it warns on stderr.
         int logical = 1;
-        if (const char* e = getenv("MXEC_LOGICAL_DEVICES")) logical = std::max(1, std::min(8, atoi(e)));
+        if (const char* e = getenv("MXEC_TEST_LOGICAL_DEVICES")) {
+            logical = std::max(1, std::min(8, atoi(e)));
+            if (logical > 1)
+                fprintf(stderr, "maxio_ec: MXEC_TEST_LOGICAL_DEVICES=%d: every selected GPU is opened %d times "
+                                "as separate devices (test-only setting)\n", logical, logical);
+        }
         auto* ctx = new mxec_ctx();
         for (int dl = 0; dl < n * logical && dl < 32 * logical; ++dl) {
             const int d = dl / logical;
@@ -328,9 +326,12 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* c
         MXEC_TRY(upload_segments(slot, s, base, up));
         for (int i = 0; i < m; ++i) out[size_t(i)] = base + sa * uint64_t(k + i);
         uint32_t off = 0;
-        MXEC_TRY(encode_coef(*ds.d, k, m, &off));
-        RsObject ob{in.data(), len.data(), out.data(), len.data() + k, off};
-        MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, m, {ob}));
+        MXEC_TRY(with_stable_coef(
+            *ds.d, [&] { return encode_coef(*ds.d, k, m, &off); },
+            [&] {
+                RsObject ob{in.data(), len.data(), out.data(), len.data() + k, off};
+                return run_rs(*ds.d, slot, s, shard_size, k, m, {ob});
+            }));
         std::vector<DownloadSeg> down;
         for (int i = 0; i < m; ++i) down.push_back({sa * uint64_t(k + i), parity[i], shard_size});
         MXEC_TRY(download_segments(slot, s, base, down));
@@ -394,12 +395,20 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
         const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
         std::shared_ptr<const DecodePlan> plan;
         uint32_t off = 0;
-        MXEC_TRY(decode_plan(*ds.d, k, m, present.data(), data_only, &plan, &off));
-        if (!plan) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
-        if (!plan->missing.empty()) {
-            std::vector<const uint8_t*> in;
-            std::vector<uint64_t> in_len, out_len;
-            std::vector<uint8_t*> out;
+        std::vector<const uint8_t*> in;
+        std::vector<uint64_t> in_len, out_len;
+        std::vector<uint8_t*> out;
+        auto collect = [&]() -> int {
+            MXEC_TRY(decode_plan(*ds.d, k, m, present.data(), data_only, &plan, &off));
+            if (!plan) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
+            return MXEC_OK;
+        };
+        auto launch = [&]() -> int {
+            if (plan->missing.empty()) return MXEC_OK;
+            in.clear();
+            in_len.clear();
+            out.clear();
+            out_len.clear();
             for (int v : plan->valid) {
                 in.push_back(base + sa * uint64_t(v));
                 in_len.push_back(len[size_t(v)]);
@@ -409,7 +418,10 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
                 out_len.push_back(len[size_t(e)]);
             }
             RsObject ob{in.data(), in_len.data(), out.data(), out_len.data(), off};
-            MXEC_TRY(run_rs(*ds.d, slot, s, shard_size, k, int(out.size()), {ob}));
+            return run_rs(*ds.d, slot, s, shard_size, k, int(out.size()), {ob});
+        };
+        MXEC_TRY(with_stable_coef(*ds.d, collect, launch));
+        if (!plan->missing.empty()) {
             std::vector<DownloadSeg> down;
             for (size_t t = 0; t < out.size(); ++t)
                 if (out_len[t]) down.push_back({sa * uint64_t(plan->missing[t]), shards[plan->missing[t]], out_len[t]});
@@ -441,7 +453,6 @@ int mxec_encode_strided_device(mxec_ctx* ctx, int dev, void* stream, int k, int 
         MXEC_TRY(ds.open(ctx, dev));
         hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
         uint32_t off = 0;
-        MXEC_TRY(encode_coef(*ds.d, k, m, &off));
         std::vector<uint64_t> len(static_cast<size_t>(k + m), shard_size);
         for (int j = 0; j < k; ++j)
             if (data_len) len[size_t(j)] = std::min<uint64_t>(data_len[j], shard_size);
@@ -451,9 +462,14 @@ int mxec_encode_strided_device(mxec_ctx* ctx, int dev, void* stream, int k, int 
         for (uint64_t o = 0; o < n_obj; ++o) {
             for (int j = 0; j < k; ++j) in[o * k + j] = data + o * data_obj_stride + j * data_shard_stride;
             for (int i = 0; i < m; ++i) out[o * m + i] = parity + o * parity_obj_stride + i * parity_shard_stride;
-            objs[o] = RsObject{&in[o * k], len.data(), &out[o * m], len.data() + k, off};
+            objs[o] = RsObject{&in[o * k], len.data(), &out[o * m], len.data() + k, 0};
         }
-        MXEC_TRY(run_rs(*ds.d, *ds.slot, s, shard_size, k, m, objs));
+        MXEC_TRY(with_stable_coef(
+            *ds.d, [&] { return encode_coef(*ds.d, k, m, &off); },
+            [&] {
+                for (auto& ob : objs) ob.coef_off = off;
+                return run_rs(*ds.d, *ds.slot, s, shard_size, k, m, objs);
+            }));
         if (digests_dev) {
             std::vector<const uint8_t*> ptrs;
             std::vector<uint64_t> lens;
@@ -519,8 +535,7 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_ob
                                                            &pl[pofs[o]], it->second}});
             }
             return MXEC_OK;
-        }));
-        MXEC_TRY(run_rs_mixed(*ds.d, *ds.slot, s, groups));
+        }, [&] { return run_rs_mixed(*ds.d, *ds.slot, s, groups); }));
         if (digests_dev) {
             std::vector<const uint8_t*> ptrs;
             std::vector<uint64_t> lens;

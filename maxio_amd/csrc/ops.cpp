@@ -11,6 +11,7 @@
 #include <map>
 
 #include "kernels.hpp"
+#include "sha_plan.hpp"
 
 namespace mxec {
 
@@ -288,8 +289,15 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
         const char* e = getenv("MXEC_SHA_FORM");
         return e && !strcmp(e, "stream") ? 3 : 0;
     }();
+    uint64_t longest = 0;
+    for (uint64_t l : lens) longest = std::max(longest, l);
+    const uint64_t seg_max = sha_stream_seg_max(longest, kShaSegBlocks);
+    // The stream kernel's 32-bit item counter must not wrap (sha_plan.hpp).
+    const bool items_fit = sha_stream_items_fit(n, seg_max, simds);
     bool stream = false;
-    if (tmo_dev && !arena && (form == 0 || form == 3) && n < (uint64_t(1) << 31)) {
+    if (!items_fit) {
+        // many messages plus one very long one: the split / one-wave forms
+    } else if (tmo_dev && !arena && (form == 0 || form == 3) && n < (uint64_t(1) << 31)) {
         bool aligned = true;
         for (const uint8_t* p : ptrs) aligned = aligned && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
         stream = aligned && (sha_stream_size(groups, simds) || form == 3 || env_form == 3);
@@ -322,8 +330,6 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     if (stream) {
         void* st = nullptr;
         MXEC_TRY(w.scratch(32 * n, &st));
-        uint64_t longest = 0;
-        for (uint64_t l : lens) longest = std::max(longest, l);
         a.force = 3;
         a.work = reinterpret_cast<uint32_t*>(db + o_w);
         a.state = static_cast<uint32_t*>(st);
@@ -340,7 +346,7 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
         // 110 ms vs 56; tools/sha_stream_lab place / repeat,
         // profiles/r2_sha_stream_placement.txt).
         a.wg_waves = simds % 4 == 0 ? 4 : 1;
-        a.seg_max = uint32_t(longest / 64 / kShaSegBlocks + 1);
+        a.seg_max = uint32_t(seg_max);
         *tmo_dev = a.work + 1;
     }
     MXEC_HIP(launch_sha256(a, s));

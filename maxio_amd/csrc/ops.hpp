@@ -145,4 +145,30 @@ int run_body_sums(Device& d, Slot& slot, hipStream_t s, const std::vector<const 
 // filesystem.rs:1095 guard, then the crate's ReedSolomon::new checks.
 int check_km(int k, int m);
 
+// Coefficient-table offsets are only valid until the device's 64 MiB table
+// arena is recycled (runtime.cpp coef_offset: it waits for the device, then
+// reuses the arena from the start).  `collect` takes a batch's offsets,
+// `launch` enqueues the kernels that read them; the pair runs again until no
+// recycle happened between the start of `collect` and the end of the
+// enqueue.  A recycle waits for every launch queued before it, so only a
+// launch queued after one can have read foreign tables: such a launch is
+// queued again with fresh offsets, behind it on the same stream and over the
+// same outputs (the RS kernels read only inputs and write only outputs), so
+// the last pass wins and the result is exact.
+template <class C, class L>
+int with_stable_coef(Device& d, C&& collect, L&& launch) {
+    auto epoch = [&] {
+        std::lock_guard<std::mutex> g(d.coef_mu);
+        return d.coef_epoch;
+    };
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        const uint64_t e0 = epoch();
+        MXEC_TRY(collect());
+        MXEC_TRY(launch());
+        if (epoch() == e0) return MXEC_OK;
+    }
+    return set_error(MXEC_E_INVALID_ARG,
+                     "the coefficient tables of one batch exceed the device's table arena (recycled 4 times)");
+}
+
 }  // namespace mxec

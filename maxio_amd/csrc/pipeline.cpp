@@ -2,7 +2,8 @@
 // sees it: request bodies in host memory, parity chunks and digests back in
 // host memory), spread over every device of the context.
 //
-// Per device (one host thread each, objects dealt round-robin over devices):
+// Per device (one host thread each; objects dealt round-robin over devices
+// when the batch is uniform, by bytes when it is mixed, deal.hpp):
 //   * an HBM object pool holds a whole wave of objects (k+m shard slots and
 //     k+m digests each, up to kPoolCap bytes), so the latency-bound SHA-256
 //     launches of many groups run concurrently instead of waiting on a small
@@ -27,6 +28,7 @@
 #include <vector>
 
 #include "../../include/maxio_ec.h"
+#include "deal.hpp"
 #include "ops.hpp"
 
 namespace mxec {
@@ -273,7 +275,6 @@ private:
                 const int k = std::get<0>(c.first), m = std::get<1>(c.first);
                 const uint64_t S = std::get<2>(c.first);
                 uint32_t coff = 0;
-                MXEC_TRY(encode_coef(d_, k, m, &coff));
                 const size_t n = c.second.size();
                 std::vector<const uint8_t*> ins(n * size_t(k));
                 std::vector<uint8_t*> outs(n * size_t(m));
@@ -287,9 +288,14 @@ private:
                         lens[t * (k + m) + j] = std::min<uint64_t>(h.dlen[j], S);
                     }
                     for (int i = 0; i < m; ++i) outs[t * m + i] = ob + uint64_t(k + i) * h.slot();
-                    ro[t] = RsObject{&ins[t * k], &lens[t * (k + m)], &outs[t * m], &lens[t * (k + m) + k], coff};
+                    ro[t] = RsObject{&ins[t * k], &lens[t * (k + m)], &outs[t * m], &lens[t * (k + m) + k], 0};
                 }
-                MXEC_TRY(run_rs(d_, slot, rs_s, S, k, m, ro, &arena_));
+                MXEC_TRY(with_stable_coef(
+                    d_, [&] { return encode_coef(d_, k, m, &coff); },
+                    [&] {
+                        for (auto& r : ro) r.coef_off = coff;
+                        return run_rs(d_, slot, rs_s, S, k, m, ro, &arena_);
+                    }));
             }
             MXEC_HIP(hipEventRecord(done[g], rs_s));
         }
@@ -358,6 +364,12 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
         for (uint64_t o = 0; o < n_obj; ++o) dsum += uint64_t(std::max(objs[o].k, 0));
         std::vector<uint64_t> dlen(size_t(dsum), 0);
         std::vector<std::vector<HostObj>> per(D);
+        // Device of each object: o mod D for a uniform batch, balanced by
+        // bytes for a mixed one (deal.hpp).
+        std::vector<uint64_t> obj_bytes(size_t(n_obj), 0);
+        for (uint64_t o = 0; o < n_obj; ++o)
+            obj_bytes[o] = uint64_t(std::max(objs[o].k, 0) + std::max(objs[o].m, 0)) * rup(objs[o].shard_size, kAlign);
+        const std::vector<uint32_t> owner = deal_objects(obj_bytes, uint32_t(D));
         uint64_t doff = 0, poff = 0, goff = 0;
         int first_err = MXEC_OK;
         std::string first_msg;
@@ -379,7 +391,7 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
                 }
             } else {
                 HostObj h{k, m, S, data + doff, &dlen[size_t(doff)], parity + poff, digests ? digests + goff : nullptr};
-                per[o % D].push_back(h);
+                per[owner[o]].push_back(h);
             }
             doff += uint64_t(std::max(k, 0));
             poff += uint64_t(std::max(m, 0));

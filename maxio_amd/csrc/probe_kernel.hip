@@ -9,6 +9,8 @@
 // grid-stride.
 //
 //   mxprobe_copy       read n bytes, write n bytes             (1:1)
+//   mxprobe_copy_float4  the same with the guide's float4 copy: plain loads
+//                      and stores, one element per lane, no grid-stride
 //   mxprobe_read2_write1  read 2n bytes (two sources), write n (2:1, the
 //                      encode stream of k=4 m=2 and k=8 m=4)
 //   mxprobe_read       read n bytes                            (read-only)
@@ -38,6 +40,14 @@ __global__ __launch_bounds__(256) void probe_copy(const u32x4* __restrict__ s, u
         __builtin_nontemporal_store(e, d + i + 3 * stride);
     }
     for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
+// The guide's float4 copy (MI355X_MICROARCH.md: 6.29 TB/s measured): one
+// 16-byte element per lane, plain (temporal) loads and stores, one
+// workgroup per 256 elements, no grid-stride loop.
+__global__ __launch_bounds__(256) void probe_copy_float4(const float4* __restrict__ s, float4* __restrict__ d, uint64_t n) {
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i < n) d[i] = s[i];
 }
 
 __global__ __launch_bounds__(256) void probe_read2_write1(const u32x4* __restrict__ s0, const u32x4* __restrict__ s1,
@@ -142,6 +152,17 @@ extern "C" int mxprobe_copy(void* dst, const void* src, uint64_t bytes, void* st
         return int(hipErrorInvalidValue);
     hipLaunchKernelGGL(probe_copy, dim3(grid()), dim3(256), 0, static_cast<hipStream_t>(stream),
                        static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), bytes / 16);
+    return int(hipGetLastError());
+}
+
+// The guide's float4 copy over `bytes` (multiple of 16, at most 2^40).
+extern "C" int mxprobe_copy_float4(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if ((bytes & 15) || bytes > (uint64_t(1) << 40) || (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15)
+        return int(hipErrorInvalidValue);
+    const uint64_t n = bytes / 16, blocks = (n + 255) / 256;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(probe_copy_float4, dim3(uint32_t(blocks)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const float4*>(src), static_cast<float4*>(dst), n);
     return int(hipGetLastError());
 }
 

@@ -402,12 +402,15 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* const
     gu32* state = (gu32*)(state_p);
     const uint32_t lane = threadIdx.x & 63;  // every wave of a workgroup works alone
     const uint32_t groups = (n + 63) / 64;
-    const uint32_t n_items = groups * seg_max;
+    // The host (ops.cpp run_sha) picks this form only when n_items plus one
+    // overshoot take per wave stays below 2^32, so the item counter never
+    // wraps back onto item 0.
+    const uint64_t n_items = uint64_t(groups) * seg_max;
     for (;;) {
         uint32_t t = 0;
         if (lane == 0) t = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = __builtin_amdgcn_readfirstlane(t);
-        if (t >= n_items) break;
+        if (uint64_t(t) >= n_items) break;
         const uint32_t sg = t / groups, g = t - sg * groups;
         const uint32_t i = g * 64 + lane;
         const bool live = i < n;
@@ -503,8 +506,11 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* const
         if (sg + 1 < segs) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's state stores have landed
             if (lane == 0) SHA_DBG(t, 5, uint32_t(__builtin_amdgcn_s_memtime() >> 4));
-            // Every lane, the same word and value: no divergent region.
-            __hip_atomic_store(prog, sg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // Every lane, the same word and value: no divergent region.  The
+            // release orders the state stores before the hand-off in the
+            // memory model (the reader's acquire fence pairs with it), not
+            // only through the vmcnt drain above.
+            __hip_atomic_store(prog, sg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             if (lane == 0) SHA_DBG(t, 3, sg + 1);
         }
     }

@@ -1,0 +1,80 @@
+#!/bin/bash
+# One parametrised GPU-box script (replaces round 2's one-off lease scripts).
+#
+#   scripts/gpu.sh <out-subdir> step[,step...]
+#
+# Steps (each under its own time limit; the first failure ends the call):
+#   tests     full `pytest -m gpu` (one process) -> pytest_gpu.log
+#   smoke     __graft_entry__.smoke()
+#   bench     the driver's default command: python bench.py -> bench.json
+#   refuse2   python bench.py --gpus 2 on a one-GPU box: must exit 2, no line
+#   rehearse  BENCH_REHEARSE_LOGICAL=1 bench.py --gpus 2 (labelled in-process
+#             multi-device rehearsal on two logical devices of the one card)
+#   prof      rocprofv3 --kernel-trace --stats of the default bench command
+#   pmc       FETCH_SIZE / WRITE_SIZE passes (one run each) of rs_apply_fast
+#             for configs 2 and ns, summarised with the grid they ran at
+#   rust      probe for rustc / cargo
+#   cfg:<c>   python bench.py --config <c> --no-extra -> cfg_<c>.json
+# Env: BENCH_ARGS (extra bench.py args for bench/prof).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+O="$R/gpurun_out/${1:?out subdir}"
+mkdir -p "$O"
+IFS=, read -ra STEPS <<< "${2:?steps}"
+export TMPDIR=/tmp
+for st in "${STEPS[@]}"; do
+  echo "== $st $(date +%T)"
+  case "$st" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$O/pytest_gpu.log" 2>&1 || { tail -40 "$O/pytest_gpu.log"; exit 1; }
+      tail -2 "$O/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { cat "$O/smoke.log"; exit 1; }
+      cat "$O/smoke.log" ;;
+    bench)
+      timeout -k 10 900 python bench.py $BENCH_ARGS > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
+      cat "$O/bench.json" ;;
+    refuse2)
+      rc=0; timeout -k 10 300 python bench.py --gpus 2 --steps 2 > "$O/refuse2.out" 2> "$O/refuse2.err" || rc=$?
+      echo "exit $rc"; cat "$O/refuse2.err"
+      [ "$rc" = 2 ] && [ ! -s "$O/refuse2.out" ] || { echo "expected exit 2 and no line"; exit 1; } ;;
+    rehearse)
+      BENCH_REHEARSE_LOGICAL=1 timeout -k 10 600 python bench.py --gpus 2 --objects 256 --steps 10 --warmup 2 \
+        > "$O/rehearse2.json" 2> "$O/rehearse2.err" || { tail -20 "$O/rehearse2.err"; exit 1; }
+      cat "$O/rehearse2.json" ;;
+    prof)
+      ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run --output-format csv \
+          -- python3 "$R/bench.py" $BENCH_ARGS > "$O/prof_bench.json" 2> "$O/prof_bench.err" ) || { tail -20 "$O/prof_bench.err"; exit 1; }
+      find /tmp/prof -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
+      find /tmp/prof -name "*kernel_trace.csv" -exec cp {} "$O/kernel_trace.csv" \;
+      cat "$O/prof_bench.json" ;;
+    pmc)
+      for cfg in 2 ns; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast -d "/tmp/pmc/${cfg}_$c" \
+              -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --cpu-seconds 0 \
+              --no-extra --no-e2e > "$O/pmc_${cfg}_$c.log" 2>&1 ) || { tail -5 "$O/pmc_${cfg}_$c.log"; exit 1; }
+          find "/tmp/pmc/${cfg}_$c" -name "*counter_collection.csv" -exec cp {} "$O/pmc_${cfg}_$c.csv" \;
+        done
+      done
+      # configs[1]: 1024 x 4+2 x 10 MiB, 163 840 tiles of 64 KiB, 1024 WG/CU;
+      # north star: 4096 x 8+4 x 1 MiB, 65 536 tiles, 512 WG/CU.
+      python tools/pmc_summary.py "$O/pmc_2_FETCH_SIZE.csv" "$O/pmc_2_WRITE_SIZE.csv" "rs_apply_fast<2, 4, true, false" \
+        64424509440 --blocks-per-cu 1024 --tiles 163840 --what "config 2, rs_apply_fast<2,4,nt> at 1024 WG/CU" \
+        --out "$O/pmc_k4m2_traffic.json" || exit 1
+      python tools/pmc_summary.py "$O/pmc_ns_FETCH_SIZE.csv" "$O/pmc_ns_WRITE_SIZE.csv" "rs_apply_fast<4, 4, true, false" \
+        51539607552 --blocks-per-cu 512 --tiles 65536 --what "north star, rs_apply_fast<4,4,nt> at 512 WG/CU" \
+        --out "$O/pmc_k8m4_traffic.json" || exit 1 ;;
+    rust)
+      { command -v rustc; command -v cargo; rustc --version; cargo --version; } > "$O/rust_probe.txt" 2>&1 || true
+      cat "$O/rust_probe.txt" ;;
+    cfg:*)
+      c="${st#cfg:}"
+      timeout -k 10 900 python bench.py --config "$c" --no-extra $BENCH_ARGS > "$O/cfg_$c.json" 2> "$O/cfg_$c.err" || { tail -20 "$O/cfg_$c.err"; exit 1; }
+      cat "$O/cfg_$c.json" ;;
+    *) echo "unknown step $st"; exit 1 ;;
+  esac
+done
+echo "== done $(date +%T)"

@@ -7,7 +7,7 @@ object checked (not a sample):
   chunks, encoded then reconstructed with 1..m seeded erasures in one stream,
   per class (the bench's layout) and as one mixed-shape launch;
 * configs[3] — 10+4 at 1 MiB, one object per device, on eight logical
-  devices of one GPU (MXEC_LOGICAL_DEVICES=8, each with its own streams,
+  devices of one GPU (MXEC_TEST_LOGICAL_DEVICES=8, each with its own streams,
   arenas and pipeline, as MaxIO's one process would open eight MI355X), and
   the literal reading k=64 m=4.
 
@@ -146,9 +146,9 @@ def test_config5_one_mixed_launch(ctx):
 
 @pytest.fixture()
 def ctx8(monkeypatch):
-    monkeypatch.setenv("MXEC_LOGICAL_DEVICES", "8")
+    monkeypatch.setenv("MXEC_TEST_LOGICAL_DEVICES", "8")
     c = maxio_amd.Context(device_mask=1, streams_per_device=1)
-    monkeypatch.delenv("MXEC_LOGICAL_DEVICES")
+    monkeypatch.delenv("MXEC_TEST_LOGICAL_DEVICES")
     assert c.device_ids() == [0] * 8
     yield c
     c.close()

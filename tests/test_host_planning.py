@@ -1,0 +1,30 @@
+"""CPU unit tests of host-side planning helpers, built with
+-fsanitize=address,undefined:
+
+* the SHA-256 stream form is refused when its 32-bit item counter could
+  wrap (many short messages plus one very long one would leave
+  the tail items unhashed and their ok flags stale);
+* mxec_encode_batch_host deals a mixed batch over devices by bytes (within
+  10 % per device at 2/4/8 devices) and a uniform one as object o -> o mod D
+  (VERDICT r2 item 6)."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.join(ROOT, "tests", "c_manifest")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+@pytest.mark.parametrize("src,ok", [("sha_guard_check.cpp", "sha guard ok"), ("deal_check.cpp", "deal ok")])
+def test_host_planning(tmp_path, src, ok):
+    exe = str(tmp_path / src.split(".")[0])
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", os.path.join(HERE, src), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert ok in r.stdout

@@ -259,9 +259,9 @@ def test_mixed_reconstruct_async_matches(ctx):
 def ctx8(monkeypatch):
     import maxio_amd
 
-    monkeypatch.setenv("MXEC_LOGICAL_DEVICES", "8")
+    monkeypatch.setenv("MXEC_TEST_LOGICAL_DEVICES", "8")
     c = maxio_amd.Context(device_mask=1, streams_per_device=1)
-    monkeypatch.delenv("MXEC_LOGICAL_DEVICES")
+    monkeypatch.delenv("MXEC_TEST_LOGICAL_DEVICES")
     assert c.device_ids() == [0] * 8
     yield c
     c.close()
