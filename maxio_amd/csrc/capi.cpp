@@ -172,10 +172,12 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
             bool ok = true;
             for (int s = 0; s < streams_per_device; ++s) {
                 auto slot = std::make_unique<Slot>();
+                slot->owner = dev.get();
                 if (hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking) != hipSuccess) {
                     ok = false;
                     break;
                 }
+                affinity_tag(slot->stream, dev.get());
                 // Descriptor ring entries at their 1 MiB floor now, so the
                 // first calls on each slot do not allocate (and a later
                 // re-size, which frees and so waits for the device, is rare).
@@ -207,6 +209,7 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
 void mxec_close(mxec_ctx* ctx) {
     if (!ctx) return;
     async_shutdown(ctx->c);  // every queued *_async call finishes first
+    affinity_report();
     for (auto& d : ctx->c.devs) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();

@@ -216,11 +216,13 @@ ShaCombiner* combiner_of(Device& d) {
         auto c = std::make_shared<ShaCombiner>();
         for (size_t i = 0; i < combine_streams(); ++i) {
             auto sl = std::make_unique<Slot>();
+            sl->owner = &d;
             int least = 0, greatest = 0;
             const bool prio = combine_priority() &&
                               hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
                               hipStreamCreateWithPriority(&sl->stream, hipStreamNonBlocking, greatest) == hipSuccess;
             if (!prio && hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+            affinity_tag(sl->stream, &d);
             c->free_slots.push_back(sl.get());
             c->slots.push_back(std::move(sl));
         }

@@ -213,6 +213,7 @@ int run_frames(Device& d, Slot& slot, hipStream_t s, const std::vector<Job>& job
     std::memcpy(w.data() + o_fr, frames.data(), frames.size() * sizeof(GcmFrame));
     char* dev = nullptr;
     MXEC_TRY(w.commit(s, &dev));
+    MXEC_TRY(affinity_check(d, &slot, s, "gcm frames"));
     GcmArgs a{};
     a.te = te;
     a.keys = reinterpret_cast<const GcmKey*>(dev + o_keys);

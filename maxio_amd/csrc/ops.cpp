@@ -95,6 +95,14 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
            const std::vector<RsObject>& objs, DescArena* arena) {
     if (objs.empty() || r == 0) return MXEC_OK;
     const size_t n = objs.size();
+    if (affinity_on()) {
+        std::vector<const void*> ps;
+        for (const RsObject& ob : objs) {
+            for (int j = 0; j < k; ++j) ps.push_back(ob.in[j]);
+            for (int i = 0; i < r; ++i) ps.push_back(ob.out[i]);
+        }
+        MXEC_TRY(affinity_check(dev, &slot, s, "run_rs", arena, ps.data(), ps.size()));
+    }
     DescWriter w(slot, arena);
     const uint64_t tile = rs_tile_bytes(rs_default_variant(uint32_t(r)));
     const uint64_t tiles_per_obj = (shard_size + tile - 1) / tile;
@@ -212,6 +220,15 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         for (const auto& key : order) MXEC_TRY(run_rs(dev, slot, s, key.second, key.first, g.first, by[key]));
     }
     if (grouped.empty()) return MXEC_OK;
+    if (affinity_on()) {
+        std::vector<const void*> ps;
+        for (const Plan& p : grouped)
+            for (const RsMixedObject& ob : *p.objs) {
+                for (int j = 0; j < ob.k; ++j) ps.push_back(ob.o.in[j]);
+                for (int i = 0; i < p.r; ++i) ps.push_back(ob.o.out[i]);
+            }
+        MXEC_TRY(affinity_check(dev, &slot, s, "run_rs_mixed", nullptr, ps.data(), ps.size()));
+    }
     // Every grouped launch's tables in one upload: one host-to-device copy
     // ahead of the launches instead of one between each pair of them (a
     // copy in the stream costs ~25-50 us of idle GPU at that point).
@@ -281,6 +298,12 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     const size_t n = ptrs.size();
     if (tmo_dev) *tmo_dev = nullptr;
     if (!n) return MXEC_OK;
+    if (affinity_on()) {
+        std::vector<const void*> ps(ptrs.begin(), ptrs.end());
+        ps.push_back(digests_dev);
+        ps.push_back(ok_dev);
+        MXEC_TRY(affinity_check(dev, &slot, s, "run_sha", arena, ps.data(), ps.size()));
+    }
     // The stream form: more 64-message groups than SIMDs, every message
     // 16-byte aligned, a caller that checks the timeout word, ring tables.
     // MXEC_SHA_FORM=stream forces it whenever it is allowed (tests).

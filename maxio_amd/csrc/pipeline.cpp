@@ -106,11 +106,16 @@ struct PipeRes {
     DevBuf pool, digests;
     Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
     bool ready = false;
-    int init() {
+    int init(const Device& dev) {
         if (ready) return MXEC_OK;
+        desc_slot.owner = &dev;
+        arena.owner = &dev;
         MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
         MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
         for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        affinity_tag(h2d, &dev);
+        affinity_tag(d2h, &dev);
+        for (auto s : cs) affinity_tag(s, &dev);
         MXEC_TRY(in.init());
         MXEC_TRY(out.init());
         ready = true;
@@ -179,6 +184,10 @@ private:
 
     int upload(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
+        if (affinity_on()) {
+            const void* p = dst;
+            MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload", &arena_, &p, 1));
+        }
         if (is_pinned(src, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, h2d_));
             return MXEC_OK;
@@ -209,6 +218,10 @@ private:
 
     int download(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
+        if (affinity_on()) {
+            const void* p = src;
+            MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download", &arena_, &p, 1));
+        }
         if (is_pinned(dst, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, d2h_));
             return MXEC_OK;
@@ -417,7 +430,7 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
                     std::lock_guard<std::mutex> g(dev.pipe_mu);
                     if (!dev.pipe) dev.pipe = std::make_shared<PipeRes>();
                     PipeRes& r = *static_cast<PipeRes*>(dev.pipe.get());
-                    MXEC_TRY(r.init());
+                    MXEC_TRY(r.init(dev));
                     DevicePipeline p(dev, r);
                     return p.run(per[d]);
                 }();

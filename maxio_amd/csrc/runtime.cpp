@@ -2,6 +2,7 @@
 #include "runtime.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -128,6 +129,10 @@ bool pinned_range(const void* p, uint64_t len) {
 }
 
 int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
+    if (slot.owner) {
+        const void* b = dev_base;
+        MXEC_TRY(affinity_check(*slot.owner, &slot, s, "upload_segments", nullptr, &b, 1));
+    }
     if (segs.empty()) return MXEC_OK;
     bool all_pinned = true;
     for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.src, g.len));
@@ -181,6 +186,10 @@ int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vec
 }
 
 int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs) {
+    if (slot.owner) {
+        const void* b = dev_base;
+        MXEC_TRY(affinity_check(*slot.owner, &slot, s, "download_segments", nullptr, &b, 1));
+    }
     if (segs.empty()) return slot_wait(slot, s);
     bool all_pinned = true;
     for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.dst, g.len));
@@ -262,6 +271,7 @@ size_t DescWriter::add(size_t bytes) {
 }
 
 int DescWriter::commit(hipStream_t stream, char** dev_base) {
+    if (slot_.owner) MXEC_TRY(affinity_check(*slot_.owner, &slot_, stream, "descriptor upload", arena_));
     if (arena_) {
         const size_t n = (tmp_.size() + 255) & ~size_t(255);
         if (arena_->used + n > arena_->host.cap || arena_->used + n > arena_->dev.cap)
@@ -298,7 +308,10 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
         // The entry's previous launches are done (waited above), so the copy
         // needs no ordering against `stream`; only the launches that follow
         // wait for it.
-        if (!slot_.upload) MXEC_HIP(hipStreamCreateWithFlags(&slot_.upload, hipStreamNonBlocking));
+        if (!slot_.upload) {
+            MXEC_HIP(hipStreamCreateWithFlags(&slot_.upload, hipStreamNonBlocking));
+            affinity_tag(slot_.upload, slot_.owner);
+        }
         if (!buf_->uploaded) MXEC_HIP(hipEventCreateWithFlags(&buf_->uploaded, hipEventDisableTiming));
         MXEC_HIP(hipMemcpyAsync(buf_->dev.p, buf_->host.p, n, hipMemcpyHostToDevice, slot_.upload));
         MXEC_HIP(hipEventRecord(buf_->uploaded, slot_.upload));
@@ -354,6 +367,66 @@ int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<
     dev.coef_index.emplace(key, o);
     *off = o;
     return MXEC_OK;
+}
+
+namespace {
+std::atomic<uint64_t> g_aff_checks{0}, g_aff_bad{0};
+std::mutex g_aff_mu;
+std::unordered_map<hipStream_t, const Device*>& aff_streams() {
+    static auto* m = new std::unordered_map<hipStream_t, const Device*>();
+    return *m;
+}
+}  // namespace
+
+bool affinity_on() {
+    const char* e = getenv("MXEC_DEBUG_AFFINITY");
+    return e && *e && std::strcmp(e, "0") != 0;
+}
+
+void affinity_tag(hipStream_t s, const Device* d) {
+    if (!s || !affinity_on()) return;
+    std::lock_guard<std::mutex> g(g_aff_mu);
+    aff_streams()[s] = d;
+}
+
+int affinity_check(const Device& d, const Slot* slot, hipStream_t s, const char* where, const DescArena* arena,
+                   const void* const* ptrs, size_t n_ptrs) {
+    if (!affinity_on()) return MXEC_OK;
+    g_aff_checks.fetch_add(1);
+    std::string bad;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != d.id)
+        bad = "current HIP device " + std::to_string(cur) + ", work for device " + std::to_string(d.id);
+    if (bad.empty() && slot && slot->owner && slot->owner != &d) bad = "slot of another (logical) device";
+    if (bad.empty() && arena && arena->owner && arena->owner != &d) bad = "descriptor arena of another (logical) device";
+    if (bad.empty() && s) {
+        {
+            std::lock_guard<std::mutex> g(g_aff_mu);
+            auto it = aff_streams().find(s);
+            if (it != aff_streams().end() && it->second != &d) bad = "stream of another (logical) device";
+        }
+        int sd = -1;
+        if (bad.empty() && hipStreamGetDevice(s, &sd) == hipSuccess && sd != d.id)
+            bad = "stream on HIP device " + std::to_string(sd);
+        (void)hipGetLastError();
+    }
+    for (size_t i = 0; bad.empty() && i < n_ptrs; ++i) {
+        hipPointerAttribute_t at{};
+        if (ptrs[i] && hipPointerGetAttributes(&at, ptrs[i]) == hipSuccess && at.type == hipMemoryTypeDevice &&
+            at.device != d.id)
+            bad = "device pointer of HIP device " + std::to_string(at.device);
+        (void)hipGetLastError();
+    }
+    if (bad.empty()) return MXEC_OK;
+    g_aff_bad.fetch_add(1);
+    fprintf(stderr, "maxio_ec affinity violation in %s: %s\n", where, bad.c_str());
+    return set_error(MXEC_E_DEVICE, std::string("affinity violation in ") + where + ": " + bad);
+}
+
+void affinity_report() {
+    if (!affinity_on()) return;
+    fprintf(stderr, "maxio_ec affinity: %llu checks, %llu violations\n",
+            static_cast<unsigned long long>(g_aff_checks.load()), static_cast<unsigned long long>(g_aff_bad.load()));
 }
 
 Device* pick_device(Ctx* ctx, int dev_index) {

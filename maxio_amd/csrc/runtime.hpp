@@ -76,8 +76,11 @@ struct DescBuf {
     bool pending = false;
 };
 
+struct Device;
+
 struct Slot {
     std::mutex mu;
+    const Device* owner = nullptr;  // the (logical) device whose queues these are
     hipStream_t stream = nullptr;
     DevBuf shards;    // host-API staging: shard images on the device
     DevBuf digests;   // host-API digests / ok flags
@@ -204,6 +207,7 @@ void async_shutdown(Ctx& c);
 // Descriptor tables of many launches in flight at once (host pipeline): one
 // pinned + device region, bump-allocated, never reused until reset().
 struct DescArena {
+    const Device* owner = nullptr;
     PinnedBuf host;
     DevBuf dev;
     size_t used = 0;
@@ -245,6 +249,20 @@ int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<
                 uint32_t* off);
 
 Device* pick_device(Ctx* ctx, int dev_index);
+
+// MXEC_DEBUG_AFFINITY=1 (tests; read per call): every launch and copy checks
+// that the HIP current device, the stream, the slot, the descriptor arena and
+// the data pointers all belong to the device doing the work.  Internal
+// streams are tagged with their (logical) device when created, so on
+// MXEC_TEST_LOGICAL_DEVICES runs -- one card presented as several devices,
+// where physical ids cannot tell them apart -- a stream, slot or arena of
+// another logical device is still caught.  A violation fails the call with
+// MXEC_E_DEVICE; mxec_close prints the running totals to stderr.
+bool affinity_on();
+void affinity_tag(hipStream_t s, const Device* d);
+int affinity_check(const Device& d, const Slot* slot, hipStream_t s, const char* where,
+                   const DescArena* arena = nullptr, const void* const* ptrs = nullptr, size_t n_ptrs = 0);
+void affinity_report();
 
 }  // namespace mxec
 

@@ -149,6 +149,7 @@ int run_body_sums(Device& d, Slot& slot, hipStream_t s, const std::vector<const 
         for (size_t i = 0; i < n; ++i)
             for (uint64_t t = 0; t < bodies[i].n_tiles; ++t) tb[bodies[i].tile0 + t] = uint32_t(i);
     }
+    MXEC_TRY(affinity_check(d, &slot, s, "run_body_sums"));
     char* dev = nullptr;
     MXEC_TRY(w.commit(s, &dev));
     if (!polys.empty()) {

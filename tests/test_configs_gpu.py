@@ -15,6 +15,8 @@ Reference: filesystem.rs:1084-1145 (encode), chunk_reader.rs:157-226
 (reconstruct); SURVEY §8(d) maps the configs."""
 from __future__ import annotations
 
+import re
+
 import hashlib
 
 import numpy as np
@@ -145,13 +147,21 @@ def test_config5_one_mixed_launch(ctx):
 
 
 @pytest.fixture()
-def ctx8(monkeypatch):
+def ctx8(monkeypatch, capfd):
+    """Eight logical devices of the one card, with the debug affinity check
+    on (MXEC_DEBUG_AFFINITY: every launch and copy asserts that its stream,
+    slot, arena and pointers belong to the launching logical device); the
+    totals printed at close must show checks and no violation."""
     monkeypatch.setenv("MXEC_TEST_LOGICAL_DEVICES", "8")
+    monkeypatch.setenv("MXEC_DEBUG_AFFINITY", "1")
     c = maxio_amd.Context(device_mask=1, streams_per_device=1)
     monkeypatch.delenv("MXEC_TEST_LOGICAL_DEVICES")
     assert c.device_ids() == [0] * 8
     yield c
     c.close()
+    err = capfd.readouterr().err
+    m = re.search(r"maxio_ec affinity: (\d+) checks, (\d+) violations", err)
+    assert m and int(m.group(1)) > 0 and m.group(2) == "0", err[-2000:]
 
 
 @pytest.mark.parametrize("k,m,n_obj", [(10, 4, 8), (10, 4, 13), (64, 4, 8)])
@@ -184,3 +194,40 @@ def test_config4_one_object_per_device(ctx8, k, m, n_obj):
         got = [dig[(o * (k + m) + t) * 32:(o * (k + m) + t + 1) * 32].tobytes() for t in range(k + m)]
         assert got == want_dig, o
         assert got[0] == hashlib.sha256(chunks[0].tobytes()).digest()
+
+
+def test_config5_mixed_host_batch_over_eight_devices(ctx8):
+    """configs[4]'s mixed stream as a host batch (mxec_encode_batch_host) over
+    eight devices: 4+2 / 8+4 / 10+4 at 64 KiB .. 10 MiB chunks with short last
+    chunks, dealt by bytes (deal.hpp; the balance itself is unit-tested on
+    the CPU, tests/test_host_planning.py).  Every parity chunk and digest
+    equals the oracle's, with the affinity check on."""
+    rng = np.random.default_rng(SEED + 55)
+    kms = [(4, 2), (8, 4), (10, 4)]
+    sizes = [64 << 10, 256 << 10, 1 << 20, 4 << 20, 10 << 20]
+    objs, dptr, pptr, dlen, keep = [], [], [], [], []
+    for o in range(20):
+        k, m = kms[o % 3]
+        S = sizes[int(rng.integers(0, len(sizes)))] if o >= 5 else sizes[o]
+        chunks = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+        chunks[-1] = chunks[-1][: int(rng.integers(1, S + 1))].copy()
+        outs = [np.full(S, 0xEE, np.uint8) for _ in range(m)]
+        objs.append((k, m, S))
+        dptr += [c.ctypes.data for c in chunks]
+        dlen += [c.size for c in chunks]
+        pptr += [x.ctypes.data for x in outs]
+        keep.append((chunks, outs, m, S))
+    n_msgs = sum(k + m for (k, m, S) in objs)
+    dig = np.zeros(n_msgs * 32, np.uint8)
+    st = ctx8.encode_batch_host(objs, dptr, pptr, data_len=dlen, digests=dig)
+    assert not st.any()
+    row = 0
+    for o, (chunks, outs, m, S) in enumerate(keep):
+        want, want_dig, rc = oracle.compute_parity(chunks, m, S)
+        assert rc == 0
+        for i in range(m):
+            assert np.array_equal(outs[i], want[i]), (o, i)
+        k = len(chunks)
+        got = [dig[(row + t) * 32:(row + t + 1) * 32].tobytes() for t in range(k + m)]
+        assert got == want_dig, o
+        row += k + m

@@ -8,6 +8,8 @@ Reference: filesystem.rs:1084-1145 (encode of each object),
 chunk_reader.rs:157-226 (verify -> erasure -> reconstruct of each object)."""
 from __future__ import annotations
 
+import re
+
 import numpy as np
 import pytest
 
@@ -256,15 +258,23 @@ def test_mixed_reconstruct_async_matches(ctx):
 
 
 @pytest.fixture()
-def ctx8(monkeypatch):
+def ctx8(monkeypatch, capfd):
+    """Eight logical devices of the one card, with the debug affinity check
+    on (MXEC_DEBUG_AFFINITY: every launch and copy asserts that its stream,
+    slot, arena and pointers belong to the launching logical device); the
+    totals printed at close must show checks and no violation."""
     import maxio_amd
 
     monkeypatch.setenv("MXEC_TEST_LOGICAL_DEVICES", "8")
+    monkeypatch.setenv("MXEC_DEBUG_AFFINITY", "1")
     c = maxio_amd.Context(device_mask=1, streams_per_device=1)
     monkeypatch.delenv("MXEC_TEST_LOGICAL_DEVICES")
     assert c.device_ids() == [0] * 8
     yield c
     c.close()
+    err = capfd.readouterr().err
+    m = re.search(r"maxio_ec affinity: (\d+) checks, (\d+) violations", err)
+    assert m and int(m.group(1)) > 0 and m.group(2) == "0", err[-2000:]
 
 
 def test_mixed_batches_over_eight_devices(ctx8):
