@@ -295,15 +295,23 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // batch size is a floor, not a cap.  Without this, eight concurrent
         // 10 240-chunk verifications (config 3c) settled into two launches of
         // four (split form, 640 groups each) instead of one of 81 920
-        // messages, which takes the stream form.  Only while the batch is
-        // still short of the stream form's size: past it a bigger launch
-        // gains nothing, and small latency-bound verifications should not
-        // pay the idle window.
-        const uint64_t simds = uint64_t(d.n_cus) * 4;
-        auto short_of_stream = [&] { return !sha_stream_size((c->pending_msgs + 63) / 64, simds); };
-        if (c->pending.size() >= 2 && short_of_stream()) {
+        // messages, which takes the stream form.  Only when the launch will
+        // be long next to the idle window: a chain takes ~1.8 us per 64-byte
+        // block of the longest pending message, and the extension is taken
+        // only while one idle window costs at most 2 % of that, so small
+        // latency-bound verifications (64 KiB chunks: a ~1.8 ms launch) do
+        // not pay it, while 1 MiB chunks (~29 ms) still gather.
+        // (Stopping at the stream form's size instead split config 3c's
+        // eight batches into launches of five and three: 585 vs 970 GiB/s.)
+        auto long_launch = [&] {
+            uint64_t longest = 0;
+            for (const ShaCombiner::Req* r : c->pending)
+                for (uint64_t l : *r->lens) longest = std::max(longest, l);
+            return double(longest / 64) * 1.8 * 0.02 >= double(gather_idle_us());
+        };
+        if (c->pending.size() >= 2 && long_launch()) {
             const auto hard = t0 + std::chrono::microseconds(gather_max_us());
-            for (size_t seen = c->pending.size(); short_of_stream() && std::chrono::steady_clock::now() < hard;) {
+            for (size_t seen = c->pending.size(); std::chrono::steady_clock::now() < hard;) {
                 c->cv_gather.wait_for(lk, std::chrono::microseconds(gather_idle_us()),
                                       [&] { return c->pending.size() > seen; });
                 if (c->pending.size() == seen) break;
