@@ -59,13 +59,13 @@ for st in "${STEPS[@]}"; do
           find "/tmp/pmc/${cfg}_$c" -name "*counter_collection.csv" -exec cp {} "$O/pmc_${cfg}_$c.csv" \;
         done
       done
-      # configs[1]: 1024 x 4+2 x 10 MiB, 163 840 tiles of 64 KiB, 1024 WG/CU;
-      # north star: 4096 x 8+4 x 1 MiB, 65 536 tiles, 512 WG/CU.
+      # configs[1]: 1024 x 4+2 x 10 MiB, 655 360 tiles of 16 KiB, 1024 WG/CU;
+      # north star: 4096 x 8+4 x 1 MiB, 262 144 tiles, 512 WG/CU.
       python tools/pmc_summary.py "$O/pmc_2_FETCH_SIZE.csv" "$O/pmc_2_WRITE_SIZE.csv" "rs_apply_fast<2, 4, true, false" \
-        64424509440 --blocks-per-cu 1024 --tiles 163840 --what "config 2, rs_apply_fast<2,4,nt> at 1024 WG/CU" \
+        64424509440 --blocks-per-cu 1024 --tiles 655360 --what "config 2, rs_apply_fast<2,4,nt> at 1024 WG/CU" \
         --out "$O/pmc_k4m2_traffic.json" || exit 1
       python tools/pmc_summary.py "$O/pmc_ns_FETCH_SIZE.csv" "$O/pmc_ns_WRITE_SIZE.csv" "rs_apply_fast<4, 4, true, false" \
-        51539607552 --blocks-per-cu 512 --tiles 65536 --what "north star, rs_apply_fast<4,4,nt> at 512 WG/CU" \
+        51539607552 --blocks-per-cu 512 --tiles 262144 --what "north star, rs_apply_fast<4,4,nt> at 512 WG/CU" \
         --out "$O/pmc_k8m4_traffic.json" || exit 1 ;;
     rust)
       { command -v rustc; command -v cargo; rustc --version; cargo --version; } > "$O/rust_probe.txt" 2>&1 || true
