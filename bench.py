@@ -822,33 +822,6 @@ def float4_copy_on_buffers(torch, stream, w):
     return round(2 * half / (ms * 1e-3) / 1e9, 1)
 
 
-def rw_bound_on_buffers(torch, stream, w):
-    """A ceiling for a read:write stream that shares nothing with the RS
-    kernel's schedule: a plain read stream and a plain write stream, each
-    alone, over the workload's own allocation (read at the RS kernel's 512
-    workgroups per CU, nontemporal stores as the kernel's), combined for the
-    encode's k:m mix as time-shared bandwidth -- HBM reads and writes share
-    each channel's bus, so an encode moving k*S in and m*S out per object
-    cannot beat k*S / read_rate + m*S / write_rate.  Overwrites the objects."""
-    lib = probe_lib()
-    n = w.obj.numel() & ~((1 << 20) - 1)
-    sink = torch.zeros(16, dtype=torch.uint8, device=w.obj.device)
-    sh = stream.cuda_stream
-    lib.mxprobe_set_stream_wpc(512)
-    try:
-        ms_r = event_ms(torch, stream, lambda: lib.mxprobe_read(w.obj.data_ptr(), n, sink.data_ptr(), sh), 3)
-    finally:
-        lib.mxprobe_set_stream_wpc(16)
-    ms_w = event_ms(torch, stream, lambda: lib.mxprobe_write(w.obj.data_ptr(), n, 0, sh), 3)
-    rd, wr = n / (ms_r * 1e-3) / 1e9, n / (ms_w * 1e-3) / 1e9
-    k, m = w.k, w.m
-    bound = (k + m) / (k / rd + m / wr)
-    return {"read_GBps": round(rd, 1), "write_GBps": round(wr, 1), "rw_bound_GBps": round(bound, 1),
-            "what": (f"read and write streams alone over the workload's {n / 2**30:.0f} GiB buffer (read at 512 WG/CU, "
-                     f"nontemporal dwordx4 stores), combined for the {k}:{m} read:write mix as "
-                     "(k+m) / (k/read + m/write)")}
-
-
 def valu_bound_GBps(form: str, n_cus: int) -> float:
     """Hashed-bytes ceiling of the SHA-256 form when every SIMD issues INT32
     VALU at its measured rate: 64 B per block / lane-ops per block."""
@@ -921,7 +894,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     ms = event_ms(torch, stream, w.step, max(5, steps // 2))
     ok = w.spot_check()
     same = pattern_on_buffers(torch, stream, w)
-    rw_ns = rw_bound_on_buffers(torch, stream, w)
+    f4_ns = float4_copy_on_buffers(torch, stream, w)
     cal_ns = dict(cal or {}, rs_pattern_same_buffers_GBps=same)
     out["ns"] = {"workload": w.name, "GiBps_payload": round(w.payload / GIB / (ms * 1e-3), 3),
                  "spot_check_vs_oracle": ok,
@@ -929,8 +902,9 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                                        "rs_pattern_same_buffers_GBps" if same else "rs_pattern_k8m4_GBps")}
     tr, src = pmc_traffic("k8m4", w.alg_bytes, rs_blocks_per_cu(4))
     out["ns"]["roofline"]["traffic"], out["ns"]["roofline"]["traffic_source"] = tr, src
-    out["ns"]["roofline"]["rw_bound"] = rw_ns
-    out["ns"]["roofline"]["frac_of_rw_bound"] = round(out["ns"]["roofline"]["achieved"] / rw_ns["rw_bound_GBps"], 4)
+    if f4_ns:
+        out["ns"]["roofline"]["float4_copy_GBps"] = f4_ns
+        out["ns"]["roofline"]["frac_of_float4_copy"] = round(out["ns"]["roofline"]["achieved"] / f4_ns, 4)
     if cal and cal.get("read_wpc512_GBps"):  # north_star: >= 80 % of per-GPU HBM read bandwidth
         rd = max(cal["read_wpc512_GBps"], cal.get("read_GBps") or 0)
         out["ns"]["roofline"]["box_read_GBps"] = rd
@@ -1385,7 +1359,6 @@ def main() -> int:
         f4 = float4_copy_on_buffers(torch, stream, w)
         if f4:
             cal["float4_copy_same_buffers_GBps"] = f4
-        cal["rw_bound_same_buffers"] = rw_bound_on_buffers(torch, stream, w)
     copy_peak = cal.get(box_key) if cal else None
 
     extra = {}
@@ -1484,10 +1457,6 @@ def main() -> int:
             "spot_check_vs_oracle": spot_ok,
             "extra": extra or None,
         }
-        if cal and cal.get("rw_bound_same_buffers"):
-            rb = cal["rw_bound_same_buffers"]["rw_bound_GBps"]
-            line["roofline"]["rw_bound_GBps"] = rb
-            line["roofline"]["frac_of_rw_bound"] = round(achieved / rb, 4)
         if cal and cal.get("float4_copy_same_buffers_GBps"):
             line["roofline"]["float4_copy_GBps"] = cal["float4_copy_same_buffers_GBps"]
             line["roofline"]["frac_of_float4_copy"] = round(achieved / cal["float4_copy_same_buffers_GBps"], 4)

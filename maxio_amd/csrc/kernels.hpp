@@ -43,7 +43,13 @@ struct RsArgs {
     // unused.
     const RsTileRec* tiles = nullptr;
     uint64_t n_tiles = 0;
+    // Multi-r grouped launch (tiles set): objects of every r <= kMultiR in
+    // one grid; tiles[t].k holds k | r << 16, object o's outputs are
+    // out_ptrs / out_len [o * kMultiR, o * kMultiR + r), its coefficient
+    // table rows r apart.  r, r_total and row0 above are unused.
+    uint32_t multi = 0;
 };
+constexpr uint32_t kMultiR = 4;
 
 // Tuning knobs of the interior kernel (tools/kernel_lab.cpp sweeps them).
 struct RsVariant {

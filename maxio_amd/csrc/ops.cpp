@@ -229,6 +229,75 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
             }
         MXEC_TRY(affinity_check(dev, &slot, s, "run_rs_mixed", nullptr, ps.data(), ps.size()));
     }
+    // Two or more grouped launches of r <= kMultiR with the same tile: one
+    // multi-r launch instead (rs_apply_multi; MXEC_RS_MULTI=0 keeps one
+    // launch per r; read per call, so tests can run both forms).
+    const char* multi_env = getenv("MXEC_RS_MULTI");
+    const bool multi_on = !(multi_env && !strcmp(multi_env, "0"));
+    bool multi = multi_on && grouped.size() >= 2;
+    uint64_t m_obj = 0, m_k = 0, m_tiles = 0;
+    const uint64_t m_tile = rs_tile_bytes(rs_group_variant(kMultiR));
+    for (const Plan& p : grouped) {
+        multi = multi && p.r <= int(kMultiR) && p.tile == m_tile;
+        m_obj += p.objs->size();
+        m_k += p.sum_k;
+        m_tiles += p.n_tiles;
+    }
+    multi = multi && m_obj <= UINT32_MAX / kMultiR && m_k <= UINT32_MAX && m_tiles <= (uint64_t(1) << 32);
+    if (multi) {
+        DescWriter w(slot);
+        const size_t o_in = w.add(sizeof(void*) * m_k);
+        const size_t o_out = w.add(sizeof(void*) * m_obj * kMultiR);
+        const size_t o_inlen = w.add(8 * m_k);
+        const size_t o_outlen = w.add(8 * m_obj * kMultiR);  // zero: unused output entries
+        const size_t o_coef = w.add(4 * m_obj);
+        const size_t o_tiles = w.add(sizeof(RsTileRec) * m_tiles);
+        char* hb = w.data();
+        auto** ip = reinterpret_cast<const uint8_t**>(hb + o_in);
+        auto** op = reinterpret_cast<uint8_t**>(hb + o_out);
+        auto* il = reinterpret_cast<uint64_t*>(hb + o_inlen);
+        auto* ol = reinterpret_cast<uint64_t*>(hb + o_outlen);
+        auto* co = reinterpret_cast<uint32_t*>(hb + o_coef);
+        auto* tr = reinterpret_cast<RsTileRec*>(hb + o_tiles);
+        uint64_t o = 0, in0 = 0, t0 = 0;
+        for (const Plan& p : grouped) {
+            for (const RsMixedObject& ob : *p.objs) {
+                for (int j = 0; j < ob.k; ++j) {
+                    ip[in0 + j] = ob.o.in[j];
+                    il[in0 + j] = std::min<uint64_t>(ob.o.in_len[j], ob.shard_size);
+                }
+                for (int i = 0; i < p.r; ++i) {
+                    op[o * kMultiR + i] = ob.o.out[i];
+                    ol[o * kMultiR + i] = std::min<uint64_t>(ob.o.out_len[i], ob.shard_size);
+                }
+                co[o] = ob.o.coef_off;
+                const uint64_t nt = (ob.shard_size + m_tile - 1) / m_tile;
+                const uint32_t kr = uint32_t(ob.k) | uint32_t(p.r) << 16;
+                for (uint64_t t = 0; t < nt; ++t) tr[t0 + t] = RsTileRec{uint32_t(o), kr, uint32_t(in0), uint32_t(t)};
+                in0 += uint64_t(ob.k);
+                t0 += nt;
+                ++o;
+            }
+        }
+        char* db = nullptr;
+        MXEC_TRY(w.commit(s, &db));
+        RsArgs a{};
+        a.in_ptrs = reinterpret_cast<const uint8_t* const*>(db + o_in);
+        a.out_ptrs = reinterpret_cast<uint8_t* const*>(db + o_out);
+        a.in_len = reinterpret_cast<const uint64_t*>(db + o_inlen);
+        a.out_len = reinterpret_cast<const uint64_t*>(db + o_outlen);
+        a.coef = static_cast<const uint32_t*>(dev.coef.p);
+        a.coef_off = reinterpret_cast<const uint32_t*>(db + o_coef);
+        a.n_obj = uint32_t(m_obj);
+        a.r = a.r_total = kMultiR;
+        a.row0 = 0;
+        a.aligned = 1;
+        a.multi = 1;
+        a.tiles = reinterpret_cast<const RsTileRec*>(db + o_tiles);
+        a.n_tiles = m_tiles;
+        MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
+        return w.finish(s);
+    }
     // Every grouped launch's tables in one upload: one host-to-device copy
     // ahead of the launches instead of one between each pair of them (a
     // copy in the stream costs ~25-50 us of idle GPU at that point).

@@ -39,8 +39,10 @@ struct RsMixedObject {
 // Applies each object's matrix, objects grouped by r (map key).  Per r, the
 // objects whose pointers are all 16-byte aligned (r <= 8) share one grouped
 // launch (rs_apply_fast<GRP>), every grouped launch's tables in one upload;
-// the others run one run_rs per (k, shard_size).  A lone uniform group runs
-// the uniform kernel.
+// when two or more such groups all have r <= 4 they run as ONE multi-r
+// launch instead (rs_apply_multi; MXEC_RS_MULTI=0 disables).  The others run
+// one run_rs per (k, shard_size).  A lone uniform group runs the uniform
+// kernel.
 int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups);
 
 // SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be

@@ -277,12 +277,109 @@ __device__ __forceinline__ Vec4 gload16_upto(gcptr p, int32_t valid, gcptr safe)
     return mask_tail(gload16<NT>(valid > 0 ? p : safe), valid);
 }
 
-// Every tile of every object, 16-byte aligned pointers.  An input whose
-// length ends at or before the tile reads as zero without a load, an output
-// whose length ends there is not stored; a tile that a length boundary cuts
+// One tile of one object, 16-byte aligned pointers.  An input whose length
+// ends at or before the tile reads as zero without a load, an output whose
+// length ends there is not stored; a tile that a length boundary cuts
 // through takes the masked loads / stores above for the cut shard only, in
 // the same pass (config 5's short last chunks put one such tile in every
-// object: a quarter of all tiles at 64 KiB chunks).
+// object: a quarter of all tiles at 64 KiB chunks).  ip / il: the object's
+// k inputs and lengths; op / ol: its R outputs and lengths; tab: its
+// coefficient table at the first output row, input j's rows `stride` x 8
+// dwords apart.
+template <int R, int V, bool NT>
+__device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, const uint64_t* __restrict__ il,
+                                        uint8_t* const* __restrict__ op, const uint64_t* __restrict__ ol,
+                                        const uint32_t* __restrict__ tab, uint32_t k, uint32_t stride,
+                                        uint64_t base, gcptr safe) {
+    constexpr uint32_t kTile = kThreads * 16 * V;
+    const uint64_t end = base + kTile;
+    const uint64_t lane = base + threadIdx.x * 16;
+    const int32_t lane_off = int32_t(threadIdx.x * 16);
+
+    uint32_t acc[V][4][R];
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int i = 0; i < R; ++i) acc[v][w][i] = 0;
+
+    // Input jj of a group: whole (the common case), zero, or cut.
+    auto load_in = [&](uint32_t jj, Vec4 (&x)[V]) {
+        const uint64_t len = il[jj];
+        gcptr p = ((gcptr)(ip[jj])) + lane;
+        if (len >= end) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) x[v] = gload16<NT>(p + v * kThreads * 16);
+        } else if (len <= base) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) x[v] = Vec4{{0, 0, 0, 0}};
+        } else {
+            const int32_t d = int32_t(len - base) - lane_off;
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                x[v] = gload16_upto<NT>(p + v * kThreads * 16, d - v * int32_t(kThreads * 16), safe);
+        }
+    };
+
+    uint32_t j = 0;
+    for (; j + 4 <= k; j += 4) {
+        Vec4 x[4][V];
+        // Wave-uniform: all four inputs reach past this tile (every tile
+        // but the few at or past a short last chunk).  The common case
+        // loads unconditionally; the per-input select would zero 4V
+        // registers and branch around every load, one VALU per input
+        // dword.
+        if (il[j] >= end && il[j + 1] >= end && il[j + 2] >= end && il[j + 3] >= end) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                gcptr p = ((gcptr)(ip[j + jj])) + lane;
+#pragma unroll
+                for (int v = 0; v < V; ++v) x[jj][v] = gload16<NT>(p + v * kThreads * 16);
+            }
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) load_in(j + jj, x[jj]);
+        }
+        if constexpr (R >= 3) {
+            mac_column_pair<R, V>(acc, x[0], x[1], tab + (j + 0) * stride * 8, tab + (j + 1) * stride * 8);
+            mac_column_pair<R, V>(acc, x[2], x[3], tab + (j + 2) * stride * 8, tab + (j + 3) * stride * 8);
+        } else {  // VALU has slack at R <= 2; one column at a time needs fewer VGPRs
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * stride * 8);
+        }
+    }
+    for (; j < k; ++j) {
+        if (il[j] <= base) continue;  // zero column: contributes nothing
+        Vec4 x[V];
+        load_in(j, x);
+        mac_column<R, V>(acc, x, tab + j * stride * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const uint64_t olen = ol[i];
+        if (olen <= base) continue;  // output ends at/before base
+        gptr o = ((gptr)(op[i])) + lane;
+        const int32_t d = olen >= end ? int32_t(kTile) : int32_t(olen - base) - lane_off;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            uint32_t ov[4] = {acc[v][0][i], acc[v][1][i], acc[v][2][i], acc[v][3][i]};
+            if (olen >= end) {
+                gstore16<NT>(o + v * kThreads * 16, ov);
+            } else {
+                const int32_t valid = d - v * int32_t(kThreads * 16);
+                if (valid >= 16) {
+                    gstore16<NT>(o + v * kThreads * 16, ov);
+                } else if (valid > 0) {  // the one straddling lane
+                    for (int b = 0; b < valid; ++b)
+                        o[v * kThreads * 16 + b] = uint8_t(ov[b >> 2] >> (8 * (b & 3)));
+                }
+            }
+        }
+    }
+}
+
+// Every tile of every object of a launch (grid-stride).
 //
 // GRP: a grouped launch — objects of different k and shard size that share
 // r (config 5's mixed classes, a server's batch of mixed requests) in one
@@ -317,97 +414,44 @@ __global__ __launch_bounds__(kThreads, OCC) void rs_apply_fast(
             k = k_uniform;
             in0 = uint64_t(obj) * k;
         }
-        const uint64_t end = base + kTile;
         // Lengths are clamped to the shard size by the host, so a tile past
         // the shard end is cut by the same tests.
-        const uint64_t* __restrict__ il = in_len + in0;
-        const uint64_t* __restrict__ ol = out_len + uint64_t(obj) * r_total + row0;
-        const uint32_t* __restrict__ tab = coef + coef_off[obj] + row0 * 8;
-        const uint8_t* const* __restrict__ ip = in_ptrs + in0;
-        uint8_t* const* __restrict__ op = out_ptrs + uint64_t(obj) * r_total + row0;
-        const uint64_t lane = base + threadIdx.x * 16;
-        const int32_t lane_off = int32_t(threadIdx.x * 16);
+        rs_tile<R, V, NT>(in_ptrs + in0, in_len + in0, out_ptrs + uint64_t(obj) * r_total + row0,
+                          out_len + uint64_t(obj) * r_total + row0, coef + coef_off[obj] + row0 * 8, k, r_total,
+                          base, safe);
+    }
+}
 
-        uint32_t acc[V][4][R];
-#pragma unroll
-        for (int v = 0; v < V; ++v)
-#pragma unroll
-            for (int w = 0; w < 4; ++w)
-#pragma unroll
-                for (int i = 0; i < R; ++i) acc[v][w][i] = 0;
-
-        // Input jj of a group: whole (the common case), zero, or cut.
-        auto load_in = [&](uint32_t jj, Vec4 (&x)[V]) {
-            const uint64_t len = il[jj];
-            gcptr p = ((gcptr)(ip[jj])) + lane;
-            if (len >= end) {
-#pragma unroll
-                for (int v = 0; v < V; ++v) x[v] = gload16<NT>(p + v * kThreads * 16);
-            } else if (len <= base) {
-#pragma unroll
-                for (int v = 0; v < V; ++v) x[v] = Vec4{{0, 0, 0, 0}};
-            } else {
-                const int32_t d = int32_t(len - base) - lane_off;
-#pragma unroll
-                for (int v = 0; v < V; ++v)
-                    x[v] = gload16_upto<NT>(p + v * kThreads * 16, d - v * int32_t(kThreads * 16), safe);
-            }
-        };
-
-        uint32_t j = 0;
-        for (; j + 4 <= k; j += 4) {
-            Vec4 x[4][V];
-            // Wave-uniform: all four inputs reach past this tile (every tile
-            // but the few at or past a short last chunk).  The common case
-            // loads unconditionally; the per-input select would zero 4V
-            // registers and branch around every load, one VALU per input
-            // dword.
-            if (il[j] >= end && il[j + 1] >= end && il[j + 2] >= end && il[j + 3] >= end) {
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    gcptr p = ((gcptr)(ip[j + jj])) + lane;
-#pragma unroll
-                    for (int v = 0; v < V; ++v) x[jj][v] = gload16<NT>(p + v * kThreads * 16);
-                }
-            } else {
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) load_in(j + jj, x[jj]);
-            }
-            if constexpr (R >= 3) {
-                mac_column_pair<R, V>(acc, x[0], x[1], tab + (j + 0) * r_total * 8, tab + (j + 1) * r_total * 8);
-                mac_column_pair<R, V>(acc, x[2], x[3], tab + (j + 2) * r_total * 8, tab + (j + 3) * r_total * 8);
-            } else {  // VALU has slack at R <= 2; one column at a time needs fewer VGPRs
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * r_total * 8);
-            }
-        }
-        for (; j < k; ++j) {
-            if (il[j] <= base) continue;  // zero column: contributes nothing
-            Vec4 x[V];
-            load_in(j, x);
-            mac_column<R, V>(acc, x, tab + j * r_total * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            const uint64_t olen = ol[i];
-            if (olen <= base) continue;  // output ends at/before base
-            gptr o = ((gptr)(op[i])) + lane;
-            const int32_t d = olen >= end ? int32_t(kTile) : int32_t(olen - base) - lane_off;
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                uint32_t ov[4] = {acc[v][0][i], acc[v][1][i], acc[v][2][i], acc[v][3][i]};
-                if (olen >= end) {
-                    gstore16<NT>(o + v * kThreads * 16, ov);
-                } else {
-                    const int32_t valid = d - v * int32_t(kThreads * 16);
-                    if (valid >= 16) {
-                        gstore16<NT>(o + v * kThreads * 16, ov);
-                    } else if (valid > 0) {  // the one straddling lane
-                        for (int b = 0; b < valid; ++b)
-                            o[v * kThreads * 16 + b] = uint8_t(ov[b >> 2] >> (8 * (b & 3)));
-                    }
-                }
-            }
+// One grouped launch for objects of every output count r <= kMultiR (a
+// step's encode of mixed m, or its decode of mixed erasure counts): the
+// tile record's k field carries r in bits 16-23, an object's outputs sit at
+// out_ptrs / out_len + obj * kMultiR (unused entries length 0), and each
+// tile runs the body compiled for its r (a wave-uniform switch).  One launch
+// instead of one per r: no ramp-down and ramp-up between them.
+template <int V, bool NT>
+__global__ __launch_bounds__(kThreads) void rs_apply_multi(
+    const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
+    const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
+    const uint32_t* __restrict__ coef, const uint32_t* __restrict__ coef_off, uint64_t n_tiles,
+    const RsTileRec* __restrict__ tiles) {
+    constexpr uint32_t kTile = kThreads * 16 * V;
+    const gcptr safe = (gcptr)(reinterpret_cast<const uint8_t*>(coef));
+    RsTileRec next = tiles[blockIdx.x];  // the grid never exceeds n_tiles
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const RsTileRec cur = next;
+        if (tile + gridDim.x < n_tiles) next = tiles[tile + gridDim.x];
+        const uint32_t k = cur.k & 0xFFFFu, r = (cur.k >> 16) & 0xFFu;
+        const uint64_t base = uint64_t(cur.local) * kTile;
+        const uint8_t* const* ip = in_ptrs + cur.in0;
+        const uint64_t* il = in_len + cur.in0;
+        uint8_t* const* op = out_ptrs + uint64_t(cur.obj) * kMultiR;
+        const uint64_t* ol = out_len + uint64_t(cur.obj) * kMultiR;
+        const uint32_t* tab = coef + coef_off[cur.obj];
+        switch (r) {
+            case 1: rs_tile<1, V, NT>(ip, il, op, ol, tab, k, 1, base, safe); break;
+            case 2: rs_tile<2, V, NT>(ip, il, op, ol, tab, k, 2, base, safe); break;
+            case 3: rs_tile<3, V, NT>(ip, il, op, ol, tab, k, 3, base, safe); break;
+            default: rs_tile<4, V, NT>(ip, il, op, ol, tab, k, 4, base, safe); break;
         }
     }
 }
@@ -418,6 +462,16 @@ hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles
     hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP, OCC>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                        a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.k, a.r_total,
                        a.row0, tiles_per_obj, n_tiles, a.tiles);
+    return hipGetLastError();
+}
+
+// Multi-r grouped launches (a.multi): V = 4, nontemporal, rs_group_variant's grid.
+hipError_t launch_multi(const RsArgs& a, int n_cus, hipStream_t s) {
+    const RsVariant v = rs_group_variant(kMultiR);
+    uint64_t blocks = uint64_t(n_cus) * uint64_t(v.blocks_per_cu);
+    if (blocks > a.n_tiles) blocks = a.n_tiles;
+    hipLaunchKernelGGL((rs_apply_multi<4, true>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s, a.in_ptrs,
+                       a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.n_tiles, a.tiles);
     return hipGetLastError();
 }
 
@@ -533,6 +587,11 @@ hipError_t launch_rs_apply_variant(const RsArgs& a, int n_cus, hipStream_t s, co
 }
 
 hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
+    if (a.tiles && a.multi) {
+        if (!a.aligned || a.row0 != 0) return hipErrorInvalidValue;
+        if (a.n_tiles == 0) return hipSuccess;
+        return launch_multi(a, n_cus, s);
+    }
     if (a.tiles) {
         if (!a.aligned || a.row0 != 0 || a.r != a.r_total) return hipErrorInvalidValue;
         if (a.n_tiles == 0) return hipSuccess;
