@@ -123,7 +123,12 @@ struct PipeRes {
     }
     ~PipeRes() {
         for (auto s : cs)
-            if (s) (void)hipStreamDestroy(s);
+            if (s) {
+                affinity_untag(s);
+                (void)hipStreamDestroy(s);
+            }
+        affinity_untag(h2d);
+        affinity_untag(d2h);
         if (h2d) (void)hipStreamDestroy(h2d);
         if (d2h) (void)hipStreamDestroy(d2h);
     }

@@ -80,6 +80,8 @@ void slot_destroy(Slot& slot) {
         if (rb.done) (void)hipEventDestroy(rb.done);
         if (rb.uploaded) (void)hipEventDestroy(rb.uploaded);
     }
+    affinity_untag(slot.upload);
+    affinity_untag(slot.stream);
     if (slot.upload) (void)hipStreamDestroy(slot.upload);
     slot.upload = nullptr;
     for (auto& e : slot.stage_done)
@@ -387,6 +389,14 @@ void affinity_tag(hipStream_t s, const Device* d) {
     if (!s || !affinity_on()) return;
     std::lock_guard<std::mutex> g(g_aff_mu);
     aff_streams()[s] = d;
+}
+
+void affinity_untag(hipStream_t s) {
+    // Always (the tag may have been set while the check was on): a destroyed
+    // stream's handle can come back as another device's stream.
+    if (!s) return;
+    std::lock_guard<std::mutex> g(g_aff_mu);
+    aff_streams().erase(s);
 }
 
 int affinity_check(const Device& d, const Slot* slot, hipStream_t s, const char* where, const DescArena* arena,

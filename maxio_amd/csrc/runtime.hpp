@@ -260,6 +260,7 @@ Device* pick_device(Ctx* ctx, int dev_index);
 // MXEC_E_DEVICE; mxec_close prints the running totals to stderr.
 bool affinity_on();
 void affinity_tag(hipStream_t s, const Device* d);
+void affinity_untag(hipStream_t s);  // before the stream is destroyed
 int affinity_check(const Device& d, const Slot* slot, hipStream_t s, const char* where,
                    const DescArena* arena = nullptr, const void* const* ptrs = nullptr, size_t n_ptrs = 0);
 void affinity_report();
