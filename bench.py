@@ -1349,7 +1349,9 @@ def main() -> int:
     cal = calibrate(torch, dev, stream) if rank == 0 else None
     box_key = {(4, 2): "rs_pattern_k4m2_GBps", (8, 4): "rs_pattern_k8m4_GBps"}.get(
         (getattr(w, "k", 0), getattr(w, "m", 0)), "copy_GBps")
-    if not isinstance(w, Encode):
+    if isinstance(w, Mixed):
+        box_key = "rs_pattern_k4m2_GBps"  # as the default line's extra.config5
+    elif not isinstance(w, Encode):
         box_key = "copy_GBps"
     elif cal is not None:
         same = pattern_on_buffers(torch, stream, w)
