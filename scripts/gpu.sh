@@ -10,6 +10,8 @@
 #   refuse2   python bench.py --gpus 2 on a one-GPU box: must exit 2, no line
 #   rehearse  BENCH_REHEARSE_LOGICAL=1 bench.py --gpus 2 (labelled in-process
 #             multi-device rehearsal on two logical devices of the one card)
+#   ranks2    the torch.distributed.run path with two ranks on the one GPU
+#             (BENCH_GPU_OF_RANK=0, gloo for the timing collectives)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench command
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (one run each) of rs_apply_fast
 #             for configs 2 and ns, summarised with the grid they ran at
@@ -44,6 +46,11 @@ for st in "${STEPS[@]}"; do
       BENCH_REHEARSE_LOGICAL=1 timeout -k 10 600 python bench.py --gpus 2 --objects 256 --steps 10 --warmup 2 \
         > "$O/rehearse2.json" 2> "$O/rehearse2.err" || { tail -20 "$O/rehearse2.err"; exit 1; }
       cat "$O/rehearse2.json" ;;
+    ranks2)
+      BENCH_GPU_OF_RANK=0 BENCH_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --objects 256 --steps 10 \
+        --warmup 2 > "$O/ranks2.json" 2> "$O/ranks2.err" || { tail -20 "$O/ranks2.err"; exit 1; }
+      cat "$O/ranks2.json" ;;
     prof)
       ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/prof -o run --output-format csv \
           -- python3 "$R/bench.py" $BENCH_ARGS > "$O/prof_bench.json" 2> "$O/prof_bench.err" ) || { tail -20 "$O/prof_bench.err"; exit 1; }
