@@ -1175,6 +1175,7 @@ def pcie_rates(torch, devs, nbytes: int = 1 << 30) -> dict:
     """The box's raw copy rates between pinned host memory and the devices:
     every device at once (one pinned buffer and one stream each), each
     direction alone, 4 copies per device, wall clock."""
+    barrier()  # every rank measures at the same time, as its batches will run
     hb = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in devs]
     db = [torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", d)) for d in devs]
     st = [torch.cuda.Stream(device=torch.device("cuda", d)) for d in devs]
