@@ -1200,7 +1200,9 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
     """mxec_encode_batch_host from mxec_host_alloc (page-locked) memory: the
     PUT path as MaxIO sees it -- request bodies in host memory, parity and
     digests back in host memory (filesystem.rs:1107-1135) -- over every
-    device of the context, with and without the SHA-256 of every chunk.
+    device of the context, with and without the SHA-256 of every chunk; then
+    the GET side, mxec_reconstruct_batch_host over the same objects with two
+    erasures each, without and with verification.
     Payload GiB/s (k * chunk_size per object) over all ranks, next to the
     box's raw pinned copy rates and the bound they set."""
     import numpy as np
@@ -1223,8 +1225,11 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
     h2d_s = n * k * S / (rates["h2d_GBps"] * 1e9)
     d2h_s = n * m * S / (rates["d2h_GBps"] * 1e9)
     bound_s = max(h2d_s, d2h_s)
+    dig_all = None
     for sha in (False, True):
         dig = np.zeros(n * (k + m) * 32, np.uint8) if sha else None
+        if sha:
+            dig_all = dig
         ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm: pools, tables
         barrier()
         t0 = time.perf_counter()
@@ -1235,6 +1240,48 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
         key = "rs_sha256" if sha else "rs_only"
         res[key] = {"s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
                     "frac_of_pcie_bound": round(bound_s / el, 4)}
+    # GET side (chunk_reader.rs:157-226 from the shard files in host memory):
+    # mxec_reconstruct_batch_host over the same objects with two seeded
+    # erasures each -- the 4 present shards go up, the 2 rebuilt ones come
+    # back (the same bytes per object as the PUT leg moves) -- without and
+    # with the SHA-256 verification of the present shards.
+    sptr = []
+    for o in range(n):
+        sptr += [data[o, j].ctypes.data for j in range(k)] + [par[o, i].ctypes.data for i in range(m)]
+    rng = np.random.default_rng(SEED + 11 + plan.rank)
+    present0 = np.ones(n * (k + m), np.uint8)
+    for o in range(n):
+        for i in rng.choice(k + m, 2, replace=False):
+            present0[o * (k + m) + i] = 0
+    get_up_s = n * (k + m - 2) * S / (rates["h2d_GBps"] * 1e9)
+    get_down_s = n * 2 * S / (rates["d2h_GBps"] * 1e9)
+    for verify in (False, True):
+        exp = dig_all if verify else None
+        pr = present0.copy()
+        rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)  # warm
+        assert rc == 0, rc
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            pr = present0.copy()
+            rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)
+            assert rc == 0, rc
+        el = reduce_max((time.perf_counter() - t0) / reps)
+        payload = reduce_sum(float(n * k * S))
+        res["get_verify_sha256" if verify else "get_rs_only"] = {
+            "s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
+            "frac_of_pcie_bound": round(max(get_up_s, get_down_s) / el, 4)}
+    if plan.rank == 0:
+        # the rebuilt shards of one object, scribbled first, come back exact
+        o = n // 3
+        want = [data[o, j].copy() for j in range(k)] + [par[o, i].copy() for i in range(m)]
+        pr = present0.copy()
+        for i in range(k + m):
+            if not pr[o * (k + m) + i]:
+                (data[o, i] if i < k else par[o, i - k])[:] = 0x5A
+        rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=dig_all)
+        got = [data[o, j] for j in range(k)] + [par[o, i] for i in range(m)]
+        res["get_spot_check"] = rc == 0 and all(np.array_equal(a, b) for a, b in zip(got, want))
     res["pcie_bound_s_per_batch"] = round(bound_s, 4)
     res["bound"] = ("max(upload k*S*n / h2d_GBps, download m*S*n / d2h_GBps), the raw pinned copy rates "
                     "measured above on the same devices at once")

@@ -23,6 +23,8 @@
  *   mxec_reconstruct         try_reconstruct_data_chunk, chunk_reader.rs:157-226
  *                            (verify :176-196, count :199-208, reconstruct :211,
  *                            truncate :216-222) — minus the file I/O
+ *   mxec_*_batch_host        many mxec_encode / mxec_reconstruct calls at once
+ *                            from host memory, pipelined over every device
  *   mxec_*_device            the same two operations over device-resident
  *                            batches (objects of any k and chunk size that share
  *                            the output count share one launch)
@@ -241,6 +243,26 @@ int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs,
                            uint64_t n_obj, const uint8_t* const* data,
                            const uint64_t* data_len, uint8_t* const* parity,
                            uint8_t (*digests)[32], int32_t* status_out);
+
+/* End-to-end GET compute for many objects whose shards are in HOST memory
+ * (the shard files as read from disk) -- the batched form of
+ * mxec_reconstruct (try_reconstruct_data_chunk, chunk_reader.rs:157-226, per
+ * object).  Same array layout as mxec_reconstruct_batch_device but host
+ * pointers: shards (sum(k+m), object-major; a missing shard's pointer is the
+ * buffer its rebuilt bytes go to), shard_len (NULL = shard_size), present
+ * (in/out); expected_sha256 (host, sum(k+m) digests) or NULL to skip
+ * verification; status_out (host, n_obj) may be NULL.  Objects are dealt
+ * over the ctx's devices as mxec_encode_batch_host deals them; per device the
+ * present shards go up (direct from pinned memory, else via a pinned ring),
+ * are verified and rebuilt there, and only the rebuilt shards come back.  An
+ * object short of k verified shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT and
+ * none of its buffers is written; the call returns the first such status.
+ * Blocks until every rebuilt shard is in host memory. */
+int mxec_reconstruct_batch_host(mxec_ctx* ctx, const mxec_object* objs,
+                                uint64_t n_obj, uint8_t* const* shards,
+                                const uint64_t* shard_len, uint8_t* present,
+                                const uint8_t (*expected_sha256)[32],
+                                uint32_t flags, int32_t* status_out);
 
 /* Uniform reconstruct batch.  Object o, shard i (0 <= i < k+m) lives at
  * shards + o*obj_stride + i*shard_stride.  shard_len (host, k+m entries,

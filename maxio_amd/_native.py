@@ -110,6 +110,7 @@ _SIGS = {
         INT, [P, INT, P, INT, INT, U64, U64, P, U64, U64, U64P, P, U64, U64, P]),
     "mxec_encode_batch_device": (INT, [P, INT, P, ctypes.POINTER(Object), U64, PP, U64P, PP, P]),
     "mxec_encode_batch_host": (INT, [P, ctypes.POINTER(Object), U64, PP, U64P, PP, U8P, I32P]),
+    "mxec_reconstruct_batch_host": (INT, [P, ctypes.POINTER(Object), U64, PP, U64P, U8P, U8P, ctypes.c_uint32, I32P]),
     "mxec_reconstruct_strided_device": (
         INT, [P, INT, P, INT, INT, U64, U64, P, U64, U64, U64P, U8P, P, ctypes.c_uint32, I32P]),
     "mxec_reconstruct_batch_device": (

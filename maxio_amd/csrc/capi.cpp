@@ -18,12 +18,6 @@ using namespace mxec;
 namespace {
 
 
-std::string too_few_msg(int present, int k, int total) {
-    return "too many missing/corrupt shards: only " + std::to_string(present) + " of " +
-           std::to_string(k) + " required shards available (" + std::to_string(total - present) +
-           " missing)";
-}
-
 // One object of a device-resident reconstruct batch (device shard pointers).
 struct BatchObj {
     int k, m;

@@ -167,7 +167,8 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     return w.finish(s);
 }
 
-int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups) {
+int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups,
+                 DescArena* arena) {
     // Which groups take the grouped kernel: every pointer 16-byte aligned,
     // r <= 8, index ranges that fit its 32-bit fields.  A call that is one
     // uniform group keeps the uniform kernel (no tile table).
@@ -217,7 +218,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
             if (v.empty()) order.push_back(key);
             v.push_back(ob.o);
         }
-        for (const auto& key : order) MXEC_TRY(run_rs(dev, slot, s, key.second, key.first, g.first, by[key]));
+        for (const auto& key : order) MXEC_TRY(run_rs(dev, slot, s, key.second, key.first, g.first, by[key], arena));
     }
     if (grouped.empty()) return MXEC_OK;
     if (affinity_on()) {
@@ -227,7 +228,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
                 for (int j = 0; j < ob.k; ++j) ps.push_back(ob.o.in[j]);
                 for (int i = 0; i < p.r; ++i) ps.push_back(ob.o.out[i]);
             }
-        MXEC_TRY(affinity_check(dev, &slot, s, "run_rs_mixed", nullptr, ps.data(), ps.size()));
+        MXEC_TRY(affinity_check(dev, &slot, s, "run_rs_mixed", arena, ps.data(), ps.size()));
     }
     // Two or more grouped launches of r <= kMultiR with the same tile: one
     // multi-r launch instead (rs_apply_multi; MXEC_RS_MULTI=0 keeps one
@@ -245,7 +246,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
     }
     multi = multi && m_obj <= UINT32_MAX / kMultiR && m_k <= UINT32_MAX && m_tiles <= (uint64_t(1) << 32);
     if (multi) {
-        DescWriter w(slot);
+        DescWriter w(slot, arena);
         const size_t o_in = w.add(sizeof(void*) * m_k);
         const size_t o_out = w.add(sizeof(void*) * m_obj * kMultiR);
         const size_t o_inlen = w.add(8 * m_k);
@@ -301,7 +302,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
     // Every grouped launch's tables in one upload: one host-to-device copy
     // ahead of the launches instead of one between each pair of them (a
     // copy in the stream costs ~25-50 us of idle GPU at that point).
-    DescWriter w(slot);
+    DescWriter w(slot, arena);
     for (Plan& p : grouped) {
         const size_t n = p.objs->size();
         p.o_in = w.add(sizeof(void*) * p.sum_k);

@@ -7,6 +7,7 @@
 #include <new>
 #include <functional>
 #include <map>
+#include <string>
 #include <vector>
 
 #include "gf256.hpp"
@@ -43,7 +44,8 @@ struct RsMixedObject {
 // launch instead (rs_apply_multi; MXEC_RS_MULTI=0 disables).  The others run
 // one run_rs per (k, shard_size).  A lone uniform group runs the uniform
 // kernel.
-int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups);
+int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups,
+                 DescArena* arena = nullptr);
 
 // SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be
 // null (see ShaArgs).
@@ -146,6 +148,13 @@ int run_body_sums(Device& d, Slot& slot, hipStream_t s, const std::vector<const 
 
 // filesystem.rs:1095 guard, then the crate's ReedSolomon::new checks.
 int check_km(int k, int m);
+
+// chunk_reader.rs:203-206's error text for an object short of k shards.
+inline std::string too_few_msg(int present, int k, int total) {
+    return "too many missing/corrupt shards: only " + std::to_string(present) + " of " +
+           std::to_string(k) + " required shards available (" + std::to_string(total - present) +
+           " missing)";
+}
 
 // Coefficient-table offsets are only valid until the device's 64 MiB table
 // arena is recycled (runtime.cpp coef_offset: it waits for the device, then

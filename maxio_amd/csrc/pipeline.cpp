@@ -57,6 +57,20 @@ struct HostObj {
     uint64_t bytes() const { return uint64_t(k + m) * slot(); }
 };
 
+// One object of a host reconstruct batch (mxec_reconstruct_batch_host).
+struct RecObj {
+    int k, m;
+    uint64_t S;
+    uint8_t* const* shards;          // k + m host buffers (present: read; missing: rebuilt into)
+    const uint64_t* len;             // k + m, clamped to S
+    uint8_t* present;                // k + m, in/out
+    const uint8_t (*expected)[32];   // k + m digests, or null (no verification)
+    int32_t* status;                 // out: MXEC_OK or MXEC_E_TOO_FEW_SHARDS_PRESENT
+    uint64_t pool_off = 0;
+    uint64_t slot() const { return rup(S, kAlign); }
+    uint64_t bytes() const { return uint64_t(k + m) * slot(); }
+};
+
 class PinRing {
 public:
     int init() {
@@ -104,6 +118,7 @@ struct PipeRes {
     PinRing in, out;
     DescArena arena;
     DevBuf pool, digests;
+    PinnedBuf flags;  // verification verdicts read back (host reconstruct)
     Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
     bool ready = false;
     int init(const Device& dev) {
@@ -138,7 +153,7 @@ class DevicePipeline {
 public:
     DevicePipeline(Device& d, PipeRes& r)
         : d_(d), h2d_(r.h2d), d2h_(r.d2h), cs_(r.cs), in_(r.in), out_(r.out), arena_(r.arena),
-          pool_(r.pool), scratch_(r.digests), slot_(r.desc_slot) {}
+          pool_(r.pool), scratch_(r.digests), flags_(r.flags), slot_(r.desc_slot) {}
     ~DevicePipeline() {
         for (auto e : events_) (void)hipEventDestroy(e);
     }
@@ -162,7 +177,169 @@ public:
         return MXEC_OK;
     }
 
+    // Host reconstruct batch: waves that fit the pool, as run().
+    int run_rec(std::vector<RecObj>& objs, bool data_only) {
+        size_t o = 0;
+        while (o < objs.size()) {
+            uint64_t need = 0, desc = 1 << 20;
+            size_t e = o;
+            while (e < objs.size() && (e == o || need + objs[e].bytes() <= kPoolCap)) {
+                objs[e].pool_off = need;
+                need += objs[e].bytes();
+                // pointer / length / digest-index tables, the SHA tables and one
+                // 16-byte record per tile of the grouped launch (tiles >= 8 KiB)
+                desc += uint64_t(objs[e].k + objs[e].m) * 96 + 512 + (objs[e].S / 8192 + 2) * 32;
+                ++e;
+            }
+            MXEC_TRY(pool_.ensure(need));
+            MXEC_TRY(arena_.reserve(desc * 2));
+            MXEC_TRY(rec_wave(objs, o, e, data_only));
+            o = e;
+        }
+        return MXEC_OK;
+    }
+
 private:
+    // One wave of a host reconstruct batch (try_reconstruct_data_chunk,
+    // chunk_reader.rs:157-226, per object): the present shards go up
+    // (coalesced, direct from pinned memory), their digests are checked on
+    // the device against the expected ones when given (a mismatch is an
+    // erasure, :176-196), every object with at least k verified shards is
+    // rebuilt in one grouped launch per call (run_rs_mixed), and only the
+    // rebuilt shards come back.  An object short of k shards gets
+    // MXEC_E_TOO_FEW_SHARDS_PRESENT and none of its buffers is written.
+    int rec_wave(std::vector<RecObj>& objs, size_t o0, size_t o1, bool data_only) {
+        uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        hipStream_t cs = cs_[0];
+        for (size_t o = o0; o < o1; ++o) {
+            const RecObj& h = objs[o];
+            for (int i = 0; i < h.k + h.m; ++i) {
+                if (!h.present[i]) continue;
+                MXEC_TRY(queue_up(base + h.pool_off + uint64_t(i) * h.slot(), h.shards[i], h.len[i]));
+                if (h.len[i] != h.slot()) MXEC_TRY(flush_up());
+            }
+        }
+        MXEC_TRY(flush_up());
+        // Verification: digests of every present shard of an object that
+        // carries expected digests, compared on the device.
+        std::vector<const uint8_t*> sp;
+        std::vector<uint64_t> sl, idx;
+        uint64_t msgs = 0;
+        for (size_t o = o0; o < o1; ++o) msgs += uint64_t(objs[o].k + objs[o].m);
+        uint64_t g = 0;
+        for (size_t o = o0; o < o1; ++o) {
+            const RecObj& h = objs[o];
+            for (int i = 0; i < h.k + h.m; ++i, ++g) {
+                if (!h.expected || !h.present[i]) continue;
+                sp.push_back(base + h.pool_off + uint64_t(i) * h.slot());
+                sl.push_back(h.len[i]);
+                idx.push_back(g);
+            }
+        }
+        hipEvent_t up;
+        MXEC_TRY(new_event(&up));
+        if (!sp.empty()) {
+            // expected digests of the wave, message order, after the ok flags
+            const uint64_t fo = rup(sp.size(), 256);
+            MXEC_TRY(scratch_.ensure(fo + msgs * 32));
+            uint8_t* ok = static_cast<uint8_t*>(scratch_.p);
+            uint8_t* exp = ok + fo;
+            g = 0;
+            for (size_t o = o0; o < o1; ++o) {
+                const RecObj& h = objs[o];
+                if (h.expected) MXEC_TRY(queue_up(exp + g * 32, &h.expected[0][0], uint64_t(h.k + h.m) * 32));
+                g += uint64_t(h.k + h.m);
+            }
+            MXEC_TRY(flush_up());
+            MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
+            MXEC_TRY(run_sha(d_, slot_, cs, sp, sl, nullptr, exp, ok, &idx, &arena_));
+            MXEC_TRY(flags_.ensure(sp.size()));
+            MXEC_HIP(hipMemcpyAsync(flags_.p, ok, sp.size(), hipMemcpyDeviceToHost, cs));
+            MXEC_HIP(hipStreamSynchronize(cs));
+            const auto* okh = static_cast<const uint8_t*>(flags_.p);
+            for (size_t t = 0; t < idx.size(); ++t) {
+                if (okh[t]) continue;
+                // idx[t] is the wave-relative message index: find its object
+                uint64_t gg = 0;
+                for (size_t o = o0; o < o1; ++o) {
+                    const uint64_t n = uint64_t(objs[o].k + objs[o].m);
+                    if (idx[t] < gg + n) {
+                        objs[o].present[idx[t] - gg] = 0;
+                        break;
+                    }
+                    gg += n;
+                }
+            }
+        } else {
+            MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
+        }
+        // Rebuild: one decode plan per object, one launch for the wave.
+        std::vector<std::shared_ptr<const DecodePlan>> plans(o1 - o0);
+        std::vector<uint32_t> offs(o1 - o0);
+        std::vector<const uint8_t*> in;
+        std::vector<uint8_t*> out;
+        std::vector<uint64_t> il, ol;
+        std::map<int, std::vector<RsMixedObject>> groups;
+        auto collect = [&]() -> int {
+            for (size_t o = o0; o < o1; ++o)
+                MXEC_TRY(decode_plan(d_, objs[o].k, objs[o].m, objs[o].present, data_only, &plans[o - o0], &offs[o - o0]));
+            return MXEC_OK;
+        };
+        auto launch = [&]() -> int {
+            size_t n_in = 0, n_out = 0;
+            for (size_t t = 0; t < plans.size(); ++t)
+                if (plans[t] && !plans[t]->missing.empty()) {
+                    n_in += size_t(objs[o0 + t].k);
+                    n_out += plans[t]->missing.size();
+                }
+            in.assign(n_in, nullptr);
+            out.assign(n_out, nullptr);
+            il.assign(n_in, 0);
+            ol.assign(n_out, 0);
+            groups.clear();
+            size_t pi = 0, po = 0;
+            for (size_t t = 0; t < plans.size(); ++t) {
+                if (!plans[t] || plans[t]->missing.empty()) continue;
+                const RecObj& h = objs[o0 + t];
+                const DecodePlan& p = *plans[t];
+                const int r = int(p.missing.size());
+                uint8_t* ob = base + h.pool_off;
+                for (int v = 0; v < h.k; ++v) {
+                    in[pi + v] = ob + uint64_t(p.valid[size_t(v)]) * h.slot();
+                    il[pi + v] = h.len[p.valid[size_t(v)]];
+                }
+                for (int e = 0; e < r; ++e) {
+                    out[po + e] = ob + uint64_t(p.missing[size_t(e)]) * h.slot();
+                    ol[po + e] = h.len[p.missing[size_t(e)]];
+                }
+                groups[r].push_back(RsMixedObject{h.k, h.S, RsObject{&in[pi], &il[pi], &out[po], &ol[po], offs[t]}});
+                pi += size_t(h.k);
+                po += size_t(r);
+            }
+            return run_rs_mixed(d_, slot_, cs, groups, &arena_);
+        };
+        MXEC_TRY(with_stable_coef(d_, collect, launch));
+        hipEvent_t rs_done;
+        MXEC_TRY(new_event(&rs_done));
+        MXEC_HIP(hipEventRecord(rs_done, cs));
+        MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
+        for (size_t o = o0; o < o1; ++o) {
+            RecObj& h = objs[o];
+            const auto& p = plans[o - o0];
+            *h.status = p ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
+            if (!p) continue;
+            for (int e : p->missing) {
+                MXEC_TRY(queue_down(h.shards[e], base + h.pool_off + uint64_t(e) * h.slot(), h.len[e]));
+                if (h.len[e] != h.slot()) MXEC_TRY(flush_down());
+                h.present[e] = 1;
+            }
+        }
+        MXEC_TRY(flush_down());
+        return flush();
+    }
+
     struct Pending {  // ring DMA to copy out into pageable memory
         int ring;
         uint8_t* dst;
@@ -177,6 +354,7 @@ private:
     DescArena& arena_;
     DevBuf& pool_;
     DevBuf& scratch_;  // the wave's digests, message order
+    PinnedBuf& flags_;
     Slot& slot_;
     std::vector<Pending> pend_;
     std::vector<hipEvent_t> events_;
@@ -512,6 +690,107 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
             if (rcs[d] != MXEC_OK) return set_error(rcs[d], errs[d]);
         if (first_err != MXEC_OK) return set_error(first_err, first_msg);
         return MXEC_OK;
+    } catch (const std::bad_alloc&) {
+        return set_error(MXEC_E_OOM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return set_error(MXEC_E_INVALID_ARG, e.what());
+    }
+}
+
+extern "C" int mxec_reconstruct_batch_host(mxec_ctx* ctx, const mxec_object* objs, uint64_t n_obj,
+                                           uint8_t* const* shards, const uint64_t* shard_len, uint8_t* present,
+                                           const uint8_t (*expected_sha256)[32], uint32_t flags,
+                                           int32_t* status_out) {
+    try {
+        if (n_obj == 0) return MXEC_OK;
+        if (!ctx || !objs || !shards || !present) return set_error(MXEC_E_INVALID_ARG, "null argument");
+        const size_t D = ctx->c.devs.size();
+        if (!D) return set_error(MXEC_E_NO_DEVICE, "context has no device");
+        uint64_t sum = 0;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            if (int rc = rs_check(objs[o].k, objs[o].m))
+                return set_error(rc, std::string("RS init error: ") + mxec_strerror(rc));
+            if (objs[o].shard_size == 0) return set_error(MXEC_E_EMPTY_SHARD, mxec_strerror(MXEC_E_EMPTY_SHARD));
+            sum += uint64_t(objs[o].k + objs[o].m);
+        }
+        // Every shard pointer is needed: present ones are read, missing ones
+        // are where the rebuilt bytes go.
+        for (uint64_t g = 0; g < sum; ++g)
+            if (!shards[g]) return set_error(MXEC_E_INVALID_ARG, "null shard pointer " + std::to_string(g));
+        std::vector<uint64_t> len(size_t(sum), 0);
+        std::vector<int32_t> st(size_t(n_obj), MXEC_OK);
+        std::vector<uint64_t> obj_bytes(size_t(n_obj), 0);
+        std::vector<RecObj> all;
+        all.reserve(size_t(n_obj));
+        uint64_t g0 = 0;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            const int k = objs[o].k, m = objs[o].m;
+            const uint64_t S = objs[o].shard_size;
+            for (int i = 0; i < k + m; ++i) len[g0 + uint64_t(i)] = shard_len ? std::min<uint64_t>(shard_len[g0 + i], S) : S;
+            all.push_back(RecObj{k, m, S, shards + g0, &len[g0], present + g0,
+                                 expected_sha256 ? expected_sha256 + g0 : nullptr, &st[o]});
+            obj_bytes[o] = all.back().bytes();
+            g0 += uint64_t(k + m);
+        }
+        const std::vector<uint32_t> owner = deal_objects(obj_bytes, uint32_t(D));
+        std::vector<std::vector<RecObj>> per(D);
+        for (uint64_t o = 0; o < n_obj; ++o) per[owner[o]].push_back(all[o]);
+        const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
+        std::vector<int> rcs(D, MXEC_OK);
+        std::vector<std::string> errs(D);
+        struct Joiner {
+            std::vector<std::thread> th;
+            ~Joiner() {
+                for (auto& t : th)
+                    if (t.joinable()) t.join();
+            }
+        } j;
+        auto work = [&](size_t d) {
+            try {
+                Device& dev = *ctx->c.devs[d];
+                rcs[d] = [&]() -> int {
+                    MXEC_HIP(hipSetDevice(dev.id));
+                    std::lock_guard<std::mutex> g(dev.pipe_mu);
+                    if (!dev.pipe) dev.pipe = std::make_shared<PipeRes>();
+                    PipeRes& r = *static_cast<PipeRes*>(dev.pipe.get());
+                    MXEC_TRY(r.init(dev));
+                    DevicePipeline p(dev, r);
+                    return p.run_rec(per[d], data_only);
+                }();
+                if (rcs[d] != MXEC_OK) errs[d] = last_error();
+            } catch (const std::bad_alloc&) {
+                rcs[d] = MXEC_E_OOM;
+                errs[d] = "host allocation failed";
+            } catch (const std::exception& e) {
+                rcs[d] = MXEC_E_INVALID_ARG;
+                errs[d] = e.what();
+            }
+        };
+        for (size_t d = 0; d < D; ++d) {
+            if (per[d].empty()) continue;
+            try {
+                j.th.emplace_back(work, d);
+            } catch (const std::system_error&) {
+                work(d);
+            }
+        }
+        for (auto& t : j.th) t.join();
+        for (size_t d = 0; d < D; ++d)
+            if (rcs[d] != MXEC_OK) return set_error(rcs[d], errs[d]);
+        int first_err = MXEC_OK;
+        g0 = 0;
+        for (uint64_t o = 0; o < n_obj; ++o) {
+            const int total = objs[o].k + objs[o].m;
+            if (status_out) status_out[o] = st[o];
+            if (st[o] != MXEC_OK && first_err == MXEC_OK) {
+                int np = 0;
+                for (int i = 0; i < total; ++i) np += present[g0 + uint64_t(i)] != 0;
+                first_err = st[o];
+                set_error(first_err, too_few_msg(np, objs[o].k, total));
+            }
+            g0 += uint64_t(total);
+        }
+        return first_err;
     } catch (const std::bad_alloc&) {
         return set_error(MXEC_E_OOM, "host allocation failed");
     } catch (const std::exception& e) {

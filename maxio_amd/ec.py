@@ -343,6 +343,25 @@ class Context:
         _check(rc)
         return status[: len(objs)]
 
+    def reconstruct_batch_host(self, objs: Sequence[tuple], shard_ptrs, present: np.ndarray, shard_len=None,
+                               expected: Optional[np.ndarray] = None, data_only: bool = False):
+        """mxec_reconstruct_batch_host: host pointers (ints) for every shard,
+        sum(k+m) object-major (a missing shard's pointer receives its rebuilt
+        bytes); present (uint8, sum(k+m)) updated in place; expected: uint8
+        array of sum(k+m)*32 digests or None.  Returns (rc, per-object
+        status array)."""
+        n = len(objs)
+        arr = objs if isinstance(objs, ctypes.Array) else (N.Object * n)(*[N.Object(k, m, s) for (k, m, s) in objs])
+        assert present.dtype == np.uint8
+        status = np.zeros(max(1, n), np.int32)
+        sp = shard_ptrs if isinstance(shard_ptrs, ctypes.Array) else _pp(shard_ptrs)
+        sl = None if shard_len is None else (shard_len if isinstance(shard_len, ctypes.Array) else _u64p(shard_len))
+        rc = self._lib.mxec_reconstruct_batch_host(
+            self._h, arr, n, sp, sl, present.ctypes.data_as(N.U8P),
+            expected.ctypes.data_as(N.U8P) if expected is not None else None,
+            DATA_ONLY if data_only else 0, status.ctypes.data_as(N.I32P))
+        return rc, status[:n]
+
     def reconstruct_strided_device(self, k, m, shard_size, n_obj, shards_ptr, obj_stride,
                                    shard_stride, present: np.ndarray, shard_len=None,
                                    expected_ptr=None, data_only=False, dev=0, stream=None):

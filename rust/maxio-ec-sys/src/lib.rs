@@ -155,6 +155,7 @@ extern "C" {
     pub fn mxec_encode_strided_device(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, k: c_int, m: c_int, shard_size: u64, n_obj: u64, data: *const u8, data_obj_stride: u64, data_shard_stride: u64, data_len: *const u64, parity: *mut u8, parity_obj_stride: u64, parity_shard_stride: u64, digests_dev: *mut u8) -> c_int;
     pub fn mxec_encode_batch_device(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, objs: *const MxecObject, n_obj: u64, data: *const *const u8, data_len: *const u64, parity: *const *mut u8, digests_dev: *mut u8) -> c_int;
     pub fn mxec_encode_batch_host(ctx: *mut MxecCtx, objs: *const MxecObject, n_obj: u64, data: *const *const u8, data_len: *const u64, parity: *const *mut u8, digests: *mut [u8; 32], status_out: *mut i32) -> c_int;
+    pub fn mxec_reconstruct_batch_host(ctx: *mut MxecCtx, objs: *const MxecObject, n_obj: u64, shards: *const *mut u8, shard_len: *const u64, present: *mut u8, expected_sha256: *const [u8; 32], flags: u32, status_out: *mut i32) -> c_int;
     pub fn mxec_reconstruct_strided_device(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, k: c_int, m: c_int, shard_size: u64, n_obj: u64, shards: *mut u8, obj_stride: u64, shard_stride: u64, shard_len: *const u64, present: *mut u8, expected_sha_dev: *const u8, flags: u32, status_out: *mut i32) -> c_int;
     pub fn mxec_reconstruct_batch_device(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, objs: *const MxecObject, n_obj: u64, shards: *const *mut u8, shard_len: *const u64, present: *mut u8, expected_sha_dev: *const u8, flags: u32, status_out: *mut i32) -> c_int;
     pub fn mxec_reconstruct_batch_device_async(ctx: *mut MxecCtx, dev: c_int, stream: *mut c_void, objs: *const MxecObject, n_obj: u64, shards: *const *mut u8, shard_len: *const u64, present: *mut u8, expected_sha_dev: *const u8, flags: u32, status_out: *mut i32, ticket: *mut *mut MxecTicket) -> c_int;

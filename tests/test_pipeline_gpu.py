@@ -88,3 +88,107 @@ def test_batch_host_per_object_errors(ctx):
                               data_len=dlen + [4] * 250)
     assert e.value.name == "TooManyShards255"
     _check(objs, chunks_of, None)  # the valid object was still encoded
+
+
+# ---- mxec_reconstruct_batch_host (GET from host memory) -------------------------------
+
+
+def _rec_batch(rng, specs, pinned=None):
+    """Encoded objects (oracle parity, hashlib digests) with seeded erasures
+    (buffers of missing shards filled with 0xEE), silently corrupt shards as
+    given: returns (objs, ptrs, lens, present, expected, originals, buffers)."""
+    import hashlib
+
+    objs, ptrs, lens, present, expected, originals, bufs = [], [], [], [], [], [], []
+    for (k, m, s, last, lost, corrupt) in specs:
+        chunks = [rng.integers(0, 256, s, dtype=np.uint8) for _ in range(k)]
+        if last is not None:
+            chunks[-1] = chunks[-1][:last].copy()
+        par, dig, rc = oracle.compute_parity(chunks, m, s)
+        assert rc == 0
+        shards = [c.copy() for c in chunks] + [np.asarray(p, np.uint8).copy() for p in par]
+        originals.append([x.copy() for x in shards])
+        objs.append((k, m, s))
+        for i, x in enumerate(shards):
+            b = pinned(x.size) if pinned else np.empty(max(1, x.size), np.uint8)
+            b[:x.size] = x
+            if i in lost:
+                b[:x.size] = 0xEE
+            if i in corrupt:
+                b[x.size // 2] ^= 0x40
+            bufs.append(b)
+            ptrs.append(b.ctypes.data)
+            lens.append(x.size)
+            present.append(0 if i in lost else 1)
+            expected.append(np.frombuffer(dig[i], np.uint8))
+    return (objs, ptrs, lens, np.array(present, np.uint8), np.concatenate(expected).copy(), originals, bufs)
+
+
+@pytest.mark.parametrize("verify", [True, False])
+def test_reconstruct_batch_host_mixed(ctx, verify):
+    """Mixed shapes, short last chunks, 1..m erasures (data and parity), and
+    with verification a silently corrupt present shard per object that still
+    has room: every object comes back bit-exact (oracle parity), present
+    all 1."""
+    rng = np.random.default_rng(41)
+    specs = []
+    for t in range(18):
+        k, m = [(4, 2), (8, 4), (10, 4), (1, 2)][t % 4]
+        s = [4096, 65536 + 16, 1 << 20, 300][t % 4]
+        last = None if t % 3 else int(rng.integers(1, s))
+        e = int(rng.integers(1, m + 1)) - (1 if verify and m > 1 else 0)
+        lost = set(int(x) for x in rng.choice(k + m, max(1, e), replace=False))
+        keep = [i for i in range(k + m) if i not in lost]
+        corrupt = {int(rng.choice(keep))} if verify and len(lost) < m else set()
+        specs.append((k, m, s, last, lost, corrupt))
+    objs, ptrs, lens, present, expected, originals, bufs = _rec_batch(rng, specs)
+    rc, status = ctx.reconstruct_batch_host(objs, ptrs, present, shard_len=lens,
+                                            expected=expected if verify else None)
+    assert rc == 0 and not status.any() and present.all()
+    g = 0
+    for o, (k, m, s) in enumerate(objs):
+        for i in range(k + m):
+            n = lens[g + i]
+            assert np.array_equal(bufs[g + i][:n], originals[o][i]), (o, i)
+        g += k + m
+
+
+def test_reconstruct_batch_host_failing_object(ctx):
+    """An object with more than m shards lost or corrupt: -10 for it and the
+    call, its buffers untouched, the present mask minus the mismatches; the
+    other objects bit-exact (chunk_reader.rs:199-208)."""
+    rng = np.random.default_rng(42)
+    specs = [(4, 2, 8192, None, {0}, set()), (4, 2, 8192, None, {1, 5}, {0}), (8, 4, 4096, 100, {2}, set())]
+    objs, ptrs, lens, present, expected, originals, bufs = _rec_batch(rng, specs)
+    before = [b.copy() for b in bufs]
+    p = present.copy()
+    rc, status = ctx.reconstruct_batch_host(objs, ptrs, p, shard_len=lens, expected=expected)
+    assert rc == -10 and list(status) == [0, -10, 0]
+    assert "too many missing/corrupt shards" in ctx._lib.mxec_last_error().decode()
+    for i in range(6):
+        assert np.array_equal(bufs[6 + i], before[6 + i])  # failing object untouched
+    assert list(p[6:12]) == [0, 0, 1, 1, 1, 0]
+    for o, g in ((0, 0), (2, 12)):
+        k, m, s = objs[o]
+        for i in range(k + m):
+            assert np.array_equal(bufs[g + i][:lens[g + i]], originals[o][i]), (o, i)
+
+
+def test_reconstruct_batch_host_pinned_config2_shape(ctx):
+    """configs[1]'s shape from page-locked memory (the direct-DMA path):
+    8 x 4+2 x 10 MiB, two erasures each, verified: bit-exact."""
+    rng = np.random.default_rng(43)
+    keep = []
+
+    def pinned(n):
+        a = ctx.host_array(max(1, n))
+        keep.append(a)
+        return a
+
+    specs = [(4, 2, 10 << 20, None, set(int(x) for x in rng.choice(6, 2, replace=False)), set()) for _ in range(8)]
+    objs, ptrs, lens, present, expected, originals, bufs = _rec_batch(rng, specs, pinned=pinned)
+    rc, status = ctx.reconstruct_batch_host(objs, ptrs, present, shard_len=lens, expected=expected)
+    assert rc == 0 and present.all()
+    for o in range(8):
+        for i in range(6):
+            assert np.array_equal(bufs[o * 6 + i][:lens[o * 6 + i]], originals[o][i]), (o, i)
