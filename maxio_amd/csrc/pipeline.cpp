@@ -201,142 +201,165 @@ public:
 
 private:
     // One wave of a host reconstruct batch (try_reconstruct_data_chunk,
-    // chunk_reader.rs:157-226, per object): the present shards go up
-    // (coalesced, direct from pinned memory), their digests are checked on
-    // the device against the expected ones when given (a mismatch is an
-    // erasure, :176-196), every object with at least k verified shards is
-    // rebuilt in one grouped launch per call (run_rs_mixed), and only the
-    // rebuilt shards come back.  An object short of k shards gets
-    // MXEC_E_TOO_FEW_SHARDS_PRESENT and none of its buffers is written.
+    // chunk_reader.rs:157-226, per object): the present shards go up group
+    // by group (coalesced, direct from pinned memory), their digests are
+    // checked on the device against the expected ones when given (one
+    // SHA-256 launch for the whole wave once every group is up: a chain's
+    // latency does not depend on how many share the launch; a mismatch is an
+    // erasure, :176-196), each group is rebuilt (one grouped launch,
+    // run_rs_mixed) as soon as it is up (and verified), and its rebuilt
+    // shards go down while later groups still upload.  An object short of k
+    // shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT and none of its buffers is
+    // written.
     int rec_wave(std::vector<RecObj>& objs, size_t o0, size_t o1, bool data_only) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         hipStream_t cs = cs_[0];
-        for (size_t o = o0; o < o1; ++o) {
-            const RecObj& h = objs[o];
-            for (int i = 0; i < h.k + h.m; ++i) {
-                if (!h.present[i]) continue;
-                MXEC_TRY(queue_up(base + h.pool_off + uint64_t(i) * h.slot(), h.shards[i], h.len[i]));
-                if (h.len[i] != h.slot()) MXEC_TRY(flush_up());
+        // Groups: consecutive objects up to kGroupBytes of present input.
+        std::vector<std::pair<size_t, size_t>> groups;
+        for (size_t g0 = o0; g0 < o1;) {
+            size_t g1 = g0;
+            uint64_t in_bytes = 0;
+            while (g1 < o1) {
+                uint64_t b = 0;
+                for (int i = 0; i < objs[g1].k + objs[g1].m; ++i) b += objs[g1].present[i] ? objs[g1].len[i] : 0;
+                if (g1 > g0 && in_bytes + b > kGroupBytes) break;
+                in_bytes += b;
+                ++g1;
             }
+            groups.emplace_back(g0, g1);
+            g0 = g1;
         }
-        MXEC_TRY(flush_up());
-        // Verification: digests of every present shard of an object that
-        // carries expected digests, compared on the device.
-        std::vector<const uint8_t*> sp;
-        std::vector<uint64_t> sl, idx;
         uint64_t msgs = 0;
-        for (size_t o = o0; o < o1; ++o) msgs += uint64_t(objs[o].k + objs[o].m);
-        uint64_t g = 0;
+        bool verify = false;
         for (size_t o = o0; o < o1; ++o) {
-            const RecObj& h = objs[o];
-            for (int i = 0; i < h.k + h.m; ++i, ++g) {
-                if (!h.expected || !h.present[i]) continue;
-                sp.push_back(base + h.pool_off + uint64_t(i) * h.slot());
-                sl.push_back(h.len[i]);
-                idx.push_back(g);
-            }
+            msgs += uint64_t(objs[o].k + objs[o].m);
+            verify = verify || objs[o].expected;
         }
-        hipEvent_t up;
-        MXEC_TRY(new_event(&up));
-        if (!sp.empty()) {
-            // expected digests of the wave, message order, after the ok flags
-            const uint64_t fo = rup(sp.size(), 256);
+        // Expected digests of the wave (message order) after room for the
+        // verdict flags, on the device.
+        const uint64_t fo = rup(msgs, 256);
+        uint8_t* ok = nullptr;
+        uint8_t* exp = nullptr;
+        if (verify) {
             MXEC_TRY(scratch_.ensure(fo + msgs * 32));
-            uint8_t* ok = static_cast<uint8_t*>(scratch_.p);
-            uint8_t* exp = ok + fo;
-            g = 0;
-            for (size_t o = o0; o < o1; ++o) {
+            ok = static_cast<uint8_t*>(scratch_.p);
+            exp = ok + fo;
+        }
+        // Phase 1: every upload, one event per group.
+        std::vector<hipEvent_t> up(groups.size());
+        uint64_t g = 0;
+        for (size_t q = 0; q < groups.size(); ++q) {
+            for (size_t o = groups[q].first; o < groups[q].second; ++o) {
                 const RecObj& h = objs[o];
+                for (int i = 0; i < h.k + h.m; ++i) {
+                    if (!h.present[i]) continue;
+                    MXEC_TRY(queue_up(base + h.pool_off + uint64_t(i) * h.slot(), h.shards[i], h.len[i]));
+                    if (h.len[i] != h.slot()) MXEC_TRY(flush_up());
+                }
+                MXEC_TRY(flush_up());
                 if (h.expected) MXEC_TRY(queue_up(exp + g * 32, &h.expected[0][0], uint64_t(h.k + h.m) * 32));
                 g += uint64_t(h.k + h.m);
             }
             MXEC_TRY(flush_up());
-            MXEC_HIP(hipEventRecord(up, h2d_));
-            MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
-            MXEC_TRY(run_sha(d_, slot_, cs, sp, sl, nullptr, exp, ok, &idx, &arena_));
-            MXEC_TRY(flags_.ensure(sp.size()));
-            MXEC_HIP(hipMemcpyAsync(flags_.p, ok, sp.size(), hipMemcpyDeviceToHost, cs));
-            MXEC_HIP(hipStreamSynchronize(cs));
-            const auto* okh = static_cast<const uint8_t*>(flags_.p);
-            for (size_t t = 0; t < idx.size(); ++t) {
-                if (okh[t]) continue;
-                // idx[t] is the wave-relative message index: find its object
-                uint64_t gg = 0;
-                for (size_t o = o0; o < o1; ++o) {
-                    const uint64_t n = uint64_t(objs[o].k + objs[o].m);
-                    if (idx[t] < gg + n) {
-                        objs[o].present[idx[t] - gg] = 0;
-                        break;
+            MXEC_TRY(new_event(&up[q]));
+            MXEC_HIP(hipEventRecord(up[q], h2d_));
+        }
+        // Phase 2 (verification only): one launch over every present shard
+        // of the objects that carry digests, verdicts read back.
+        if (verify) {
+            std::vector<const uint8_t*> sp;
+            std::vector<uint64_t> sl, idx;
+            std::vector<std::pair<size_t, int>> who;  // message -> (object, shard)
+            g = 0;
+            for (size_t o = o0; o < o1; ++o) {
+                const RecObj& h = objs[o];
+                for (int i = 0; i < h.k + h.m; ++i, ++g) {
+                    if (!h.expected || !h.present[i]) continue;
+                    sp.push_back(base + h.pool_off + uint64_t(i) * h.slot());
+                    sl.push_back(h.len[i]);
+                    idx.push_back(g);
+                    who.emplace_back(o, i);
+                }
+            }
+            MXEC_HIP(hipStreamWaitEvent(cs, up.back(), 0));
+            if (!sp.empty()) {
+                MXEC_TRY(run_sha(d_, slot_, cs, sp, sl, nullptr, exp, ok, &idx, &arena_));
+                MXEC_TRY(flags_.ensure(sp.size()));
+                MXEC_HIP(hipMemcpyAsync(flags_.p, ok, sp.size(), hipMemcpyDeviceToHost, cs));
+                MXEC_HIP(hipStreamSynchronize(cs));
+                const auto* okh = static_cast<const uint8_t*>(flags_.p);
+                for (size_t t = 0; t < who.size(); ++t)
+                    if (!okh[t]) objs[who[t].first].present[who[t].second] = 0;
+            }
+        }
+        // Phase 3: per group, rebuild once it is up, then its shards down.
+        for (size_t q = 0; q < groups.size(); ++q) {
+            const size_t q0 = groups[q].first, q1 = groups[q].second;
+            if (!verify) MXEC_HIP(hipStreamWaitEvent(cs, up[q], 0));
+            std::vector<std::shared_ptr<const DecodePlan>> plans(q1 - q0);
+            std::vector<uint32_t> offs(q1 - q0);
+            std::vector<const uint8_t*> in;
+            std::vector<uint8_t*> out;
+            std::vector<uint64_t> il, ol;
+            std::map<int, std::vector<RsMixedObject>> rs_groups;
+            auto collect = [&]() -> int {
+                for (size_t o = q0; o < q1; ++o)
+                    MXEC_TRY(decode_plan(d_, objs[o].k, objs[o].m, objs[o].present, data_only, &plans[o - q0],
+                                         &offs[o - q0]));
+                return MXEC_OK;
+            };
+            auto launch = [&]() -> int {
+                size_t n_in = 0, n_out = 0;
+                for (size_t t = 0; t < plans.size(); ++t)
+                    if (plans[t] && !plans[t]->missing.empty()) {
+                        n_in += size_t(objs[q0 + t].k);
+                        n_out += plans[t]->missing.size();
                     }
-                    gg += n;
+                in.assign(n_in, nullptr);
+                out.assign(n_out, nullptr);
+                il.assign(n_in, 0);
+                ol.assign(n_out, 0);
+                rs_groups.clear();
+                size_t pi = 0, po = 0;
+                for (size_t t = 0; t < plans.size(); ++t) {
+                    if (!plans[t] || plans[t]->missing.empty()) continue;
+                    const RecObj& h = objs[q0 + t];
+                    const DecodePlan& p = *plans[t];
+                    const int r = int(p.missing.size());
+                    uint8_t* ob = base + h.pool_off;
+                    for (int v = 0; v < h.k; ++v) {
+                        in[pi + v] = ob + uint64_t(p.valid[size_t(v)]) * h.slot();
+                        il[pi + v] = h.len[p.valid[size_t(v)]];
+                    }
+                    for (int e = 0; e < r; ++e) {
+                        out[po + e] = ob + uint64_t(p.missing[size_t(e)]) * h.slot();
+                        ol[po + e] = h.len[p.missing[size_t(e)]];
+                    }
+                    rs_groups[r].push_back(
+                        RsMixedObject{h.k, h.S, RsObject{&in[pi], &il[pi], &out[po], &ol[po], offs[t]}});
+                    pi += size_t(h.k);
+                    po += size_t(r);
+                }
+                return run_rs_mixed(d_, slot_, cs, rs_groups, &arena_);
+            };
+            MXEC_TRY(with_stable_coef(d_, collect, launch));
+            hipEvent_t rs_done;
+            MXEC_TRY(new_event(&rs_done));
+            MXEC_HIP(hipEventRecord(rs_done, cs));
+            MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
+            for (size_t o = q0; o < q1; ++o) {
+                RecObj& h = objs[o];
+                const auto& p = plans[o - q0];
+                *h.status = p ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
+                if (!p) continue;
+                for (int e : p->missing) {
+                    MXEC_TRY(queue_down(h.shards[e], base + h.pool_off + uint64_t(e) * h.slot(), h.len[e]));
+                    if (h.len[e] != h.slot()) MXEC_TRY(flush_down());
+                    h.present[e] = 1;
                 }
             }
-        } else {
-            MXEC_HIP(hipEventRecord(up, h2d_));
-            MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
+            MXEC_TRY(flush_down());
         }
-        // Rebuild: one decode plan per object, one launch for the wave.
-        std::vector<std::shared_ptr<const DecodePlan>> plans(o1 - o0);
-        std::vector<uint32_t> offs(o1 - o0);
-        std::vector<const uint8_t*> in;
-        std::vector<uint8_t*> out;
-        std::vector<uint64_t> il, ol;
-        std::map<int, std::vector<RsMixedObject>> groups;
-        auto collect = [&]() -> int {
-            for (size_t o = o0; o < o1; ++o)
-                MXEC_TRY(decode_plan(d_, objs[o].k, objs[o].m, objs[o].present, data_only, &plans[o - o0], &offs[o - o0]));
-            return MXEC_OK;
-        };
-        auto launch = [&]() -> int {
-            size_t n_in = 0, n_out = 0;
-            for (size_t t = 0; t < plans.size(); ++t)
-                if (plans[t] && !plans[t]->missing.empty()) {
-                    n_in += size_t(objs[o0 + t].k);
-                    n_out += plans[t]->missing.size();
-                }
-            in.assign(n_in, nullptr);
-            out.assign(n_out, nullptr);
-            il.assign(n_in, 0);
-            ol.assign(n_out, 0);
-            groups.clear();
-            size_t pi = 0, po = 0;
-            for (size_t t = 0; t < plans.size(); ++t) {
-                if (!plans[t] || plans[t]->missing.empty()) continue;
-                const RecObj& h = objs[o0 + t];
-                const DecodePlan& p = *plans[t];
-                const int r = int(p.missing.size());
-                uint8_t* ob = base + h.pool_off;
-                for (int v = 0; v < h.k; ++v) {
-                    in[pi + v] = ob + uint64_t(p.valid[size_t(v)]) * h.slot();
-                    il[pi + v] = h.len[p.valid[size_t(v)]];
-                }
-                for (int e = 0; e < r; ++e) {
-                    out[po + e] = ob + uint64_t(p.missing[size_t(e)]) * h.slot();
-                    ol[po + e] = h.len[p.missing[size_t(e)]];
-                }
-                groups[r].push_back(RsMixedObject{h.k, h.S, RsObject{&in[pi], &il[pi], &out[po], &ol[po], offs[t]}});
-                pi += size_t(h.k);
-                po += size_t(r);
-            }
-            return run_rs_mixed(d_, slot_, cs, groups, &arena_);
-        };
-        MXEC_TRY(with_stable_coef(d_, collect, launch));
-        hipEvent_t rs_done;
-        MXEC_TRY(new_event(&rs_done));
-        MXEC_HIP(hipEventRecord(rs_done, cs));
-        MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
-        for (size_t o = o0; o < o1; ++o) {
-            RecObj& h = objs[o];
-            const auto& p = plans[o - o0];
-            *h.status = p ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
-            if (!p) continue;
-            for (int e : p->missing) {
-                MXEC_TRY(queue_down(h.shards[e], base + h.pool_off + uint64_t(e) * h.slot(), h.len[e]));
-                if (h.len[e] != h.slot()) MXEC_TRY(flush_down());
-                h.present[e] = 1;
-            }
-        }
-        MXEC_TRY(flush_down());
         return flush();
     }
 

@@ -10,6 +10,7 @@
 #   refuse2   python bench.py --gpus 2 on a one-GPU box: must exit 2, no line
 #   rehearse  BENCH_REHEARSE_LOGICAL=1 bench.py --gpus 2 (labelled in-process
 #             multi-device rehearsal on two logical devices of the one card)
+#   rehearse8 the same with --gpus 8 on eight logical devices (64 objects each)
 #   ranks2    the torch.distributed.run path with two ranks on the one GPU
 #             (BENCH_GPU_OF_RANK=0, gloo for the timing collectives)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench command
@@ -46,6 +47,10 @@ for st in "${STEPS[@]}"; do
       BENCH_REHEARSE_LOGICAL=1 timeout -k 10 600 python bench.py --gpus 2 --objects 256 --steps 10 --warmup 2 \
         > "$O/rehearse2.json" 2> "$O/rehearse2.err" || { tail -20 "$O/rehearse2.err"; exit 1; }
       cat "$O/rehearse2.json" ;;
+    rehearse8)
+      BENCH_REHEARSE_LOGICAL=1 timeout -k 10 600 python bench.py --gpus 8 --objects 64 --steps 10 --warmup 2 \
+        > "$O/rehearse8.json" 2> "$O/rehearse8.err" || { tail -20 "$O/rehearse8.err"; exit 1; }
+      cat "$O/rehearse8.json" ;;
     ranks2)
       BENCH_GPU_OF_RANK=0 BENCH_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --objects 256 --steps 10 \
