@@ -30,6 +30,7 @@
 #include "kernels.hpp"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace mxec {
 namespace {
@@ -286,7 +287,7 @@ __device__ __forceinline__ Vec4 gload16_upto(gcptr p, int32_t valid, gcptr safe)
 // k inputs and lengths; op / ol: its R outputs and lengths; tab: its
 // coefficient table at the first output row, input j's rows `stride` x 8
 // dwords apart.
-template <int R, int V, bool NT>
+template <int R, int V, bool NT, bool LNT = NT>
 __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, const uint64_t* __restrict__ il,
                                         uint8_t* const* __restrict__ op, const uint64_t* __restrict__ ol,
                                         const uint32_t* __restrict__ tab, uint32_t k, uint32_t stride,
@@ -310,7 +311,7 @@ __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, c
         gcptr p = ((gcptr)(ip[jj])) + lane;
         if (len >= end) {
 #pragma unroll
-            for (int v = 0; v < V; ++v) x[v] = gload16<NT>(p + v * kThreads * 16);
+            for (int v = 0; v < V; ++v) x[v] = gload16<LNT>(p + v * kThreads * 16);
         } else if (len <= base) {
 #pragma unroll
             for (int v = 0; v < V; ++v) x[v] = Vec4{{0, 0, 0, 0}};
@@ -318,7 +319,7 @@ __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, c
             const int32_t d = int32_t(len - base) - lane_off;
 #pragma unroll
             for (int v = 0; v < V; ++v)
-                x[v] = gload16_upto<NT>(p + v * kThreads * 16, d - v * int32_t(kThreads * 16), safe);
+                x[v] = gload16_upto<LNT>(p + v * kThreads * 16, d - v * int32_t(kThreads * 16), safe);
         }
     };
 
@@ -335,7 +336,7 @@ __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, c
             for (int jj = 0; jj < 4; ++jj) {
                 gcptr p = ((gcptr)(ip[j + jj])) + lane;
 #pragma unroll
-                for (int v = 0; v < V; ++v) x[jj][v] = gload16<NT>(p + v * kThreads * 16);
+                for (int v = 0; v < V; ++v) x[jj][v] = gload16<LNT>(p + v * kThreads * 16);
             }
         } else {
 #pragma unroll
@@ -387,7 +388,7 @@ __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, c
 // the object), one wave-uniform scalar load, fetched one tile ahead so it
 // is in SGPRs when the tile starts (the uniform kernel computes the same
 // from the tile index).
-template <int R, int V, bool NT, bool GRP, int OCC = 1>
+template <int R, int V, bool NT, bool GRP, int OCC = 1, bool LNT = NT>
 __global__ __launch_bounds__(kThreads, OCC) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
@@ -416,7 +417,7 @@ __global__ __launch_bounds__(kThreads, OCC) void rs_apply_fast(
         }
         // Lengths are clamped to the shard size by the host, so a tile past
         // the shard end is cut by the same tests.
-        rs_tile<R, V, NT>(in_ptrs + in0, in_len + in0, out_ptrs + uint64_t(obj) * r_total + row0,
+        rs_tile<R, V, NT, LNT>(in_ptrs + in0, in_len + in0, out_ptrs + uint64_t(obj) * r_total + row0,
                           out_len + uint64_t(obj) * r_total + row0, coef + coef_off[obj] + row0 * 8, k, r_total,
                           base, safe);
     }
@@ -456,10 +457,10 @@ __global__ __launch_bounds__(kThreads) void rs_apply_multi(
     }
 }
 
-template <int R, int V, bool NT, bool GRP = false, int OCC = 1>
+template <int R, int V, bool NT, bool GRP = false, int OCC = 1, bool LNT = NT>
 hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
-    hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP, OCC>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP, OCC, LNT>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                        a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.k, a.r_total,
                        a.row0, tiles_per_obj, n_tiles, a.tiles);
     return hipGetLastError();
@@ -502,6 +503,8 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
                                            : launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (R == 4 && var.vecs == 4 && var.nt && var.min_waves == 3)
             e = launch_fast<R, 4, true, false, R == 4 ? 3 : 1>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (R <= 4 && var.vecs == 4 && var.nt && !var.load_nt)  // lab: plain loads, nontemporal stores
+            e = launch_fast<R, 4, true, false, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                            : launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
         return e;
@@ -545,6 +548,9 @@ RsVariant rs_default_variant(uint32_t r_total) {
     RsVariant v;
     v.vecs = r_total <= 4 ? 4 : 2;
     v.nt = true;
+    // MXEC_RS_LOAD_NT=0 (lab, read per launch): plain loads with the
+    // nontemporal stores, R <= 4.
+    if (const char* e = getenv("MXEC_RS_LOAD_NT")) v.load_nt = std::strcmp(e, "0") != 0;
     // R <= 2 (config 2, two-erasure decodes) gained another 0-2 % at 1024 in
     // every layout swept; R = 4 went either way (profiles/r2_lab_rs_grid_*).
     v.blocks_per_cu = r_total <= 2 ? 1024 : 512;
