@@ -139,8 +139,9 @@ class Encode:
 
     bound = "hbm"
 
-    def __init__(self, torch, ctx, dev, sh, k, m, S, n, label, seed, streams=1):
+    def __init__(self, torch, ctx, dev, sh, k, m, S, n, label, seed, streams=1, separate=False):
         self.torch, self.ctx, self.sh = torch, ctx, sh
+        self.separate = separate
         self.k, self.m, self.S, self.n = k, m, S, n
         # streams > 1 (BENCH_ENCODE_STREAMS, lab): the batch as that many
         # launches over consecutive object ranges on their own streams,
@@ -160,14 +161,25 @@ class Encode:
         # unpadded layout fell to 5.2 TB/s on 2 of 8 allocations and the
         # padded one on none; elsewhere the pad measured +1 %
         # (profiles/r2_shard_pad_spread.txt).
-        self.pad = (2 << 20) + (64 << 10) if S >= (4 << 20) else 0
+        self.pad = (2 << 20) + (64 << 10) if S >= (4 << 20) and not separate else 0
         self.sstride = S + self.pad
-        self.obj = torch.empty((n, k + m, self.sstride), dtype=torch.uint8, device=dev)
-        for o in range(n):  # per object keeps the randint temporary small
-            self.obj[o, :k, :S].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
-        self.obj[:, k:].zero_()
-        self.data, self.parity = self.obj[:, :k, :S], self.obj[:, k:, :S]
-        self.stride = (k + m) * self.sstride
+        if separate:
+            # What a caller with its own buffers hands the *_device API: data
+            # [n][k][S] and parity [n][m][S] as two allocations, no pad
+            # (extra.config2_separate_buffers).
+            self.obj = torch.empty((n, k, S), dtype=torch.uint8, device=dev)
+            for o in range(n):
+                self.obj[o].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
+            self.par_buf = torch.zeros((n, m, S), dtype=torch.uint8, device=dev)
+            self.data, self.parity = self.obj, self.par_buf
+            self.stride, self.pstride = k * S, m * S
+        else:
+            self.obj = torch.empty((n, k + m, self.sstride), dtype=torch.uint8, device=dev)
+            for o in range(n):  # per object keeps the randint temporary small
+                self.obj[o, :k, :S].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
+            self.obj[:, k:].zero_()
+            self.data, self.parity = self.obj[:, :k, :S], self.obj[:, k:, :S]
+            self.stride = self.pstride = (k + m) * self.sstride
         self.payload = n * k * S
         self.alg_bytes = n * (k + m) * S
         r = min(m, 8)
@@ -178,7 +190,7 @@ class Encode:
         k, m, S = self.k, self.m, self.S
         if len(self.streams) == 1:
             self.ctx.encode_strided_device(k, m, S, self.n, self.data.data_ptr(), self.stride, self.sstride,
-                                           self.parity.data_ptr(), self.stride, self.sstride, stream=self.sh)
+                                           self.parity.data_ptr(), self.pstride, self.sstride, stream=self.sh)
             return
         ns = len(self.streams)
         for st in self.streams:
@@ -186,7 +198,7 @@ class Encode:
         for i, st in enumerate(self.streams):
             a, b = self.n * i // ns, self.n * (i + 1) // ns
             self.ctx.encode_strided_device(k, m, S, b - a, self.data[a].data_ptr(), self.stride, self.sstride,
-                                           self.parity[a].data_ptr(), self.stride, self.sstride,
+                                           self.parity[a].data_ptr(), self.pstride, self.sstride,
                                            stream=st.cuda_stream)
         for st in self.streams:
             self.main.wait_stream(st)
@@ -210,6 +222,8 @@ class Encode:
 
     def drop(self):
         del self.data, self.parity, self.obj
+        if self.separate:
+            del self.par_buf
 
 
 class Reconstruct:
@@ -801,7 +815,7 @@ def pattern_on_buffers(torch, stream, w) -> float:
     if k % 4 or m not in (1, 2, 4) or S % 16384:
         return None
     ms = event_ms(torch, stream, lambda: lib.mxprobe_rs_pattern_strided(
-        w.data.data_ptr(), w.parity.data_ptr(), k, m, S, n, w.stride, w.stride, w.sstride, stream.cuda_stream), 5)
+        w.data.data_ptr(), w.parity.data_ptr(), k, m, S, n, w.stride, w.pstride, w.sstride, stream.cuda_stream), 5)
     return round(n * (k + m) * S / (ms * 1e-3) / 1e9, 1)
 
 
@@ -994,12 +1008,31 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     rs.drop()
     del rs
     torch.cuda.empty_cache()
+    # -- config 2 with caller-owned separate data / parity buffers -----------
+    w = Encode(torch, ctx, dev, sh, 4, 2, 10 << 20, 1024,
+               "RS encode k=4 m=2, 10 MiB chunks, 1024 objects, data [n][k][S] and parity [n][m][S] as two "
+               "allocations (no pad)", SEED + 3, separate=True)
+    torch.cuda.synchronize()
+    ms = event_ms(torch, stream, w.step, max(5, steps // 4))
+    ok = w.spot_check()
+    same = pattern_on_buffers(torch, stream, w)
+    f4 = float4_copy_on_buffers(torch, stream, w)  # over the data allocation
+    blk = hbm_block(w.alg_bytes, ms, w.kernel, dict(cal or {}, rs_pattern_same_buffers_GBps=same),
+                    "rs_pattern_same_buffers_GBps")
+    if f4:
+        blk["float4_copy_data_buffer_GBps"] = f4
+        blk["frac_of_float4_copy"] = round(blk["achieved"] / f4, 4)
+    out["config2_separate_buffers"] = {"workload": w.name, "GiBps_payload": round(w.payload / GIB / (ms * 1e-3), 3),
+                                       "spot_check_vs_oracle": ok, "roofline": blk}
+    w.drop()
+    del w
+    torch.cuda.empty_cache()
     # -- PUT compute: encode + SHA-256 of all k+m chunks, config 2 shape -----
     w = make_workload("2", torch, ctx, dev, sh, 256, 0)
     kk, mm, SS, nn = w.k, w.m, w.S, w.n
     dig = torch.empty((nn, kk + mm, 32), dtype=torch.uint8, device=dev)
     ms = event_ms(torch, stream, lambda: ctx.encode_strided_device(
-        kk, mm, SS, nn, w.data.data_ptr(), w.stride, w.sstride, w.parity.data_ptr(), w.stride, w.sstride,
+        kk, mm, SS, nn, w.data.data_ptr(), w.stride, w.sstride, w.parity.data_ptr(), w.pstride, w.sstride,
         digests_ptr=dig.data_ptr(), stream=sh), 2)
     out["put_path_encode_plus_sha256"] = {
         "GiBps_payload": round(nn * kk * SS / GIB / (ms * 1e-3), 3), "ms": round(ms, 2),
