@@ -37,6 +37,7 @@ struct ShaCombiner {
         // waits for the digests (the caller is blocked meanwhile, so its slot
         // and stream are free to use): work that should run beside the hash.
         const std::function<int()>* after_launch = nullptr;
+        uint64_t longest = 0;  // bytes of the longest message (set before queueing)
         int after_rc = MXEC_OK;
         std::string after_msg;
         int rc = MXEC_OK;
@@ -264,6 +265,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     }
     me.ready = ready;
     me.after_launch = after_launch;
+    for (uint64_t l : lens) me.longest = std::max(me.longest, l);  // outside the lock
     std::unique_lock<std::mutex> lk(c->mu);
     c->pending.push_back(&me);
     c->pending_msgs += ptrs.size();
@@ -311,8 +313,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // part: it only continues while requests keep arriving.
         auto launch_us = [&] {
             uint64_t longest = 0;
-            for (const ShaCombiner::Req* r : c->pending)
-                for (uint64_t l : *r->lens) longest = std::max(longest, l);
+            for (const ShaCombiner::Req* r : c->pending) longest = std::max(longest, r->longest);
             return double(longest / 64) * 1.8;
         };
         const double est_us = c->pending.size() >= 2 ? launch_us() : 0.0;

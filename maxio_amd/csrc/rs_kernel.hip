@@ -554,6 +554,11 @@ RsVariant rs_default_variant(uint32_t r_total) {
     // R <= 2 (config 2, two-erasure decodes) gained another 0-2 % at 1024 in
     // every layout swept; R = 4 went either way (profiles/r2_lab_rs_grid_*).
     v.blocks_per_cu = r_total <= 2 ? 1024 : 512;
+    // MXEC_RS_BPC (lab, read per launch): workgroups per CU of uniform launches.
+    if (const char* e = getenv("MXEC_RS_BPC")) {
+        const int b = atoi(e);
+        if (b > 0 && b <= 4096) v.blocks_per_cu = b;
+    }
     return v;
 }
 

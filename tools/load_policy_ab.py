@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""Within-process A/B of the RS kernel's load form on the bench's own
-buffers: nontemporal loads (default) vs plain loads, both with nontemporal
-stores (MXEC_RS_LOAD_NT, read per launch), alternating rounds, HIP-event
-timed; then the guide's float4 copy on the same buffers.  Config 2 and the
-north-star shape.  Lab tool, not product.
+"""Within-process A/B of RS kernel knobs on the bench's own buffers,
+alternating rounds, HIP-event timed; then the guide's float4 copy on the
+same buffers.  Config 2 and the north-star shape.  Lab tool, not product.
 
   python tools/load_policy_ab.py [--rounds 4] [--reps 10]
+      nontemporal loads (default) vs plain loads, both with nontemporal
+      stores (MXEC_RS_LOAD_NT, read per launch)
+  python tools/load_policy_ab.py --env MXEC_RS_BPC --values 512,1024,2048
+      any knob read per launch, one arm per value ("" = unset)
 """
 from __future__ import annotations
 
@@ -25,6 +27,8 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--configs", default="2,ns")
+    ap.add_argument("--env", default="MXEC_RS_LOAD_NT")
+    ap.add_argument("--values", default="1,0")
     a = ap.parse_args()
     import torch
 
@@ -37,12 +41,15 @@ def main() -> int:
         w = bench.make_workload(cfg, torch, ctx, dev, st.cuda_stream, 0, 0)
         torch.cuda.synchronize()
         for rnd in range(a.rounds):
-            for mode in ("1", "0"):
-                os.environ["MXEC_RS_LOAD_NT"] = mode
+            for val in a.values.split(","):
+                if val:
+                    os.environ[a.env] = val
+                else:
+                    os.environ.pop(a.env, None)
                 ms = bench.event_ms(torch, st, w.step, a.reps)
-                print(json.dumps({"config": cfg, "round": rnd, "load_nt": mode == "1", "ms": round(ms, 4),
+                print(json.dumps({"config": cfg, "round": rnd, a.env: val, "ms": round(ms, 4),
                                   "TBps": round(w.alg_bytes / (ms * 1e-3) / 1e12, 4)}), flush=True)
-        os.environ["MXEC_RS_LOAD_NT"] = "1"
+        os.environ.pop(a.env, None)
         ok = w.spot_check()
         f4 = bench.float4_copy_on_buffers(torch, st, w)
         print(json.dumps({"config": cfg, "spot_check": ok, "float4_copy_same_buffers_GBps": f4}), flush=True)
