@@ -733,9 +733,11 @@ def probe_lib():
     return lib
 
 
-def event_ms(torch, stream, fn, reps: int) -> float:
-    """Average HIP-event time of fn() on `stream` (one warm-up call first)."""
-    fn()
+def event_ms(torch, stream, fn, reps: int, warm: int = 1) -> float:
+    """Average HIP-event time of fn() on `stream` after `warm` untimed calls
+    (5 for RS launches: the grid tuner times launches 2-5 of a shape)."""
+    for _ in range(warm):
+        fn()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     torch.cuda.synchronize()
     for a, b in ev:
@@ -905,7 +907,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     # -- north star: encode k=8 m=4, 1 MiB, 4096 objects -------------------
     w = make_workload("ns", torch, ctx, dev, sh, 0, 0)
     torch.cuda.synchronize()
-    ms = event_ms(torch, stream, w.step, max(5, steps // 2))
+    ms = event_ms(torch, stream, w.step, max(5, steps // 2), warm=5)
     ok = w.spot_check()
     same = pattern_on_buffers(torch, stream, w)
     f4_ns = float4_copy_on_buffers(torch, stream, w)
@@ -914,7 +916,9 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                  "spot_check_vs_oracle": ok,
                  "roofline": hbm_block(w.alg_bytes, ms, w.kernel, cal_ns,
                                        "rs_pattern_same_buffers_GBps" if same else "rs_pattern_k8m4_GBps")}
-    tr, src = pmc_traffic("k8m4", w.alg_bytes, rs_blocks_per_cu(4))
+    ns_bpc = ctx.rs_grid(8, 4, 1 << 20)
+    tr, src = pmc_traffic("k8m4", w.alg_bytes, ns_bpc)
+    out["ns"]["roofline"]["blocks_per_cu"] = ns_bpc
     out["ns"]["roofline"]["traffic"], out["ns"]["roofline"]["traffic_source"] = tr, src
     if f4_ns:
         out["ns"]["roofline"]["float4_copy_GBps"] = f4_ns
@@ -928,7 +932,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     torch.cuda.empty_cache()
     # -- config 3: reconstruct 8+4, 2 erasures + verify, 1024 objects --------
     r = Reconstruct(torch, ctx, dev, sh, 1024, SEED)
-    ms_call = event_ms(torch, stream, r.step, 5)
+    ms_call = event_ms(torch, stream, r.step, 5, warm=5)
     ok = r.spot_check()
     k, m, S, n = r.k, r.m, r.S, r.n
     present_ptrs, present_lens = [], []
@@ -949,7 +953,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
         pr = r.present0.copy()
         rc, _ = ctx.reconstruct_strided_device(k, m, S, n, r.obj.data_ptr(), (k + m) * S, S, pr, stream=sh)
         assert rc == 0
-    ms_rs = event_ms(torch, stream, decode_only, 3)
+    ms_rs = event_ms(torch, stream, decode_only, 3, warm=2)
     # its denominator: the RS pattern on the same buffers, 8 shards read and
     # 2 written per object (shards 0-7 -> 10-11; after the spot check)
     lib = probe_lib()
@@ -1013,7 +1017,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                "RS encode k=4 m=2, 10 MiB chunks, 1024 objects, data [n][k][S] and parity [n][m][S] as two "
                "allocations (no pad)", SEED + 3, separate=True)
     torch.cuda.synchronize()
-    ms = event_ms(torch, stream, w.step, max(5, steps // 4))
+    ms = event_ms(torch, stream, w.step, max(5, steps // 4), warm=5)
     ok = w.spot_check()
     same = pattern_on_buffers(torch, stream, w)
     f4 = float4_copy_on_buffers(torch, stream, w)  # over the data allocation
@@ -1119,7 +1123,7 @@ class DevView:
     combiner_stats) goes to ctx device `di`."""
 
     _DEV_CALLS = frozenset((
-        "encode_strided_device", "encode_batch_device", "reconstruct_strided_device",
+        "rs_grid", "encode_strided_device", "encode_batch_device", "reconstruct_strided_device",
         "reconstruct_strided_device_async", "reconstruct_batch_device", "reconstruct_batch_device_async",
         "sha256_batch_device", "body_sums_device", "frames_device", "combiner_stats"))
 
@@ -1333,7 +1337,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 5: the RS grid tuner times launches 2-5 of a shape (ops.cpp rs_grid_pick)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="2", choices=["2", "3", "3c", "ns", "4a", "4b", "5", "sums", "frames"])
     ap.add_argument("--workers", type=int, default=8, help="config 3c: concurrent batches")
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
@@ -1413,6 +1418,8 @@ def main() -> int:
     if getattr(w, "wall_timed", False):  # work on the workers' streams, not `stream`
         ms_dev = [elapsed * 1e3 / args.steps] * D
 
+    # The grid the RS grid tuner settled on for the encode shape (0: still tuning).
+    grid_bpc = w.ctx.rs_grid(w.k, w.m, w.S) if isinstance(w, Encode) else None
     payload_local = float(sum(l[0].payload for l in lanes))
     value = reduce_sum(payload_local) * args.steps / GIB / elapsed  # weak scaling: every GPU of every rank
     per_dev = [{"gpu": plan.torch_devs[i] if plan.mode != "logical" else f"logical {i} of card 0",
@@ -1486,9 +1493,8 @@ def main() -> int:
                              f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={nc})"}
 
     if rank == 0:
-        tag = {"2": ("k4m2", rs_blocks_per_cu(2)), "ns": ("k8m4", rs_blocks_per_cu(4)),
-               "4a": ("k10m4", rs_blocks_per_cu(4)), "sums": ("crc_tiles", None),
-               "frames": ("gcm_frames", None)}.get(args.config)
+        tag = {"2": ("k4m2", grid_bpc), "ns": ("k8m4", grid_bpc), "4a": ("k10m4", grid_bpc),
+               "sums": ("crc_tiles", None), "frames": ("gcm_frames", None)}.get(args.config)
         if mixed_batch:
             tag = ("cfg5_grouped", RS_GROUP_BLOCKS_PER_CU)
         traffic, tsrc = pmc_traffic(tag[0], alg_bytes, tag[1]) if tag else (None, None)
@@ -1531,6 +1537,7 @@ def main() -> int:
                 "bytes_per_launch": float(alg_bytes),
                 "ms_per_launch": round(ms_launch, 4),
                 "traffic_source": tsrc,
+                "blocks_per_cu": grid_bpc,
                 "box_stream": box_key if copy_peak else None,
                 "box_stream_GBps": round(copy_peak, 1) if copy_peak else None,
                 "frac_of_box_stream": round(achieved / copy_peak, 4) if copy_peak else None,

@@ -103,6 +103,13 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
  * the device's combiner (concurrent small requests share one launch) and the
  * messages they hashed. */
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages);
+/* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
+ * (k inputs, m outputs, shard_size) at: the grid tuner times the first
+ * launches of a shape at two grid sizes and keeps the faster one (which of
+ * them wins depends on the box and on where the batch sits in HBM).  0 while
+ * the shape is still being tuned; the default grid for shapes never launched
+ * or too small to tune.  Diagnostics (the bench reports it). */
+int mxec_ctx_rs_grid(mxec_ctx* ctx, int dev, int k, int m, uint64_t shard_size);
 /* Page-locked host memory for request bodies and GET buffers (the Axum body
  * MaxIO hands to a PUT, the buffer a GET fills).  Every host-pointer entry
  * point accepts any host memory; when a buffer comes from here, its bytes

@@ -207,6 +207,7 @@ void mxec_close(mxec_ctx* ctx) {
     for (auto& d : ctx->c.devs) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
+        rs_grid_release(*d);
         for (auto& s : d->slots) slot_destroy(*s);
     }
     delete ctx;
@@ -224,6 +225,12 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
         return set_error(MXEC_E_INVALID_ARG, "invalid argument");
     combiner_stats(*ctx->c.devs[size_t(i)], launches, messages);
     return MXEC_OK;
+}
+
+int mxec_ctx_rs_grid(mxec_ctx* ctx, int dev, int k, int m, uint64_t shard_size) {
+    if (!ctx || dev < 0 || dev >= int(ctx->c.devs.size()) || k < 1 || m < 1)
+        return set_error(MXEC_E_INVALID_ARG, "invalid argument");
+    return guarded([&] { return rs_grid_in_use(*ctx->c.devs[size_t(dev)], k, m, shard_size); });
 }
 
 void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes) {

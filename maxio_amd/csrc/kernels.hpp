@@ -48,6 +48,9 @@ struct RsArgs {
     // out_ptrs / out_len [o * kMultiR, o * kMultiR + r), its coefficient
     // table rows r apart.  r, r_total and row0 above are unused.
     uint32_t multi = 0;
+    // Uniform launches: workgroups per CU chosen by the caller (the grid
+    // tuner, ops.cpp); 0 = rs_default_variant's.
+    uint32_t blocks_per_cu = 0;
 };
 constexpr uint32_t kMultiR = 4;
 

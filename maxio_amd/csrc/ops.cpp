@@ -159,12 +159,122 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     a.k = uint32_t(k);
     a.r_total = uint32_t(r);
     a.aligned = aligned ? 1u : 0u;
+    // Large aligned single-launch batches take the grid tuner's pick.
+    GridTuner::Trial trial;
+    const double gb = double(n) * double(k + r) * double(shard_size) / 1e9;
+    if (aligned && r <= 4) MXEC_TRY(rs_grid_pick(dev, k, r, shard_size, gb, &a.blocks_per_cu, &trial));
+    if (trial.a) MXEC_HIP(hipEventRecord(trial.a, s));
     for (int row0 = 0; row0 < r; row0 += 8) {
         a.row0 = uint32_t(row0);
         a.r = uint32_t(std::min(8, r - row0));
         MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
     }
+    if (trial.a) {
+        MXEC_HIP(hipEventRecord(trial.b, s));
+        rs_grid_record(dev, k, r, shard_size, trial);
+    }
     return w.finish(s);
+}
+
+namespace {
+// Tuning pays only where a launch is long enough for the grid to matter
+// and an event pair costs nothing next to it.
+constexpr double kTuneMinGB = 1.0;
+
+bool tuning_on() {
+    const char* e = getenv("MXEC_RS_TUNE");
+    if (e && !strcmp(e, "0")) return false;
+    return getenv("MXEC_RS_BPC") == nullptr;  // a lab override fixes the grid
+}
+
+// Reads every finished trial of a shape into its best times; decides once
+// both candidates have two samples (launches 2-5 of the shape alternate the
+// two grids; the sixth waits for them if they are still running).
+void tuner_poll(GridTuner::State& st) {
+    for (size_t i = 0; i < st.pending.size();) {
+        GridTuner::Trial& t = st.pending[i];
+        if (hipEventQuery(t.b) != hipSuccess) {
+            (void)hipGetLastError();
+            ++i;
+            continue;
+        }
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess && t.gb > 0) {
+            st.best_ms_per_gb[t.cand] = std::min(st.best_ms_per_gb[t.cand], double(ms) / t.gb);
+            ++st.samples[t.cand];
+        }
+        (void)hipGetLastError();
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+        st.pending.erase(st.pending.begin() + long(i));
+    }
+    if (st.decided < 0 && st.samples[0] >= 2 && st.samples[1] >= 2)
+        st.decided = st.best_ms_per_gb[1] < st.best_ms_per_gb[0] ? 1 : 0;
+}
+}  // namespace
+
+int rs_grid_pick(Device& dev, int k, int r, uint64_t shard_size, double gb, uint32_t* bpc,
+                 GridTuner::Trial* trial) {
+    *bpc = 0;
+    if (!tuning_on() || gb < kTuneMinGB) return MXEC_OK;
+    std::lock_guard<std::mutex> g(dev.tuner.mu);
+    GridTuner::State& st = dev.tuner.states[std::make_tuple(k, r, shard_size)];
+    if (!st.cands[0]) {
+        st.cands[0] = rs_default_variant(uint32_t(r)).blocks_per_cu;
+        st.cands[1] = st.cands[0] / 2;  // r <= 2: 1024 / 512; r = 3, 4: 512 / 256
+    }
+    tuner_poll(st);
+    if (st.decided < 0 && st.launches >= 5) {
+        // Launches 2-5 were the trials (two per grid): wait for them once,
+        // so a caller that queues far ahead still gets the decision now.
+        for (auto& t : st.pending) (void)hipEventSynchronize(t.b);
+        tuner_poll(st);
+        if (st.decided < 0) st.decided = st.best_ms_per_gb[1] < st.best_ms_per_gb[0] ? 1 : 0;
+    }
+    if (st.decided >= 0) {
+        *bpc = uint32_t(st.cands[st.decided]);
+        return MXEC_OK;
+    }
+    const int l = st.launches++;
+    if (l == 0) return MXEC_OK;  // first launch of a shape: cold, untimed
+    trial->cand = (l - 1) & 1;
+    trial->gb = gb;
+    MXEC_HIP(hipEventCreate(&trial->a));
+    if (hipEventCreate(&trial->b) != hipSuccess) {
+        (void)hipEventDestroy(trial->a);
+        trial->a = nullptr;
+        return set_error(MXEC_E_DEVICE, "hipEventCreate failed");
+    }
+    *bpc = uint32_t(st.cands[trial->cand]);
+    return MXEC_OK;
+}
+
+void rs_grid_record(Device& dev, int k, int r, uint64_t shard_size, const GridTuner::Trial& trial) {
+    std::lock_guard<std::mutex> g(dev.tuner.mu);
+    dev.tuner.states[std::make_tuple(k, r, shard_size)].pending.push_back(trial);
+}
+
+int rs_grid_in_use(Device& dev, int k, int r, uint64_t shard_size) {
+    const int def = rs_default_variant(uint32_t(r)).blocks_per_cu;
+    if (const char* e = getenv("MXEC_RS_BPC")) {
+        const int b = atoi(e);
+        if (b > 0 && b <= 4096) return b;
+    }
+    std::lock_guard<std::mutex> g(dev.tuner.mu);
+    auto it = dev.tuner.states.find(std::make_tuple(k, r, shard_size));
+    if (it == dev.tuner.states.end()) return def;
+    tuner_poll(it->second);
+    return it->second.decided >= 0 ? it->second.cands[it->second.decided] : 0;
+}
+
+void rs_grid_release(Device& dev) {
+    std::lock_guard<std::mutex> g(dev.tuner.mu);
+    for (auto& kv : dev.tuner.states)
+        for (auto& t : kv.second.pending) {
+            (void)hipEventDestroy(t.a);
+            (void)hipEventDestroy(t.b);
+        }
+    dev.tuner.states.clear();
 }
 
 int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups,

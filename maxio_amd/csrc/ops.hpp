@@ -31,6 +31,18 @@ struct RsObject {
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
            const std::vector<RsObject>& objs, DescArena* arena = nullptr);
 
+// Grid tuner of large uniform RS launches (runtime.hpp GridTuner):
+// rs_grid_pick sets *bpc (0 = the default grid) and, while a shape is still
+// being tuned, hands back a trial whose events the caller records around
+// the launch and passes to rs_grid_record.  rs_grid_in_use: the workgroups
+// per CU a shape runs at now (0 while undecided).  MXEC_RS_TUNE=0 disables,
+// MXEC_RS_BPC fixes the grid.
+int rs_grid_pick(Device& dev, int k, int r, uint64_t shard_size, double gb, uint32_t* bpc,
+                 GridTuner::Trial* trial);
+void rs_grid_record(Device& dev, int k, int r, uint64_t shard_size, const GridTuner::Trial& trial);
+int rs_grid_in_use(Device& dev, int k, int r, uint64_t shard_size);
+void rs_grid_release(Device& dev);
+
 // An object of a mixed batch: its own k and shard size.
 struct RsMixedObject {
     int k;

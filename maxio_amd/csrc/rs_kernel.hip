@@ -618,7 +618,9 @@ hipError_t launch_rs_apply(const RsArgs& a, int n_cus, hipStream_t s) {
             default: return hipErrorInvalidValue;
         }
     }
-    return launch_rs_apply_variant(a, n_cus, s, rs_default_variant(a.r_total));
+    RsVariant v = rs_default_variant(a.r_total);
+    if (a.blocks_per_cu) v.blocks_per_cu = int(a.blocks_per_cu);
+    return launch_rs_apply_variant(a, n_cus, s, v);
 }
 
 }  // namespace mxec

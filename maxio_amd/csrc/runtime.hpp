@@ -153,9 +153,35 @@ void pinned_unregister(const void* p);
 // True when every byte of [p, p + len) is page-locked host memory.
 bool pinned_range(const void* p, uint64_t len);
 
+// Online choice between two grid sizes for the large uniform RS launches
+// of one shape (ops.cpp rs_grid_pick): which of them runs faster depends on
+// the box and on where the batch sits in HBM (profiles/r3/grid_ab/: 512
+// workgroups per CU 3.6 % ahead of 1024 on one box, 0.8 % behind on
+// another), so the first launches of a shape alternate between the two,
+// timed with events on the caller's stream, and the faster one is kept for
+// the context's life.
+struct GridTuner {
+    struct Trial {
+        hipEvent_t a = nullptr, b = nullptr;
+        int cand = 0;
+        double gb = 0;  // bytes of the launch, in GB
+    };
+    struct State {
+        int cands[2] = {0, 0};
+        int launches = 0;
+        int samples[2] = {0, 0};
+        double best_ms_per_gb[2] = {1e30, 1e30};
+        int decided = -1;
+        std::vector<Trial> pending;
+    };
+    std::mutex mu;
+    std::map<std::tuple<int, int, uint64_t>, State> states;  // (k, r, shard_size)
+};
+
 struct Device {
     int id = 0;
     int n_cus = 256;
+    GridTuner tuner;
     std::vector<std::unique_ptr<Slot>> slots;
     std::atomic<unsigned> next_slot{0};
     // Coefficient tables (gf256.hpp coef_tables) for every matrix in use,

@@ -172,6 +172,14 @@ class Context:
         _check(self._lib.mxec_ctx_combiner_stats(self._h, dev, ctypes.byref(b), ctypes.byref(m)))
         return {"batches": b.value, "messages": m.value}
 
+    def rs_grid(self, k: int, m: int, shard_size: int, dev: int = 0) -> int:
+        """Workgroups per CU large uniform RS launches of this shape run at on
+        device `dev` (the grid tuner's pick; 0 while still tuning)."""
+        rc = self._lib.mxec_ctx_rs_grid(self._h, dev, k, m, shard_size)
+        if rc < 0:
+            _check(rc)
+        return rc
+
     def host_array(self, n: int) -> np.ndarray:
         """A uint8 array of n bytes in page-locked memory (mxec_host_alloc):
         uploads from it and downloads into it skip the staging copy.  The

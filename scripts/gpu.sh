@@ -63,22 +63,32 @@ for st in "${STEPS[@]}"; do
       find /tmp/prof -name "*kernel_trace.csv" -exec cp {} "$O/kernel_trace.csv" \;
       cat "$O/prof_bench.json" ;;
     pmc)
-      for cfg in 2 ns; do
+      # each (config, grid) with the grid fixed (MXEC_RS_BPC also turns the
+      # grid tuner off), counters only on rs_apply_fast, one run per counter
+      for cb in 2:1024 2:512 ns:512 ns:256; do
+        cfg=${cb%%:*}; bpc=${cb##*:}
         for c in FETCH_SIZE WRITE_SIZE; do
-          ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast -d "/tmp/pmc/${cfg}_$c" \
-              -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 2 --warmup 1 --cpu-seconds 0 \
-              --no-extra --no-e2e > "$O/pmc_${cfg}_$c.log" 2>&1 ) || { tail -5 "$O/pmc_${cfg}_$c.log"; exit 1; }
-          find "/tmp/pmc/${cfg}_$c" -name "*counter_collection.csv" -exec cp {} "$O/pmc_${cfg}_$c.csv" \;
+          ( cd /tmp && MXEC_RS_BPC=$bpc timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast \
+              -d "/tmp/pmc/${cfg}_${bpc}_$c" -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 2 \
+              --warmup 1 --cpu-seconds 0 --no-extra --no-e2e > "$O/pmc_${cfg}_${bpc}_$c.log" 2>&1 ) \
+              || { tail -5 "$O/pmc_${cfg}_${bpc}_$c.log"; exit 1; }
+          find "/tmp/pmc/${cfg}_${bpc}_$c" -name "*counter_collection.csv" -exec cp {} "$O/pmc_${cfg}_${bpc}_$c.csv" \;
         done
       done
-      # configs[1]: 1024 x 4+2 x 10 MiB, 655 360 tiles of 16 KiB, 1024 WG/CU;
-      # north star: 4096 x 8+4 x 1 MiB, 262 144 tiles, 512 WG/CU.
-      python tools/pmc_summary.py "$O/pmc_2_FETCH_SIZE.csv" "$O/pmc_2_WRITE_SIZE.csv" "rs_apply_fast<2, 4, true, false" \
-        64424509440 --blocks-per-cu 1024 --tiles 655360 --what "config 2, rs_apply_fast<2,4,nt> at 1024 WG/CU" \
-        --out "$O/pmc_k4m2_traffic.json" || exit 1
-      python tools/pmc_summary.py "$O/pmc_ns_FETCH_SIZE.csv" "$O/pmc_ns_WRITE_SIZE.csv" "rs_apply_fast<4, 4, true, false" \
-        51539607552 --blocks-per-cu 512 --tiles 262144 --what "north star, rs_apply_fast<4,4,nt> at 512 WG/CU" \
-        --out "$O/pmc_k8m4_traffic.json" || exit 1 ;;
+      # configs[1]: 1024 x 4+2 x 10 MiB = 655 360 tiles of 16 KiB;
+      # north star: 4096 x 8+4 x 1 MiB = 262 144 tiles.
+      for cb in 2:1024 2:512; do
+        bpc=${cb##*:}
+        python tools/pmc_summary.py "$O/pmc_2_${bpc}_FETCH_SIZE.csv" "$O/pmc_2_${bpc}_WRITE_SIZE.csv" \
+          "rs_apply_fast<2, 4, true, false" 64424509440 --blocks-per-cu $bpc --tiles 655360 \
+          --what "config 2, rs_apply_fast<2,4,nt> at $bpc WG/CU" --out "$O/pmc_k4m2_bpc${bpc}_traffic.json" || exit 1
+      done
+      for cb in ns:512 ns:256; do
+        bpc=${cb##*:}
+        python tools/pmc_summary.py "$O/pmc_ns_${bpc}_FETCH_SIZE.csv" "$O/pmc_ns_${bpc}_WRITE_SIZE.csv" \
+          "rs_apply_fast<4, 4, true, false" 51539607552 --blocks-per-cu $bpc --tiles 262144 \
+          --what "north star, rs_apply_fast<4,4,nt> at $bpc WG/CU" --out "$O/pmc_k8m4_bpc${bpc}_traffic.json" || exit 1
+      done ;;
     rust)
       { command -v rustc; command -v cargo; rustc --version; cargo --version; } > "$O/rust_probe.txt" 2>&1 || true
       cat "$O/rust_probe.txt" ;;

@@ -604,3 +604,33 @@ def test_put_data_chunk_write_error_wins(ctx, tmp_path):
     ok = tmp_path / "ok.ec"
     ctx.put_object_chunked(str(ok), 4096, 2, body)
     assert ctx.get_object_chunked(str(ok)) == body.tobytes()
+
+
+def test_grid_tuner_decides_and_stays_exact():
+    """The RS grid tuner (ops.cpp rs_grid_pick): launches 2-5 of a large
+    uniform shape alternate two grid sizes, the sixth keeps the faster; every
+    launch's parity is bit-exact (the grid never changes the bytes).  A fresh
+    context so the shape's tuning starts here."""
+    torch = _torch()
+    import maxio_amd
+
+    k, m, s, n = 4, 2, 1 << 20, 180  # 1.13 GB per launch (tuning starts at 1 GB)
+    with maxio_amd.Context(device_mask=1, streams_per_device=1) as c:
+        g = torch.Generator(device="cuda").manual_seed(9)
+        obj = torch.randint(0, 256, (n, k + m, s), dtype=torch.uint8, device="cuda", generator=g)
+        torch.cuda.synchronize()
+        assert c.rs_grid(k, m, s) == 1024  # never launched: the default
+        ref = None
+        for it in range(8):
+            obj[:, k:].zero_()
+            torch.cuda.synchronize()
+            c.encode_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s, obj[:, k:].data_ptr(), (k + m) * s, s)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = obj[:, k:].clone()
+                h = obj[0].cpu().numpy()
+                want = oracle.encode(list(h[:k]), m, s)
+                assert all(np.array_equal(h[k + i], want[i]) for i in range(m))
+            else:
+                assert torch.equal(obj[:, k:], ref), it
+        assert c.rs_grid(k, m, s) in (1024, 512)
