@@ -306,10 +306,10 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // (Stopping at the stream form's size instead split config 3c's
         // eight batches into launches of five and three: 585 vs 970 GiB/s.)
         // For such long launches the idle window grows to 2 % of the launch
-        // (590 us for 1 MiB chunks) and the whole gather may run to 8 % of
-        // it (2.4 ms) while arrivals keep coming: a 2 ms cap sometimes split
-        // a config-3c step's eight arrivals into two launches, doubling that
-        // step (831 vs 1 040 GiB/s).  A lone request never waits for this
+        // (590 us for 1 MiB chunks) and the whole gather may run to 15 % of
+        // it (4.4 ms) while arrivals keep coming: a 2 ms cap (and then 8 %)
+        // sometimes split a config-3c step's eight arrivals into two
+        // launches, doubling that step (831 / 942 vs 1 040 GiB/s).  A lone request never waits for this
         // part: it only continues while requests keep arriving.
         auto launch_us = [&] {
             uint64_t longest = 0;
@@ -318,7 +318,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         };
         const double est_us = c->pending.size() >= 2 ? launch_us() : 0.0;
         if (c->pending.size() >= 2 && est_us * 0.02 >= double(gather_idle_us())) {
-            const auto hard = t0 + std::chrono::microseconds(std::max<long>(gather_max_us(), long(est_us * 0.08)));
+            const auto hard = t0 + std::chrono::microseconds(std::max<long>(gather_max_us(), long(est_us * 0.15)));
             const long idle = std::max<long>(gather_idle_us(), long(est_us * 0.02));
             for (size_t seen = c->pending.size(); std::chrono::steady_clock::now() < hard;) {
                 c->cv_gather.wait_for(lk, std::chrono::microseconds(idle),
