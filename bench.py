@@ -996,7 +996,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     # -- config 3c: 8 concurrent batches -----------------------------------
     rs = ReconstructStream(torch, ctx, dev, sh, 1024, 8, SEED)
     torch.cuda.synchronize()
-    for _ in range(2):  # the first steps gather and place unevenly
+    for _ in range(4):  # the first steps gather and place unevenly (the combiner adapts to 8 callers)
         rs.step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -218,7 +218,10 @@ int rs_grid_pick(Device& dev, int k, int r, uint64_t shard_size, double gb, uint
     *bpc = 0;
     if (!tuning_on() || gb < kTuneMinGB) return MXEC_OK;
     std::lock_guard<std::mutex> g(dev.tuner.mu);
-    GridTuner::State& st = dev.tuner.states[std::make_tuple(k, r, shard_size)];
+    const auto key = std::make_tuple(k, r, shard_size);
+    // A server sees a handful of shapes; past 256 new ones keep the default.
+    if (dev.tuner.states.size() >= 256 && !dev.tuner.states.count(key)) return MXEC_OK;
+    GridTuner::State& st = dev.tuner.states[key];
     if (!st.cands[0]) {
         st.cands[0] = rs_default_variant(uint32_t(r)).blocks_per_cu;
         st.cands[1] = st.cands[0] / 2;  // r <= 2: 1024 / 512; r = 3, 4: 512 / 256
