@@ -61,6 +61,7 @@ struct RsVariant {
     int blocks_per_cu = 8;  // grid = n_cus * blocks_per_cu (grid-stride)
     int min_waves = 0;      // 3: compile for >= 3 waves per SIMD (<= 168 VGPRs; V = 4, nt)
     bool load_nt = true;    // with nt: false = plain loads, nontemporal stores (V = 4, R <= 4; lab)
+    bool store_nt = true;   // with nt: false = nontemporal loads, plain stores (V = 4, R <= 4; lab)
 };
 
 // Uniform launches, or grouped ones (a.tiles set: rs_group_variant, aligned).

@@ -505,6 +505,8 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
             e = launch_fast<R, 4, true, false, R == 4 ? 3 : 1>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (R <= 4 && var.vecs == 4 && var.nt && !var.load_nt)  // lab: plain loads, nontemporal stores
             e = launch_fast<R, 4, true, false, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (R <= 4 && var.vecs == 4 && var.nt && !var.store_nt)  // lab: nontemporal loads, plain stores
+            e = launch_fast<R, 4, false, false, 1, true>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                            : launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
         return e;
@@ -551,6 +553,9 @@ RsVariant rs_default_variant(uint32_t r_total) {
     // MXEC_RS_LOAD_NT=0 (lab, read per launch): plain loads with the
     // nontemporal stores, R <= 4.
     if (const char* e = getenv("MXEC_RS_LOAD_NT")) v.load_nt = std::strcmp(e, "0") != 0;
+    // MXEC_RS_STORE_NT=0 (lab, read per launch): plain stores with the
+    // nontemporal loads, R <= 4.
+    if (const char* e = getenv("MXEC_RS_STORE_NT")) v.store_nt = std::strcmp(e, "0") != 0;
     // R <= 2 (config 2, two-erasure decodes) gained another 0-2 % at 1024 in
     // every layout swept; R = 4 went either way (profiles/r2_lab_rs_grid_*).
     v.blocks_per_cu = r_total <= 2 ? 1024 : 512;
