@@ -62,6 +62,7 @@ struct RsVariant {
     int min_waves = 0;      // 3: compile for >= 3 waves per SIMD (<= 168 VGPRs; V = 4, nt)
     bool load_nt = true;    // with nt: false = plain loads, nontemporal stores (V = 4, R <= 4; lab)
     bool store_nt = true;   // with nt: false = nontemporal loads, plain stores (V = 4, R <= 4; lab)
+    int group = 4;          // inputs loaded per step; 8 with V = 2, R = 3..4 (lab)
 };
 
 // Uniform launches, or grouped ones (a.tiles set: rs_group_variant, aligned).

@@ -287,7 +287,7 @@ __device__ __forceinline__ Vec4 gload16_upto(gcptr p, int32_t valid, gcptr safe)
 // k inputs and lengths; op / ol: its R outputs and lengths; tab: its
 // coefficient table at the first output row, input j's rows `stride` x 8
 // dwords apart.
-template <int R, int V, bool NT, bool LNT = NT>
+template <int R, int V, bool NT, bool LNT = NT, int G = 4>
 __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, const uint64_t* __restrict__ il,
                                         uint8_t* const* __restrict__ op, const uint64_t* __restrict__ ol,
                                         const uint32_t* __restrict__ tab, uint32_t k, uint32_t stride,
@@ -324,6 +324,37 @@ __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, c
     };
 
     uint32_t j = 0;
+    if constexpr (G == 8) {
+        // Eight inputs' loads in flight per step (the lab's G = 8 form: with
+        // V = 2 the same bytes in flight per lane as V = 4 x 4 inputs, half
+        // the accumulators, so more waves fit).
+        for (; j + 8 <= k; j += 8) {
+            Vec4 x[8][V];
+            bool full = true;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) full = full && il[j + jj] >= end;
+            if (full) {
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                    gcptr p = ((gcptr)(ip[j + jj])) + lane;
+#pragma unroll
+                    for (int v = 0; v < V; ++v) x[jj][v] = gload16<LNT>(p + v * kThreads * 16);
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) load_in(j + jj, x[jj]);
+            }
+            if constexpr (R >= 3) {
+#pragma unroll
+                for (int jj = 0; jj < 8; jj += 2)
+                    mac_column_pair<R, V>(acc, x[jj], x[jj + 1], tab + (j + jj) * stride * 8,
+                                          tab + (j + jj + 1) * stride * 8);
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) mac_column<R, V>(acc, x[jj], tab + (j + jj) * stride * 8);
+            }
+        }
+    }
     for (; j + 4 <= k; j += 4) {
         Vec4 x[4][V];
         // Wave-uniform: all four inputs reach past this tile (every tile
@@ -388,7 +419,7 @@ __device__ __forceinline__ void rs_tile(const uint8_t* const* __restrict__ ip, c
 // the object), one wave-uniform scalar load, fetched one tile ahead so it
 // is in SGPRs when the tile starts (the uniform kernel computes the same
 // from the tile index).
-template <int R, int V, bool NT, bool GRP, int OCC = 1, bool LNT = NT>
+template <int R, int V, bool NT, bool GRP, int OCC = 1, bool LNT = NT, int G = 4>
 __global__ __launch_bounds__(kThreads, OCC) void rs_apply_fast(
     const uint8_t* const* __restrict__ in_ptrs, uint8_t* const* __restrict__ out_ptrs,
     const uint64_t* __restrict__ in_len, const uint64_t* __restrict__ out_len,
@@ -417,7 +448,7 @@ __global__ __launch_bounds__(kThreads, OCC) void rs_apply_fast(
         }
         // Lengths are clamped to the shard size by the host, so a tile past
         // the shard end is cut by the same tests.
-        rs_tile<R, V, NT, LNT>(in_ptrs + in0, in_len + in0, out_ptrs + uint64_t(obj) * r_total + row0,
+        rs_tile<R, V, NT, LNT, G>(in_ptrs + in0, in_len + in0, out_ptrs + uint64_t(obj) * r_total + row0,
                           out_len + uint64_t(obj) * r_total + row0, coef + coef_off[obj] + row0 * 8, k, r_total,
                           base, safe);
     }
@@ -457,10 +488,10 @@ __global__ __launch_bounds__(kThreads) void rs_apply_multi(
     }
 }
 
-template <int R, int V, bool NT, bool GRP = false, int OCC = 1, bool LNT = NT>
+template <int R, int V, bool NT, bool GRP = false, int OCC = 1, bool LNT = NT, int G = 4>
 hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
-    hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP, OCC, LNT>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
+    hipLaunchKernelGGL((rs_apply_fast<R, V, NT, GRP, OCC, LNT, G>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                        a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.k, a.r_total,
                        a.row0, tiles_per_obj, n_tiles, a.tiles);
     return hipGetLastError();
@@ -499,6 +530,8 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
         hipError_t e = hipErrorInvalidValue;
         if (var.vecs == 1) e = var.nt ? launch_fast<R, 1, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                       : launch_fast<R, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (R >= 3 && R <= 4 && var.vecs == 2 && var.nt && var.group == 8)  // lab: 8-input steps
+            e = launch_fast<R, 2, true, false, 1, true, 8>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (var.vecs == 2) e = var.nt ? launch_fast<R, 2, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                            : launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (R == 4 && var.vecs == 4 && var.nt && var.min_waves == 3)
@@ -553,6 +586,13 @@ RsVariant rs_default_variant(uint32_t r_total) {
     // MXEC_RS_LOAD_NT=0 (lab, read per launch): plain loads with the
     // nontemporal stores, R <= 4.
     if (const char* e = getenv("MXEC_RS_LOAD_NT")) v.load_nt = std::strcmp(e, "0") != 0;
+    // MXEC_RS_G8=1 (lab, read per launch): r = 3, 4 with V = 2 and eight
+    // inputs' loads in flight per step.
+    if (const char* e = getenv("MXEC_RS_G8"))
+        if (!std::strcmp(e, "1") && r_total >= 3 && r_total <= 4) {
+            v.vecs = 2;
+            v.group = 8;
+        }
     // MXEC_RS_STORE_NT=0 (lab, read per launch): plain stores with the
     // nontemporal loads, R <= 4.
     if (const char* e = getenv("MXEC_RS_STORE_NT")) v.store_nt = std::strcmp(e, "0") != 0;
