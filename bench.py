@@ -68,6 +68,10 @@ GIB = float(1 << 30)
 # one-wave form 1410 (64 x 14 rounds + 48 x 10 schedule + 16 byte swaps + 18);
 # stream form 1415 (the one-wave rounds plus the clamped prefetch).
 SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415}
+# The split form's serial wave (the consumer) issues 905 of those per block;
+# a wave issues at most one VALU every 4 cycles, so a lone message's chain
+# cannot beat 905 x 4 cycles per block at the clock the chip holds.
+SHA_SPLIT_CONSUMER_VALU_PER_BLOCK = 905
 # Chip INT32 issue ceiling for those instructions (v_alignbit / v_bitop3 /
 # v_add3 / v_add / v_perm): CUs x 4 SIMDs x lanes per cycle x 2.4 GHz, lanes
 # per cycle measured with tools/valu_lab chip (profiles/r2_lab_valu_chip.jsonl).
@@ -838,6 +842,20 @@ def float4_copy_on_buffers(torch, stream, w):
     return round(2 * half / (ms * 1e-3) / 1e9, 1)
 
 
+def measured_clock(kernel: str, cfg: str):
+    """The shader clock a kernel ran at, from the committed GRBM_GUI_ACTIVE
+    pass (profiles/r*/clock/clock_<cfg>.json, tools/clock_summary.py; newest
+    round first), or (None, None)."""
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "clock", f"clock_{cfg}.json")), reverse=True):
+        try:
+            with open(p) as f:
+                k = json.load(f)["kernels"][kernel]
+            return float(k["clock_GHz_median"]), os.path.relpath(p, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
 def valu_bound_GBps(form: str, n_cus: int) -> float:
     """Hashed-bytes ceiling of the SHA-256 form when every SIMD issues INT32
     VALU at its measured rate: 64 B per block / lane-ops per block."""
@@ -849,6 +867,26 @@ def valu_bound_GBps(form: str, n_cus: int) -> float:
 # rs_apply_fast<2,4,true> retires 2.84e9 wave-instructions x 64 lanes per
 # launch over 42.9 GB of input (profiles/r2_pmc_valu.json).
 RS_R2_VALU_PER_INPUT_BYTE = 4.24
+
+
+def sha_chain_block(form: str, us_per_block: float):
+    """Config 3's binding roofline: the serial chain of one message.  The
+    split form's consumer wave issues SHA_SPLIT_CONSUMER_VALU_PER_BLOCK VALU
+    per block, one per 4 cycles, at the clock the chip held for this kernel
+    (GRBM_GUI_ACTIVE pass) and at the 2.4 GHz maximum."""
+    if form != "split":
+        return None
+    clk, src = measured_clock("sha256_split_kernel", "3")
+    cyc = SHA_SPLIT_CONSUMER_VALU_PER_BLOCK * 4
+    d = {"bound": "valu-chain", "consumer_valu_per_block": SHA_SPLIT_CONSUMER_VALU_PER_BLOCK,
+         "cycles_per_valu": 4, "us_per_block": round(us_per_block, 4),
+         "floor_us_per_block_at_2.4GHz": round(cyc / (CLOCK_GHZ * 1e3), 4),
+         "frac_at_2.4GHz": round(cyc / (CLOCK_GHZ * 1e3) / us_per_block, 4)}
+    if clk:
+        d.update({"clock_GHz_measured": clk, "clock_source": src,
+                  "floor_us_per_block": round(cyc / (clk * 1e3), 4),
+                  "frac": round(cyc / (clk * 1e3) / us_per_block, 4)})
+    return d
 
 
 def stream_step_roofline(ms: float, workers: int, n: int, n_cus: int) -> dict:
@@ -971,7 +1009,8 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                      "ms_per_launch": round(ms_sha, 3), "us_per_block": round(ms_sha * 1e3 / (S / 64), 4),
                      "frac_of_hbm": round(sha_GBps / HBM_PEAK_GBPS, 4),
                      "note": ("10 240 messages fill 160 of 1024 SIMDs: this launch is bound by the serial "
-                              "chain of one 1 MiB message (16 384 blocks), not by chip-wide VALU issue")},
+                              "chain of one 1 MiB message (16 384 blocks), not by chip-wide VALU issue"),
+                     "chain": sha_chain_block(form, ms_sha * 1e3 / (S / 64))},
         "rs_decode": hbm_block(float(n) * (k + 2) * S, ms_rs, "rs_apply_fast<R=2> (decode 8 -> 2, no verify)",
                                cal3, "rs_pattern_same_buffers_GBps"),
     }

@@ -127,12 +127,8 @@ __global__ __launch_bounds__(64) void sha256_kernel(const uint8_t* const* __rest
     SHA_RNDKW(c, d, e, f, g, h, a, b, (v).z);        \
     SHA_RNDKW(b, c, d, e, f, g, h, a, (v).w)
 
-// 64 rounds with K[t] + W[t] precomputed in LDS (kwl[q * 64] = words 4q..4q+3).
-__device__ __forceinline__ void compress_kw(uint32_t (&st)[8], const u32x4* kwl) {
-    // All 16 reads issued up front so their latency overlaps the first rounds.
-    u32x4 v[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = kwl[q * 64];
+// 64 rounds with K[t] + W[t] already in registers (v[q] = words 4q..4q+3).
+__device__ __forceinline__ void compress_regs(uint32_t (&st)[8], const u32x4 (&v)[16]) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
     uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
@@ -142,6 +138,20 @@ __device__ __forceinline__ void compress_kw(uint32_t (&st)[8], const u32x4* kwl)
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// The K + W of one block from LDS (kwl[q * 64] = words 4q..4q+3).
+__device__ __forceinline__ void load_kw(const u32x4* kwl, u32x4 (&v)[16]) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = kwl[q * 64];
+}
+
+// 64 rounds reading K + W from LDS: all 16 reads issued up front so their
+// latency overlaps the first rounds.
+__device__ __forceinline__ void compress_kw(uint32_t (&st)[8], const u32x4* kwl) {
+    u32x4 v[16];
+    load_kw(kwl, v);
+    compress_regs(st, v);
 }
 
 __constant__ uint32_t kK256[64] = {
@@ -190,14 +200,23 @@ __device__ __forceinline__ void message_words(const uint8_t* p, bool aligned, ui
 constexpr int kShaPrefetch = 4;
 __device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
+// NB = 3 (default): the producer runs two blocks ahead, so the consumer
+// issues block b+1's 16 LDS reads right after the barrier that opens block b
+// and runs block b's rounds from registers: no read latency at the top of a
+// block and one wait per block instead of one per four rounds.  NB = 2 is
+// the earlier one-ahead form (MXEC_SHA_SPLIT_BUFS=2, lab).  Buffer of block
+// b: b % NB; 16 KiB each.
+template <int NB>
 __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const* __restrict__ ptrs,
                                                            const uint64_t* __restrict__ lens,
                                                            uint8_t* __restrict__ digests,
                                                            const uint8_t* __restrict__ expected,
                                                            const uint64_t* __restrict__ exp_idx,
                                                            uint8_t* __restrict__ ok, uint32_t n, uint32_t prio) {
+    static_assert(NB == 2 || NB == 3, "two or three K+W buffers");
+    constexpr int AHEAD = NB - 1;  // blocks the producer runs ahead of the consumer
     sha_priority(prio);
-    __shared__ u32x4 kw[2][16][64];
+    __shared__ u32x4 kw[NB][16][64];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * 64 + lane;
     const bool live = i < n;
@@ -220,13 +239,38 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
     uint32_t w[16];
     uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                       0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    // The two roles run separate loops with one barrier per block each (the
-    // trip counts match, so the barriers pair up).
+    // The two roles run separate loops with one barrier per block each plus
+    // one before the first (the trip counts match, so the barriers pair up).
     if (wave == 0) {
         __syncthreads();
-        for (uint64_t b = 0; b < nmax; ++b) {
-            if (b < nfull) compress_kw(st, &kw[b & 1][0][lane]);
-            __syncthreads();
+        if constexpr (NB == 2) {
+            for (uint64_t b = 0; b < nmax; ++b) {
+                if (b < nfull) compress_kw(st, &kw[b & 1][0][lane]);
+                __syncthreads();
+            }
+        } else {
+            // Blocks 0 and 1 were written before the first barrier; block
+            // b+1 before the barrier that opens block b.  Two register sets
+            // swap roles every block (the loop is unrolled by two), and the
+            // reads of a block past the last land in registers nobody uses.
+            u32x4 cur[16], nxt[16];
+            load_kw(&kw[0][0][lane], cur);
+            // Retire these reads here: otherwise the loop's first wait, sized
+            // for 32 reads in flight on entry, also stalls every later block
+            // on its just-issued prefetch (lgkmcnt counts to 15).
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            uint32_t rb = 1;  // buffer of the block after the current one
+            for (uint64_t b = 0; b < nmax; b += 2) {
+                load_kw(&kw[rb][0][lane], nxt);
+                if (b < nfull) compress_regs(st, cur);
+                __syncthreads();
+                rb = rb == 2 ? 0 : rb + 1;
+                if (b + 1 >= nmax) break;
+                load_kw(&kw[rb][0][lane], cur);
+                if (b + 1 < nfull) compress_regs(st, nxt);
+                __syncthreads();
+                rb = rb == 2 ? 0 : rb + 1;
+            }
         }
     } else if (__all(!live || nfull == 0 || aligned)) {
         // Producer, every message 16-byte aligned: the raw bytes of the next
@@ -240,7 +284,8 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
         // their last block re-read it, lanes without one read a donor lane's
         // -- because a load under a branch makes the compiler's wait before
         // the next use drain every load in flight (it cannot count the ones
-        // that may have been skipped).
+        // that may have been skipped).  Blocks at or past nmax are scheduled
+        // into buffers nobody reads as a real block.
         const uint64_t donor_mask = __ballot(nfull == nmax);
         const int donor = __ffsll((unsigned long long)donor_mask) - 1;
         const uint8_t* dp = reinterpret_cast<const uint8_t*>(
@@ -250,28 +295,33 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
         const uint64_t last = (own ? nfull : nmax) - 1;  // nmax > 0 when the loop runs
         u32x4 ring[kShaPrefetch][4];
         if (nmax > 0) {
-            u32x4 blk[4];
-            load_block(ps, blk);
+            u32x4 blk[AHEAD][4];
 #pragma unroll
-            for (int j = 0; j < kShaPrefetch; ++j) load_block(ps + 64 * min_u64(j + 1, last), ring[j]);
-            block_words(blk, w);
-            schedule_kw(w, &kw[0][0][lane]);
+            for (int j = 0; j < AHEAD; ++j) load_block(ps + 64 * min_u64(j, last), blk[j]);
+#pragma unroll
+            for (int j = 0; j < kShaPrefetch; ++j) load_block(ps + 64 * min_u64(j + AHEAD, last), ring[j]);
+#pragma unroll
+            for (int j = 0; j < AHEAD; ++j) {
+                block_words(blk[j], w);
+                schedule_kw(w, &kw[j][0][lane]);
+            }
         }
         __syncthreads();
         // Whole groups of kShaPrefetch steps, then the rest: an exit in the
         // middle of a group would join the loop's back edge with fewer loads
         // issued, and the waits at the top would drain the ring again.
+        uint32_t wb = AHEAD % NB;  // buffer of block b + AHEAD
         uint64_t b0 = 0;
         for (; b0 + kShaPrefetch <= nmax; b0 += kShaPrefetch) {
 #pragma unroll
             for (int j = 0; j < kShaPrefetch; ++j) {
                 const uint64_t b = b0 + j;
-                // ring[j] holds block b + 1 (or a clamped re-read nobody
-                // consumes: lanes compress only blocks below their nfull, and
-                // kw[nmax & 1] is never read).
+                // ring[j] holds block b + AHEAD (or a clamped re-read nobody
+                // consumes: lanes compress only blocks below their nfull).
                 block_words(ring[j], w);
-                load_block(ps + 64 * min_u64(b + 1 + kShaPrefetch, last), ring[j]);
-                schedule_kw(w, &kw[(b + 1) & 1][0][lane]);
+                load_block(ps + 64 * min_u64(b + AHEAD + kShaPrefetch, last), ring[j]);
+                schedule_kw(w, &kw[wb][0][lane]);
+                wb = wb + 1 == NB ? 0 : wb + 1;
                 __syncthreads();
             }
         }
@@ -279,23 +329,28 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
         for (int j = 0; j < kShaPrefetch - 1; ++j) {  // the ring already holds these blocks
             if (b0 + j < nmax) {
                 block_words(ring[j], w);
-                schedule_kw(w, &kw[(b0 + j + 1) & 1][0][lane]);
+                schedule_kw(w, &kw[wb][0][lane]);
+                wb = wb + 1 == NB ? 0 : wb + 1;
                 __syncthreads();
             }
         }
     } else {
         // Producer with an unaligned message in the wave: byte loads, one
         // block at a time.
-        if (nfull > 0) {
-            message_words(p, aligned, w);
-            schedule_kw(w, &kw[0][0][lane]);
-        }
-        __syncthreads();
-        for (uint64_t b = 0; b < nmax; ++b) {
-            if (b + 1 < nfull) {
-                message_words(p + 64 * (b + 1), aligned, w);
-                schedule_kw(w, &kw[(b + 1) & 1][0][lane]);
+#pragma unroll
+        for (int j = 0; j < AHEAD; ++j)
+            if (uint64_t(j) < nfull) {
+                message_words(p + 64 * j, aligned, w);
+                schedule_kw(w, &kw[j][0][lane]);
             }
+        __syncthreads();
+        uint32_t wb = AHEAD % NB;
+        for (uint64_t b = 0; b < nmax; ++b) {
+            if (b + AHEAD < nfull) {
+                message_words(p + 64 * (b + AHEAD), aligned, w);
+                schedule_kw(w, &kw[wb][0][lane]);
+            }
+            wb = wb + 1 == NB ? 0 : wb + 1;
             __syncthreads();
         }
     }
@@ -527,6 +582,13 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* const
 // profiles/r2_sha_stream_lab_sizes.jsonl).
 constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 
+// MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read
+// per launch), default 3.
+int split_bufs() {
+    const char* e = getenv("MXEC_SHA_SPLIT_BUFS");
+    return e && atoi(e) == 2 ? 2 : 3;
+}
+
 // MXEC_SHA_PRIO=0..3 (lab A/B; read per launch), default 3.
 uint32_t sha_prio() {
     const char* e = getenv("MXEC_SHA_PRIO");
@@ -552,8 +614,11 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const bool split = form == 2;
-    if (split)
-        hipLaunchKernelGGL(sha256_split_kernel, dim3(blocks), dim3(128), 0, s, a.ptrs, a.lens,
+    if (split && split_bufs() == 2)
+        hipLaunchKernelGGL(sha256_split_kernel<2>, dim3(blocks), dim3(128), 0, s, a.ptrs, a.lens,
+                           a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
+    else if (split)
+        hipLaunchKernelGGL(sha256_split_kernel<3>, dim3(blocks), dim3(128), 0, s, a.ptrs, a.lens,
                            a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
     else
         hipLaunchKernelGGL(sha256_kernel, dim3(blocks), dim3(64), 0, s, a.ptrs, a.lens, a.digests,

@@ -16,6 +16,9 @@
 #   prof      rocprofv3 --kernel-trace --stats of the default bench command
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (one run each) of rs_apply_fast
 #             for configs 2 and ns, summarised with the grid they ran at
+#   clock     GRBM_GUI_ACTIVE / GRBM_COUNT pass (one run per config) of configs
+#             3 (SHA-256 split form + decode) and 2 / ns (RS encode):
+#             effective clock per kernel (tools/clock_summary.py)
 #   rust      probe for rustc / cargo
 #   cfg:<c>   python bench.py --config <c> --no-extra -> cfg_<c>.json
 # Env: BENCH_ARGS (extra bench.py args for bench/prof).
@@ -88,6 +91,16 @@ for st in "${STEPS[@]}"; do
         python tools/pmc_summary.py "$O/pmc_ns_${bpc}_FETCH_SIZE.csv" "$O/pmc_ns_${bpc}_WRITE_SIZE.csv" \
           "rs_apply_fast<4, 4, true, false" 51539607552 --blocks-per-cu $bpc --tiles 262144 \
           --what "north star, rs_apply_fast<4,4,nt> at $bpc WG/CU" --out "$O/pmc_k8m4_bpc${bpc}_traffic.json" || exit 1
+      done ;;
+    clock)
+      for cfg in 3 2 ns; do
+        ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT \
+            --kernel-include-regex 'sha256|rs_apply' -d "/tmp/clk/$cfg" -o run --output-format csv \
+            -- python3 "$R/bench.py" --config $cfg --steps 3 --warmup 1 --cpu-seconds 0 --no-extra --no-e2e \
+            > "$O/clock_$cfg.log" 2>&1 ) || { tail -5 "$O/clock_$cfg.log"; exit 1; }
+        find "/tmp/clk/$cfg" -name "*counter_collection.csv" -exec cp {} "$O/clock_$cfg.csv" \;
+        python tools/clock_summary.py "$O/clock_$cfg.csv" --what "bench.py --config $cfg, GRBM pass" \
+          --out "$O/clock_$cfg.json" || exit 1
       done ;;
     rust)
       { command -v rustc; command -v cargo; rustc --version; cargo --version; } > "$O/rust_probe.txt" 2>&1 || true

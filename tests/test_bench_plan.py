@@ -116,3 +116,16 @@ def test_pmc_traffic_needs_matching_grid(tmp_path, monkeypatch):
     assert bench.pmc_traffic("k4m2", 1000.0, 1024) == (None, None)
     t, src = bench.pmc_traffic("k4m2", 1000.0, 512)
     assert t == 1010.0 and src.endswith("r9_pmc_k4m2_traffic.json")
+
+
+def test_sha_chain_block_reads_committed_clock():
+    """Config 3's chain roofline: 905 consumer VALU x 4 cycles per block at
+    the clock of the committed GRBM pass (profiles/r*/clock/clock_3.json)."""
+    import bench
+
+    d = bench.sha_chain_block("split", 1.669)
+    assert d["bound"] == "valu-chain" and d["consumer_valu_per_block"] == 905
+    assert 1.0 < d["clock_GHz_measured"] <= 2.4 and d["clock_source"].startswith("profiles/")
+    assert abs(d["floor_us_per_block"] - 905 * 4 / (d["clock_GHz_measured"] * 1e3)) < 1e-3
+    assert 0.5 < d["frac"] <= 1.0
+    assert bench.sha_chain_block("stream", 1.0) is None
