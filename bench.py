@@ -67,11 +67,18 @@ GIB = float(1 << 30)
 # consumer 905 (64 rounds x 14 + 9) + producer 565 (2261 per 4-block step);
 # one-wave form 1410 (64 x 14 rounds + 48 x 10 schedule + 16 byte swaps + 18);
 # stream form 1415 (the one-wave rounds plus the clamped prefetch).
-SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415}
-# The split form's serial wave (the consumer) issues 905 of those per block;
-# a wave issues at most one VALU every 4 cycles, so a lone message's chain
-# cannot beat 905 x 4 cycles per block at the clock the chip holds.
-SHA_SPLIT_CONSUMER_VALU_PER_BLOCK = 905
+# Quad form (four lanes per message, 48 messages per workgroup): producer
+# 566 + 3 consumers x 649 wave-instructions per block over 48 messages =
+# 3351 lane-ops per message-block; it spends more lane-ops per hash to cut
+# the serial wave's count, so config 3 keeps the one-lane split form's 1470
+# as its chip-wide denominator (comparable across rounds).
+SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415, "quad": 3351}
+# The serial wave (the consumer) of each latency form issues this many VALU
+# per block (split: 64 rounds x 14 + 9; quad: 64 x 10 + 9); a wave issues at
+# most one VALU every 4 cycles, so a lone message's chain cannot beat that
+# x 4 cycles per block at the clock the chip holds.
+SHA_CONSUMER_VALU_PER_BLOCK = {"split": 905, "quad": 649}
+SHA_QUAD_MSGS_PER_CU = 48
 # Chip INT32 issue ceiling for those instructions (v_alignbit / v_bitop3 /
 # v_add3 / v_add / v_perm): CUs x 4 SIMDs x lanes per cycle x 2.4 GHz, lanes
 # per cycle measured with tools/valu_lab chip (profiles/r2_lab_valu_chip.jsonl).
@@ -258,7 +265,7 @@ class Reconstruct:
                 self.present0[o * (k + m) + i] = 0
         self.payload = n * k * S
         self.alg_bytes = n * (k + m) * S  # hash 10 present + write 2 rebuilt
-        self.kernel = "sha256_split_kernel + rs_apply_fast<R=2>"
+        self.kernel = "sha256_quad_kernel + rs_apply_fast<R=2>"
         self.name = ("RS reconstruct k=8 m=4, 2 data erasures + SHA-256 verify of the 10 present "
                      f"shards, chunk_size=1 MiB, {n} objects per GPU (BASELINE configs[2])")
 
@@ -296,9 +303,9 @@ class ReconstructStream:
     MaxIO's tokio workers) each own an 8192-chunk batch and a HIP stream and
     call mxec_reconstruct_strided_device concurrently through the one
     context; a step is one batch per worker.  The SHA-256 verify of a batch
-    is a per-message latency chain (~1.8 us per 64-byte block, one lane per
-    1 MiB shard: 29 ms) that occupies ~160 of the 1024 SIMDs, so batches in
-    flight side by side are what fills the chip."""
+    is a per-message latency chain (~1.2 us per 64-byte block in the quad
+    form: ~20 ms per 1 MiB shard) that leaves most SIMDs' issue slots idle, so
+    batches in flight side by side are what fills the chip."""
 
     bound = "valu"
     wall_timed = True
@@ -314,7 +321,7 @@ class ReconstructStream:
         self.k, self.m, self.S, self.n = 8, 4, 1 << 20, n * workers
         self.payload = sum(p.payload for p in self.parts)
         self.alg_bytes = sum(p.alg_bytes for p in self.parts)
-        self.kernel = "sha256_kernel / sha256_split_kernel + rs_apply_fast<R=2>, W streams"
+        self.kernel = "sha256_stream_kernel (combined) / sha256_quad_kernel + rs_apply_fast<R=2>, W streams"
         self.lat = []
         self.name = (f"RS reconstruct k=8 m=4, 2 data erasures + SHA-256 verify, chunk_size=1 MiB: "
                      f"{workers} concurrent batches of {n} objects (8192-chunk batches, BASELINE "
@@ -871,14 +878,14 @@ RS_R2_VALU_PER_INPUT_BYTE = 4.24
 
 def sha_chain_block(form: str, us_per_block: float):
     """Config 3's binding roofline: the serial chain of one message.  The
-    split form's consumer wave issues SHA_SPLIT_CONSUMER_VALU_PER_BLOCK VALU
-    per block, one per 4 cycles, at the clock the chip held for this kernel
+    form's consumer wave issues SHA_CONSUMER_VALU_PER_BLOCK VALU per block,
+    one per 4 cycles, at the clock the chip held for this kernel
     (GRBM_GUI_ACTIVE pass) and at the 2.4 GHz maximum."""
-    if form != "split":
+    if form not in SHA_CONSUMER_VALU_PER_BLOCK:
         return None
-    clk, src = measured_clock("sha256_split_kernel", "3")
-    cyc = SHA_SPLIT_CONSUMER_VALU_PER_BLOCK * 4
-    d = {"bound": "valu-chain", "consumer_valu_per_block": SHA_SPLIT_CONSUMER_VALU_PER_BLOCK,
+    clk, src = measured_clock(f"sha256_{form}_kernel", "3")
+    cyc = SHA_CONSUMER_VALU_PER_BLOCK[form] * 4
+    d = {"bound": "valu-chain", "form": form, "consumer_valu_per_block": SHA_CONSUMER_VALU_PER_BLOCK[form],
          "cycles_per_valu": 4, "us_per_block": round(us_per_block, 4),
          "floor_us_per_block_at_2.4GHz": round(cyc / (CLOCK_GHZ * 1e3), 4),
          "frac_at_2.4GHz": round(cyc / (CLOCK_GHZ * 1e3) / us_per_block, 4)}
@@ -983,9 +990,13 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     ms_sha = event_ms(torch, stream, lambda: ctx.sha256_batch_device(present_ptrs, present_lens, dig.data_ptr(),
                                                                      stream=sh), 3)
     hashed = float(len(present_ptrs)) * S
-    form = "split" if len(present_ptrs) <= 49152 else "stream"
+    nmsg = len(present_ptrs)
+    form = "quad" if nmsg <= SHA_QUAD_MSGS_PER_CU * n_cus else "split" if nmsg <= 49152 else "stream"
     sha_GBps = hashed / (ms_sha * 1e-3) / 1e9
-    vb = valu_bound_GBps(form, n_cus)
+    # chip-wide INT32 bound of the one-lane SHA-256 (the split form's count
+    # for the latency forms): the same denominator whatever form ran
+    vform = "split" if form == "quad" else form
+    vb = valu_bound_GBps(vform, n_cus)
     # decode alone: the same erasures, no digests (RS over the 8 survivors -> 2)
     def decode_only():
         pr = r.present0.copy()
@@ -1004,12 +1015,15 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
         "roofline": {"bound": "valu", "kernel": f"sha256_{form}_kernel (alone, {len(present_ptrs)} x 1 MiB)",
                      "achieved": round(sha_GBps, 1), "unit": "GB/s hashed",
                      "peak": round(vb, 1), "frac": round(sha_GBps / vb, 4),
-                     "valu_lane_ops_per_block": SHA_VALU_PER_BLOCK[form],
+                     "valu_lane_ops_per_block": SHA_VALU_PER_BLOCK[vform],
+                     "form_lane_ops_per_block": SHA_VALU_PER_BLOCK[form],
                      "valu_peak_lane_ops_per_s": n_cus * 4 * VALU_LANES_PER_SIMD_CYCLE * CLOCK_GHZ * 1e9,
                      "ms_per_launch": round(ms_sha, 3), "us_per_block": round(ms_sha * 1e3 / (S / 64), 4),
                      "frac_of_hbm": round(sha_GBps / HBM_PEAK_GBPS, 4),
-                     "note": ("10 240 messages fill 160 of 1024 SIMDs: this launch is bound by the serial "
-                              "chain of one 1 MiB message (16 384 blocks), not by chip-wide VALU issue"),
+                     "note": ("10 240 messages: this launch is bound by the serial chain of one 1 MiB "
+                              "message (16 384 blocks), not by chip-wide VALU issue; peak is the one-lane "
+                              "SHA-256's INT32 bound (1470 lane-ops per block), the chain block is the "
+                              "binding floor of the form that ran"),
                      "chain": sha_chain_block(form, ms_sha * 1e3 / (S / 64))},
         "rs_decode": hbm_block(float(n) * (k + 2) * S, ms_rs, "rs_apply_fast<R=2> (decode 8 -> 2, no verify)",
                                cal3, "rs_pattern_same_buffers_GBps"),

@@ -86,7 +86,8 @@ struct ShaArgs {
     uint8_t* ok;                 // [n] or null
     uint32_t n;
     int force = 0;               // 0 auto, 1 one wave per 64 messages, 2 split,
-                                 // 3 stream (needs the fields below)
+                                 // 3 stream (needs the fields below), 4 quad
+    uint32_t n_cus = 0;          // the device's CUs (auto form choice; 0: 256)
     // Stream form (batches of more 64-message groups than the chip has
     // SIMDs): persistent waves take (group, segment) items in segment-major
     // order; a group's running state is handed from segment to segment
@@ -98,6 +99,8 @@ struct ShaArgs {
     uint32_t wg_waves = 1;       // waves per workgroup (1 or 4; waves divisible by it)
     uint32_t seg_max = 0;        // segments of the longest message
 };
+// Messages per workgroup of the quad form (three consumer waves of 16).
+constexpr uint32_t kShaQuadMsgs = 48;
 // Blocks per stream-form segment (32 KiB of each message).
 constexpr uint32_t kShaSegBlocks = 512;
 // Timeout code the stream form leaves in work[1] when a wave gave up

@@ -532,6 +532,7 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     a.exp_idx = exp_idx ? reinterpret_cast<const uint64_t*>(db + o_e) : nullptr;
     a.ok = ok_dev;
     a.n = uint32_t(n);
+    a.n_cus = uint32_t(dev.n_cus);
     a.force = form == 3 && !stream ? 0 : form;
     if (stream) {
         void* st = nullptr;

@@ -140,10 +140,11 @@ __device__ __forceinline__ void compress_regs(uint32_t (&st)[8], const u32x4 (&v
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// The K + W of one block from LDS (kwl[q * 64] = words 4q..4q+3).
+// The K + W of one block from LDS (kwl[q * ROW] = words 4q..4q+3).
+template <int ROW = 64>
 __device__ __forceinline__ void load_kw(const u32x4* kwl, u32x4 (&v)[16]) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = kwl[q * 64];
+    for (int q = 0; q < 16; ++q) v[q] = kwl[q * ROW];
 }
 
 // 64 rounds reading K + W from LDS: all 16 reads issued up front so their
@@ -165,6 +166,7 @@ __constant__ uint32_t kK256[64] = {
     0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
 
 // Producer: K + W of one block (w = its 16 big-endian words) into LDS.
+template <int ROW = 64>
 __device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], u32x4* dst) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -175,7 +177,7 @@ __device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], u32x4* dst) {
             if (t >= 16) SHA_W(t);
             o[u] = w[t & 15] + kK256[t];
         }
-        dst[q * 64] = u32x4{o[0], o[1], o[2], o[3]};
+        dst[q * ROW] = u32x4{o[0], o[1], o[2], o[3]};
     }
 }
 
@@ -200,6 +202,101 @@ __device__ __forceinline__ void message_words(const uint8_t* p, bool aligned, ui
 constexpr int kShaPrefetch = 4;
 __device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
+// The producer wave of the split and quad forms: K + W of blocks 0 .. nmax-1
+// of the wave's 64 messages (one per lane; `live` lanes with `nfull` full
+// blocks each) into the NB-buffer LDS ring kw[NB][16][ROW] at column `lane`.
+// Blocks 0 .. NB-2 are written before a first barrier, block b + NB - 1
+// before the barrier that opens block b: 1 + nmax barriers in all, which the
+// consumer waves match.
+template <int NB, int ROW>
+__device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live, const uint8_t* p,
+                                            uint64_t nfull, uint64_t nmax, bool aligned) {
+    constexpr int AHEAD = NB - 1;  // blocks the producer runs ahead of the consumer
+    constexpr int BUF = 16 * ROW;  // u32x4 per buffer
+    uint32_t w[16];
+    if (__all(!live || nfull == 0 || aligned)) {
+        // Every message 16-byte aligned: the raw bytes of the next
+        // kShaPrefetch blocks stay in flight across the barriers in a
+        // register ring indexed at compile time (the loop is unrolled by the
+        // ring size), so the producer's step is the schedule alone.  One
+        // block ahead was not enough for a lone workgroup: with the chip
+        // otherwise idle a load's round trip can outlast a 1.8 us step, and
+        // the consumer then waited at the barrier (29-52 ms for one 1 MiB
+        // message, run to run).  Every load is unconditional -- lanes past
+        // their last block re-read it, lanes without one read a donor lane's
+        // -- because a load under a branch makes the compiler's wait before
+        // the next use drain every load in flight (it cannot count the ones
+        // that may have been skipped).  Blocks at or past nmax are scheduled
+        // into buffers nobody reads as a real block.
+        const uint64_t donor_mask = __ballot(nfull == nmax);
+        const int donor = __ffsll((unsigned long long)donor_mask) - 1;
+        const uint8_t* dp = reinterpret_cast<const uint8_t*>(
+            __shfl(reinterpret_cast<uintptr_t>(p), donor));
+        const bool own = live && nfull > 0;
+        const uint8_t* ps = own ? p : dp;
+        const uint64_t last = (own ? nfull : nmax) - 1;  // nmax > 0 when the loop runs
+        u32x4 ring[kShaPrefetch][4];
+        if (nmax > 0) {
+            u32x4 blk[AHEAD][4];
+#pragma unroll
+            for (int j = 0; j < AHEAD; ++j) load_block(ps + 64 * min_u64(j, last), blk[j]);
+#pragma unroll
+            for (int j = 0; j < kShaPrefetch; ++j) load_block(ps + 64 * min_u64(j + AHEAD, last), ring[j]);
+#pragma unroll
+            for (int j = 0; j < AHEAD; ++j) {
+                block_words(blk[j], w);
+                schedule_kw<ROW>(w, kw + j * BUF + lane);
+            }
+        }
+        __syncthreads();
+        // Whole groups of kShaPrefetch steps, then the rest: an exit in the
+        // middle of a group would join the loop's back edge with fewer loads
+        // issued, and the waits at the top would drain the ring again.
+        uint32_t wb = AHEAD % NB;  // buffer of block b + AHEAD
+        uint64_t b0 = 0;
+        for (; b0 + kShaPrefetch <= nmax; b0 += kShaPrefetch) {
+#pragma unroll
+            for (int j = 0; j < kShaPrefetch; ++j) {
+                const uint64_t b = b0 + j;
+                // ring[j] holds block b + AHEAD (or a clamped re-read nobody
+                // consumes: lanes compress only blocks below their nfull).
+                block_words(ring[j], w);
+                load_block(ps + 64 * min_u64(b + AHEAD + kShaPrefetch, last), ring[j]);
+                schedule_kw<ROW>(w, kw + wb * BUF + lane);
+                wb = wb + 1 == NB ? 0 : wb + 1;
+                __syncthreads();
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kShaPrefetch - 1; ++j) {  // the ring already holds these blocks
+            if (b0 + j < nmax) {
+                block_words(ring[j], w);
+                schedule_kw<ROW>(w, kw + wb * BUF + lane);
+                wb = wb + 1 == NB ? 0 : wb + 1;
+                __syncthreads();
+            }
+        }
+    } else {
+        // An unaligned message in the wave: byte loads, one block at a time.
+#pragma unroll
+        for (int j = 0; j < AHEAD; ++j)
+            if (uint64_t(j) < nfull) {
+                message_words(p + 64 * j, aligned, w);
+                schedule_kw<ROW>(w, kw + j * BUF + lane);
+            }
+        __syncthreads();
+        uint32_t wb = AHEAD % NB;
+        for (uint64_t b = 0; b < nmax; ++b) {
+            if (b + AHEAD < nfull) {
+                message_words(p + 64 * (b + AHEAD), aligned, w);
+                schedule_kw<ROW>(w, kw + wb * BUF + lane);
+            }
+            wb = wb + 1 == NB ? 0 : wb + 1;
+            __syncthreads();
+        }
+    }
+}
+
 // NB = 3 (default): the producer runs two blocks ahead, so the consumer
 // issues block b+1's 16 LDS reads right after the barrier that opens block b
 // and runs block b's rounds from registers: no read latency at the top of a
@@ -214,7 +311,6 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
                                                            const uint64_t* __restrict__ exp_idx,
                                                            uint8_t* __restrict__ ok, uint32_t n, uint32_t prio) {
     static_assert(NB == 2 || NB == 3, "two or three K+W buffers");
-    constexpr int AHEAD = NB - 1;  // blocks the producer runs ahead of the consumer
     sha_priority(prio);
     __shared__ u32x4 kw[NB][16][64];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -272,93 +368,183 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
                 rb = rb == 2 ? 0 : rb + 1;
             }
         }
-    } else if (__all(!live || nfull == 0 || aligned)) {
-        // Producer, every message 16-byte aligned: the raw bytes of the next
-        // kShaPrefetch blocks stay in flight across the barriers in a
-        // register ring indexed at compile time (the loop is unrolled by the
-        // ring size), so the producer's step is the schedule alone.  One
-        // block ahead was not enough for a lone workgroup: with the chip
-        // otherwise idle a load's round trip can outlast a 1.8 us step, and
-        // the consumer then waited at the barrier (29-52 ms for one 1 MiB
-        // message, run to run).  Every load is unconditional -- lanes past
-        // their last block re-read it, lanes without one read a donor lane's
-        // -- because a load under a branch makes the compiler's wait before
-        // the next use drain every load in flight (it cannot count the ones
-        // that may have been skipped).  Blocks at or past nmax are scheduled
-        // into buffers nobody reads as a real block.
-        const uint64_t donor_mask = __ballot(nfull == nmax);
-        const int donor = __ffsll((unsigned long long)donor_mask) - 1;
-        const uint8_t* dp = reinterpret_cast<const uint8_t*>(
-            __shfl(reinterpret_cast<uintptr_t>(p), donor));
-        const bool own = live && nfull > 0;
-        const uint8_t* ps = own ? p : dp;
-        const uint64_t last = (own ? nfull : nmax) - 1;  // nmax > 0 when the loop runs
-        u32x4 ring[kShaPrefetch][4];
-        if (nmax > 0) {
-            u32x4 blk[AHEAD][4];
-#pragma unroll
-            for (int j = 0; j < AHEAD; ++j) load_block(ps + 64 * min_u64(j, last), blk[j]);
-#pragma unroll
-            for (int j = 0; j < kShaPrefetch; ++j) load_block(ps + 64 * min_u64(j + AHEAD, last), ring[j]);
-#pragma unroll
-            for (int j = 0; j < AHEAD; ++j) {
-                block_words(blk[j], w);
-                schedule_kw(w, &kw[j][0][lane]);
-            }
-        }
-        __syncthreads();
-        // Whole groups of kShaPrefetch steps, then the rest: an exit in the
-        // middle of a group would join the loop's back edge with fewer loads
-        // issued, and the waits at the top would drain the ring again.
-        uint32_t wb = AHEAD % NB;  // buffer of block b + AHEAD
-        uint64_t b0 = 0;
-        for (; b0 + kShaPrefetch <= nmax; b0 += kShaPrefetch) {
-#pragma unroll
-            for (int j = 0; j < kShaPrefetch; ++j) {
-                const uint64_t b = b0 + j;
-                // ring[j] holds block b + AHEAD (or a clamped re-read nobody
-                // consumes: lanes compress only blocks below their nfull).
-                block_words(ring[j], w);
-                load_block(ps + 64 * min_u64(b + AHEAD + kShaPrefetch, last), ring[j]);
-                schedule_kw(w, &kw[wb][0][lane]);
-                wb = wb + 1 == NB ? 0 : wb + 1;
-                __syncthreads();
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < kShaPrefetch - 1; ++j) {  // the ring already holds these blocks
-            if (b0 + j < nmax) {
-                block_words(ring[j], w);
-                schedule_kw(w, &kw[wb][0][lane]);
-                wb = wb + 1 == NB ? 0 : wb + 1;
-                __syncthreads();
-            }
-        }
     } else {
-        // Producer with an unaligned message in the wave: byte loads, one
-        // block at a time.
-#pragma unroll
-        for (int j = 0; j < AHEAD; ++j)
-            if (uint64_t(j) < nfull) {
-                message_words(p + 64 * j, aligned, w);
-                schedule_kw(w, &kw[j][0][lane]);
-            }
-        __syncthreads();
-        uint32_t wb = AHEAD % NB;
-        for (uint64_t b = 0; b < nmax; ++b) {
-            if (b + AHEAD < nfull) {
-                message_words(p + 64 * (b + AHEAD), aligned, w);
-                schedule_kw(w, &kw[wb][0][lane]);
-            }
-            wb = wb + 1 == NB ? 0 : wb + 1;
-            __syncthreads();
-        }
+        kw_producer<NB, 64>(&kw[0][0][0], lane, live, p, nfull, nmax, aligned);
     }
     if (wave == 1 || !live) return;
     const uint32_t rem = uint32_t(len - nfull * 64);
     const uint8_t* tp = p + nfull * 64;
     const int nblk = (rem + 9 <= 64) ? 1 : 2;
     const uint64_t bits = len * 8;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = tail_word(tp, rem, t, nblk, bits);
+    compress(st, w);
+    if (nblk == 2) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) w[t] = tail_word(tp, rem, 16 + t, nblk, bits);
+        compress(st, w);
+    }
+    bool match = true;
+    const uint64_t ei = exp_idx ? exp_idx[i] : i;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const uint32_t be = bswap(st[t]);
+        if (digests) reinterpret_cast<uint32_t*>(digests + 32 * uint64_t(i))[t] = be;
+        if (expected) match &= reinterpret_cast<const uint32_t*>(expected + 32 * ei)[t] == be;
+    }
+    if (ok) ok[i] = match ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Quad form for latency-bound batches (at most 48 messages per CU).
+//
+// The split form's consumer sits on the one-lane floor: 14 VALU per round
+// (Σ1, Ch, Σ0, Maj, the adds), issued one every ~4.4 cycles by one wave.
+// Here four lanes of a consumer wave serve one message, and the e-side and
+// a-side halves of a round run as the SAME instructions in two lanes with
+// per-lane operands:
+//   lane E (4j):       X = e, rotations 6/11/25 -> Σ1(e); Ch(e, f, g)
+//   lane A (4j + 1):   X = a, rotations 2/13/22 -> Σ0(a); Maj(a, b, c)
+//   lanes 4j + 2, + 3: all zero (the zero source of the DPP reads below).
+// Maj(a, b, c) = Ch(~(a ^ b), b, c), so one v_bitop3 makes the selector
+// (e in lane E, ~(a ^ b) in lane A) and one more is Ch in both lanes.  With
+// H = h + d + K + W in lane E and -d in lane A,
+//   P  = Σ + Ch + H       is d + T1 = e' in lane E and T2 - d in lane A;
+//   X' = P + P[lane E]    (one v_add_u32 with a quad_perm DPP source)
+// is e' in lane E (its DPP source is a zero lane) and T1 + T2 = a' in lane A.
+// The next round's H is X[t-2] + X[t-2][lane A] (h + d in lane E, d in lane
+// A: DPP again), then one v_xad_u32: xor with a per-lane mask (all ones in
+// lane A: ~d + 1 = -d) plus the K + W word (K + W in lane E, 1 in lane A, 0
+// in the zero lanes).  10 VALU per round instead of 14; the idle lanes cost
+// nothing, the chain being bound by the wave's issue rate.
+//
+// A workgroup is one producer wave (the split form's, kw_producer: K + W of
+// 48 messages, one per lane) and three consumer waves of 16 messages each,
+// so each wave has a SIMD of its own.  K + W rows are kQuadRow columns wide:
+// 0..47 the producer's, 64 all zero and 65 all one, so every consumer lane
+// reads its word at the same row offset from its own column.  The padded
+// tail (1 or 2 blocks) runs in lane E after the main loop, one-lane form.
+// ---------------------------------------------------------------------------
+constexpr int kQuadRow = 66;  // u32x4 per K + W row: 64 producer lanes, zeros, ones
+
+#define QDPP(x, ctrl) uint32_t(__builtin_amdgcn_update_dpp(0, int(x), (ctrl), 0xF, 0xF, true))
+constexpr int kQuadFromE = 0xA2;   // quad_perm [2, 0, 2, 2]: lane A reads lane E, the rest a zero lane
+constexpr int kQuadFromA = 0xA9;   // quad_perm [1, 2, 2, 2]: lane E reads lane A, the rest a zero lane
+constexpr int kQuadBcastA = 0x55;  // quad_perm [1, 1, 1, 1]
+
+struct QuadLane {
+    uint32_t sh1, sh2, sh3;  // rotations: Σ1's in lane E, Σ0's in lane A
+    uint32_t ma;             // all ones in lane A (selector ~(a ^ b); negated d), else 0
+};
+
+// One block.  s[0..3] = (e, f, g, h) in lane E, (a, b, c, d) in lane A, zero
+// in the zero lanes; v = the block's K + W rows as this lane reads them.
+__device__ __forceinline__ void compress_quad(uint32_t (&s)[4], const u32x4 (&v)[16], const QuadLane& q) {
+    uint32_t x[4];  // x[t & 3] = X[t]; X[-1], X[-2], X[-3] = s[1], s[2], s[3]
+    x[0] = s[0];
+    x[3] = s[1];
+    x[2] = s[2];
+    x[1] = s[3];
+    uint32_t h = ((x[1] + QDPP(x[1], kQuadFromA)) ^ q.ma) + v[0].x;
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+        const uint32_t X0 = x[t & 3], X1 = x[(t + 3) & 3], X2 = x[(t + 2) & 3];
+        const uint32_t S = xor3(rotr(X0, q.sh1), rotr(X0, q.sh2), rotr(X0, q.sh3));
+        const uint32_t sel = __builtin_amdgcn_bitop3_b32(X0, X1, q.ma, 0xD2);  // X0 ^ (~X1 & ma)
+        const uint32_t P = S + bsel(sel, X1, X2) + h;
+        if (t < 63) h = ((X2 + QDPP(X2, kQuadFromA)) ^ q.ma) + v[(t + 1) >> 2][(t + 1) & 3];
+        x[(t + 1) & 3] = P + QDPP(P, kQuadFromE);
+    }
+    s[0] += x[0];
+    s[1] += x[3];
+    s[2] += x[2];
+    s[3] += x[1];
+}
+
+__global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* __restrict__ ptrs,
+                                                         const uint64_t* __restrict__ lens,
+                                                         uint8_t* __restrict__ digests,
+                                                         const uint8_t* __restrict__ expected,
+                                                         const uint64_t* __restrict__ exp_idx,
+                                                         uint8_t* __restrict__ ok, uint32_t n, uint32_t prio) {
+    constexpr int NB = 3, BUF = 16 * kQuadRow;
+    sha_priority(prio);
+    __shared__ u32x4 kw[NB][16][kQuadRow];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < NB * 16 * 2) {  // the constant columns; the first barrier publishes them
+        const uint32_t r = threadIdx.x >> 1, c = threadIdx.x & 1;
+        kw[r / 16][r % 16][64 + c] = u32x4{c, c, c, c};
+    }
+    const uint32_t base = blockIdx.x * kShaQuadMsgs;
+    // Every wave derives the same trip count from the workgroup's messages
+    // (one per lane below kShaQuadMsgs), so the barriers pair up.
+    const uint32_t pi = base + lane;
+    const bool plive = lane < kShaQuadMsgs && pi < n;
+    const uint8_t* pp = plive ? ptrs[pi] : nullptr;
+    const uint64_t pfull = plive ? lens[pi] / 64 : 0;
+    uint64_t nmax = pfull;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        const uint64_t o = __shfl_xor(nmax, s);
+        nmax = o > nmax ? o : nmax;
+    }
+    nmax = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(nmax >> 32))) << 32) |
+           __builtin_amdgcn_readfirstlane(uint32_t(nmax));
+    if (wave == 0) {
+        kw_producer<NB, kQuadRow>(&kw[0][0][0], lane, plive, pp, pfull, nmax,
+                                  (reinterpret_cast<uintptr_t>(pp) & 15) == 0);
+        return;
+    }
+    const uint32_t role = lane & 3, ml = (wave - 1) * 16 + (lane >> 2);
+    const uint32_t i = base + ml;
+    const bool live = i < n;
+    const uint8_t* p = live ? ptrs[i] : nullptr;
+    const uint64_t len = live ? lens[i] : 0;
+    const uint64_t nfull = len / 64;
+    QuadLane q;
+    q.sh1 = role == 0 ? 6 : 2;
+    q.sh2 = role == 0 ? 11 : 13;
+    q.sh3 = role == 0 ? 25 : 22;
+    q.ma = role == 1 ? ~0u : 0u;
+    uint32_t s[4] = {0, 0, 0, 0};
+    if (role == 0) {
+        s[0] = 0x510e527fu; s[1] = 0x9b05688cu; s[2] = 0x1f83d9abu; s[3] = 0x5be0cd19u;
+    } else if (role == 1) {
+        s[0] = 0x6a09e667u; s[1] = 0xbb67ae85u; s[2] = 0x3c6ef372u; s[3] = 0xa54ff53au;
+    }
+    const u32x4* kcol = &kw[0][0][role == 0 ? ml : role == 1 ? 65 : 64];
+    // As the split form's NB = 3 consumer: block b + 1's reads go out right
+    // after the barrier that opens block b, block b runs from registers.
+    __syncthreads();
+    u32x4 cur[16], nxt[16];
+    load_kw<kQuadRow>(kcol, cur);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    uint32_t rb = 1;
+    for (uint64_t b = 0; b < nmax; b += 2) {
+        load_kw<kQuadRow>(kcol + rb * BUF, nxt);
+        if (b < nfull) compress_quad(s, cur, q);
+        __syncthreads();
+        rb = rb == 2 ? 0 : rb + 1;
+        if (b + 1 >= nmax) break;
+        load_kw<kQuadRow>(kcol + rb * BUF, cur);
+        if (b + 1 < nfull) compress_quad(s, nxt, q);
+        __syncthreads();
+        rb = rb == 2 ? 0 : rb + 1;
+    }
+    // Lane E takes (a, b, c, d) from lane A and finishes alone: padded tail,
+    // digest, expected-digest check.
+    uint32_t st[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        st[t] = QDPP(s[t], kQuadBcastA);
+        st[4 + t] = s[t];
+    }
+    if (role != 0 || !live) return;
+    const uint32_t rem = uint32_t(len - nfull * 64);
+    const uint8_t* tp = p + nfull * 64;
+    const int nblk = (rem + 9 <= 64) ? 1 : 2;
+    const uint64_t bits = len * 8;
+    uint32_t w[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) w[t] = tail_word(tp, rem, t, nblk, bits);
     compress(st, w);
@@ -600,11 +786,20 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
     const uint32_t blocks = (a.n + 63) / 64;
     int form = a.force;
     if (form == 0) {
-        // MXEC_SHA_FORM=one|split pins the form (tests, lab).
+        // MXEC_SHA_FORM=one|split|quad pins the form (tests, lab).  Auto:
+        // quad while its workgroups fit one per CU (one wave per SIMD), then
+        // split, then one wave per 64 messages.
+        const uint64_t n_cus = a.n_cus ? a.n_cus : 256;
         const char* env = getenv("MXEC_SHA_FORM");
         if (env && !strcmp(env, "one")) form = 1;
         else if (env && !strcmp(env, "split")) form = 2;
-        else form = a.n <= kSplitMaxMessages ? 2 : 1;
+        else if (env && !strcmp(env, "quad")) form = 4;
+        else form = a.n <= kShaQuadMsgs * n_cus ? 4 : a.n <= kSplitMaxMessages ? 2 : 1;
+    }
+    if (form == 4) {
+        hipLaunchKernelGGL(sha256_quad_kernel, dim3((a.n + kShaQuadMsgs - 1) / kShaQuadMsgs), dim3(256), 0, s,
+                           a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
+        return hipGetLastError();
     }
     if (form == 3) {
         const uint32_t per = a.wg_waves ? a.wg_waves : 1;

@@ -374,10 +374,11 @@ def test_short_last_chunk_device_encode_and_rebuild(ctx, last):
     assert np.array_equal(got[:, 2], host[:, 2])
 
 
-@pytest.mark.parametrize("form", ["split", "one"])
+@pytest.mark.parametrize("form", ["quad", "split", "one"])
 def test_sha256_every_kernel_form(ctx, form, monkeypatch):
-    """MXEC_SHA_FORM pins the SHA-256 kernel (split: producer/consumer waves;
-    one: one wave per 64 messages).
+    """MXEC_SHA_FORM pins the SHA-256 kernel (quad: four lanes per message
+    behind a producer wave; split: producer/consumer waves; one: one wave per
+    64 messages).
     Mixed lengths (multi-block, tails 0..63, unaligned starts) per form."""
     monkeypatch.setenv("MXEC_SHA_FORM", form)
     rng = np.random.default_rng(13)
@@ -392,7 +393,7 @@ def test_sha256_every_kernel_form(ctx, form, monkeypatch):
     assert got == [hashlib.sha256(b).digest() for b in bufs]
 
 
-@pytest.mark.parametrize("form", ["split", "one"])
+@pytest.mark.parametrize("form", ["quad", "split", "one"])
 @pytest.mark.parametrize("shift", [0, 16, 3])
 def test_sha256_device_messages_ring_edges(ctx, form, shift, monkeypatch):
     """Device-resident messages straight into the kernel (no staging copy),
