@@ -461,6 +461,92 @@ __device__ __forceinline__ void compress_quad(uint32_t (&s)[4], const u32x4 (&v)
     s[3] += x[1];
 }
 
+// Lag variant (MXEC_SHA_FORM=lag; kShaQuadAuto picks the auto form).  Above, lane A's
+// a' = T1 + T2 needs lane E's T1 of the same round, so a DPP add sits on
+// every round's critical path (X -> rotations -> xor3 -> add3 -> DPP add ->
+// X'): the rounds measured ~54 cycles against 40 of issue.  Here lane A runs
+// TWO rounds behind lane E (tools/sha_lag_model.py is the lane-level model,
+// checked against hashlib):
+//   step t, lane E:  e[t+1] = Σ1(e[t]) + Ch(e[t], e[t-1], e[t-2]) + H,
+//                    H = e[t-3] + a[t-3] + K[t] + W[t]         (h + d + K + W)
+//   step t, lane A:  a[t-1] = Σ0(a[t-2]) + Maj(a[t-2], a[t-3], a[t-4]) + H,
+//                    H = T1[t-2] = e[t-1] - a[t-5]
+// With the history in an 8-slot ring x[t & 7] (X0 newest), the cross-lane
+// operand of BOTH lanes is the other lane's X1 (a[t-3] for lane E, e[t-1]
+// for lane A): one DPP swap of a value written a step earlier, off the
+// chain.  A step is 3 alignbit + xor3 + selector + Ch + v_xad (X3 ^ mask +
+// c) + v_add_dpp + add3 = 9 VALU, chain X -> alignbit -> xor3 -> add3 -> X'.
+// A block is 66 steps (lane A's last two rounds run beside two unused lane-E
+// values); lane A's first two outputs are forced to the known b and a, and
+// lane A keeps its state rotated as (c, d, a, b) so both lanes load the ring
+// from, and mostly add back, the same slots.  Lanes 2 and 3 of a quad swap
+// among themselves and compute nothing anyone reads.
+constexpr int kLagSwap = 0xB1;  // quad_perm [1, 0, 3, 2]
+
+// (X3 ^ ma) + c as one v_xad: left free, the compiler sums X3 ^ ma, c and a
+// v_mov_dpp with an add3 (10 VALU per step instead of 9).
+__device__ __forceinline__ uint32_t lag_xc(uint32_t x3, uint32_t ma, uint32_t c) {
+    uint32_t r = (x3 ^ ma) + c;
+    asm("" : "+v"(r));
+    return r;
+}
+
+// PIN = true holds the instructions of a step in the order written (a
+// scheduling barrier after each): the three rotations first, then the
+// off-chain work (selector, next step's H and the xad after it) while they
+// retire, then xor3, Ch, add3.  PIN = false leaves the order to the compiler,
+// which emits each step in dependency order (lab A/B: MXEC_SHA_LAG_PIN=0).
+#define LAG_FENCE() do { if constexpr (PIN) __builtin_amdgcn_sched_barrier(0); } while (0)
+
+template <bool PIN>
+__device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[16], const QuadLane& q) {
+    const bool is_a = q.ma != 0;
+    const uint32_t one = q.ma & 1;  // c after lane E's rounds: 1 in lane A (-X3 = ~X3 + 1), 0 elsewhere
+    uint32_t x[8];
+    x[0] = s[0];
+    x[7] = s[1];
+    x[6] = s[2];
+    x[5] = s[3];
+    // Software-pipelined: step t finds its H ready and leaves H[t+1]
+    // (DPP of its own X0, which is step t+1's X1) and xc[t+2] (X3 of step
+    // t+2 is step t's X1) for the steps after it.
+    uint32_t H = QDPP(x[7], kLagSwap) + lag_xc(x[5], q.ma, v[0][0]);
+    uint32_t xc = lag_xc(x[6], q.ma, v[0][1]);
+#pragma unroll
+    for (int t = 0; t < 66; ++t) {
+        const uint32_t X0 = x[t & 7], X1 = x[(t + 7) & 7], X2 = x[(t + 6) & 7];
+        const uint32_t r1 = rotr(X0, q.sh1), r2 = rotr(X0, q.sh2), r3 = rotr(X0, q.sh3);
+        LAG_FENCE();
+        const uint32_t sel = __builtin_amdgcn_bitop3_b32(X0, X1, q.ma, 0xD2);  // X0 ^ (~X1 & ma)
+        LAG_FENCE();
+        uint32_t Hn = QDPP(X0, kLagSwap) + xc;
+        asm("" : "+v"(Hn));  // one v_add_u32_dpp (not reassociated into the add3)
+        LAG_FENCE();
+        const int u = t + 2;
+        xc = lag_xc(X1, q.ma, u < 64 ? v[u >> 2][u & 3] : one);
+        LAG_FENCE();
+        const uint32_t S = xor3(r1, r2, r3);
+        LAG_FENCE();
+        const uint32_t ch = bsel(sel, X1, X2);
+        LAG_FENCE();
+        uint32_t P = S + ch + H;
+        if (t == 0) P = is_a ? s[3] : P;  // b = a[-1]
+        if (t == 1) P = is_a ? s[2] : P;  // a = a[0]
+        LAG_FENCE();
+        x[(t + 1) & 7] = P;
+        H = Hn;
+    }
+    // Lane E: e[64], e[63], e[62], e[61] in x[0], x[7], x[6], x[5];
+    // lane A: a[62], a[61], a[64], a[63] in x[0], x[7], x[2], x[1].
+    s[0] += x[0];
+    s[1] += x[7];
+    s[2] += is_a ? x[2] : x[6];
+    s[3] += is_a ? x[1] : x[5];
+}
+
+// VAR 0: the same-round quad (compress_quad); 1: lag, compiler order; 2: lag,
+// pinned order.
+template <int VAR>
 __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* __restrict__ ptrs,
                                                          const uint64_t* __restrict__ lens,
                                                          uint8_t* __restrict__ digests,
@@ -509,6 +595,8 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     uint32_t s[4] = {0, 0, 0, 0};
     if (role == 0) {
         s[0] = 0x510e527fu; s[1] = 0x9b05688cu; s[2] = 0x1f83d9abu; s[3] = 0x5be0cd19u;
+    } else if (role == 1 && VAR > 0) {  // (c, d, a, b)
+        s[0] = 0x3c6ef372u; s[1] = 0xa54ff53au; s[2] = 0x6a09e667u; s[3] = 0xbb67ae85u;
     } else if (role == 1) {
         s[0] = 0x6a09e667u; s[1] = 0xbb67ae85u; s[2] = 0x3c6ef372u; s[3] = 0xa54ff53au;
     }
@@ -522,21 +610,28 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     uint32_t rb = 1;
     for (uint64_t b = 0; b < nmax; b += 2) {
         load_kw<kQuadRow>(kcol + rb * BUF, nxt);
-        if (b < nfull) compress_quad(s, cur, q);
+        if (b < nfull) {
+            if constexpr (VAR > 0) compress_lag<VAR == 2>(s, cur, q);
+            else compress_quad(s, cur, q);
+        }
         __syncthreads();
         rb = rb == 2 ? 0 : rb + 1;
         if (b + 1 >= nmax) break;
         load_kw<kQuadRow>(kcol + rb * BUF, cur);
-        if (b + 1 < nfull) compress_quad(s, nxt, q);
+        if (b + 1 < nfull) {
+            if constexpr (VAR > 0) compress_lag<VAR == 2>(s, nxt, q);
+            else compress_quad(s, nxt, q);
+        }
         __syncthreads();
         rb = rb == 2 ? 0 : rb + 1;
     }
     // Lane E takes (a, b, c, d) from lane A and finishes alone: padded tail,
-    // digest, expected-digest check.
+    // digest, expected-digest check.  (The lag form's lane A holds
+    // (c, d, a, b).)
     uint32_t st[8];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        st[t] = QDPP(s[t], kQuadBcastA);
+        st[t] = QDPP(s[VAR > 0 ? (t + 2) & 3 : t], kQuadBcastA);
         st[4 + t] = s[t];
     }
     if (role != 0 || !live) return;
@@ -770,6 +865,9 @@ constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 
 // MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read
 // per launch), default 3.
+// The quad form the auto choice takes: 4 = same-round, 5 = lag.
+constexpr int kShaQuadAuto = 4;
+
 int split_bufs() {
     const char* e = getenv("MXEC_SHA_SPLIT_BUFS");
     return e && atoi(e) == 2 ? 2 : 3;
@@ -786,7 +884,7 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
     const uint32_t blocks = (a.n + 63) / 64;
     int form = a.force;
     if (form == 0) {
-        // MXEC_SHA_FORM=one|split|quad pins the form (tests, lab).  Auto:
+        // MXEC_SHA_FORM=one|split|quad|lag pins the form (tests, lab).  Auto:
         // quad while its workgroups fit one per CU (one wave per SIMD), then
         // split, then one wave per 64 messages.
         const uint64_t n_cus = a.n_cus ? a.n_cus : 256;
@@ -794,11 +892,18 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         if (env && !strcmp(env, "one")) form = 1;
         else if (env && !strcmp(env, "split")) form = 2;
         else if (env && !strcmp(env, "quad")) form = 4;
-        else form = a.n <= kShaQuadMsgs * n_cus ? 4 : a.n <= kSplitMaxMessages ? 2 : 1;
+        else if (env && !strcmp(env, "lag")) form = 5;
+        else form = a.n <= kShaQuadMsgs * n_cus ? kShaQuadAuto : a.n <= kSplitMaxMessages ? 2 : 1;
     }
-    if (form == 4) {
-        hipLaunchKernelGGL(sha256_quad_kernel, dim3((a.n + kShaQuadMsgs - 1) / kShaQuadMsgs), dim3(256), 0, s,
-                           a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
+    if (form == 4 || form == 5) {
+        // form 4: the same-round quad; 5: the lag quad (MXEC_SHA_LAG_PIN=0
+        // leaves its step order to the compiler, lab A/B).
+        const char* pin = getenv("MXEC_SHA_LAG_PIN");
+        const int var = form == 4 ? 0 : pin && atoi(pin) == 0 ? 1 : 2;
+        const dim3 grid((a.n + kShaQuadMsgs - 1) / kShaQuadMsgs);
+        auto k = var == 0 ? sha256_quad_kernel<0> : var == 1 ? sha256_quad_kernel<1> : sha256_quad_kernel<2>;
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, s, a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n,
+                           sha_prio());
         return hipGetLastError();
     }
     if (form == 3) {

@@ -374,13 +374,27 @@ def test_short_last_chunk_device_encode_and_rebuild(ctx, last):
     assert np.array_equal(got[:, 2], host[:, 2])
 
 
-@pytest.mark.parametrize("form", ["quad", "split", "one"])
+# MXEC_SHA_FORM pins the SHA-256 kernel (quad: four lanes per message behind a
+# producer wave, e-side and a-side of a round in one instruction stream; lag:
+# the same with lane A two rounds behind lane E, pinned step order; lag-nopin:
+# the lag form in the compiler's order; split: producer/consumer waves; one:
+# one wave per 64 messages).
+SHA_FORMS = ["quad", "lag", "lag-nopin", "split", "one"]
+
+
+def _pin_sha_form(monkeypatch, form):
+    monkeypatch.setenv("MXEC_SHA_FORM", "lag" if form == "lag-nopin" else form)
+    if form == "lag-nopin":
+        monkeypatch.setenv("MXEC_SHA_LAG_PIN", "0")
+    else:
+        monkeypatch.delenv("MXEC_SHA_LAG_PIN", raising=False)
+
+
+@pytest.mark.parametrize("form", SHA_FORMS)
 def test_sha256_every_kernel_form(ctx, form, monkeypatch):
-    """MXEC_SHA_FORM pins the SHA-256 kernel (quad: four lanes per message
-    behind a producer wave; split: producer/consumer waves; one: one wave per
-    64 messages).
-    Mixed lengths (multi-block, tails 0..63, unaligned starts) per form."""
-    monkeypatch.setenv("MXEC_SHA_FORM", form)
+    """Every SHA-256 kernel form on mixed lengths (multi-block, tails 0..63,
+    unaligned starts)."""
+    _pin_sha_form(monkeypatch, form)
     rng = np.random.default_rng(13)
     lens = list(rng.integers(0, 5000, 300)) + [0, 55, 56, 64, 4096, 100_003]
     blob = rng.integers(0, 256, int(sum(lens)) + 64, dtype=np.uint8).tobytes()
@@ -393,7 +407,7 @@ def test_sha256_every_kernel_form(ctx, form, monkeypatch):
     assert got == [hashlib.sha256(b).digest() for b in bufs]
 
 
-@pytest.mark.parametrize("form", ["quad", "split", "one"])
+@pytest.mark.parametrize("form", SHA_FORMS)
 @pytest.mark.parametrize("shift", [0, 16, 3])
 def test_sha256_device_messages_ring_edges(ctx, form, shift, monkeypatch):
     """Device-resident messages straight into the kernel (no staging copy),
@@ -402,7 +416,7 @@ def test_sha256_device_messages_ring_edges(ctx, form, shift, monkeypatch):
     ring phase and tail count), a wave whose lanes end at different blocks,
     empty messages (their lanes borrow a donor lane's address) and a batch
     past one workgroup."""
-    monkeypatch.setenv("MXEC_SHA_FORM", form)
+    _pin_sha_form(monkeypatch, form)
     torch = _torch()
     rng = np.random.default_rng(21 + shift)
     cases = [[64 * b + t] for b in range(10) for t in (0, 37)]
