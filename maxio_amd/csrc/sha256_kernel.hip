@@ -461,10 +461,10 @@ __device__ __forceinline__ void compress_quad(uint32_t (&s)[4], const u32x4 (&v)
     s[3] += x[1];
 }
 
-// Lag variant (MXEC_SHA_FORM=lag; kShaQuadAuto picks the auto form).  Above, lane A's
+// Lag variant (the auto quad form; MXEC_SHA_FORM=lag pins it).  Above, lane A's
 // a' = T1 + T2 needs lane E's T1 of the same round, so a DPP add sits on
 // every round's critical path (X -> rotations -> xor3 -> add3 -> DPP add ->
-// X'): the rounds measured ~54 cycles against 40 of issue.  Here lane A runs
+// X'): the rounds measured ~54 cycles for 10 VALU.  Here lane A runs
 // TWO rounds behind lane E (tools/sha_lag_model.py is the lane-level model,
 // checked against hashlib):
 //   step t, lane E:  e[t+1] = Σ1(e[t]) + Ch(e[t], e[t-1], e[t-2]) + H,
@@ -491,14 +491,13 @@ __device__ __forceinline__ uint32_t lag_xc(uint32_t x3, uint32_t ma, uint32_t c)
     return r;
 }
 
-// PIN = true holds the instructions of a step in the order written (a
-// scheduling barrier after each): the three rotations first, then the
-// off-chain work (selector, next step's H and the xad after it) while they
-// retire, then xor3, Ch, add3.  PIN = false leaves the order to the compiler,
-// which emits each step in dependency order (lab A/B: MXEC_SHA_LAG_PIN=0).
-#define LAG_FENCE() do { if constexpr (PIN) __builtin_amdgcn_sched_barrier(0); } while (0)
-
-template <bool PIN>
+// The step's order is the compiler's: r1 H' r2 r3 sel xc S ch P, with H'
+// the NEXT step's H (DPP of this step's X0, which is step t+1's X1) and xc
+// the xad of the step after that.  A lone wave issues independent VALU at
+// ~5-5.8 cycles (tools/valu_lab.cpp), so 9 per step at ~46 cycles is that
+// floor; a hand order spacing every on-chain pair two slots apart, held
+// with sched_barriers, measured 1.48 us per block against 1.265
+// (profiles/r3/sha_lag/ab_order.jsonl).
 __device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[16], const QuadLane& q) {
     const bool is_a = q.ma != 0;
     const uint32_t one = q.ma & 1;  // c after lane E's rounds: 1 in lane A (-X3 = ~X3 + 1), 0 elsewhere
@@ -507,32 +506,23 @@ __device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[
     x[7] = s[1];
     x[6] = s[2];
     x[5] = s[3];
-    // Software-pipelined: step t finds its H ready and leaves H[t+1]
-    // (DPP of its own X0, which is step t+1's X1) and xc[t+2] (X3 of step
-    // t+2 is step t's X1) for the steps after it.
+    // Step t finds its H ready and leaves H[t+1] (DPP of its own X0,
+    // which is step t+1's X1) and xc[t+2] (X3 of step t+2 is step t's
+    // X1) for the steps after it.
     uint32_t H = QDPP(x[7], kLagSwap) + lag_xc(x[5], q.ma, v[0][0]);
     uint32_t xc = lag_xc(x[6], q.ma, v[0][1]);
 #pragma unroll
     for (int t = 0; t < 66; ++t) {
         const uint32_t X0 = x[t & 7], X1 = x[(t + 7) & 7], X2 = x[(t + 6) & 7];
-        const uint32_t r1 = rotr(X0, q.sh1), r2 = rotr(X0, q.sh2), r3 = rotr(X0, q.sh3);
-        LAG_FENCE();
+        const uint32_t S = xor3(rotr(X0, q.sh1), rotr(X0, q.sh2), rotr(X0, q.sh3));
         const uint32_t sel = __builtin_amdgcn_bitop3_b32(X0, X1, q.ma, 0xD2);  // X0 ^ (~X1 & ma)
-        LAG_FENCE();
         uint32_t Hn = QDPP(X0, kLagSwap) + xc;
         asm("" : "+v"(Hn));  // one v_add_u32_dpp (not reassociated into the add3)
-        LAG_FENCE();
         const int u = t + 2;
         xc = lag_xc(X1, q.ma, u < 64 ? v[u >> 2][u & 3] : one);
-        LAG_FENCE();
-        const uint32_t S = xor3(r1, r2, r3);
-        LAG_FENCE();
-        const uint32_t ch = bsel(sel, X1, X2);
-        LAG_FENCE();
-        uint32_t P = S + ch + H;
+        uint32_t P = S + bsel(sel, X1, X2) + H;
         if (t == 0) P = is_a ? s[3] : P;  // b = a[-1]
         if (t == 1) P = is_a ? s[2] : P;  // a = a[0]
-        LAG_FENCE();
         x[(t + 1) & 7] = P;
         H = Hn;
     }
@@ -544,9 +534,8 @@ __device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[
     s[3] += is_a ? x[1] : x[5];
 }
 
-// VAR 0: the same-round quad (compress_quad); 1: lag, compiler order; 2: lag,
-// pinned order.
-template <int VAR>
+// LAG: compress_lag (default) or the same-round compress_quad (lab A/B).
+template <bool LAG>
 __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* __restrict__ ptrs,
                                                          const uint64_t* __restrict__ lens,
                                                          uint8_t* __restrict__ digests,
@@ -595,7 +584,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     uint32_t s[4] = {0, 0, 0, 0};
     if (role == 0) {
         s[0] = 0x510e527fu; s[1] = 0x9b05688cu; s[2] = 0x1f83d9abu; s[3] = 0x5be0cd19u;
-    } else if (role == 1 && VAR > 0) {  // (c, d, a, b)
+    } else if (role == 1 && LAG) {  // (c, d, a, b)
         s[0] = 0x3c6ef372u; s[1] = 0xa54ff53au; s[2] = 0x6a09e667u; s[3] = 0xbb67ae85u;
     } else if (role == 1) {
         s[0] = 0x6a09e667u; s[1] = 0xbb67ae85u; s[2] = 0x3c6ef372u; s[3] = 0xa54ff53au;
@@ -611,7 +600,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     for (uint64_t b = 0; b < nmax; b += 2) {
         load_kw<kQuadRow>(kcol + rb * BUF, nxt);
         if (b < nfull) {
-            if constexpr (VAR > 0) compress_lag<VAR == 2>(s, cur, q);
+            if constexpr (LAG) compress_lag(s, cur, q);
             else compress_quad(s, cur, q);
         }
         __syncthreads();
@@ -619,7 +608,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
         if (b + 1 >= nmax) break;
         load_kw<kQuadRow>(kcol + rb * BUF, cur);
         if (b + 1 < nfull) {
-            if constexpr (VAR > 0) compress_lag<VAR == 2>(s, nxt, q);
+            if constexpr (LAG) compress_lag(s, nxt, q);
             else compress_quad(s, nxt, q);
         }
         __syncthreads();
@@ -631,7 +620,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     uint32_t st[8];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        st[t] = QDPP(s[VAR > 0 ? (t + 2) & 3 : t], kQuadBcastA);
+        st[t] = QDPP(s[LAG ? (t + 2) & 3 : t], kQuadBcastA);
         st[4 + t] = s[t];
     }
     if (role != 0 || !live) return;
@@ -866,7 +855,7 @@ constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 // MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read
 // per launch), default 3.
 // The quad form the auto choice takes: 4 = same-round, 5 = lag.
-constexpr int kShaQuadAuto = 4;
+constexpr int kShaQuadAuto = 5;
 
 int split_bufs() {
     const char* e = getenv("MXEC_SHA_SPLIT_BUFS");
@@ -895,15 +884,10 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         else if (env && !strcmp(env, "lag")) form = 5;
         else form = a.n <= kShaQuadMsgs * n_cus ? kShaQuadAuto : a.n <= kSplitMaxMessages ? 2 : 1;
     }
-    if (form == 4 || form == 5) {
-        // form 4: the same-round quad; 5: the lag quad (MXEC_SHA_LAG_PIN=0
-        // leaves its step order to the compiler, lab A/B).
-        const char* pin = getenv("MXEC_SHA_LAG_PIN");
-        const int var = form == 4 ? 0 : pin && atoi(pin) == 0 ? 1 : 2;
+    if (form == 4 || form == 5) {  // 4: the same-round quad (lab A/B), 5: the lag quad
         const dim3 grid((a.n + kShaQuadMsgs - 1) / kShaQuadMsgs);
-        auto k = var == 0 ? sha256_quad_kernel<0> : var == 1 ? sha256_quad_kernel<1> : sha256_quad_kernel<2>;
-        hipLaunchKernelGGL(k, grid, dim3(256), 0, s, a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n,
-                           sha_prio());
+        hipLaunchKernelGGL(form == 5 ? sha256_quad_kernel<true> : sha256_quad_kernel<false>, grid, dim3(256), 0, s,
+                           a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
         return hipGetLastError();
     }
     if (form == 3) {

@@ -374,20 +374,15 @@ def test_short_last_chunk_device_encode_and_rebuild(ctx, last):
     assert np.array_equal(got[:, 2], host[:, 2])
 
 
-# MXEC_SHA_FORM pins the SHA-256 kernel (quad: four lanes per message behind a
-# producer wave, e-side and a-side of a round in one instruction stream; lag:
-# the same with lane A two rounds behind lane E, pinned step order; lag-nopin:
-# the lag form in the compiler's order; split: producer/consumer waves; one:
-# one wave per 64 messages).
-SHA_FORMS = ["quad", "lag", "lag-nopin", "split", "one"]
+# MXEC_SHA_FORM pins the SHA-256 kernel (lag: the default quad form, four
+# lanes per message behind a producer wave with the a-side two rounds behind
+# the e-side; quad: the same-round quad form; split: producer/consumer waves;
+# one: one wave per 64 messages).
+SHA_FORMS = ["lag", "quad", "split", "one"]
 
 
 def _pin_sha_form(monkeypatch, form):
-    monkeypatch.setenv("MXEC_SHA_FORM", "lag" if form == "lag-nopin" else form)
-    if form == "lag-nopin":
-        monkeypatch.setenv("MXEC_SHA_LAG_PIN", "0")
-    else:
-        monkeypatch.delenv("MXEC_SHA_LAG_PIN", raising=False)
+    monkeypatch.setenv("MXEC_SHA_FORM", form)
 
 
 @pytest.mark.parametrize("form", SHA_FORMS)
