@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <functional>
 
+#include "kernels.hpp"
 #include "ops.hpp"
 
 namespace mxec {
@@ -91,14 +92,18 @@ struct ShaCombiner {
         for (const Req* r : batch)
             if (r->ready) MXEC_HIP(hipStreamWaitEvent(s, r->ready, 0));
         MXEC_TRY(slot.digests.grow(n * 32));
-        // The split (producer / consumer) form up to 3/4 of a 64-message
-        // group per SIMD; beyond, the stream form (segments of every chain
-        // dealt to persistent waves) keeps every SIMD busy to the end
-        // (81 920 x 1 MiB: 55.8 ms vs 96.1 split); its timeout word comes
-        // back with the digests.
+        // The kernel's own choice by message count: the quad (lag) form up
+        // to 48 messages per CU, the split form up to 3/4 of a 64-message
+        // group per SIMD, beyond that the stream form (segments of every
+        // chain dealt to persistent waves keep every SIMD busy to the end:
+        // 81 920 x 1 MiB 55.8 ms vs 96.1 split), whose timeout word comes
+        // back with the digests.  (Until late round 3 this call pinned the
+        // split form below the stream size, so combined verifications -- a
+        // lone GET's included -- never got the quad forms: configs[0]'s
+        // 10 MiB GET took 280 ms against a 203 ms chain.)
         const uint32_t* tmo = nullptr;
         MXEC_TRY(run_sha(d, slot, s, ptrs, lens, static_cast<uint8_t*>(slot.digests.p), nullptr, nullptr, nullptr,
-                         nullptr, sha_stream_size((n + 63) / 64, uint64_t(d.n_cus) * 4) ? 0 : 2, &tmo));
+                         nullptr, 0, &tmo));
         // The callers' work to run beside the hash is queued before this
         // launch's digest copy: copies of different streams can share a copy
         // engine queue in submission order, and work queued behind the
@@ -187,7 +192,7 @@ namespace {
 
 // MXEC_COMBINE_STREAMS: launches in flight per device (default 2).  A second
 // launch starts beside a running one only while both together stay under
-// one workgroup per CU of messages (lane_limit): light request traffic then
+// one quad-form workgroup per CU of messages (lane_limit): light request traffic then
 // no longer waits out the batch in flight (16-thread GET 2.5 -> 3.5 GiB/s,
 // profiles/r1_combine_lanes2.txt), while chip-filling batches still go one
 // at a time -- unconditional lanes split them and issue-bound launches side
@@ -227,7 +232,9 @@ ShaCombiner* combiner_of(Device& d) {
             c->free_slots.push_back(sl.get());
             c->slots.push_back(std::move(sl));
         }
-        c->lane_limit = size_t(d.n_cus) * 64;
+        // Both lanes' launches together within one quad-form workgroup
+        // (48 messages, one wave per SIMD) per CU.
+        c->lane_limit = size_t(d.n_cus) * kShaQuadMsgs;
         d.comb = c;
     }
     return static_cast<ShaCombiner*>(d.comb.get());
