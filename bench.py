@@ -1282,7 +1282,32 @@ def pcie_rates(torch, devs, nbytes: int = 1 << 30) -> dict:
         t0 = time.perf_counter()
         go(4)
         out[f"{name}_GBps"] = round(4 * nbytes * len(devs) / (time.perf_counter() - t0) / 1e9, 1)
-    del hb, db
+    # Both directions at once in the PUT / GET legs' 2:1 byte ratio (4 shards
+    # up, 2 down per object): two bytes up for every byte down, on separate
+    # streams, every device together.  A PCIe link is full duplex, but the
+    # DMA engines and host memory are shared, so this sets the legs' real
+    # bound when it is below the one-way rates added together.
+    hb2 = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in devs]
+    db2 = [torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", d)) for d in devs]
+    st2 = [torch.cuda.Stream(device=torch.device("cuda", d)) for d in devs]
+
+    def duplex(reps):
+        for _ in range(reps):
+            for h, d, h2, d2, s, s2 in zip(hb, db, hb2, db2, st, st2):
+                with torch.cuda.stream(s):
+                    d.copy_(h, non_blocking=True)
+                    d.copy_(h, non_blocking=True)
+                with torch.cuda.stream(s2):
+                    h2.copy_(d2, non_blocking=True)
+        sync_all(torch, devs)
+
+    duplex(1)
+    t0 = time.perf_counter()
+    duplex(2)
+    el = time.perf_counter() - t0
+    out["duplex_2to1_up_GBps"] = round(4 * nbytes * len(devs) / el / 1e9, 1)
+    out["duplex_2to1_down_GBps"] = round(2 * nbytes * len(devs) / el / 1e9, 1)
+    del hb, db, hb2, db2
     return out
 
 
@@ -1315,6 +1340,8 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
     h2d_s = n * k * S / (rates["h2d_GBps"] * 1e9)
     d2h_s = n * m * S / (rates["d2h_GBps"] * 1e9)
     bound_s = max(h2d_s, d2h_s)
+    # The same bytes at the measured simultaneous 2:1 rates (pcie_rates).
+    duplex_s = max(n * k * S / (rates["duplex_2to1_up_GBps"] * 1e9), n * m * S / (rates["duplex_2to1_down_GBps"] * 1e9))
     dig_all = None
     for sha in (False, True):
         dig = np.zeros(n * (k + m) * 32, np.uint8) if sha else None
@@ -1329,7 +1356,8 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
         payload = reduce_sum(float(n * k * S))
         key = "rs_sha256" if sha else "rs_only"
         res[key] = {"s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
-                    "frac_of_pcie_bound": round(bound_s / el, 4)}
+                    "frac_of_pcie_bound": round(bound_s / el, 4),
+                    "frac_of_duplex_bound": round(duplex_s / el, 4)}
     # GET side (chunk_reader.rs:157-226 from the shard files in host memory):
     # mxec_reconstruct_batch_host over the same objects with two seeded
     # erasures each -- the 4 present shards go up, the 2 rebuilt ones come
@@ -1345,6 +1373,8 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
             present0[o * (k + m) + i] = 0
     get_up_s = n * (k + m - 2) * S / (rates["h2d_GBps"] * 1e9)
     get_down_s = n * 2 * S / (rates["d2h_GBps"] * 1e9)
+    get_duplex_s = max(n * (k + m - 2) * S / (rates["duplex_2to1_up_GBps"] * 1e9),
+                       n * 2 * S / (rates["duplex_2to1_down_GBps"] * 1e9))
     for verify in (False, True):
         exp = dig_all if verify else None
         pr = present0.copy()
@@ -1360,7 +1390,8 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
         payload = reduce_sum(float(n * k * S))
         res["get_verify_sha256" if verify else "get_rs_only"] = {
             "s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
-            "frac_of_pcie_bound": round(max(get_up_s, get_down_s) / el, 4)}
+            "frac_of_pcie_bound": round(max(get_up_s, get_down_s) / el, 4),
+            "frac_of_duplex_bound": round(get_duplex_s / el, 4)}
     if plan.rank == 0:
         # the rebuilt shards of one object, scribbled first, come back exact
         o = n // 3
@@ -1373,8 +1404,10 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
         got = [data[o, j] for j in range(k)] + [par[o, i] for i in range(m)]
         res["get_spot_check"] = rc == 0 and all(np.array_equal(a, b) for a, b in zip(got, want))
     res["pcie_bound_s_per_batch"] = round(bound_s, 4)
+    res["duplex_bound_s_per_batch"] = round(duplex_s, 4)
     res["bound"] = ("max(upload k*S*n / h2d_GBps, download m*S*n / d2h_GBps), the raw pinned copy rates "
-                    "measured above on the same devices at once")
+                    "measured above on the same devices at once; duplex bound: the same bytes at the rates "
+                    "measured with both directions running at once in a 2:1 ratio")
     if plan.rank == 0:
         o = n // 2
         want = _oracle().encode(list(data[o]), m, S)

@@ -76,6 +76,22 @@ uint64_t rs_tile_bytes(const RsVariant& v);
 
 // SHA-256 over n messages, one lane per message.  If `expected` is set the
 // kernel also writes ok[i] = (digest == expected[i]).
+// Piece mode of the quad forms (the host pipeline hashes every chunk piece by
+// piece while later pieces still upload): launch message i is the next piece
+// of the chain kept in state slot slot[i].  With resume the chain continues
+// from state[slot] (else from the IV).  total[i] == kShaNotFinal: the piece
+// ends mid-message (a multiple of 64 bytes) and the running state goes back
+// to state[slot]; otherwise it is the last piece of a total[i]-byte message,
+// padded and finished into digests[slot] (ok[slot] against
+// expected[exp_idx ? exp_idx[slot] : slot]).
+constexpr uint64_t kShaNotFinal = ~uint64_t(0);
+struct ShaPiece {
+    uint32_t* state = nullptr;        // [slots][8] (a..h); null: whole messages
+    const uint32_t* slot = nullptr;   // [n]
+    const uint64_t* total = nullptr;  // [n]
+    uint32_t resume = 0;
+};
+
 struct ShaArgs {
     const uint8_t* const* ptrs;  // [n]
     const uint64_t* lens;        // [n]
@@ -86,7 +102,8 @@ struct ShaArgs {
     uint8_t* ok;                 // [n] or null
     uint32_t n;
     int force = 0;               // 0 auto, 1 one wave per 64 messages, 2 split,
-                                 // 3 stream (needs the fields below), 4 quad
+                                 // 3 stream (needs the fields below), 4 quad,
+                                 // 5 lag quad
     uint32_t n_cus = 0;          // the device's CUs (auto form choice; 0: 256)
     // Stream form (batches of more 64-message groups than the chip has
     // SIMDs): persistent waves take (group, segment) items in segment-major
@@ -98,6 +115,7 @@ struct ShaArgs {
     uint32_t waves = 0;          // persistent waves
     uint32_t wg_waves = 1;       // waves per workgroup (1 or 4; waves divisible by it)
     uint32_t seg_max = 0;        // segments of the longest message
+    ShaPiece piece;              // piece mode (quad forms, force 4 or 5 only)
 };
 // Messages per workgroup of the quad form (three consumer waves of 16).
 constexpr uint32_t kShaQuadMsgs = 48;

@@ -560,4 +560,51 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     return w.finish(s);
 }
 
+int run_sha_pieces(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
+                   const std::vector<uint64_t>& lens, const std::vector<uint32_t>& slots,
+                   const std::vector<uint64_t>& totals, uint32_t* state_dev, bool resume, uint8_t* digests_dev,
+                   DescArena* arena, const uint8_t* expected_dev, uint8_t* ok_dev) {
+    const size_t n = ptrs.size();
+    if (!n) return MXEC_OK;
+    if (lens.size() != n || slots.size() != n || totals.size() != n || !state_dev ||
+        n > uint64_t(kShaQuadMsgs) * uint64_t(dev.n_cus ? dev.n_cus : 256))
+        return set_error(MXEC_E_INVALID_ARG, "sha pieces: table sizes or message count");
+    for (size_t i = 0; i < n; ++i)
+        if (totals[i] == kShaNotFinal ? lens[i] % 64 != 0 : totals[i] < lens[i])
+            return set_error(MXEC_E_INVALID_ARG, "sha pieces: a mid-message piece must be whole 64-byte blocks");
+    if (affinity_on()) {
+        std::vector<const void*> ps(ptrs.begin(), ptrs.end());
+        ps.push_back(digests_dev);
+        ps.push_back(state_dev);
+        MXEC_TRY(affinity_check(dev, &slot, s, "run_sha_pieces", arena, ps.data(), ps.size()));
+    }
+    DescWriter w(slot, arena);
+    const size_t o_p = w.add(sizeof(void*) * n);
+    const size_t o_l = w.add(8 * n);
+    const size_t o_t = w.add(8 * n);
+    const size_t o_s = w.add(4 * n);
+    char* hb = w.data();
+    std::memcpy(hb + o_p, ptrs.data(), sizeof(void*) * n);
+    std::memcpy(hb + o_l, lens.data(), 8 * n);
+    std::memcpy(hb + o_t, totals.data(), 8 * n);
+    std::memcpy(hb + o_s, slots.data(), 4 * n);
+    char* db = nullptr;
+    MXEC_TRY(w.commit(s, &db));
+    ShaArgs a{};
+    a.ptrs = reinterpret_cast<const uint8_t* const*>(db + o_p);
+    a.lens = reinterpret_cast<const uint64_t*>(db + o_l);
+    a.digests = digests_dev;
+    a.expected = expected_dev;
+    a.ok = ok_dev;
+    a.n = uint32_t(n);
+    a.n_cus = uint32_t(dev.n_cus);
+    a.force = 5;
+    a.piece.state = state_dev;
+    a.piece.slot = reinterpret_cast<const uint32_t*>(db + o_s);
+    a.piece.total = reinterpret_cast<const uint64_t*>(db + o_t);
+    a.piece.resume = resume ? 1u : 0u;
+    MXEC_HIP(launch_sha256(a, s));
+    return w.finish(s);
+}
+
 }  // namespace mxec

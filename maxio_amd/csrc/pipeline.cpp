@@ -20,6 +20,7 @@
 //     after the SHA launch, direct to pinned destinations or via a pinned ring.
 // Results are bit-identical to mxec_encode (same kernels, same planner).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <system_error>
@@ -29,6 +30,7 @@
 
 #include "../../include/maxio_ec.h"
 #include "deal.hpp"
+#include "kernels.hpp"
 #include "ops.hpp"
 
 namespace mxec {
@@ -118,6 +120,7 @@ struct PipeRes {
     PinRing in, out;
     DescArena arena;
     DevBuf pool, digests;
+    DevBuf chain_state;  // SHA-256 chain states between pieces (host reconstruct)
     PinnedBuf flags;  // verification verdicts read back (host reconstruct)
     Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
     bool ready = false;
@@ -153,7 +156,7 @@ class DevicePipeline {
 public:
     DevicePipeline(Device& d, PipeRes& r)
         : d_(d), h2d_(r.h2d), d2h_(r.d2h), cs_(r.cs), in_(r.in), out_(r.out), arena_(r.arena),
-          pool_(r.pool), scratch_(r.digests), flags_(r.flags), slot_(r.desc_slot) {}
+          pool_(r.pool), scratch_(r.digests), state_(r.chain_state), flags_(r.flags), slot_(r.desc_slot) {}
     ~DevicePipeline() {
         for (auto e : events_) (void)hipEventDestroy(e);
     }
@@ -245,56 +248,27 @@ private:
             ok = static_cast<uint8_t*>(scratch_.p);
             exp = ok + fo;
         }
-        // Phase 1: every upload, one event per group.
-        std::vector<hipEvent_t> up(groups.size());
-        uint64_t g = 0;
-        for (size_t q = 0; q < groups.size(); ++q) {
-            for (size_t o = groups[q].first; o < groups[q].second; ++o) {
-                const RecObj& h = objs[o];
-                for (int i = 0; i < h.k + h.m; ++i) {
-                    if (!h.present[i]) continue;
-                    MXEC_TRY(queue_up(base + h.pool_off + uint64_t(i) * h.slot(), h.shards[i], h.len[i]));
-                    if (h.len[i] != h.slot()) MXEC_TRY(flush_up());
-                }
-                MXEC_TRY(flush_up());
-                if (h.expected) MXEC_TRY(queue_up(exp + g * 32, &h.expected[0][0], uint64_t(h.k + h.m) * 32));
-                g += uint64_t(h.k + h.m);
-            }
-            MXEC_TRY(flush_up());
-            MXEC_TRY(new_event(&up[q]));
-            MXEC_HIP(hipEventRecord(up[q], h2d_));
-        }
-        // Phase 2 (verification only): one launch over every present shard
-        // of the objects that carry digests, verdicts read back.
-        if (verify) {
-            std::vector<const uint8_t*> sp;
-            std::vector<uint64_t> sl, idx;
-            std::vector<std::pair<size_t, int>> who;  // message -> (object, shard)
-            g = 0;
-            for (size_t o = o0; o < o1; ++o) {
-                const RecObj& h = objs[o];
-                for (int i = 0; i < h.k + h.m; ++i, ++g) {
-                    if (!h.expected || !h.present[i]) continue;
-                    sp.push_back(base + h.pool_off + uint64_t(i) * h.slot());
-                    sl.push_back(h.len[i]);
-                    idx.push_back(g);
-                    who.emplace_back(o, i);
-                }
-            }
-            MXEC_HIP(hipStreamWaitEvent(cs, up.back(), 0));
-            if (!sp.empty()) {
-                MXEC_TRY(run_sha(d_, slot_, cs, sp, sl, nullptr, exp, ok, &idx, &arena_));
-                MXEC_TRY(flags_.ensure(sp.size()));
-                MXEC_HIP(hipMemcpyAsync(flags_.p, ok, sp.size(), hipMemcpyDeviceToHost, cs));
-                MXEC_HIP(hipStreamSynchronize(cs));
-                const auto* okh = static_cast<const uint8_t*>(flags_.p);
-                for (size_t t = 0; t < who.size(); ++t)
-                    if (!okh[t]) objs[who[t].first].present[who[t].second] = 0;
-            }
+        uint64_t vmsgs = 0;  // present shards to verify
+        for (size_t o = o0; o < o1; ++o)
+            if (objs[o].expected)
+                for (int i = 0; i < objs[o].k + objs[o].m; ++i) vmsgs += objs[o].present[i] ? 1 : 0;
+        const uint64_t P = piece_bytes();
+        std::vector<hipEvent_t> up;  // per group (group form): its upload is done
+        if (verify && P && vmsgs && vmsgs <= uint64_t(kShaQuadMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256)) {
+            // Piece-major upload + verification (the PUT wave's scheme, see
+            // wave_pieces): piece p of every present shard goes up and is
+            // hashed, chains carried in state slots, so every chain starts
+            // after the first piece instead of after the whole upload; the
+            // verdicts come back after the last piece, then the rebuild as
+            // below (nothing is written to the caller's buffers before).
+            MXEC_TRY(verify_in_pieces(objs, o0, o1, ok, exp, msgs, P));
+        } else {
+            MXEC_TRY(upload_and_verify(objs, o0, o1, groups, ok, exp, verify, cs, &up));
         }
         // Phase 3: per group, rebuild once it is up, then its shards down.
         for (size_t q = 0; q < groups.size(); ++q) {
             const size_t q0 = groups[q].first, q1 = groups[q].second;
+            // without verification a group is rebuilt as soon as it is up
             if (!verify) MXEC_HIP(hipStreamWaitEvent(cs, up[q], 0));
             std::vector<std::shared_ptr<const DecodePlan>> plans(q1 - q0);
             std::vector<uint32_t> offs(q1 - q0);
@@ -363,6 +337,121 @@ private:
         return flush();
     }
 
+    // Piece-major upload of every present shard (and the expected digests),
+    // each piece of the shards to verify hashed as soon as it is up with the
+    // chains carried in device state slots (run_sha_pieces, slot = message
+    // index in the wave, verdict ok[slot]); after the last piece the verdicts
+    // come back and a mismatch becomes an erasure (chunk_reader.rs:176-196).
+    // Leaves cs after every upload.
+    int verify_in_pieces(std::vector<RecObj>& objs, size_t o0, size_t o1, uint8_t* ok, uint8_t* exp, uint64_t msgs,
+                         uint64_t P) {
+        uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        hipStream_t cs = cs_[0];
+        MXEC_TRY(state_.ensure(msgs * 32));
+        uint32_t* state = static_cast<uint32_t*>(state_.p);
+        uint64_t longest = 0;
+        for (size_t o = o0; o < o1; ++o)
+            for (int i = 0; i < objs[o].k + objs[o].m; ++i)
+                if (objs[o].present[i]) longest = std::max(longest, objs[o].len[i]);
+        const uint64_t npieces = std::max<uint64_t>(1, (longest + P - 1) / P);
+        for (uint64_t pc = 0; pc < npieces; ++pc) {
+            const uint64_t off = pc * P;
+            uint64_t g = 0;
+            std::vector<const uint8_t*> sp;
+            std::vector<uint64_t> sl, st;
+            std::vector<uint32_t> ss;
+            for (size_t o = o0; o < o1; ++o) {
+                const RecObj& h = objs[o];
+                if (pc == 0 && h.expected) MXEC_TRY(queue_up(exp + g * 32, &h.expected[0][0], uint64_t(h.k + h.m) * 32));
+                for (int i = 0; i < h.k + h.m; ++i, ++g) {
+                    if (!h.present[i]) continue;
+                    const uint64_t L = h.len[i];
+                    uint8_t* dev = base + h.pool_off + uint64_t(i) * h.slot();
+                    if (off < L) MXEC_TRY(queue_up(dev + off, h.shards[i] + off, std::min(P, L - off)));
+                    if (!h.expected || (off >= L && !(pc == 0 && L == 0))) continue;
+                    const uint64_t len = L > off ? std::min(P, L - off) : 0;
+                    sp.push_back(dev + off);
+                    sl.push_back(len);
+                    st.push_back(off + len == L ? L : kShaNotFinal);
+                    ss.push_back(uint32_t(g));
+                }
+            }
+            MXEC_TRY(flush_up());
+            hipEvent_t up;
+            MXEC_TRY(new_event(&up));
+            MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
+            if (!sp.empty())
+                MXEC_TRY(run_sha_pieces(d_, slot_, cs, sp, sl, ss, st, state, pc > 0, nullptr, &arena_, exp, ok));
+        }
+        MXEC_TRY(flags_.ensure(msgs));
+        MXEC_HIP(hipMemcpyAsync(flags_.p, ok, msgs, hipMemcpyDeviceToHost, cs));
+        MXEC_HIP(hipStreamSynchronize(cs));
+        const auto* okh = static_cast<const uint8_t*>(flags_.p);
+        uint64_t g = 0;
+        for (size_t o = o0; o < o1; ++o) {
+            RecObj& h = objs[o];
+            for (int i = 0; i < h.k + h.m; ++i, ++g)
+                if (h.expected && h.present[i] && !okh[g]) h.present[i] = 0;
+        }
+        return MXEC_OK;
+    }
+
+    // Phase 1: every upload, one event per group; phase 2 (verification
+    // only): one launch over every present shard of the objects that carry
+    // digests once all are up, verdicts read back.
+    int upload_and_verify(std::vector<RecObj>& objs, size_t o0, size_t o1,
+                          const std::vector<std::pair<size_t, size_t>>& groups, uint8_t* ok, uint8_t* exp, bool verify,
+                          hipStream_t cs, std::vector<hipEvent_t>* up_out) {
+        uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        std::vector<hipEvent_t>& up = *up_out;
+        up.assign(groups.size(), nullptr);
+        uint64_t g = 0;
+        for (size_t q = 0; q < groups.size(); ++q) {
+            for (size_t o = groups[q].first; o < groups[q].second; ++o) {
+                const RecObj& h = objs[o];
+                for (int i = 0; i < h.k + h.m; ++i) {
+                    if (!h.present[i]) continue;
+                    MXEC_TRY(queue_up(base + h.pool_off + uint64_t(i) * h.slot(), h.shards[i], h.len[i]));
+                    if (h.len[i] != h.slot()) MXEC_TRY(flush_up());
+                }
+                MXEC_TRY(flush_up());
+                if (h.expected) MXEC_TRY(queue_up(exp + g * 32, &h.expected[0][0], uint64_t(h.k + h.m) * 32));
+                g += uint64_t(h.k + h.m);
+            }
+            MXEC_TRY(flush_up());
+            MXEC_TRY(new_event(&up[q]));
+            MXEC_HIP(hipEventRecord(up[q], h2d_));
+        }
+        if (verify) {
+            std::vector<const uint8_t*> sp;
+            std::vector<uint64_t> sl, idx;
+            std::vector<std::pair<size_t, int>> who;  // message -> (object, shard)
+            g = 0;
+            for (size_t o = o0; o < o1; ++o) {
+                const RecObj& h = objs[o];
+                for (int i = 0; i < h.k + h.m; ++i, ++g) {
+                    if (!h.expected || !h.present[i]) continue;
+                    sp.push_back(base + h.pool_off + uint64_t(i) * h.slot());
+                    sl.push_back(h.len[i]);
+                    idx.push_back(g);
+                    who.emplace_back(o, i);
+                }
+            }
+            MXEC_HIP(hipStreamWaitEvent(cs, up.back(), 0));
+            if (!sp.empty()) {
+                MXEC_TRY(run_sha(d_, slot_, cs, sp, sl, nullptr, exp, ok, &idx, &arena_));
+                MXEC_TRY(flags_.ensure(sp.size()));
+                MXEC_HIP(hipMemcpyAsync(flags_.p, ok, sp.size(), hipMemcpyDeviceToHost, cs));
+                MXEC_HIP(hipStreamSynchronize(cs));
+                const auto* okh = static_cast<const uint8_t*>(flags_.p);
+                for (size_t t = 0; t < who.size(); ++t)
+                    if (!okh[t]) objs[who[t].first].present[who[t].second] = 0;
+            }
+        }
+        return MXEC_OK;
+    }
+
     struct Pending {  // ring DMA to copy out into pageable memory
         int ring;
         uint8_t* dst;
@@ -377,6 +466,7 @@ private:
     DescArena& arena_;
     DevBuf& pool_;
     DevBuf& scratch_;  // the wave's digests, message order
+    DevBuf& state_;    // chain states of a piece-major verification
     PinnedBuf& flags_;
     Slot& slot_;
     std::vector<Pending> pend_;
@@ -495,7 +585,152 @@ private:
         return MXEC_OK;
     }
 
+    // Piece-major form of a wave with digests (MXEC_PIPE_PIECE_MB, default 1;
+    // 0 = the group form below).  The group form uploads object after object
+    // and hashes once all parity exists, so the last-uploaded chunk's chain
+    // (163 840 blocks for 10 MiB) starts after the whole upload: 94 + 203 ms
+    // for 128 x 4+2 x 10 MiB.  Here piece p (bytes [pP, (p+1)P) of every
+    // chunk) goes up, is encoded, hashed -- the chains carried from piece to
+    // piece in device state slots (run_sha_pieces) -- and its parity goes
+    // down, piece after piece, so every chain starts after the first piece
+    // (~9 ms) and the wave ends near one chain's length.  Taken when the
+    // wave's messages fit the lag quad form (48 per CU).
+    static uint64_t piece_bytes() {  // read per wave (tests and labs switch it)
+        const char* e = getenv("MXEC_PIPE_PIECE_MB");
+        const long v = e ? atol(e) : 1;
+        return v <= 0 ? uint64_t(0) : uint64_t(v) << 20;
+    }
+
+    int wave_pieces(std::vector<HostObj>& objs, size_t o0, size_t o1, uint64_t P) {
+        Slot& slot = slot_;
+        uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        // Chains: every chunk of every object that wants digests, message order.
+        struct Chain {
+            uint8_t* dev;
+            uint64_t len;
+        };
+        std::vector<Chain> ch;
+        uint64_t longest = 0;
+        for (size_t o = o0; o < o1; ++o) {
+            const HostObj& h = objs[o];
+            longest = std::max(longest, h.S);
+            if (!h.dig) continue;
+            for (int j = 0; j < h.k + h.m; ++j)
+                ch.push_back(Chain{base + h.pool_off + uint64_t(j) * h.slot(),
+                                   j < h.k ? std::min<uint64_t>(h.dlen[j], h.S) : h.S});
+        }
+        const uint64_t nm = ch.size();
+        MXEC_TRY(scratch_.ensure(nm * 64));  // digests [nm][32], then chain states [nm][8] words
+        uint8_t* digests = static_cast<uint8_t*>(scratch_.p);
+        uint32_t* state = reinterpret_cast<uint32_t*>(digests + nm * 32);
+        const uint64_t npieces = std::max<uint64_t>(1, (longest + P - 1) / P);
+        hipStream_t rs_s = cs_[0], sha_s = cs_[1];
+        hipEvent_t sha_done = nullptr;
+        for (uint64_t pc = 0; pc < npieces; ++pc) {
+            const uint64_t off = pc * P;
+            for (size_t o = o0; o < o1; ++o) {
+                const HostObj& h = objs[o];
+                for (int j = 0; j < h.k; ++j) {
+                    const uint64_t L = std::min<uint64_t>(h.dlen[j], h.S);
+                    if (off < L)
+                        MXEC_TRY(queue_up(base + h.pool_off + uint64_t(j) * h.slot() + off, h.data[j] + off,
+                                          std::min(P, L - off)));
+                }
+            }
+            MXEC_TRY(flush_up());
+            hipEvent_t up, rs_done;
+            MXEC_TRY(new_event(&up));
+            MXEC_TRY(new_event(&rs_done));
+            MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_HIP(hipStreamWaitEvent(rs_s, up, 0));
+            // Parity of this piece: RS is bytewise, so bytes [off, off + P) of
+            // the parity come from the same bytes of the data (short data
+            // chunks read as zeros past their end, as in the whole-chunk form).
+            std::map<std::tuple<int, int, uint64_t>, std::vector<size_t>> classes;
+            for (size_t o = o0; o < o1; ++o)
+                if (objs[o].S > off) classes[{objs[o].k, objs[o].m, objs[o].S}].push_back(o);
+            for (auto& c : classes) {
+                const int k = std::get<0>(c.first), m = std::get<1>(c.first);
+                const uint64_t S = std::get<2>(c.first), W = std::min(P, S - off);
+                uint32_t coff = 0;
+                const size_t n = c.second.size();
+                std::vector<const uint8_t*> ins(n * size_t(k));
+                std::vector<uint8_t*> outs(n * size_t(m));
+                std::vector<uint64_t> lens(n * size_t(k + m), W);
+                std::vector<RsObject> ro(n);
+                for (size_t t = 0; t < n; ++t) {
+                    const HostObj& h = objs[c.second[t]];
+                    uint8_t* ob = base + h.pool_off + off;
+                    for (int j = 0; j < k; ++j) {
+                        ins[t * k + j] = ob + uint64_t(j) * h.slot();
+                        const uint64_t L = std::min<uint64_t>(h.dlen[j], S);
+                        lens[t * (k + m) + j] = L > off ? std::min(W, L - off) : 0;
+                    }
+                    for (int i = 0; i < m; ++i) outs[t * m + i] = ob + uint64_t(k + i) * h.slot();
+                    ro[t] = RsObject{&ins[t * k], &lens[t * (k + m)], &outs[t * m], &lens[t * (k + m) + k], 0};
+                }
+                MXEC_TRY(with_stable_coef(
+                    d_, [&] { return encode_coef(d_, k, m, &coff); },
+                    [&] {
+                        for (auto& r : ro) r.coef_off = coff;
+                        return run_rs(d_, slot, rs_s, W, k, m, ro, &arena_);
+                    }));
+            }
+            MXEC_HIP(hipEventRecord(rs_done, rs_s));
+            // This piece of every chain (the hash stream runs the pieces in
+            // order, each continuing the chains the previous one left).
+            std::vector<const uint8_t*> sp;
+            std::vector<uint64_t> sl, st;
+            std::vector<uint32_t> ss;
+            for (uint64_t q = 0; q < nm; ++q) {
+                const Chain& c = ch[q];
+                if (off >= c.len && !(pc == 0 && c.len == 0)) continue;  // ended in an earlier piece
+                const uint64_t len = c.len > off ? std::min(P, c.len - off) : 0;
+                sp.push_back(c.dev + off);
+                sl.push_back(len);
+                st.push_back(off + len == c.len ? c.len : kShaNotFinal);
+                ss.push_back(uint32_t(q));
+            }
+            if (!sp.empty()) {
+                MXEC_HIP(hipStreamWaitEvent(sha_s, rs_done, 0));
+                MXEC_TRY(run_sha_pieces(d_, slot, sha_s, sp, sl, ss, st, state, pc > 0, digests, &arena_));
+            }
+            // This piece of every parity chunk goes down.
+            MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
+            for (size_t o = o0; o < o1; ++o) {
+                const HostObj& h = objs[o];
+                if (h.S <= off) continue;
+                uint8_t* ob = base + h.pool_off + off;
+                for (int i = 0; i < h.m; ++i)
+                    MXEC_TRY(queue_down(h.parity[i] + off, ob + uint64_t(h.k + i) * h.slot(), std::min(P, h.S - off)));
+            }
+            MXEC_TRY(flush_down());
+        }
+        if (nm) {
+            MXEC_TRY(new_event(&sha_done));
+            MXEC_HIP(hipEventRecord(sha_done, sha_s));
+            MXEC_HIP(hipStreamWaitEvent(d2h_, sha_done, 0));
+            uint64_t msg0 = 0;
+            for (size_t o = o0; o < o1; ++o) {
+                const HostObj& h = objs[o];
+                if (!h.dig) continue;
+                MXEC_TRY(queue_down(reinterpret_cast<uint8_t*>(h.dig), digests + msg0 * 32, uint64_t(h.k + h.m) * 32));
+                msg0 += uint64_t(h.k + h.m);
+            }
+            MXEC_TRY(flush_down());
+        }
+        return flush();
+    }
+
     int wave(std::vector<HostObj>& objs, size_t o0, size_t o1) {
+        {
+            uint64_t msgs = 0;
+            for (size_t o = o0; o < o1; ++o)
+                if (objs[o].dig) msgs += uint64_t(objs[o].k + objs[o].m);
+            const uint64_t P = piece_bytes();
+            if (P && msgs && msgs <= uint64_t(kShaQuadMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256))
+                return wave_pieces(objs, o0, o1, P);
+        }
         Slot& slot = slot_;
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         uint64_t msgs = 0;

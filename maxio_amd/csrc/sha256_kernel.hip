@@ -541,7 +541,8 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
                                                          uint8_t* __restrict__ digests,
                                                          const uint8_t* __restrict__ expected,
                                                          const uint64_t* __restrict__ exp_idx,
-                                                         uint8_t* __restrict__ ok, uint32_t n, uint32_t prio) {
+                                                         uint8_t* __restrict__ ok, uint32_t n, uint32_t prio,
+                                                         ShaPiece pc) {
     constexpr int NB = 3, BUF = 16 * kQuadRow;
     sha_priority(prio);
     __shared__ u32x4 kw[NB][16][kQuadRow];
@@ -581,8 +582,20 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     q.sh2 = role == 0 ? 11 : 13;
     q.sh3 = role == 0 ? 25 : 22;
     q.ma = role == 1 ? ~0u : 0u;
+    // Piece mode: the launch's message i is state slot pc.slot[i] (digest,
+    // ok and running state are indexed by the slot).
+    const uint32_t slot = live && pc.state ? pc.slot[i] : i;
     uint32_t s[4] = {0, 0, 0, 0};
-    if (role == 0) {
+    if (live && pc.resume && role < 2) {  // continue the chain (a..h in state[slot])
+        const uint32_t* sv = pc.state + 8 * uint64_t(slot);
+        if (role == 0) {
+            s[0] = sv[4]; s[1] = sv[5]; s[2] = sv[6]; s[3] = sv[7];
+        } else if (LAG) {  // (c, d, a, b)
+            s[0] = sv[2]; s[1] = sv[3]; s[2] = sv[0]; s[3] = sv[1];
+        } else {
+            s[0] = sv[0]; s[1] = sv[1]; s[2] = sv[2]; s[3] = sv[3];
+        }
+    } else if (role == 0) {
         s[0] = 0x510e527fu; s[1] = 0x9b05688cu; s[2] = 0x1f83d9abu; s[3] = 0x5be0cd19u;
     } else if (role == 1 && LAG) {  // (c, d, a, b)
         s[0] = 0x3c6ef372u; s[1] = 0xa54ff53au; s[2] = 0x6a09e667u; s[3] = 0xbb67ae85u;
@@ -624,10 +637,17 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
         st[4 + t] = s[t];
     }
     if (role != 0 || !live) return;
+    const uint64_t total = pc.state ? pc.total[i] : len;
+    if (total == kShaNotFinal) {  // mid-message piece: the running state goes back
+        uint32_t* sv = pc.state + 8 * uint64_t(slot);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) sv[t] = st[t];
+        return;
+    }
     const uint32_t rem = uint32_t(len - nfull * 64);
     const uint8_t* tp = p + nfull * 64;
     const int nblk = (rem + 9 <= 64) ? 1 : 2;
-    const uint64_t bits = len * 8;
+    const uint64_t bits = total * 8;
     uint32_t w[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) w[t] = tail_word(tp, rem, t, nblk, bits);
@@ -638,14 +658,14 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
         compress(st, w);
     }
     bool match = true;
-    const uint64_t ei = exp_idx ? exp_idx[i] : i;
+    const uint64_t ei = exp_idx ? exp_idx[slot] : slot;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         const uint32_t be = bswap(st[t]);
-        if (digests) reinterpret_cast<uint32_t*>(digests + 32 * uint64_t(i))[t] = be;
+        if (digests) reinterpret_cast<uint32_t*>(digests + 32 * uint64_t(slot))[t] = be;
         if (expected) match &= reinterpret_cast<const uint32_t*>(expected + 32 * ei)[t] == be;
     }
-    if (ok) ok[i] = match ? 1 : 0;
+    if (ok) ok[slot] = match ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -884,10 +904,11 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         else if (env && !strcmp(env, "lag")) form = 5;
         else form = a.n <= kShaQuadMsgs * n_cus ? kShaQuadAuto : a.n <= kSplitMaxMessages ? 2 : 1;
     }
+    if (a.piece.state && form != 4 && form != 5) return hipErrorInvalidValue;  // piece mode: quad forms only
     if (form == 4 || form == 5) {  // 4: the same-round quad (lab A/B), 5: the lag quad
         const dim3 grid((a.n + kShaQuadMsgs - 1) / kShaQuadMsgs);
         hipLaunchKernelGGL(form == 5 ? sha256_quad_kernel<true> : sha256_quad_kernel<false>, grid, dim3(256), 0, s,
-                           a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
+                           a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
         return hipGetLastError();
     }
     if (form == 3) {
