@@ -50,6 +50,7 @@ import argparse
 import glob
 import json
 import os
+import statistics
 import sys
 import threading
 import time
@@ -1311,15 +1312,16 @@ def pcie_rates(torch, devs, nbytes: int = 1 << 30) -> dict:
     return out
 
 
-def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
+def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
     """mxec_encode_batch_host from mxec_host_alloc (page-locked) memory: the
     PUT path as MaxIO sees it -- request bodies in host memory, parity and
     digests back in host memory (filesystem.rs:1107-1135) -- over every
     device of the context, with and without the SHA-256 of every chunk; then
     the GET side, mxec_reconstruct_batch_host over the same objects with two
     erasures each, without and with verification.
-    Payload GiB/s (k * chunk_size per object) over all ranks, next to the
-    box's raw pinned copy rates and the bound they set."""
+    Payload GiB/s (k * chunk_size per object) over all ranks at the median
+    of `reps` timed batches (each batch's time listed), next to the box's raw
+    pinned copy rates and the bounds they set."""
     import numpy as np
 
     k, m, S = 4, 2, 10 << 20
@@ -1348,16 +1350,18 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
         if sha:
             dig_all = dig
         ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm: pools, tables
-        barrier()
-        t0 = time.perf_counter()
+        ts = []
         for _ in range(reps):
+            barrier()
+            t0 = time.perf_counter()
             ctx.encode_batch_host(objs, dptr, pptr, digests=dig)
-        el = reduce_max((time.perf_counter() - t0) / reps)
+            ts.append(reduce_max(time.perf_counter() - t0))
+        el = statistics.median(ts)
         payload = reduce_sum(float(n * k * S))
         key = "rs_sha256" if sha else "rs_only"
         res[key] = {"s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
                     "frac_of_pcie_bound": round(bound_s / el, 4),
-                    "frac_of_duplex_bound": round(duplex_s / el, 4)}
+                    "frac_of_duplex_bound": round(duplex_s / el, 4), "s_each": [round(t, 4) for t in ts]}
     # GET side (chunk_reader.rs:157-226 from the shard files in host memory):
     # mxec_reconstruct_batch_host over the same objects with two seeded
     # erasures each -- the 4 present shards go up, the 2 rebuilt ones come
@@ -1380,18 +1384,20 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 3) -> dict:
         pr = present0.copy()
         rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)  # warm
         assert rc == 0, rc
-        barrier()
-        t0 = time.perf_counter()
+        ts = []
         for _ in range(reps):
             pr = present0.copy()
+            barrier()
+            t0 = time.perf_counter()
             rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)
+            ts.append(reduce_max(time.perf_counter() - t0))
             assert rc == 0, rc
-        el = reduce_max((time.perf_counter() - t0) / reps)
+        el = statistics.median(ts)
         payload = reduce_sum(float(n * k * S))
         res["get_verify_sha256" if verify else "get_rs_only"] = {
             "s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
             "frac_of_pcie_bound": round(max(get_up_s, get_down_s) / el, 4),
-            "frac_of_duplex_bound": round(get_duplex_s / el, 4)}
+            "frac_of_duplex_bound": round(get_duplex_s / el, 4), "s_each": [round(t, 4) for t in ts]}
     if plan.rank == 0:
         # the rebuilt shards of one object, scribbled first, come back exact
         o = n // 3
