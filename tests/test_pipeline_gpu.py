@@ -69,18 +69,20 @@ def test_batch_host_pinned_buffers(ctx):
 @pytest.mark.parametrize("piece_mb", ["1", "2", "0"])
 def test_batch_host_digests_in_pieces(ctx, piece_mb, monkeypatch):
     """With digests the wave runs piece-major (MXEC_PIPE_PIECE_MB, default
-    1; 0 = the group form): every chunk is hashed piece by piece, its chain
-    carried in a device state slot from launch to launch.  Shards over
-    several pieces and off the piece grid, last chunks that end mid-piece,
-    on a piece boundary, one byte into a piece, empty, and objects of one
-    piece beside them: parity and every digest equal to the oracle and
+    1; 0 = the group form):
+    every chunk is hashed piece by piece, its chain carried in a device
+    state slot from launch to launch.  Shards over several pieces and off
+    the piece grid, last chunks that end mid-piece, on a piece boundary
+    (the first one included), one byte into a piece, empty, and objects of
+    one piece beside them: parity and every digest equal to the oracle and
     hashlib."""
     monkeypatch.setenv("MXEC_PIPE_PIECE_MB", piece_mb)
     rng = np.random.default_rng(40 + int(piece_mb))
     M = 1 << 20
     specs = [(4, 2, 3 * M + 100, None), (4, 2, 3 * M + 100, 2 * M + 17), (8, 4, 2 * M, M),
              (10, 4, M + 64, M + 1), (4, 2, 3 * M + 100, 0), (1, 2, 5 * M + 3, None),
-             (4, 2, 65536, 17), (3, 5, 100, 1)]
+             (4, 2, 65536, 17), (3, 5, 100, 1), (4, 2, M + M // 4, M // 4), (4, 2, 2 * M + M // 4, None),
+             (4, 2, 2 * M, 960 << 10), (4, 2, 192 << 10, 64 << 10), (4, 2, 960 << 10, None)]
     objs, data, dlen, parity, chunks_of = _objects(rng, specs)
     digests = np.zeros(sum(k + m for (k, m, _) in objs) * 32, np.uint8)
     status = ctx.encode_batch_host(objs, data, parity, data_len=dlen, digests=digests)
@@ -188,12 +190,13 @@ def test_reconstruct_batch_host_verify_in_pieces(ctx, piece_mb, monkeypatch):
     specs = [(4, 2, 3 * M + 100, None, {1}, {4}), (4, 2, 3 * M + 100, 2 * M + 17, {0, 5}, set()),
              (8, 4, 2 * M, M, {3}, {9}), (4, 2, 3 * M + 100, 0, {2}, {0}),
              (4, 2, 2 * M + 64, None, {0, 1}, {2}),  # fails: 3 of 6 gone
-             (1, 2, 5 * M + 3, None, {1}, set()), (4, 2, 65536, 17, {3}, set())]
+             (1, 2, 5 * M + 3, None, {1}, set()), (4, 2, 65536, 17, {3}, set()),
+             (4, 2, M + M // 4, M // 4, {5}, {3}), (4, 2, 2 * M, 960 << 10, {0}, {3})]
     objs, ptrs, lens, present, expected, originals, bufs = _rec_batch(rng, specs)
     before = [b.copy() for b in bufs]
     p = present.copy()
     rc, status = ctx.reconstruct_batch_host(objs, ptrs, p, shard_len=lens, expected=expected)
-    assert rc == -10 and list(status) == [0, 0, 0, 0, -10, 0, 0]
+    assert rc == -10 and list(status) == [0, 0, 0, 0, -10, 0, 0, 0, 0]
     g = 0
     for o, (k, m, s) in enumerate(objs):
         for i in range(k + m):
