@@ -857,7 +857,9 @@ def measured_clock(kernel: str, cfg: str):
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "clock", f"clock_{cfg}.json")), reverse=True):
         try:
             with open(p) as f:
-                k = json.load(f)["kernels"][kernel]
+                ks = json.load(f)["kernels"]
+            # template arguments aside (sha256_quad_kernel<true> is the quad form's)
+            k = ks.get(kernel) or next(v for n, v in ks.items() if n.split("<")[0] == kernel)
             return float(k["clock_GHz_median"]), os.path.relpath(p, ROOT)
         except Exception:
             continue
