@@ -586,7 +586,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     // ok and running state are indexed by the slot).
     const uint32_t slot = live && pc.state ? pc.slot[i] : i;
     uint32_t s[4] = {0, 0, 0, 0};
-    if (live && pc.resume && role < 2) {  // continue the chain (a..h in state[slot])
+    if (live && pc.state && pc.resume && role < 2) {  // continue the chain (a..h in state[slot])
         const uint32_t* sv = pc.state + 8 * uint64_t(slot);
         if (role == 0) {
             s[0] = sv[4]; s[1] = sv[5]; s[2] = sv[6]; s[3] = sv[7];
