@@ -854,7 +854,11 @@ def measured_clock(kernel: str, cfg: str):
     """The shader clock a kernel ran at, from the committed GRBM_GUI_ACTIVE
     pass (profiles/r*/clock/clock_<cfg>.json, tools/clock_summary.py; newest
     round first), or (None, None)."""
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "clock", f"clock_{cfg}.json")), reverse=True):
+    # clock_<cfg>.json and clock_<cfg>_<what>.json (an earlier pass kept
+    # for the kernels that no longer run in it), newest round first
+    paths = glob.glob(os.path.join(ROOT, "profiles", "r*", "clock", f"clock_{cfg}.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", "r*", "clock", f"clock_{cfg}_*.json"))
+    for p in sorted(paths, reverse=True):
         try:
             with open(p) as f:
                 ks = json.load(f)["kernels"]
