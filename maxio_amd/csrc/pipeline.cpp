@@ -45,17 +45,35 @@ constexpr int kComputeStreams = 2;  // RS stream + SHA stream (4 HW queues per p
 
 uint64_t rup(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-// Piece grid of the piece-major host waves: pieces of P.  A short first
-// piece (P/4), or pieces ramping up from 64 KiB, should have started the
-// chains sooner but measured slower (0.223 and 0.245 vs 0.220 s for 128 x
-// 4+2 x 10 MiB with digests, profiles/r3/pieces/): a piece is one copy per
-// chunk, and small copies pay the DMA's fixed cost 512 times per piece.
+// Piece grid of the piece-major host waves: a ramp of pieces from
+// MXEC_PIPE_RAMP_KB (default 256; 0 = none) doubling up to P, then pieces of
+// P -- every chain waits for the first piece's upload.  With one 2D copy per
+// object and piece the 256 KiB ramp took the PUT with digests from 0.216 to
+// 0.211 s (64 KiB: 0.212) for 128 x 4+2 x 10 MiB; with one copy per chunk
+// the same idea measured slower than uniform pieces (a 64 KiB ramp 0.245, a
+// P/4 first piece 0.223, uniform 0.220 s): small copies pay the DMA's fixed
+// cost (profiles/r3/pieces/).
 struct PieceGrid {
-    uint64_t P;
-    explicit PieceGrid(uint64_t p) : P(p) {}
-    uint64_t start(uint64_t pc) const { return pc * P; }
-    uint64_t width(uint64_t) const { return P; }
-    uint64_t count(uint64_t longest) const { return std::max<uint64_t>(1, (longest + P - 1) / P); }
+    std::vector<uint64_t> starts;  // the ramp's pieces, then every P
+    uint64_t P, ramp_end = 0;
+    explicit PieceGrid(uint64_t p) : P(p) {
+        const char* e = getenv("MXEC_PIPE_RAMP_KB");
+        uint64_t w = uint64_t(e ? atol(e) : 256) << 10;
+        w = w / 64 * 64;
+        for (; w && w < p; w *= 2) {
+            starts.push_back(ramp_end);
+            ramp_end += w;
+        }
+    }
+    uint64_t start(uint64_t pc) const { return pc < starts.size() ? starts[pc] : ramp_end + (pc - starts.size()) * P; }
+    uint64_t width(uint64_t pc) const {
+        return pc < starts.size() ? (pc + 1 < starts.size() ? starts[pc + 1] : ramp_end) - starts[pc] : P;
+    }
+    uint64_t count(uint64_t longest) const {
+        for (uint64_t pc = 0; pc < starts.size(); ++pc)
+            if (longest <= start(pc) + width(pc)) return pc + 1;
+        return starts.size() + std::max<uint64_t>(1, (longest - ramp_end + P - 1) / P);
+    }
 };
 
 bool is_pinned(const void* p, uint64_t len) { return pinned_range(p, len); }
@@ -517,43 +535,86 @@ private:
     // host and on the device -- go as one DMA: an object's k data chunks are
     // usually contiguous in the request body and always in its device image
     // (and its m parity chunks likewise), so 4+2 objects take 2 copies
-    // instead of 6.  queue_up / queue_down collect; flush_up / flush_down
-    // issue (before an event is recorded on the copy stream).
+    // instead of 6.  Copies of one width at one pitch on each side (the same
+    // piece of an object's k chunks in the piece-major waves) go as one 2D
+    // copy when the host side is page-locked (MXEC_PIPE_COPY2D, default 1).
+    // queue_up / queue_down collect; flush_up / flush_down issue (before an
+    // event is recorded on the copy stream).
     struct Run {
         uint8_t* dst = nullptr;
         const uint8_t* src = nullptr;
-        uint64_t len = 0;
+        uint64_t len = 0;   // row width (0: empty)
+        uint64_t rows = 0;
+        uint64_t dpitch = 0, spitch = 0;
     };
+    static bool copy2d_on() {  // read per call (tests and labs switch it)
+        const char* e = getenv("MXEC_PIPE_COPY2D");
+        return !e || atoi(e) != 0;
+    }
+    static bool extend(Run& r, uint8_t* dst, const uint8_t* src, uint64_t len) {
+        if (!r.len) return false;
+        if (r.rows == 1 && r.dst + r.len == dst && r.src + r.len == src) {
+            r.len += len;
+            return true;
+        }
+        if (len != r.len || !copy2d_on()) return false;
+        if (r.rows == 1) {
+            if (dst < r.dst + len || src < r.src + len) return false;
+            r.dpitch = uint64_t(dst - r.dst);
+            r.spitch = uint64_t(src - r.src);
+            r.rows = 2;
+            return true;
+        }
+        if (dst != r.dst + r.rows * r.dpitch || src != r.src + r.rows * r.spitch) return false;
+        ++r.rows;
+        return true;
+    }
     Run up_run_, down_run_;
     int queue_up(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
-        if (up_run_.len && up_run_.dst + up_run_.len == dst && up_run_.src + up_run_.len == src) {
-            up_run_.len += len;
-            return MXEC_OK;
-        }
+        if (extend(up_run_, dst, src, len)) return MXEC_OK;
         MXEC_TRY(flush_up());
-        up_run_ = Run{dst, src, len};
+        up_run_ = Run{dst, src, len, 1, 0, 0};
         return MXEC_OK;
     }
     int flush_up() {
         const Run r = up_run_;
         up_run_ = Run{};
-        return r.len ? upload(r.dst, r.src, r.len) : MXEC_OK;
+        if (!r.len) return MXEC_OK;
+        if (r.rows == 1) return upload(r.dst, r.src, r.len);
+        if (is_pinned(r.src, (r.rows - 1) * r.spitch + r.len)) {
+            if (affinity_on()) {
+                const void* p = r.dst;
+                MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload 2d", &arena_, &p, 1));
+            }
+            MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyHostToDevice, h2d_));
+            return MXEC_OK;
+        }
+        for (uint64_t i = 0; i < r.rows; ++i) MXEC_TRY(upload(r.dst + i * r.dpitch, r.src + i * r.spitch, r.len));
+        return MXEC_OK;
     }
     int queue_down(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
-        if (down_run_.len && down_run_.dst + down_run_.len == dst && down_run_.src + down_run_.len == src) {
-            down_run_.len += len;
-            return MXEC_OK;
-        }
+        if (extend(down_run_, dst, src, len)) return MXEC_OK;
         MXEC_TRY(flush_down());
-        down_run_ = Run{dst, src, len};
+        down_run_ = Run{dst, src, len, 1, 0, 0};
         return MXEC_OK;
     }
     int flush_down() {
         const Run r = down_run_;
         down_run_ = Run{};
-        return r.len ? download(r.dst, r.src, r.len) : MXEC_OK;
+        if (!r.len) return MXEC_OK;
+        if (r.rows == 1) return download(r.dst, r.src, r.len);
+        if (is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
+            if (affinity_on()) {
+                const void* p = r.src;
+                MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download 2d", &arena_, &p, 1));
+            }
+            MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyDeviceToHost, d2h_));
+            return MXEC_OK;
+        }
+        for (uint64_t i = 0; i < r.rows; ++i) MXEC_TRY(download(r.dst + i * r.dpitch, r.src + i * r.spitch, r.len));
+        return MXEC_OK;
     }
 
     // Copy out the pending ring buffer the next take() will reuse.

@@ -90,6 +90,30 @@ def test_batch_host_digests_in_pieces(ctx, piece_mb, monkeypatch):
     _check(objs, chunks_of, digests)
 
 
+@pytest.mark.parametrize("ramp_kb,copy2d", [("0", "1"), ("", "1"), ("64", "1"), ("64", "0")])
+def test_batch_host_pinned_pieces_2d(ctx, ramp_kb, copy2d, monkeypatch):
+    """Page-locked bodies in pieces: the same piece of an object's k chunks
+    (and of its m parity chunks) goes as one 2D copy (MXEC_PIPE_COPY2D),
+    after a ramp of pieces from MXEC_PIPE_RAMP_KB (default 256, 0 = none)
+    up to 1 MiB;
+    shards off the piece grid.  Parity and digests equal to the oracle."""
+    torch = pytest.importorskip("torch")
+    if ramp_kb:
+        monkeypatch.setenv("MXEC_PIPE_RAMP_KB", ramp_kb)
+    monkeypatch.setenv("MXEC_PIPE_COPY2D", copy2d)
+    k, m, s, n = 4, 2, 3 * (1 << 20) + 128, 6
+    host = torch.randint(0, 256, (n, k, s), dtype=torch.uint8).pin_memory()
+    par = torch.zeros((n, m, s), dtype=torch.uint8).pin_memory()
+    objs = [(k, m, s)] * n
+    data = [host[o, j].data_ptr() for o in range(n) for j in range(k)]
+    parity = [par[o, i].data_ptr() for o in range(n) for i in range(m)]
+    digests = np.zeros(n * (k + m) * 32, np.uint8)
+    status = ctx.encode_batch_host(objs, data, parity, digests=digests)
+    assert (status == 0).all()
+    h, p = host.numpy(), par.numpy()
+    _check(objs, [([h[o, j] for j in range(k)], [p[o, i] for i in range(m)]) for o in range(n)], digests)
+
+
 def test_batch_host_without_digests(ctx):
     rng = np.random.default_rng(32)
     objs, data, dlen, parity, chunks_of = _objects(rng, [(8, 4, 8192, None)] * 5)

@@ -25,6 +25,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--objects", type=int, default=128)
     ap.add_argument("--chunk-size", type=int, default=10 << 20)
+    ap.add_argument("--env", default="MXEC_PIPE_PIECE_MB", help="the knob alternated (read per call)")
     ap.add_argument("--values", default="0,1,2")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--no-digests", action="store_true")
@@ -47,7 +48,7 @@ def main() -> int:
     seen = {}
     for rnd in range(a.rounds):
         for v in a.values.split(","):
-            os.environ["MXEC_PIPE_PIECE_MB"] = v
+            os.environ[a.env] = v
             dig = None if a.no_digests else np.zeros(n * (k + m) * 32, np.uint8)
             ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm
             t0 = time.perf_counter()
@@ -57,7 +58,7 @@ def main() -> int:
             if v in seen:
                 assert np.array_equal(seen[v][0], snap[0])
             seen[v] = snap
-            print(json.dumps({"round": rnd, "MXEC_PIPE_PIECE_MB": v, "s_per_batch": round(el, 4),
+            print(json.dumps({"round": rnd, a.env: v, "s_per_batch": round(el, 4),
                               "GiBps_payload": round(n * k * S / el / 2**30, 2)}), flush=True)
     if a.get and not a.no_digests:
         # GET side: two seeded erasures per object, verified against the
@@ -73,7 +74,7 @@ def main() -> int:
         want = par[n // 3].copy(), data[n // 3].copy()
         for rnd in range(a.rounds):
             for v in a.values.split(","):
-                os.environ["MXEC_PIPE_PIECE_MB"] = v
+                os.environ[a.env] = v
                 pr = present0.copy()
                 rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)  # warm
                 assert rc == 0, rc
@@ -82,7 +83,7 @@ def main() -> int:
                 rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)
                 el = time.perf_counter() - t0
                 assert rc == 0 and np.array_equal(par[n // 3], want[0]) and np.array_equal(data[n // 3], want[1])
-                print(json.dumps({"get_verify": True, "round": rnd, "MXEC_PIPE_PIECE_MB": v,
+                print(json.dumps({"get_verify": True, "round": rnd, a.env: v,
                                   "s_per_batch": round(el, 4), "GiBps_payload": round(n * k * S / el / 2**30, 2)}),
                       flush=True)
     arms = list(seen.values())
@@ -94,7 +95,7 @@ def main() -> int:
         ok = hashlib.sha256(data[o, j].tobytes()).digest() == arms[0][1][(o * (k + m) + j) * 32:
                                                                          (o * (k + m) + j + 1) * 32].tobytes()
     print(json.dumps({"equal_across_arms": bool(same), "hashlib_sample_ok": bool(ok)}), flush=True)
-    os.environ.pop("MXEC_PIPE_PIECE_MB", None)
+    os.environ.pop(a.env, None)
     ctx.close()
     return 0 if same and ok else 1
 
