@@ -45,20 +45,20 @@ constexpr int kComputeStreams = 2;  // RS stream + SHA stream (4 HW queues per p
 
 uint64_t rup(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-// Piece grid of the piece-major host waves: a ramp of pieces from
-// MXEC_PIPE_RAMP_KB (default 256; 0 = none) doubling up to P, then pieces of
-// P -- every chain waits for the first piece's upload.  With one 2D copy per
-// object and piece the 256 KiB ramp took the PUT with digests from 0.216 to
-// 0.211 s (64 KiB: 0.212) for 128 x 4+2 x 10 MiB; with one copy per chunk
-// the same idea measured slower than uniform pieces (a 64 KiB ramp 0.245, a
-// P/4 first piece 0.223, uniform 0.220 s): small copies pay the DMA's fixed
-// cost (profiles/r3/pieces/).
+// Piece grid of the piece-major host waves: pieces of P, after a ramp from
+// MXEC_PIPE_RAMP_KB doubling up to P when set (lab; every chain waits for
+// the first piece's upload).  With one copy per chunk a ramp measured slower
+// than uniform pieces (64 KiB ramp 0.245, a P/4 first piece 0.223, uniform
+// 0.220 s for 128 x 4+2 x 10 MiB with digests): small copies pay the DMA's
+// fixed cost.  With 2D copies (MXEC_PIPE_COPY2D=1) a 256 KiB ramp won 2 %
+// in one process (0.216 -> 0.211 s), but the 2D copies are off by default
+// (see queue_up), so the ramp is too (profiles/r3/pieces/).
 struct PieceGrid {
     std::vector<uint64_t> starts;  // the ramp's pieces, then every P
     uint64_t P, ramp_end = 0;
     explicit PieceGrid(uint64_t p) : P(p) {
         const char* e = getenv("MXEC_PIPE_RAMP_KB");
-        uint64_t w = uint64_t(e ? atol(e) : 256) << 10;
+        uint64_t w = uint64_t(e ? atol(e) : 0) << 10;
         w = w / 64 * 64;
         for (; w && w < p; w *= 2) {
             starts.push_back(ramp_end);
@@ -535,9 +535,13 @@ private:
     // host and on the device -- go as one DMA: an object's k data chunks are
     // usually contiguous in the request body and always in its device image
     // (and its m parity chunks likewise), so 4+2 objects take 2 copies
-    // instead of 6.  Copies of one width at one pitch on each side (the same
-    // piece of an object's k chunks in the piece-major waves) go as one 2D
-    // copy when the host side is page-locked (MXEC_PIPE_COPY2D, default 1).
+    // instead of 6.  With MXEC_PIPE_COPY2D=1 (lab), copies of one width at
+    // one pitch on each side (the same piece of an object's k chunks in the
+    // piece-major waves) go as one 2D copy when the host side is
+    // page-locked.  Off by default: within one process it won 1-2 %, but in
+    // default bench lines the GET group form (2D runs of whole 10 MiB
+    // shards) fell from 0.113 to 0.150-0.266 s and one process's PUT with
+    // digests ran 0.317 s against 0.210 in the next (profiles/r3/pieces/).
     // queue_up / queue_down collect; flush_up / flush_down issue (before an
     // event is recorded on the copy stream).
     struct Run {
@@ -547,9 +551,9 @@ private:
         uint64_t rows = 0;
         uint64_t dpitch = 0, spitch = 0;
     };
-    static bool copy2d_on() {  // read per call (tests and labs switch it)
+    static bool copy2d_on() {  // read per call (tests and labs switch it); default off, see below
         const char* e = getenv("MXEC_PIPE_COPY2D");
-        return !e || atoi(e) != 0;
+        return e && atoi(e) != 0;
     }
     static bool extend(Run& r, uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!r.len) return false;

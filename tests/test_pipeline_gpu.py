@@ -90,17 +90,18 @@ def test_batch_host_digests_in_pieces(ctx, piece_mb, monkeypatch):
     _check(objs, chunks_of, digests)
 
 
-@pytest.mark.parametrize("ramp_kb,copy2d", [("0", "1"), ("", "1"), ("64", "1"), ("64", "0")])
+@pytest.mark.parametrize("ramp_kb,copy2d", [("", ""), ("0", "1"), ("256", "1"), ("64", "1"), ("64", "0")])
 def test_batch_host_pinned_pieces_2d(ctx, ramp_kb, copy2d, monkeypatch):
-    """Page-locked bodies in pieces: the same piece of an object's k chunks
-    (and of its m parity chunks) goes as one 2D copy (MXEC_PIPE_COPY2D),
-    after a ramp of pieces from MXEC_PIPE_RAMP_KB (default 256, 0 = none)
-    up to 1 MiB;
+    """Page-locked bodies in pieces, defaults (uniform pieces, 1D copies)
+    and the lab knobs: the same piece of an object's k chunks (and of its m
+    parity chunks) as one 2D copy (MXEC_PIPE_COPY2D=1), a ramp of pieces
+    from MXEC_PIPE_RAMP_KB up to 1 MiB;
     shards off the piece grid.  Parity and digests equal to the oracle."""
     torch = pytest.importorskip("torch")
     if ramp_kb:
         monkeypatch.setenv("MXEC_PIPE_RAMP_KB", ramp_kb)
-    monkeypatch.setenv("MXEC_PIPE_COPY2D", copy2d)
+    if copy2d:
+        monkeypatch.setenv("MXEC_PIPE_COPY2D", copy2d)
     k, m, s, n = 4, 2, 3 * (1 << 20) + 128, 6
     host = torch.randint(0, 256, (n, k, s), dtype=torch.uint8).pin_memory()
     par = torch.zeros((n, m, s), dtype=torch.uint8).pin_memory()
