@@ -1332,6 +1332,31 @@ def pcie_rates(torch, devs, nbytes: int = 1 << 30) -> dict:
     return out
 
 
+def numa_nodes(addr: int, nbytes: int, samples: int = 4) -> list:
+    """NUMA node of `samples` pages spread over a host buffer
+    (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR), -errno where it fails."""
+    import ctypes
+
+    libc = ctypes.CDLL("libc.so.6", use_errno=True)
+    out = []
+    for i in range(samples):
+        node = ctypes.c_int(-1)
+        rc = libc.syscall(239, ctypes.byref(node), None, ctypes.c_ulong(0),
+                          ctypes.c_void_p(addr + nbytes // samples * i), ctypes.c_ulong(3))
+        out.append(node.value if rc == 0 else -ctypes.get_errno())
+    return out
+
+
+def gpu_numa_node(torch, d: int):
+    try:
+        pr = torch.cuda.get_device_properties(d)
+        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            return int(f.read())
+    except Exception:
+        return None
+
+
 def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
     """mxec_encode_batch_host from mxec_host_alloc (page-locked) memory: the
     PUT path as MaxIO sees it -- request bodies in host memory, parity and
@@ -1351,13 +1376,18 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
     data = ctx.host_array(n * k * S).reshape(n, k, S)
     par = ctx.host_array(n * m * S).reshape(n, m, S)
     _fill_random(data, 7 + plan.rank)
+    # where the page-locked buffers landed against the GPUs (mxec_host_alloc
+    # binds them to the GPUs' node with MXEC_HOST_NUMA=1)
+    numa = {"gpu_nodes": [gpu_numa_node(torch, d) for d in sorted(set(plan.torch_devs))],
+            "data_pages": numa_nodes(data.ctypes.data, data.nbytes),
+            "parity_pages": numa_nodes(par.ctypes.data, par.nbytes)}
     dptr = [data[o, j].ctypes.data for o in range(n) for j in range(k)]
     pptr = [par[o, i].ctypes.data for o in range(n) for i in range(m)]
     objs = [(k, m, S)] * n
     res = {"workload": (f"PUT compute from page-locked host memory: {per_dev} objects per GPU x 4+2 x 10 MiB "
                         f"(mxec_encode_batch_host over {D} device(s) per process); H2D upload, RS encode, "
                         "optional SHA-256 of all 6 chunks, D2H of parity and digests, wall clock"),
-           "objects_per_gpu": per_dev, "pcie_all_devices": rates}
+           "objects_per_gpu": per_dev, "pcie_all_devices": rates, "numa": numa}
     # H2D and D2H overlap (separate DMA streams): the bound is the slower direction.
     h2d_s = n * k * S / (rates["h2d_GBps"] * 1e9)
     d2h_s = n * m * S / (rates["d2h_GBps"] * 1e9)

@@ -2,6 +2,8 @@
 // pointer drop-ins, device-resident batches).  No exception crosses the ABI.
 #include <algorithm>
 #include <array>
+#include <cctype>
+#include <fstream>
 #include <cstdio>
 #include <cstdlib>
 #include <unordered_map>
@@ -9,6 +11,9 @@
 #include <map>
 #include <string>
 #include <tuple>
+
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../../include/maxio_ec.h"
 #include "ops.hpp"
@@ -233,10 +238,58 @@ int mxec_ctx_rs_grid(mxec_ctx* ctx, int dev, int k, int m, uint64_t shard_size) 
     return guarded([&] { return rs_grid_in_use(*ctx->c.devs[size_t(dev)], k, m, shard_size); });
 }
 
+namespace {
+
+// NUMA node of HIP device `dev` (sysfs, through its PCI bus id), or -1.
+int device_numa_node(int dev) {
+    char bus[64] = {};
+    if (hipDeviceGetPCIBusId(bus, int(sizeof bus), dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char& c : bus) c = char(std::tolower(static_cast<unsigned char>(c)));
+    std::ifstream f(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
+    int node = -1;
+    return f >> node ? node : -1;
+}
+
+// The node all of the context's devices sit on, or -1 (unknown or several).
+int ctx_numa_node(const mxec_ctx* ctx) {
+    int node = -1;
+    for (const auto& d : ctx->c.devs) {
+        const int n = device_numa_node(d->id);
+        if (n < 0 || (node >= 0 && n != node)) return -1;
+        node = n;
+    }
+    return node;
+}
+
+}  // namespace
+
+// Page-locked memory on the NUMA node of the context's GPUs with
+// MXEC_HOST_NUMA=1 (default: wherever the calling thread's policy puts it).  The pages are placed when
+// hipHostMalloc pins them, so the thread's policy is set to that node around
+// the call (hipHostMallocNumaUser) and restored after; if the node is unknown
+// or the policy calls are refused, the allocation is the plain one.  A
+// process may run on every core of a two-socket host, and a DMA from the far
+// socket's memory crosses the socket link.
 void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes) {
     if (!ctx || bytes == 0) return nullptr;
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+    constexpr unsigned long kMaxNode = 1024;
+    const char* env = getenv("MXEC_HOST_NUMA");
+    const int node = env && atoi(env) != 0 ? ctx_numa_node(ctx) : -1;  // opt-in until measured
+    int old_mode = 0;
+    unsigned long old_mask[kMaxNode / 64] = {}, mask[kMaxNode / 64] = {};
+    bool bound = false;
+    if (node >= 0 && unsigned(node) < kMaxNode &&
+        syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNode + 1, nullptr, 0) == 0) {
+        mask[node / 64] = 1ul << (node % 64);
+        bound = syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, kMaxNode + 1) == 0;
+    }
+    const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocPortable | (bound ? hipHostMallocNumaUser : 0));
+    if (bound) (void)syscall(SYS_set_mempolicy, old_mode, old_mode ? old_mask : nullptr, old_mode ? kMaxNode + 1 : 0);
+    if (e != hipSuccess) {
         (void)hipGetLastError();
         set_error(MXEC_E_OOM, "pinned host allocation failed");
         return nullptr;

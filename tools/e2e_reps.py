@@ -31,8 +31,9 @@ def main() -> int:
     ctx = maxio_amd.Context(device_mask=plan.device_mask, streams_per_device=2)
     for r in range(a.runs):
         res = bench.e2e_host_leg(ctx, torch, plan, a.objects)
-        print(json.dumps({"run": r, **{k: res[k]["s_each"] for k in
-                                       ("rs_only", "rs_sha256", "get_rs_only", "get_verify_sha256")}}), flush=True)
+        print(json.dumps({"run": r, "MXEC_HOST_NUMA": os.environ.get("MXEC_HOST_NUMA"), "numa": res.get("numa"),
+                          **{k: res[k]["s_each"] for k in
+                             ("rs_only", "rs_sha256", "get_rs_only", "get_verify_sha256")}}), flush=True)
     ctx.close()
     return 0
 
