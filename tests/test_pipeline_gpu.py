@@ -115,6 +115,44 @@ def test_batch_host_pinned_pieces_2d(ctx, ramp_kb, copy2d, monkeypatch):
     _check(objs, [([h[o, j] for j in range(k)], [p[o, i] for i in range(m)]) for o in range(n)], digests)
 
 
+def test_batch_host_digests_past_quad_capacity(ctx):
+    """A wave of more chunks than the lag quad form holds (48 per CU: 12 288
+    on 256 CUs) takes the group form (whole chunks, one launch after the
+    upload) instead of pieces: 2 200 objects of 4+2 x 4 KiB = 13 200 chunks,
+    parity and digests against the oracle for a sample, every digest against
+    hashlib; then the verified GET of the same objects with one erasure and
+    one corrupt shard in a few of them."""
+    import hashlib
+
+    rng = np.random.default_rng(61)
+    k, m, s, n = 4, 2, 4096, 2200
+    data = rng.integers(0, 256, (n, k, s), dtype=np.uint8)
+    par = np.zeros((n, m, s), np.uint8)
+    objs = [(k, m, s)] * n
+    digests = np.zeros(n * (k + m) * 32, np.uint8)
+    status = ctx.encode_batch_host(objs, [data[o, j].ctypes.data for o in range(n) for j in range(k)],
+                                   [par[o, i].ctypes.data for o in range(n) for i in range(m)], digests=digests)
+    assert (status == 0).all()
+    sample = [0, 1, n // 2, n - 1]
+    _check([objs[o] for o in sample], [([data[o, j] for j in range(k)], [par[o, i] for i in range(m)])
+                                       for o in sample], None)
+    for o in range(0, n, 97):
+        for t in range(k + m):
+            x = data[o, t] if t < k else par[o, t - k]
+            assert digests[(o * (k + m) + t) * 32:(o * (k + m) + t + 1) * 32].tobytes() == hashlib.sha256(x).digest()
+    shards = np.concatenate([data, par], axis=1).copy()
+    want = shards.copy()
+    present = np.ones(n * (k + m), np.uint8)
+    for o in range(0, n, 211):
+        present[o * (k + m) + 1] = 0
+        shards[o, 1] = 0xEE
+        shards[o, 4, 7] ^= 0x10  # silently corrupt: verification turns it into an erasure
+    ptrs = [shards[o, i].ctypes.data for o in range(n) for i in range(k + m)]
+    rc, st = ctx.reconstruct_batch_host(objs, ptrs, present, expected=digests)
+    assert rc == 0 and not st.any()
+    assert np.array_equal(shards[:, :k], want[:, :k])
+
+
 def test_batch_host_without_digests(ctx):
     rng = np.random.default_rng(32)
     objs, data, dlen, parity, chunks_of = _objects(rng, [(8, 4, 8192, None)] * 5)
