@@ -4,16 +4,18 @@
 // :1131 (parity shards) and chunk_reader.rs:108 / :184 (verify on read).
 //
 // SHA-256 of one message is a serial chain of 64-byte compressions, so the
-// only parallelism is across messages: one lane per chunk.  A lane streams its
-// own message 64 bytes at a time with four global_load_dwordx4, prefetching the
-// next block while compressing the current one.  The 64 rounds are fully
-// unrolled (K from SGPRs), the schedule rolls through 16 VGPRs, rotates are
-// v_alignbit_b32, Σ/σ XOR3, Ch and Maj are one v_bitop3_b32 each (14 VALU per
-// round).  Three forms: one wave per 64 messages, the split (producer /
-// consumer) form for latency-bound batches, and the persistent stream form for
-// batches of more groups than the chip has SIMDs (below).  Per message the
-// work is a VALU-latency chain (see DESIGN.md for the roofline), not
-// HBM-bound.
+// parallelism is across messages, plus what a round's two halves offer.  The
+// 64 rounds are fully unrolled, rotates are v_alignbit_b32, Σ/σ XOR3, Ch and
+// Maj are one v_bitop3_b32 each (14 VALU per round on one lane).  Forms, by
+// batch size: the lag quad form (up to 48 messages per CU: a producer wave
+// computes K + W, each message's e-side and a-side rounds run on two lanes of
+// a consumer wave, the a-side two rounds behind, 9 VALU per step; the default
+// latency form, with a piece mode that carries chains across launches), the
+// same-round quad form (lab A/B), the split (producer / consumer) form with
+// one lane per message, one wave per 64 messages, and the persistent stream
+// form for batches of more groups than the chip has SIMDs (below).  Per
+// message the work is a VALU-latency chain (see DESIGN.md for the roofline),
+// not HBM-bound.
 #include <cstdlib>
 #include <cstring>
 
