@@ -68,18 +68,18 @@ GIB = float(1 << 30)
 # consumer 905 (64 rounds x 14 + 9) + producer 565 (2261 per 4-block step);
 # one-wave form 1410 (64 x 14 rounds + 48 x 10 schedule + 16 byte swaps + 18);
 # stream form 1415 (the one-wave rounds plus the clamped prefetch).
-# Quad form (four lanes per message, 48 messages per workgroup; the lag
-# variant): producer 566 + 3 consumers x 607 wave-instructions per block over
-# 48 messages = 3183 lane-ops per message-block; it spends more lane-ops per hash to cut
+# Quad form (the lag variant with two messages per quad, 64 messages per
+# workgroup): producer 566 + 2 consumers x 607 wave-instructions per block
+# over 64 messages = 1780 lane-ops per message-block; it spends more lane-ops per hash to cut
 # the serial wave's count, so config 3 keeps the one-lane split form's 1470
 # as its chip-wide denominator (comparable across rounds).
-SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415, "quad": 3183}
+SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415, "quad": 1780}
 # The serial wave (the consumer) of each latency form issues this many VALU
 # per block (split: 64 rounds x 14 + 9; quad, lag variant: 66 steps x 9 + 13); a wave issues at
 # most one VALU every 4 cycles, so a lone message's chain cannot beat that
 # x 4 cycles per block at the clock the chip holds.
 SHA_CONSUMER_VALU_PER_BLOCK = {"split": 905, "quad": 607}
-SHA_QUAD_MSGS_PER_CU = 48
+SHA_QUAD_MSGS_PER_CU = 64  # the lag form, two messages per quad
 # Chip INT32 issue ceiling for those instructions (v_alignbit / v_bitop3 /
 # v_add3 / v_add / v_perm): CUs x 4 SIMDs x lanes per cycle x 2.4 GHz, lanes
 # per cycle measured with tools/valu_lab chip (profiles/r2_lab_valu_chip.jsonl).

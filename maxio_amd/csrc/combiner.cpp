@@ -92,8 +92,8 @@ struct ShaCombiner {
         for (const Req* r : batch)
             if (r->ready) MXEC_HIP(hipStreamWaitEvent(s, r->ready, 0));
         MXEC_TRY(slot.digests.grow(n * 32));
-        // The kernel's own choice by message count: the quad (lag) form up
-        // to 48 messages per CU, the split form up to 3/4 of a 64-message
+        // The kernel's own choice by message count: the lag quad form up
+        // to 64 messages per CU, the split form up to 3/4 of a 64-message
         // group per SIMD, beyond that the stream form (segments of every
         // chain dealt to persistent waves keep every SIMD busy to the end:
         // 81 920 x 1 MiB 55.8 ms vs 96.1 split), whose timeout word comes
@@ -232,9 +232,9 @@ ShaCombiner* combiner_of(Device& d) {
             c->free_slots.push_back(sl.get());
             c->slots.push_back(std::move(sl));
         }
-        // Both lanes' launches together within one quad-form workgroup
-        // (48 messages, one wave per SIMD) per CU.
-        c->lane_limit = size_t(d.n_cus) * kShaQuadMsgs;
+        // Both lanes' launches together within one lag-form workgroup
+        // (64 messages, one wave per SIMD) per CU.
+        c->lane_limit = size_t(d.n_cus) * kShaLagMsgs;
         d.comb = c;
     }
     return static_cast<ShaCombiner*>(d.comb.get());

@@ -119,6 +119,9 @@ struct ShaArgs {
 };
 // Messages per workgroup of the quad form (three consumer waves of 16).
 constexpr uint32_t kShaQuadMsgs = 48;
+// Messages per workgroup of the lag quad form with two messages per quad
+// (two consumer waves of 32): the auto latency form, one workgroup per CU.
+constexpr uint32_t kShaLagMsgs = 64;
 // Blocks per stream-form segment (32 KiB of each message).
 constexpr uint32_t kShaSegBlocks = 512;
 // Timeout code the stream form leaves in work[1] when a wave gave up

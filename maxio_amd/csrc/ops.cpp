@@ -567,7 +567,7 @@ int run_sha_pieces(Device& dev, Slot& slot, hipStream_t s, const std::vector<con
     const size_t n = ptrs.size();
     if (!n) return MXEC_OK;
     if (lens.size() != n || slots.size() != n || totals.size() != n || !state_dev ||
-        n > uint64_t(kShaQuadMsgs) * uint64_t(dev.n_cus ? dev.n_cus : 256))
+        n > uint64_t(kShaLagMsgs) * uint64_t(dev.n_cus ? dev.n_cus : 256))
         return set_error(MXEC_E_INVALID_ARG, "sha pieces: table sizes or message count");
     for (size_t i = 0; i < n; ++i)
         if (totals[i] == kShaNotFinal ? lens[i] % 64 != 0 : totals[i] < lens[i])
@@ -598,7 +598,7 @@ int run_sha_pieces(Device& dev, Slot& slot, hipStream_t s, const std::vector<con
     a.ok = ok_dev;
     a.n = uint32_t(n);
     a.n_cus = uint32_t(dev.n_cus);
-    a.force = 5;
+    a.force = 6;
     a.piece.state = state_dev;
     a.piece.slot = reinterpret_cast<const uint32_t*>(db + o_s);
     a.piece.total = reinterpret_cast<const uint64_t*>(db + o_t);

@@ -69,13 +69,14 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
             const std::vector<uint64_t>& lens, uint8_t* digests_dev, const uint8_t* expected_dev,
             uint8_t* ok_dev, const std::vector<uint64_t>* exp_idx = nullptr,
             DescArena* arena = nullptr, int form = 0, const uint32_t** tmo_dev = nullptr);
-// One piece of every listed chain (ShaPiece, kernels.hpp), lag quad form:
+// One piece of every listed chain (ShaPiece, kernels.hpp), lag quad form
+// with two messages per quad:
 // message i is the next lens[i] bytes of the chain in state slot slots[i]
 // (state_dev: [slots][8] words, carried between launches on one stream);
 // totals[i] = the message's length if this piece ends it (digest into
 // digests_dev[slots[i]]; with expected_dev, ok_dev[slots[i]] = digest ==
 // expected_dev[slots[i]]), kShaNotFinal otherwise (lens[i] a multiple of 64).
-// At most kShaQuadMsgs messages per CU.
+// At most kShaLagMsgs messages per CU.
 int run_sha_pieces(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
                    const std::vector<uint64_t>& lens, const std::vector<uint32_t>& slots,
                    const std::vector<uint64_t>& totals, uint32_t* state_dev, bool resume, uint8_t* digests_dev,

@@ -285,7 +285,7 @@ private:
                 for (int i = 0; i < objs[o].k + objs[o].m; ++i) vmsgs += objs[o].present[i] ? 1 : 0;
         const uint64_t P = piece_bytes();
         std::vector<hipEvent_t> up;  // per group (group form): its upload is done
-        if (verify && P && vmsgs && vmsgs <= uint64_t(kShaQuadMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256)) {
+        if (verify && P && vmsgs && vmsgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256)) {
             // Piece-major upload + verification (the PUT wave's scheme, see
             // wave_pieces): piece p of every present shard goes up and is
             // hashed, chains carried in state slots, so every chain starts
@@ -673,7 +673,7 @@ private:
     // piece in device state slots (run_sha_pieces) -- and its parity goes
     // down, piece after piece, so every chain starts after the first piece
     // (~9 ms) and the wave ends near one chain's length.  Taken when the
-    // wave's messages fit the lag quad form (48 per CU).
+    // wave's messages fit the lag quad form (64 per CU).
     static uint64_t piece_bytes() {  // read per wave (tests and labs switch it)
         const char* e = getenv("MXEC_PIPE_PIECE_MB");
         const long v = e ? atol(e) : 1;
@@ -808,7 +808,7 @@ private:
             for (size_t o = o0; o < o1; ++o)
                 if (objs[o].dig) msgs += uint64_t(objs[o].k + objs[o].m);
             const uint64_t P = piece_bytes();
-            if (P && msgs && msgs <= uint64_t(kShaQuadMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256))
+            if (P && msgs && msgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256))
                 return wave_pieces(objs, o0, o1, P);
         }
         Slot& slot = slot_;

@@ -433,6 +433,7 @@ constexpr int kQuadRow = 66;  // u32x4 per K + W row: 64 producer lanes, zeros, 
 constexpr int kQuadFromE = 0xA2;   // quad_perm [2, 0, 2, 2]: lane A reads lane E, the rest a zero lane
 constexpr int kQuadFromA = 0xA9;   // quad_perm [1, 2, 2, 2]: lane E reads lane A, the rest a zero lane
 constexpr int kQuadBcastA = 0x55;  // quad_perm [1, 1, 1, 1]
+constexpr int kPairBcastA = 0xF5;  // quad_perm [1, 1, 3, 3]: each message's lane A to its lane E
 
 struct QuadLane {
     uint32_t sh1, sh2, sh3;  // rotations: Σ1's in lane E, Σ0's in lane A
@@ -537,7 +538,11 @@ __device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[
 }
 
 // LAG: compress_lag (default) or the same-round compress_quad (lab A/B).
-template <bool LAG>
+// PAIR (lag only; MXEC_SHA_FORM=lagpair, lab): two messages per quad -- the
+// lag form needs no zero lanes, so lanes 4j+2 / 4j+3 run a second message's
+// E and A sides -- and a workgroup is the producer wave (64 messages) plus two
+// consumer waves of 32: 64 messages per workgroup of three waves.
+template <bool LAG, bool PAIR = false>
 __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* __restrict__ ptrs,
                                                          const uint64_t* __restrict__ lens,
                                                          uint8_t* __restrict__ digests,
@@ -545,7 +550,9 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
                                                          const uint64_t* __restrict__ exp_idx,
                                                          uint8_t* __restrict__ ok, uint32_t n, uint32_t prio,
                                                          ShaPiece pc) {
+    static_assert(LAG || !PAIR, "two messages per quad needs the lag form (no zero lanes)");
     constexpr int NB = 3, BUF = 16 * kQuadRow;
+    constexpr uint32_t MSGS = PAIR ? 64 : kShaQuadMsgs;  // messages per workgroup
     sha_priority(prio);
     __shared__ u32x4 kw[NB][16][kQuadRow];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -553,11 +560,11 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
         const uint32_t r = threadIdx.x >> 1, c = threadIdx.x & 1;
         kw[r / 16][r % 16][64 + c] = u32x4{c, c, c, c};
     }
-    const uint32_t base = blockIdx.x * kShaQuadMsgs;
+    const uint32_t base = blockIdx.x * MSGS;
     // Every wave derives the same trip count from the workgroup's messages
     // (one per lane below kShaQuadMsgs), so the barriers pair up.
     const uint32_t pi = base + lane;
-    const bool plive = lane < kShaQuadMsgs && pi < n;
+    const bool plive = lane < MSGS && pi < n;
     const uint8_t* pp = plive ? ptrs[pi] : nullptr;
     const uint64_t pfull = plive ? lens[pi] / 64 : 0;
     uint64_t nmax = pfull;
@@ -573,7 +580,8 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
                                   (reinterpret_cast<uintptr_t>(pp) & 15) == 0);
         return;
     }
-    const uint32_t role = lane & 3, ml = (wave - 1) * 16 + (lane >> 2);
+    const uint32_t role = PAIR ? lane & 1 : lane & 3;
+    const uint32_t ml = PAIR ? (wave - 1) * 32 + (lane >> 1) : (wave - 1) * 16 + (lane >> 2);
     const uint32_t i = base + ml;
     const bool live = i < n;
     const uint8_t* p = live ? ptrs[i] : nullptr;
@@ -635,7 +643,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     uint32_t st[8];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        st[t] = QDPP(s[LAG ? (t + 2) & 3 : t], kQuadBcastA);
+        st[t] = QDPP(s[LAG ? (t + 2) & 3 : t], PAIR ? kPairBcastA : kQuadBcastA);
         st[4 + t] = s[t];
     }
     if (role != 0 || !live) return;
@@ -876,8 +884,11 @@ constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 
 // MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read
 // per launch), default 3.
-// The quad form the auto choice takes: 4 = same-round, 5 = lag.
-constexpr int kShaQuadAuto = 5;
+// The quad form the auto choice takes (up to kShaLagMsgs per CU): 4 =
+// same-round, 5 = lag, 6 = lag with two messages per quad.  6 against 5 on
+// config 3's 10 240 x 1 MiB: 20.72 vs 20.89 ms; at 16 000 messages (past 5's
+// 48 per CU) 20.93 ms against the split form's 27.5 (profiles/r3/sha_lag/).
+constexpr int kShaQuadAuto = 6;
 
 int split_bufs() {
     const char* e = getenv("MXEC_SHA_SPLIT_BUFS");
@@ -895,8 +906,8 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
     const uint32_t blocks = (a.n + 63) / 64;
     int form = a.force;
     if (form == 0) {
-        // MXEC_SHA_FORM=one|split|quad|lag pins the form (tests, lab).  Auto:
-        // quad while its workgroups fit one per CU (one wave per SIMD), then
+        // MXEC_SHA_FORM=one|split|quad|lag|lagpair pins the form (tests, lab).
+        // Auto: the lag pair form while its workgroups fit one per CU, then
         // split, then one wave per 64 messages.
         const uint64_t n_cus = a.n_cus ? a.n_cus : 256;
         const char* env = getenv("MXEC_SHA_FORM");
@@ -904,13 +915,19 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         else if (env && !strcmp(env, "split")) form = 2;
         else if (env && !strcmp(env, "quad")) form = 4;
         else if (env && !strcmp(env, "lag")) form = 5;
-        else form = a.n <= kShaQuadMsgs * n_cus ? kShaQuadAuto : a.n <= kSplitMaxMessages ? 2 : 1;
+        else if (env && !strcmp(env, "lagpair")) form = 6;
+        else form = a.n <= kShaLagMsgs * n_cus ? kShaQuadAuto : a.n <= kSplitMaxMessages ? 2 : 1;
     }
-    if (a.piece.state && form != 4 && form != 5) return hipErrorInvalidValue;  // piece mode: quad forms only
+    if (a.piece.state && form != 4 && form != 5 && form != 6) return hipErrorInvalidValue;  // piece mode: quad forms
     if (form == 4 || form == 5) {  // 4: the same-round quad (lab A/B), 5: the lag quad
         const dim3 grid((a.n + kShaQuadMsgs - 1) / kShaQuadMsgs);
         hipLaunchKernelGGL(form == 5 ? sha256_quad_kernel<true> : sha256_quad_kernel<false>, grid, dim3(256), 0, s,
                            a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
+        return hipGetLastError();
+    }
+    if (form == 6) {  // the lag quad, two messages per quad (lab)
+        hipLaunchKernelGGL((sha256_quad_kernel<true, true>), dim3((a.n + 63) / 64), dim3(192), 0, s, a.ptrs, a.lens,
+                           a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
         return hipGetLastError();
     }
     if (form == 3) {

@@ -376,9 +376,10 @@ def test_short_last_chunk_device_encode_and_rebuild(ctx, last):
 
 # MXEC_SHA_FORM pins the SHA-256 kernel (lag: the default quad form, four
 # lanes per message behind a producer wave with the a-side two rounds behind
-# the e-side; quad: the same-round quad form; split: producer/consumer waves;
+# the e-side; lagpair: the lag form with two messages per quad (lab); quad:
+# the same-round quad form; split: producer/consumer waves;
 # one: one wave per 64 messages).
-SHA_FORMS = ["lag", "quad", "split", "one"]
+SHA_FORMS = ["lag", "lagpair", "quad", "split", "one"]
 
 
 def _pin_sha_form(monkeypatch, form):

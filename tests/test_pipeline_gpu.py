@@ -116,16 +116,16 @@ def test_batch_host_pinned_pieces_2d(ctx, ramp_kb, copy2d, monkeypatch):
 
 
 def test_batch_host_digests_past_quad_capacity(ctx):
-    """A wave of more chunks than the lag quad form holds (48 per CU: 12 288
+    """A wave of more chunks than the lag quad form holds (64 per CU: 16 384
     on 256 CUs) takes the group form (whole chunks, one launch after the
-    upload) instead of pieces: 2 200 objects of 4+2 x 4 KiB = 13 200 chunks,
+    upload) instead of pieces: 2 800 objects of 4+2 x 4 KiB = 16 800 chunks,
     parity and digests against the oracle for a sample, every digest against
     hashlib; then the verified GET of the same objects with one erasure and
     one corrupt shard in a few of them."""
     import hashlib
 
     rng = np.random.default_rng(61)
-    k, m, s, n = 4, 2, 4096, 2200
+    k, m, s, n = 4, 2, 4096, 2800
     data = rng.integers(0, 256, (n, k, s), dtype=np.uint8)
     par = np.zeros((n, m, s), np.uint8)
     objs = [(k, m, s)] * n
