@@ -216,11 +216,22 @@ class Encode:
             self.main.wait_stream(st)
 
     def spot_check(self):
+        """First, middle and last object, and the objects either side of
+        every grid-stride iteration boundary of the grid in use, against the
+        oracle (most of a full batch's tiles run in iterations >= 2)."""
         import numpy as np
 
-        want = _oracle().encode(list(self.data[0].cpu().numpy()), self.m, self.S)
-        got = self.parity[0].cpu().numpy()
-        return all(np.array_equal(got[i], want[i]) for i in range(self.m))
+        oracle = _oracle()
+        r = min(self.m, 8)
+        tile = 16384 if self.m <= 4 else 8192
+        n_cus = self.torch.cuda.get_device_properties(self.data.device).multi_processor_count
+        bpc = self.ctx.rs_grid(self.k, self.m, self.S) or rs_blocks_per_cu(r)
+        for o in spot_objects(self.n, -(-self.S // tile), bpc * n_cus):
+            want = oracle.encode(list(self.data[o].cpu().numpy()), self.m, self.S)
+            got = self.parity[o].cpu().numpy()
+            if not all(np.array_equal(got[i], want[i]) for i in range(self.m)):
+                return False
+        return True
 
     def cpu_work(self):
         import numpy as np
@@ -258,7 +269,11 @@ class Reconstruct:
                                   self.obj[:, k:].data_ptr(), (k + m) * S, S,
                                   digests_ptr=self.dig.data_ptr(), stream=sh)
         torch.cuda.synchronize()
-        self.ref = self.obj[0].clone()
+        # first / middle / last object and both sides of each grid-stride
+        # iteration boundary of the R = 2 decode (64 tiles per object)
+        n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        self.spot = spot_objects(n, 64, rs_blocks_per_cu(2) * n_cus)
+        self.ref = self.obj[self.spot].clone()
         rng = np.random.default_rng(seed)
         self.present0 = np.ones(n * (k + m), np.uint8)
         for o in range(n):
@@ -278,7 +293,7 @@ class Reconstruct:
         assert rc == 0, f"reconstruct rc={rc}: {self.ctx.last_error() if hasattr(self.ctx, 'last_error') else ''}"
 
     def spot_check(self):
-        return bool(self.torch.equal(self.obj[0], self.ref))
+        return bool(self.torch.equal(self.obj[self.spot], self.ref))
 
     def cpu_work(self):
         import numpy as np
@@ -684,6 +699,18 @@ def make_workload(cfg, torch, ctx, dev, sh, n_objects, rank, workers=8):
     if cfg == "frames":
         return Frames(torch, ctx, dev, sh, n_objects or 256, 40 << 20, seed)
     raise SystemExit(f"unknown --config {cfg}")
+
+
+def spot_objects(n: int, tiles_per_obj: int, grid: int) -> list:
+    """Objects a spot check compares: the first, middle and last, and those
+    either side of every grid-stride iteration boundary (tile = grid * i)."""
+    s = {0, n // 2, n - 1}
+    b = grid
+    while b < tiles_per_obj * n:
+        o = b // tiles_per_obj
+        s.update({max(o - 1, 0), o, min(o + 1, n - 1)})
+        b += grid
+    return sorted(s)
 
 
 def rs_blocks_per_cu(r_total: int) -> int:

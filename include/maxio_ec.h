@@ -110,6 +110,14 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
  * the shape is still being tuned; the default grid for shapes never launched
  * or too small to tune.  Diagnostics (the bench reports it). */
 int mxec_ctx_rs_grid(mxec_ctx* ctx, int dev, int k, int m, uint64_t shard_size);
+/* Coefficient-table arena statistics of ctx device `dev`: how often the
+ * arena's two halves were recycled (a new generation reused the older half),
+ * how many batches were queued again because their tables' half was
+ * recycled before their launches were fenced, and how many recycles had to
+ * wait for a fenced launch still running (fence_waits may be NULL).
+ * Diagnostics (tests). */
+int mxec_ctx_coef_stats(mxec_ctx* ctx, int dev, uint64_t* recycles, uint64_t* relaunches,
+                        uint64_t* fence_waits);
 /* Page-locked host memory for request bodies and GET buffers (the Axum body
  * MaxIO hands to a PUT, the buffer a GET fills).  Every host-pointer entry
  * point accepts any host memory; when a buffer comes from here, its bytes

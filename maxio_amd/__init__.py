@@ -21,6 +21,7 @@ from .ec import (  # noqa: F401
     device_count,
     parity_matrix,
     rs_check,
+    version,
 )
 from ._native import LIB_PATH, NativeLibraryMissing, declared_symbols, lib  # noqa: F401
 
@@ -38,6 +39,7 @@ __all__ = [
     "put_result",
     "device_count",
     "parity_matrix",
+    "version",
     "rs_check",
     "lib",
     "LIB_PATH",

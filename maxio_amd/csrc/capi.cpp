@@ -88,7 +88,7 @@ int rebuild_batch(Device& d, Slot& slot, hipStream_t s, bool data_only, const st
         }
         return run_rs_mixed(d, slot, s, groups);
     };
-    MXEC_TRY(with_stable_coef(d, collect, launch));
+    MXEC_TRY(with_stable_coef(d, s, collect, launch));
     for (size_t t = 0; t < which.size(); ++t)
         if (plans[t])
             for (int e : plans[t]->missing) all[which[t]].present[e] = 1;
@@ -99,7 +99,13 @@ int rebuild_batch(Device& d, Slot& slot, hipStream_t s, bool data_only, const st
 
 extern "C" {
 
-const char* mxec_version(void) { return "maxio_ec 0.1.0 (gfx950)"; }
+const char* mxec_version(void) {
+#ifdef MXEC_LAB
+    return "maxio_ec 0.1.0 (gfx950, lab build)";
+#else
+    return "maxio_ec 0.1.0 (gfx950)";
+#endif
+}
 
 const char* mxec_strerror(int code) {
     switch (code) {
@@ -146,24 +152,22 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
             return nullptr;
         }
         if (streams_per_device < 1) streams_per_device = 1;
+        // Every documented setting, read once (knobs.hpp).
         // MXEC_TEST_LOGICAL_DEVICES=L (tests and bench rehearsals only): open
         // every selected device L times, each copy with its own slots,
         // streams, arenas, combiner and pipeline, so the multi-device paths
         // (per-device workers, round robin, error aggregation) run on a
         // one-GPU box.  Never meant for production: it warns on stderr.
-        int logical = 1;
-        if (const char* e = getenv("MXEC_TEST_LOGICAL_DEVICES")) {
-            logical = std::max(1, std::min(8, atoi(e)));
-            if (logical > 1)
-                fprintf(stderr, "maxio_ec: MXEC_TEST_LOGICAL_DEVICES=%d: every selected GPU is opened %d times "
-                                "as separate devices (test-only setting)\n", logical, logical);
-        }
+        Knobs kn = read_knobs();
+        const int logical = kn.test_logical_devices;
         auto* ctx = new mxec_ctx();
+        ctx->c.knobs = kn;
         for (int dl = 0; dl < n * logical && dl < 32 * logical; ++dl) {
             const int d = dl / logical;
             if (device_mask && !(device_mask & (1u << d))) continue;
             auto dev = std::make_unique<Device>();
             dev->id = d;
+            dev->kn = &ctx->c.knobs;
             if (hipSetDevice(d) != hipSuccess) continue;
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && cus > 0)
@@ -208,11 +212,12 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
 void mxec_close(mxec_ctx* ctx) {
     if (!ctx) return;
     async_shutdown(ctx->c);  // every queued *_async call finishes first
-    affinity_report();
+    if (ctx->c.knobs.debug_affinity) affinity_report();
     for (auto& d : ctx->c.devs) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
         rs_grid_release(*d);
+        coef_release(*d);
         for (auto& s : d->slots) slot_destroy(*s);
     }
     delete ctx;
@@ -229,6 +234,17 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
     if (!ctx || i < 0 || i >= int(ctx->c.devs.size()) || !launches || !messages)
         return set_error(MXEC_E_INVALID_ARG, "invalid argument");
     combiner_stats(*ctx->c.devs[size_t(i)], launches, messages);
+    return MXEC_OK;
+}
+
+int mxec_ctx_coef_stats(mxec_ctx* ctx, int dev, uint64_t* recycles, uint64_t* relaunches, uint64_t* fence_waits) {
+    if (!ctx || dev < 0 || dev >= int(ctx->c.devs.size()) || !recycles || !relaunches)
+        return set_error(MXEC_E_INVALID_ARG, "invalid argument");
+    Device& d = *ctx->c.devs[size_t(dev)];
+    std::lock_guard<std::mutex> g(d.coef_mu);
+    *recycles = d.coef_recycles;
+    *relaunches = d.coef_relaunches;
+    if (fence_waits) *fence_waits = d.coef_fence_waits;
     return MXEC_OK;
 }
 
@@ -277,8 +293,7 @@ void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes) {
     if (!ctx || bytes == 0) return nullptr;
     void* p = nullptr;
     constexpr unsigned long kMaxNode = 1024;
-    const char* env = getenv("MXEC_HOST_NUMA");
-    const int node = env && atoi(env) != 0 ? ctx_numa_node(ctx) : -1;  // opt-in until measured
+    const int node = ctx->c.knobs.host_numa ? ctx_numa_node(ctx) : -1;  // opt-in until measured
     int old_mode = 0;
     unsigned long old_mask[kMaxNode / 64] = {}, mask[kMaxNode / 64] = {};
     bool bound = false;
@@ -384,7 +399,7 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* c
         for (int i = 0; i < m; ++i) out[size_t(i)] = base + sa * uint64_t(k + i);
         uint32_t off = 0;
         MXEC_TRY(with_stable_coef(
-            *ds.d, [&] { return encode_coef(*ds.d, k, m, &off); },
+            *ds.d, s, [&] { return encode_coef(*ds.d, k, m, &off); },
             [&] {
                 RsObject ob{in.data(), len.data(), out.data(), len.data() + k, off};
                 return run_rs(*ds.d, slot, s, shard_size, k, m, {ob});
@@ -477,7 +492,7 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
             RsObject ob{in.data(), in_len.data(), out.data(), out_len.data(), off};
             return run_rs(*ds.d, slot, s, shard_size, k, int(out.size()), {ob});
         };
-        MXEC_TRY(with_stable_coef(*ds.d, collect, launch));
+        MXEC_TRY(with_stable_coef(*ds.d, s, collect, launch));
         if (!plan->missing.empty()) {
             std::vector<DownloadSeg> down;
             for (size_t t = 0; t < out.size(); ++t)
@@ -522,7 +537,7 @@ int mxec_encode_strided_device(mxec_ctx* ctx, int dev, void* stream, int k, int 
             objs[o] = RsObject{&in[o * k], len.data(), &out[o * m], len.data() + k, 0};
         }
         MXEC_TRY(with_stable_coef(
-            *ds.d, [&] { return encode_coef(*ds.d, k, m, &off); },
+            *ds.d, s, [&] { return encode_coef(*ds.d, k, m, &off); },
             [&] {
                 for (auto& ob : objs) ob.coef_off = off;
                 return run_rs(*ds.d, *ds.slot, s, shard_size, k, m, objs);
@@ -576,7 +591,7 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream, const mxec_ob
         // One launch per parity count m: objects of every k and shard size
         // share it (run_rs_mixed; unaligned or m > 8: per (k, shard_size)).
         std::map<int, std::vector<RsMixedObject>> groups;
-        MXEC_TRY(with_stable_coef(*ds.d, [&]() -> int {
+        MXEC_TRY(with_stable_coef(*ds.d, s, [&]() -> int {
             groups.clear();
             std::map<std::pair<int, int>, uint32_t> offs;
             for (uint64_t o = 0; o < n_obj; ++o) {
@@ -653,7 +668,7 @@ int mxec_reconstruct_strided_device(mxec_ctx* ctx, int dev, void* stream, int k,
                         lens.push_back(len[size_t(i)]);
                         idx.push_back(o * total + i);
                     }
-            if (!ptrs.empty() && !sha_combines(ptrs.size())) {
+            if (!ptrs.empty() && !sha_combines(*ds.d, ptrs.size())) {
                 // A batch that fills the chip: its own launch on `stream`,
                 // digests compared on the device (the verify kernel compares
                 // message t against expected[idx[t]]), n flags read back.

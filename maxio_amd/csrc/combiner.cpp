@@ -26,7 +26,6 @@
 
 namespace mxec {
 
-bool combine_log();
 
 struct ShaCombiner {
     struct Req {
@@ -119,7 +118,7 @@ struct ShaCombiner {
             }
             if (r->after_rc) r->after_msg = last_error();
         }
-        if (combine_log())
+        if (d.kn && d.kn->combine_log)
             std::fprintf(stderr, "[mxec combine] after-launch work %lld us\n",
                          (long long)std::chrono::duration_cast<std::chrono::microseconds>(
                              std::chrono::steady_clock::now() - ta).count());
@@ -146,49 +145,25 @@ struct ShaCombiner {
 // concurrent 10 240-message batches (config 3c) ran 1.34x faster as one
 // split-form launch than as eight launches on eight streams
 // (profiles/r1_bench_cfg3c_w8_combine_below_*.json).  MXEC_COMBINE_BELOW=n
-// sends requests of n or more messages to their own launch on the caller's
-// stream instead.
-bool sha_combines(size_t n) {
-    static const size_t below = [] {
-        const char* e = getenv("MXEC_COMBINE_BELOW");
-        return e ? size_t(strtoull(e, nullptr, 10)) : size_t(0);
-    }();
+// (Knobs::combine_below) sends requests of n or more messages to their own
+// launch on the caller's stream instead.
+bool sha_combines(const Device& d, size_t n) {
+    const size_t below = d.kn ? d.kn->combine_below : 0;
     return below == 0 || n < below;
 }
 
 namespace {
 
-// MXEC_GATHER_US: how long a lone leader waits for company (default 100 us);
-// MXEC_GATHER_MAX_US: the bound when waiting for the previous batch size
-// (default 2 ms).
-long env_us(const char* name, long dflt) {
-    const char* e = getenv(name);
-    return e ? long(strtol(e, nullptr, 10)) : dflt;
+// The combiner's windows (knobs.hpp): MXEC_GATHER_US, how long a lone leader
+// waits for company (default 100 us); MXEC_GATHER_MAX_US, the bound when
+// waiting for the previous batch size (default 2 ms); MXEC_GATHER_IDLE_US,
+// once a batch is forming, how long a gap between arrivals still counts as
+// "more are coming" (default 300 us).  MXEC_COMBINE_LOG=1: one stderr line
+// per combined launch (requests, messages, gathering and launch times).
+const Knobs& knobs_of(const Device& d) {
+    static const Knobs dflt;
+    return d.kn ? *d.kn : dflt;
 }
-long gather_us() {
-    static const long us = env_us("MXEC_GATHER_US", 100);
-    return us;
-}
-long gather_max_us() {
-    static const long us = env_us("MXEC_GATHER_MAX_US", 2000);
-    return us;
-}
-// MXEC_GATHER_IDLE_US: once a batch is forming, how long a gap between
-// arrivals still counts as "more are coming" (default 300 us).
-long gather_idle_us() {
-    static const long us = env_us("MXEC_GATHER_IDLE_US", 300);
-    return us;
-}
-// MXEC_COMBINE_LOG=1: one stderr line per combined launch (requests,
-// messages, gathering and launch times) -- for tuning the windows above.
-}  // namespace
-
-bool combine_log() {
-    static const bool on = env_us("MXEC_COMBINE_LOG", 0) != 0;
-    return on;
-}
-
-namespace {
 
 // MXEC_COMBINE_STREAMS: launches in flight per device (default 2).  A second
 // launch starts beside a running one only while both together stay under
@@ -198,33 +173,22 @@ namespace {
 // at a time -- unconditional lanes split them and issue-bound launches side
 // by side share the SIMDs (config 3c 509 -> 344 GiB/s with two lanes,
 // profiles/r1_combine_lanes.txt).
-size_t combine_streams() {
-    static const size_t n = [] {
-        const long v = env_us("MXEC_COMBINE_STREAMS", 2);
-        return size_t(v < 1 ? 1 : v > 4 ? 4 : v);
-    }();
-    return n;
-}
-
+//
 // MXEC_COMBINE_PRIORITY (default 1): the combiner's streams get the highest
 // stream priority, i.e. a hardware queue of their own.  Streams share
 // GPU_MAX_HW_QUEUES = 4 queues, so a 30 ms hash launch on a normal-priority
 // stream held up the uploads of a quarter of the request streams behind it
 // (64-thread GET: host upload + wait 6.4 -> 2.7 ms per request, 7.3 -> 8.0 GiB/s).
-bool combine_priority() {
-    static const bool p = env_us("MXEC_COMBINE_PRIORITY", 1) != 0;
-    return p;
-}
 
 ShaCombiner* combiner_of(Device& d) {
     std::lock_guard<std::mutex> g(d.comb_mu);
     if (!d.comb) {
         auto c = std::make_shared<ShaCombiner>();
-        for (size_t i = 0; i < combine_streams(); ++i) {
+        for (int i = 0; i < knobs_of(d).combine_streams; ++i) {
             auto sl = std::make_unique<Slot>();
             sl->owner = &d;
             int least = 0, greatest = 0;
-            const bool prio = combine_priority() &&
+            const bool prio = knobs_of(d).combine_priority &&
                               hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
                               hipStreamCreateWithPriority(&sl->stream, hipStreamNonBlocking, greatest) == hipSuccess;
             if (!prio && hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
@@ -246,7 +210,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
                     const std::vector<uint64_t>& lens, uint8_t* out, hipEvent_t ready,
                     const std::function<int()>* after_launch) {
     if (ptrs.empty()) return MXEC_OK;
-    if (!sha_combines(ptrs.size())) {
+    if (!sha_combines(d, ptrs.size())) {
         // Opted out by MXEC_COMBINE_BELOW: its own launch on the caller's
         // stream (the kernel picks its form by message count).
         const size_t n = ptrs.size();
@@ -294,7 +258,8 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // ms per 1 MiB chunk), so the wait costs a few percent at most, and
         // the previous size is forgotten as soon as fewer come.
         const size_t want = c->last_batch;
-        const long wait_us = want > 1 ? gather_max_us() : gather_us();
+        const Knobs& kn = knobs_of(d);
+        const long wait_us = want > 1 ? kn.gather_max_us : kn.gather_us;
         const auto t0 = std::chrono::steady_clock::now();
         if (c->pending.size() < std::max<size_t>(want, 2) && wait_us > 0)
             c->cv_gather.wait_for(lk, std::chrono::microseconds(wait_us),
@@ -321,12 +286,15 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         auto launch_us = [&] {
             uint64_t longest = 0;
             for (const ShaCombiner::Req* r : c->pending) longest = std::max(longest, r->longest);
-            return double(longest / 64) * 1.8;
+            // The form the kernel will pick for this many messages sets the
+            // chain's pace (kernels.hpp kShaLagUsPerBlock / kShaSplitUsPerBlock).
+            const bool lag = c->pending_msgs <= size_t(kShaLagMsgs) * size_t(d.n_cus);
+            return double(longest / 64) * (lag ? kShaLagUsPerBlock : kShaSplitUsPerBlock);
         };
         const double est_us = c->pending.size() >= 2 ? launch_us() : 0.0;
-        if (c->pending.size() >= 2 && est_us * 0.02 >= double(gather_idle_us())) {
-            const auto hard = t0 + std::chrono::microseconds(std::max<long>(gather_max_us(), long(est_us * 0.15)));
-            const long idle = std::max<long>(gather_idle_us(), long(est_us * 0.02));
+        if (c->pending.size() >= 2 && est_us * 0.02 >= double(kn.gather_idle_us)) {
+            const auto hard = t0 + std::chrono::microseconds(std::max<long>(kn.gather_max_us, long(est_us * 0.15)));
+            const long idle = std::max<long>(kn.gather_idle_us, long(est_us * 0.02));
             for (size_t seen = c->pending.size(); std::chrono::steady_clock::now() < hard;) {
                 c->cv_gather.wait_for(lk, std::chrono::microseconds(idle),
                                       [&] { return c->pending.size() > seen; });
@@ -355,7 +323,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         } catch (...) {
             rc = set_error(MXEC_E_OOM, "host allocation failed");
         }
-        if (combine_log()) {
+        if (kn.combine_log) {
             const auto t2 = std::chrono::steady_clock::now();
             using us = std::chrono::microseconds;
             std::fprintf(stderr, "[mxec combine] requests %zu messages %zu gather_us %lld run_us %lld rc %d\n",

@@ -488,11 +488,15 @@ hipError_t launch_crc(const CrcArgs& a, int n_cus, hipStream_t s) {
         // 128 workgroups per CU of grid-stride: 8 / 32 / 128 / 512 measured
         // 4.70 / 4.74 / 4.81 / 4.79 TB/s (profiles/r2_crc_grid_ab.txt; more,
         // shorter workgroups keep the tiles in flight together, as for RS).
+#ifdef MXEC_LAB
         static const uint64_t bpc = [] {  // MXEC_CRC_BPC: lab override
             const char* e = getenv("MXEC_CRC_BPC");
             const long v = e ? atol(e) : 0;
             return v > 0 && v <= 4096 ? uint64_t(v) : uint64_t(128);
         }();
+#else
+        constexpr uint64_t bpc = 128;
+#endif
         const uint64_t grid = std::min<uint64_t>(a.n_tiles, uint64_t(n_cus) * bpc);
         hipLaunchKernelGGL(crc_tiles_kernel, dim3(uint32_t(grid)), dim3(256), 0, s, a);
         hipError_t e = hipGetLastError();

@@ -51,6 +51,9 @@ struct RsArgs {
     // Uniform launches: workgroups per CU chosen by the caller (the grid
     // tuner, ops.cpp); 0 = rs_default_variant's.
     uint32_t blocks_per_cu = 0;
+    // Every launch form: at most this many workgroups (0: no cap).  Tests
+    // (MXEC_TEST_RS_GRID) shrink the grid so each workgroup walks many tiles.
+    uint32_t max_blocks = 0;
 };
 constexpr uint32_t kMultiR = 4;
 
@@ -122,6 +125,12 @@ constexpr uint32_t kShaQuadMsgs = 48;
 // Messages per workgroup of the lag quad form with two messages per quad
 // (two consumer waves of 32): the auto latency form, one workgroup per CU.
 constexpr uint32_t kShaLagMsgs = 64;
+// A chain's pace per 64-byte block on the MI355X (us), for host-side
+// estimates of a launch's length (combiner.cpp): the lag pair form the auto
+// choice takes up to kShaLagMsgs per CU (config 3: 20.7 ms for 16 384
+// blocks), the split / one-wave forms beyond (29 ms per 1 MiB chunk).
+constexpr double kShaLagUsPerBlock = 1.27;
+constexpr double kShaSplitUsPerBlock = 1.8;
 // Blocks per stream-form segment (32 KiB of each message).
 constexpr uint32_t kShaSegBlocks = 512;
 // Timeout code the stream form leaves in work[1] when a wave gave up

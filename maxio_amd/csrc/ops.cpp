@@ -32,7 +32,8 @@ int encode_coef(Device& dev, int k, int m, uint32_t* off) {
         std::lock_guard<std::mutex> g(dev.coef_mu);
         auto it = dev.coef_index.find(key);
         if (it != dev.coef_index.end()) {
-            *off = it->second;
+            *off = it->second.first;
+            coef_note_use(it->second.second);
             return MXEC_OK;
         }
     }
@@ -66,25 +67,33 @@ int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_onl
     plan->reset();
     *off = 0;
     if (np < k) return MXEC_OK;
-    uint64_t epoch;
     {
         std::lock_guard<std::mutex> g(dev.coef_mu);
         auto it = dev.patterns.find(key);
         if (it != dev.patterns.end()) {
-            *plan = std::static_pointer_cast<const DecodePlan>(it->second.first);
-            *off = it->second.second;
+            *plan = std::static_pointer_cast<const DecodePlan>(it->second.plan);
+            *off = it->second.off;
+            if (!(*plan)->missing.empty()) coef_note_use(it->second.gen);
             return MXEC_OK;
         }
-        epoch = dev.coef_epoch;
     }
     auto p = decode_cache().get(k, m, present, data_only);
     if (!p) return set_error(MXEC_E_SINGULAR_MATRIX, "decode matrix inversion failed");
     uint32_t o = 0;
-    if (!p->missing.empty()) MXEC_TRY(decode_coef(dev, *p, data_only, &o));
+    CoefUse mine;  // the table's generation, then noted for the caller's batch too
+    if (!p->missing.empty()) {
+        CoefUse* outer = coef_use_swap(&mine);
+        const int rc = decode_coef(dev, *p, data_only, &o);
+        coef_use_swap(outer);
+        MXEC_TRY(rc);
+        coef_note_use(mine.lo);
+    }
     {
         std::lock_guard<std::mutex> g(dev.coef_mu);
-        // Only remember the offset if the arena was not recycled meanwhile.
-        if (dev.coef_epoch == epoch) dev.patterns.emplace(key, std::make_pair(p, o));
+        // Only remember the offset while its generation is live (a recycle
+        // may have come between the upload and here).
+        const uint64_t gen = mine.any() ? mine.lo : dev.coef_gen;
+        if (gen + 1 >= dev.coef_gen) dev.patterns.emplace(key, Device::PatternVal{p, o, gen});
     }
     *plan = p;
     *off = o;
@@ -95,7 +104,7 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
            const std::vector<RsObject>& objs, DescArena* arena) {
     if (objs.empty() || r == 0) return MXEC_OK;
     const size_t n = objs.size();
-    if (affinity_on()) {
+    if (affinity_on(dev)) {
         std::vector<const void*> ps;
         for (const RsObject& ob : objs) {
             for (int j = 0; j < k; ++j) ps.push_back(ob.in[j]);
@@ -159,20 +168,27 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     a.k = uint32_t(k);
     a.r_total = uint32_t(r);
     a.aligned = aligned ? 1u : 0u;
+    a.max_blocks = dev.kn ? dev.kn->test_rs_grid : 0u;
     // Large aligned single-launch batches take the grid tuner's pick.
     GridTuner::Trial trial;
     const double gb = double(n) * double(k + r) * double(shard_size) / 1e9;
     if (aligned && r <= 4) MXEC_TRY(rs_grid_pick(dev, k, r, shard_size, gb, &a.blocks_per_cu, &trial));
-    if (trial.a) MXEC_HIP(hipEventRecord(trial.a, s));
-    for (int row0 = 0; row0 < r; row0 += 8) {
+    hipError_t e = trial.a ? hipEventRecord(trial.a, s) : hipSuccess;
+    for (int row0 = 0; row0 < r && e == hipSuccess; row0 += 8) {
         a.row0 = uint32_t(row0);
         a.r = uint32_t(std::min(8, r - row0));
-        MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
+        e = launch_rs_apply(a, dev.n_cus, s);
     }
+    if (trial.a && e == hipSuccess) e = hipEventRecord(trial.b, s);
     if (trial.a) {
-        MXEC_HIP(hipEventRecord(trial.b, s));
-        rs_grid_record(dev, k, r, shard_size, trial);
+        if (e == hipSuccess) {
+            rs_grid_record(dev, k, r, shard_size, trial);
+        } else {  // the trial's events are ours to free on a failed launch
+            (void)hipEventDestroy(trial.a);
+            (void)hipEventDestroy(trial.b);
+        }
     }
+    MXEC_HIP(e);
     return w.finish(s);
 }
 
@@ -181,10 +197,12 @@ namespace {
 // and an event pair costs nothing next to it.
 constexpr double kTuneMinGB = 1.0;
 
-bool tuning_on() {
-    const char* e = getenv("MXEC_RS_TUNE");
-    if (e && !strcmp(e, "0")) return false;
-    return getenv("MXEC_RS_BPC") == nullptr;  // a lab override fixes the grid
+bool tuning_on(const Device& dev) {
+    if (dev.kn && (!dev.kn->rs_tune || dev.kn->test_rs_grid)) return false;
+#ifdef MXEC_LAB
+    if (getenv("MXEC_RS_BPC")) return false;  // a lab override fixes the grid
+#endif
+    return true;
 }
 
 // Reads every finished trial of a shape into its best times; decides once
@@ -216,7 +234,7 @@ void tuner_poll(GridTuner::State& st) {
 int rs_grid_pick(Device& dev, int k, int r, uint64_t shard_size, double gb, uint32_t* bpc,
                  GridTuner::Trial* trial) {
     *bpc = 0;
-    if (!tuning_on() || gb < kTuneMinGB) return MXEC_OK;
+    if (!tuning_on(dev) || gb < kTuneMinGB) return MXEC_OK;
     std::lock_guard<std::mutex> g(dev.tuner.mu);
     const auto key = std::make_tuple(k, r, shard_size);
     // A server sees a handful of shapes; past 256 new ones keep the default.
@@ -227,15 +245,16 @@ int rs_grid_pick(Device& dev, int k, int r, uint64_t shard_size, double gb, uint
         st.cands[1] = st.cands[0] / 2;  // r <= 2: 1024 / 512; r = 3, 4: 512 / 256
     }
     tuner_poll(st);
-    if (st.decided < 0 && st.launches >= 5) {
-        // Launches 2-5 were the trials (two per grid): wait for them once,
-        // so a caller that queues far ahead still gets the decision now.
-        for (auto& t : st.pending) (void)hipEventSynchronize(t.b);
-        tuner_poll(st);
-        if (st.decided < 0) st.decided = st.best_ms_per_gb[1] < st.best_ms_per_gb[0] ? 1 : 0;
-    }
     if (st.decided >= 0) {
         *bpc = uint32_t(st.cands[st.decided]);
+        return MXEC_OK;
+    }
+    if (st.launches >= 5) {
+        // Launches 2-5 were the trials (two per grid) and some still run (a
+        // caller that queues far ahead): the default grid until their events
+        // complete -- never a host wait inside an enqueue-only call.
+        if (st.pending.empty()) st.decided = st.best_ms_per_gb[1] < st.best_ms_per_gb[0] ? 1 : 0;
+        *bpc = uint32_t(st.cands[st.decided >= 0 ? st.decided : 0]);
         return MXEC_OK;
     }
     const int l = st.launches++;
@@ -259,10 +278,12 @@ void rs_grid_record(Device& dev, int k, int r, uint64_t shard_size, const GridTu
 
 int rs_grid_in_use(Device& dev, int k, int r, uint64_t shard_size) {
     const int def = rs_default_variant(uint32_t(r)).blocks_per_cu;
+#ifdef MXEC_LAB
     if (const char* e = getenv("MXEC_RS_BPC")) {
         const int b = atoi(e);
         if (b > 0 && b <= 4096) return b;
     }
+#endif
     std::lock_guard<std::mutex> g(dev.tuner.mu);
     auto it = dev.tuner.states.find(std::make_tuple(k, r, shard_size));
     if (it == dev.tuner.states.end()) return def;
@@ -334,7 +355,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         for (const auto& key : order) MXEC_TRY(run_rs(dev, slot, s, key.second, key.first, g.first, by[key], arena));
     }
     if (grouped.empty()) return MXEC_OK;
-    if (affinity_on()) {
+    if (affinity_on(dev)) {
         std::vector<const void*> ps;
         for (const Plan& p : grouped)
             for (const RsMixedObject& ob : *p.objs) {
@@ -345,9 +366,9 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
     }
     // Two or more grouped launches of r <= kMultiR with the same tile: one
     // multi-r launch instead (rs_apply_multi; MXEC_RS_MULTI=0 keeps one
-    // launch per r; read per call, so tests can run both forms).
-    const char* multi_env = getenv("MXEC_RS_MULTI");
-    const bool multi_on = !(multi_env && !strcmp(multi_env, "0"));
+    // launch per r).
+    const bool multi_on = !dev.kn || dev.kn->rs_multi;
+    const uint32_t max_blocks = dev.kn ? dev.kn->test_rs_grid : 0u;
     bool multi = multi_on && grouped.size() >= 2;
     uint64_t m_obj = 0, m_k = 0, m_tiles = 0;
     const uint64_t m_tile = rs_tile_bytes(rs_group_variant(kMultiR));
@@ -409,6 +430,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         a.multi = 1;
         a.tiles = reinterpret_cast<const RsTileRec*>(db + o_tiles);
         a.n_tiles = m_tiles;
+        a.max_blocks = max_blocks;
         MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
         return w.finish(s);
     }
@@ -469,6 +491,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
         a.aligned = 1;
         a.tiles = reinterpret_cast<const RsTileRec*>(db + p.o_tiles);
         a.n_tiles = p.n_tiles;
+        a.max_blocks = max_blocks;
         MXEC_HIP(launch_rs_apply(a, dev.n_cus, s));
     }
     return w.finish(s);
@@ -481,7 +504,7 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     const size_t n = ptrs.size();
     if (tmo_dev) *tmo_dev = nullptr;
     if (!n) return MXEC_OK;
-    if (affinity_on()) {
+    if (affinity_on(dev)) {
         std::vector<const void*> ps(ptrs.begin(), ptrs.end());
         ps.push_back(digests_dev);
         ps.push_back(ok_dev);
@@ -489,12 +512,10 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     }
     // The stream form: more 64-message groups than SIMDs, every message
     // 16-byte aligned, a caller that checks the timeout word, ring tables.
-    // MXEC_SHA_FORM=stream forces it whenever it is allowed (tests).
+    // MXEC_SHA_FORM=stream forces it whenever it is allowed (tests); one,
+    // split and lagpair pin the other forms the auto choice takes.
     const uint64_t groups = (n + 63) / 64, simds = uint64_t(dev.n_cus) * 4;
-    static const int env_form = [] {
-        const char* e = getenv("MXEC_SHA_FORM");
-        return e && !strcmp(e, "stream") ? 3 : 0;
-    }();
+    const int env_form = dev.kn ? dev.kn->sha_form : 0;
     uint64_t longest = 0;
     for (uint64_t l : lens) longest = std::max(longest, l);
     const uint64_t seg_max = sha_stream_seg_max(longest, kShaSegBlocks);
@@ -534,6 +555,7 @@ int run_sha(Device& dev, Slot& slot, hipStream_t s, const std::vector<const uint
     a.n = uint32_t(n);
     a.n_cus = uint32_t(dev.n_cus);
     a.force = form == 3 && !stream ? 0 : form;
+    if (a.force == 0 && (env_form == 1 || env_form == 2 || env_form == 6)) a.force = env_form;
     if (stream) {
         void* st = nullptr;
         MXEC_TRY(w.scratch(32 * n, &st));
@@ -572,7 +594,7 @@ int run_sha_pieces(Device& dev, Slot& slot, hipStream_t s, const std::vector<con
     for (size_t i = 0; i < n; ++i)
         if (totals[i] == kShaNotFinal ? lens[i] % 64 != 0 : totals[i] < lens[i])
             return set_error(MXEC_E_INVALID_ARG, "sha pieces: a mid-message piece must be whole 64-byte blocks");
-    if (affinity_on()) {
+    if (affinity_on(dev)) {
         std::vector<const void*> ps(ptrs.begin(), ptrs.end());
         ps.push_back(digests_dev);
         ps.push_back(state_dev);

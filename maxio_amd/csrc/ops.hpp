@@ -101,7 +101,7 @@ int sha256_combined(Device& dev, Slot& slot, hipStream_t s, const std::vector<co
                     const std::function<int()>* after_launch = nullptr);
 void combiner_stats(Device& dev, uint64_t* batches, uint64_t* messages);
 // Whether a request of n messages goes through the combiner.
-bool sha_combines(size_t n);
+bool sha_combines(const Device& d, size_t n);
 
 // Coefficient table of the (k, m) encoding matrix's parity rows.
 int encode_coef(Device& dev, int k, int m, uint32_t* off);
@@ -180,30 +180,32 @@ inline std::string too_few_msg(int present, int k, int total) {
            " missing)";
 }
 
-// Coefficient-table offsets are only valid until the device's 64 MiB table
-// arena is recycled (runtime.cpp coef_offset: it waits for the device, then
-// reuses the arena from the start).  `collect` takes a batch's offsets,
-// `launch` enqueues the kernels that read them; the pair runs again until no
-// recycle happened between the start of `collect` and the end of the
-// enqueue.  A recycle waits for every launch queued before it, so only a
-// launch queued after one can have read foreign tables: such a launch is
-// queued again with fresh offsets, behind it on the same stream and over the
-// same outputs (the RS kernels read only inputs and write only outputs), so
-// the last pass wins and the result is exact.
+// Coefficient-table offsets are valid while their generation's half of the
+// device's table arena is not reused (runtime.hpp Device::coef_*): `collect`
+// takes a batch's offsets (noting each table's generation), `launch`
+// enqueues the kernels that read them on `s`; then, under the arena's lock,
+// either every generation used is still live and an event on `s` fences the
+// batch (a later recycle of those halves waits for it), or one was recycled
+// between `collect` and here, and the pair runs again.  A launch queued with
+// a recycled half's offsets may have read foreign tables; its re-run is
+// queued behind it on the same stream over the same outputs (the RS kernels
+// read only inputs and write only outputs), so the last pass wins and the
+// result is exact.
 template <class C, class L>
-int with_stable_coef(Device& d, C&& collect, L&& launch) {
-    auto epoch = [&] {
-        std::lock_guard<std::mutex> g(d.coef_mu);
-        return d.coef_epoch;
-    };
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        const uint64_t e0 = epoch();
-        MXEC_TRY(collect());
-        MXEC_TRY(launch());
-        if (epoch() == e0) return MXEC_OK;
+int with_stable_coef(Device& d, hipStream_t s, C&& collect, L&& launch) {
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        CoefUse use;
+        CoefUse* outer = coef_use_swap(&use);
+        int rc = collect();
+        if (rc == MXEC_OK) rc = launch();
+        coef_use_swap(outer);
+        MXEC_TRY(rc);
+        bool live = true;
+        MXEC_TRY(coef_fence(d, use, s, &live));
+        if (live) return MXEC_OK;
     }
     return set_error(MXEC_E_INVALID_ARG,
-                     "the coefficient tables of one batch exceed the device's table arena (recycled 4 times)");
+                     "the coefficient tables of one batch exceed the device's table arena (recycled under it 8 times)");
 }
 
 }  // namespace mxec

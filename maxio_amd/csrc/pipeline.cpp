@@ -57,8 +57,12 @@ struct PieceGrid {
     std::vector<uint64_t> starts;  // the ramp's pieces, then every P
     uint64_t P, ramp_end = 0;
     explicit PieceGrid(uint64_t p) : P(p) {
-        const char* e = getenv("MXEC_PIPE_RAMP_KB");
+#ifdef MXEC_LAB
+        const char* e = getenv("MXEC_PIPE_RAMP_KB");  // lab builds only
         uint64_t w = uint64_t(e ? atol(e) : 0) << 10;
+#else
+        uint64_t w = 0;
+#endif
         w = w / 64 * 64;
         for (; w && w < p; w *= 2) {
             starts.push_back(ramp_end);
@@ -347,7 +351,7 @@ private:
                 }
                 return run_rs_mixed(d_, slot_, cs, rs_groups, &arena_);
             };
-            MXEC_TRY(with_stable_coef(d_, collect, launch));
+            MXEC_TRY(with_stable_coef(d_, cs, collect, launch));
             hipEvent_t rs_done;
             MXEC_TRY(new_event(&rs_done));
             MXEC_HIP(hipEventRecord(rs_done, cs));
@@ -512,7 +516,7 @@ private:
 
     int upload(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
-        if (affinity_on()) {
+        if (affinity_on(d_)) {
             const void* p = dst;
             MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload", &arena_, &p, 1));
         }
@@ -551,9 +555,13 @@ private:
         uint64_t rows = 0;
         uint64_t dpitch = 0, spitch = 0;
     };
-    static bool copy2d_on() {  // read per call (tests and labs switch it); default off, see below
+    static bool copy2d_on() {  // lab builds only (read per call); default off, see below
+#ifdef MXEC_LAB
         const char* e = getenv("MXEC_PIPE_COPY2D");
         return e && atoi(e) != 0;
+#else
+        return false;
+#endif
     }
     static bool extend(Run& r, uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!r.len) return false;
@@ -587,7 +595,7 @@ private:
         if (!r.len) return MXEC_OK;
         if (r.rows == 1) return upload(r.dst, r.src, r.len);
         if (is_pinned(r.src, (r.rows - 1) * r.spitch + r.len)) {
-            if (affinity_on()) {
+            if (affinity_on(d_)) {
                 const void* p = r.dst;
                 MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload 2d", &arena_, &p, 1));
             }
@@ -610,7 +618,7 @@ private:
         if (!r.len) return MXEC_OK;
         if (r.rows == 1) return download(r.dst, r.src, r.len);
         if (is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
-            if (affinity_on()) {
+            if (affinity_on(d_)) {
                 const void* p = r.src;
                 MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download 2d", &arena_, &p, 1));
             }
@@ -636,7 +644,7 @@ private:
 
     int download(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
-        if (affinity_on()) {
+        if (affinity_on(d_)) {
             const void* p = src;
             MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download", &arena_, &p, 1));
         }
@@ -674,11 +682,7 @@ private:
     // down, piece after piece, so every chain starts after the first piece
     // (~9 ms) and the wave ends near one chain's length.  Taken when the
     // wave's messages fit the lag quad form (64 per CU).
-    static uint64_t piece_bytes() {  // read per wave (tests and labs switch it)
-        const char* e = getenv("MXEC_PIPE_PIECE_MB");
-        const long v = e ? atol(e) : 1;
-        return v <= 0 ? uint64_t(0) : uint64_t(v) << 20;
-    }
+    uint64_t piece_bytes() const { return d_.kn ? d_.kn->pipe_piece : uint64_t(1) << 20; }  // MXEC_PIPE_PIECE_MB
 
     int wave_pieces(std::vector<HostObj>& objs, size_t o0, size_t o1, uint64_t P) {
         Slot& slot = slot_;
@@ -750,7 +754,7 @@ private:
                     ro[t] = RsObject{&ins[t * k], &lens[t * (k + m)], &outs[t * m], &lens[t * (k + m) + k], 0};
                 }
                 MXEC_TRY(with_stable_coef(
-                    d_, [&] { return encode_coef(d_, k, m, &coff); },
+                    d_, rs_s, [&] { return encode_coef(d_, k, m, &coff); },
                     [&] {
                         for (auto& r : ro) r.coef_off = coff;
                         return run_rs(d_, slot, rs_s, W, k, m, ro, &arena_);
@@ -872,7 +876,7 @@ private:
                     ro[t] = RsObject{&ins[t * k], &lens[t * (k + m)], &outs[t * m], &lens[t * (k + m) + k], 0};
                 }
                 MXEC_TRY(with_stable_coef(
-                    d_, [&] { return encode_coef(d_, k, m, &coff); },
+                    d_, rs_s, [&] { return encode_coef(d_, k, m, &coff); },
                     [&] {
                         for (auto& r : ro) r.coef_off = coff;
                         return run_rs(d_, slot, rs_s, S, k, m, ro, &arena_);

@@ -488,6 +488,15 @@ __global__ __launch_bounds__(kThreads) void rs_apply_multi(
     }
 }
 
+// Grid of a launch over n items (tiles or edge steps): n_cus * per_cu,
+// at most n (a grouped launch's first fetch needs every workgroup to own a
+// tile) and at most the caller's cap (tests).
+uint64_t grid_of(const RsArgs& a, int n_cus, int per_cu, uint64_t n) {
+    uint64_t blocks = uint64_t(n_cus) * uint64_t(per_cu);
+    if (a.max_blocks && blocks > a.max_blocks) blocks = a.max_blocks;
+    return blocks > n ? n : blocks;
+}
+
 template <int R, int V, bool NT, bool GRP = false, int OCC = 1, bool LNT = NT, int G = 4>
 hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles, uint64_t blocks,
                        hipStream_t s) {
@@ -500,8 +509,7 @@ hipError_t launch_fast(const RsArgs& a, uint32_t tiles_per_obj, uint64_t n_tiles
 // Multi-r grouped launches (a.multi): V = 4, nontemporal, rs_group_variant's grid.
 hipError_t launch_multi(const RsArgs& a, int n_cus, hipStream_t s) {
     const RsVariant v = rs_group_variant(kMultiR);
-    uint64_t blocks = uint64_t(n_cus) * uint64_t(v.blocks_per_cu);
-    if (blocks > a.n_tiles) blocks = a.n_tiles;
+    const uint64_t blocks = grid_of(a, n_cus, v.blocks_per_cu, a.n_tiles);
     hipLaunchKernelGGL((rs_apply_multi<4, true>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s, a.in_ptrs,
                        a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off, a.n_tiles, a.tiles);
     return hipGetLastError();
@@ -511,8 +519,7 @@ hipError_t launch_multi(const RsArgs& a, int n_cus, hipStream_t s) {
 template <int R>
 hipError_t launch_grouped(const RsArgs& a, int n_cus, hipStream_t s) {
     const RsVariant v = rs_group_variant(uint32_t(R));
-    uint64_t blocks = uint64_t(n_cus) * uint64_t(v.blocks_per_cu);
-    if (blocks > a.n_tiles) blocks = a.n_tiles;
+    const uint64_t blocks = grid_of(a, n_cus, v.blocks_per_cu, a.n_tiles);
     if constexpr (R <= 4) {
         if (v.vecs == 4) return launch_fast<R, 4, true, true>(a, 0, a.n_tiles, blocks, s);
     }
@@ -525,31 +532,38 @@ hipError_t launch_r(const RsArgs& a, int n_cus, hipStream_t s, const RsVariant& 
     if (a.aligned) {  // cut tiles run inside the fast kernel; no edge list
         const uint32_t tiles_per_obj = uint32_t((a.shard_size + tile - 1) / tile);
         const uint64_t n_tiles = uint64_t(tiles_per_obj) * a.n_obj;
-        uint64_t blocks = uint64_t(n_cus) * uint64_t(var.blocks_per_cu);
-        if (blocks > n_tiles) blocks = n_tiles;
+        const uint64_t blocks = grid_of(a, n_cus, var.blocks_per_cu, n_tiles);
         hipError_t e = hipErrorInvalidValue;
+        if (var.nt && var.load_nt && var.store_nt && var.group == 4 && var.min_waves == 0) {
+            // The shipping geometries (rs_default_variant): V = 4 while the
+            // accumulators fit (R <= 4), V = 2 beyond.
+            if constexpr (R <= 4) {
+                if (var.vecs == 4) return launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s);
+            }
+            if (var.vecs == 2) return launch_fast<R, 2, true>(a, tiles_per_obj, n_tiles, blocks, s);
+        }
+#ifdef MXEC_LAB
+        // Lab geometries (tools/kernel_lab, the MXEC_RS_* lab knobs).
         if (var.vecs == 1) e = var.nt ? launch_fast<R, 1, true>(a, tiles_per_obj, n_tiles, blocks, s)
                                       : launch_fast<R, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
-        else if (R >= 3 && R <= 4 && var.vecs == 2 && var.nt && var.group == 8)  // lab: 8-input steps
+        else if (R >= 3 && R <= 4 && var.vecs == 2 && var.nt && var.group == 8)  // 8-input steps
             e = launch_fast<R, 2, true, false, 1, true, 8>(a, tiles_per_obj, n_tiles, blocks, s);
-        else if (var.vecs == 2) e = var.nt ? launch_fast<R, 2, true>(a, tiles_per_obj, n_tiles, blocks, s)
-                                           : launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (var.vecs == 2 && !var.nt) e = launch_fast<R, 2, false>(a, tiles_per_obj, n_tiles, blocks, s);
         else if (R == 4 && var.vecs == 4 && var.nt && var.min_waves == 3)
             e = launch_fast<R, 4, true, false, R == 4 ? 3 : 1>(a, tiles_per_obj, n_tiles, blocks, s);
-        else if (R <= 4 && var.vecs == 4 && var.nt && !var.load_nt)  // lab: plain loads, nontemporal stores
+        else if (R <= 4 && var.vecs == 4 && var.nt && !var.load_nt)  // plain loads, nontemporal stores
             e = launch_fast<R, 4, true, false, 1, false>(a, tiles_per_obj, n_tiles, blocks, s);
-        else if (R <= 4 && var.vecs == 4 && var.nt && !var.store_nt)  // lab: nontemporal loads, plain stores
+        else if (R <= 4 && var.vecs == 4 && var.nt && !var.store_nt)  // nontemporal loads, plain stores
             e = launch_fast<R, 4, false, false, 1, true>(a, tiles_per_obj, n_tiles, blocks, s);
-        else if (var.vecs == 4) e = var.nt ? launch_fast<R, 4, true>(a, tiles_per_obj, n_tiles, blocks, s)
-                                           : launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
+        else if (R <= 4 && var.vecs == 4 && !var.nt) e = launch_fast<R, 4, false>(a, tiles_per_obj, n_tiles, blocks, s);
+#endif
         return e;
     }
     if (a.n_edge && a.edge_tile_bytes != tile) return hipErrorInvalidValue;  // list built for another tile
     if (a.n_edge) {
         const uint32_t steps = uint32_t(tile / kEdgeTile);
         const uint64_t n_steps = a.n_edge * steps;
-        uint64_t blocks = uint64_t(n_cus) * 8;
-        if (blocks > n_steps) blocks = n_steps;
+        const uint64_t blocks = grid_of(a, n_cus, 8, n_steps);
         hipLaunchKernelGGL((rs_apply_edge<R>), dim3(uint32_t(blocks)), dim3(kThreads), 0, s,
                            a.in_ptrs, a.out_ptrs, a.in_len, a.out_len, a.coef, a.coef_off,
                            a.shard_size, a.k, a.r_total, a.row0, a.edge_list, steps, tile, a.aligned,
@@ -583,27 +597,27 @@ RsVariant rs_default_variant(uint32_t r_total) {
     RsVariant v;
     v.vecs = r_total <= 4 ? 4 : 2;
     v.nt = true;
-    // MXEC_RS_LOAD_NT=0 (lab, read per launch): plain loads with the
-    // nontemporal stores, R <= 4.
+    // R <= 2 (config 2, two-erasure decodes) gained another 0-2 % at 1024 in
+    // every layout swept; R = 4 went either way (profiles/r2_lab_rs_grid_*).
+    v.blocks_per_cu = r_total <= 2 ? 1024 : 512;
+#ifdef MXEC_LAB
+    // Lab knobs (read per launch; `make lab` builds only):
+    // MXEC_RS_LOAD_NT=0 plain loads with the nontemporal stores (R <= 4);
+    // MXEC_RS_STORE_NT=0 plain stores with the nontemporal loads (R <= 4);
+    // MXEC_RS_G8=1 r = 3, 4 with V = 2 and eight inputs' loads per step;
+    // MXEC_RS_BPC workgroups per CU of uniform launches.
     if (const char* e = getenv("MXEC_RS_LOAD_NT")) v.load_nt = std::strcmp(e, "0") != 0;
-    // MXEC_RS_G8=1 (lab, read per launch): r = 3, 4 with V = 2 and eight
-    // inputs' loads in flight per step.
     if (const char* e = getenv("MXEC_RS_G8"))
         if (!std::strcmp(e, "1") && r_total >= 3 && r_total <= 4) {
             v.vecs = 2;
             v.group = 8;
         }
-    // MXEC_RS_STORE_NT=0 (lab, read per launch): plain stores with the
-    // nontemporal loads, R <= 4.
     if (const char* e = getenv("MXEC_RS_STORE_NT")) v.store_nt = std::strcmp(e, "0") != 0;
-    // R <= 2 (config 2, two-erasure decodes) gained another 0-2 % at 1024 in
-    // every layout swept; R = 4 went either way (profiles/r2_lab_rs_grid_*).
-    v.blocks_per_cu = r_total <= 2 ? 1024 : 512;
-    // MXEC_RS_BPC (lab, read per launch): workgroups per CU of uniform launches.
     if (const char* e = getenv("MXEC_RS_BPC")) {
         const int b = atoi(e);
         if (b > 0 && b <= 4096) v.blocks_per_cu = b;
     }
+#endif
     return v;
 }
 
@@ -611,8 +625,11 @@ RsVariant rs_default_variant(uint32_t r_total) {
 // default geometry: config 5 measured 32 / 48 / 64 / 128 / 256 / 2048 /
 // one tile per workgroup within ~1 %, V = 2 3-4 % slower
 // (profiles/r2_rs_group_geometry.txt, r2_rs_grid_bench_ab.txt).
-// MXEC_RS_GROUP_VECS (2 | 4) and MXEC_RS_GROUP_BPC override it for labs.
+// MXEC_RS_GROUP_VECS (2 | 4) and MXEC_RS_GROUP_BPC override it in lab builds.
 RsVariant rs_group_variant(uint32_t r) {
+    RsVariant v = rs_default_variant(r);
+    v.blocks_per_cu = 512;
+#ifdef MXEC_LAB
     static const int env_v = [] {
         const char* e = getenv("MXEC_RS_GROUP_VECS");
         return e ? atoi(e) : 0;
@@ -621,10 +638,9 @@ RsVariant rs_group_variant(uint32_t r) {
         const char* e = getenv("MXEC_RS_GROUP_BPC");
         return e ? atoi(e) : 0;
     }();
-    RsVariant v = rs_default_variant(r);
-    v.blocks_per_cu = 512;
     if (r <= 4 && (env_v == 2 || env_v == 4)) v.vecs = env_v;
     if (env_b > 0 && env_b <= 4096) v.blocks_per_cu = env_b;
+#endif
     return v;
 }
 

@@ -58,11 +58,7 @@ int PinnedBuf::ensure(size_t n) {
 }
 
 int slot_wait(Slot& slot, hipStream_t s) {
-    static const bool spin = [] {
-        const char* e = getenv("MXEC_SPIN_WAIT");
-        return e && *e && *e != '0';
-    }();
-    if (spin) {
+    if (slot.owner && slot.owner->kn && slot.owner->kn->spin_wait) {
         MXEC_HIP(hipStreamSynchronize(s));
         if (slot.borrowed == s) slot.borrowed = nullptr;
         return MXEC_OK;
@@ -275,14 +271,12 @@ size_t DescWriter::add(size_t bytes) {
 int DescWriter::commit(hipStream_t stream, char** dev_base) {
     if (slot_.owner) MXEC_TRY(affinity_check(*slot_.owner, &slot_, stream, "descriptor upload", arena_));
     if (arena_) {
-        const size_t n = (tmp_.size() + 255) & ~size_t(255);
-        if (arena_->used + n > arena_->host.cap || arena_->used + n > arena_->dev.cap)
-            return set_error(MXEC_E_OOM, "descriptor arena exhausted");
-        char* h = static_cast<char*>(arena_->host.p) + arena_->used;
-        char* d = static_cast<char*>(arena_->dev.p) + arena_->used;
+        const size_t n = std::max<size_t>((tmp_.size() + 255) & ~size_t(255), 256);
+        char* h = nullptr;
+        char* d = nullptr;
+        MXEC_TRY(arena_->take(n, &h, &d));
         std::memcpy(h, tmp_.data(), tmp_.size());
-        if (n) MXEC_HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream));
-        arena_->used += n;
+        MXEC_HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream));
         *dev_base = d;
         return MXEC_OK;
     }
@@ -300,10 +294,7 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
     // Large tables (a mixed batch's: MiBs) go on the side stream; small ones
     // stay in the launch stream, where the extra cross-stream wait measured
     // no better (config 3c's per-call decodes, profiles/r2_desc_upload_ab.txt).
-    static const int mode = [] {
-        const char* e = getenv("MXEC_DESC_UPLOAD");
-        return e && !strcmp(e, "inline") ? 0 : e && !strcmp(e, "stream") ? 2 : 1;
-    }();
+    const int mode = slot_.owner && slot_.owner->kn ? slot_.owner->kn->desc_upload : 1;
     if (mode == 0 || (mode == 1 && n < (size_t(256) << 10))) {
         MXEC_HIP(hipMemcpyAsync(buf_->dev.p, buf_->host.p, n, hipMemcpyHostToDevice, stream));
     } else {
@@ -337,38 +328,122 @@ int DescWriter::finish(hipStream_t stream) {
     return MXEC_OK;
 }
 
+namespace {
+thread_local CoefUse* t_coef_use = nullptr;
+
+// Drop fences whose launches finished (keeps the lists short).
+void coef_prune(Device& dev, int h) {
+    auto& v = dev.coef_fences[h];
+    size_t w = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+        if (hipEventQuery(v[i]) == hipSuccess) dev.coef_free.push_back(v[i]);
+        else v[w++] = v[i];
+    }
+    (void)hipGetLastError();  // hipErrorNotReady from the queries
+    v.resize(w);
+}
+}  // namespace
+
+void coef_note_use(uint64_t gen) {
+    if (!t_coef_use) return;
+    t_coef_use->lo = std::min(t_coef_use->lo, gen);
+    t_coef_use->hi = std::max(t_coef_use->hi, gen);
+}
+
+CoefUse* coef_use_swap(CoefUse* u) {
+    CoefUse* p = t_coef_use;
+    t_coef_use = u;
+    return p;
+}
+
 int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<uint32_t>& table,
                 uint32_t* off) {
     std::lock_guard<std::mutex> g(dev.coef_mu);
     auto it = dev.coef_index.find(key);
     if (it != dev.coef_index.end()) {
-        *off = it->second;
+        *off = it->second.first;
+        coef_note_use(it->second.second);
         return MXEC_OK;
     }
-    constexpr size_t kArenaDwords = size_t(16) << 20;  // 64 MiB of tables
     if (!dev.coef.p) {
-        MXEC_TRY(dev.coef.ensure(kArenaDwords * 4));
+        const uint64_t test = dev.kn ? dev.kn->test_coef_arena : 0;
+        dev.coef_half = test ? size_t(test / 4) : kCoefArenaDwords;
+        MXEC_TRY(dev.coef.ensure(dev.coef_half * 2 * 4));
         dev.coef_used = 0;
     }
-    if (table.size() > kArenaDwords)
+    if (table.size() > dev.coef_half)
         return set_error(MXEC_E_INVALID_ARG, "coefficient table larger than the arena");
-    if (dev.coef_used + table.size() > kArenaDwords) {
-        // Arena full: every launch that could read it must have finished.
-        MXEC_HIP(hipDeviceSynchronize());
-        dev.coef_index.clear();
-        dev.patterns.clear();
+    if (dev.coef_used + table.size() > dev.coef_half) {
+        // This half is full: the next generation takes the other half, whose
+        // tables (two generations old) may still be read by fenced launches.
+        const uint64_t next = dev.coef_gen + 1;
+        const int h = int(next & 1);
+        for (hipEvent_t e : dev.coef_fences[h]) {
+            if (hipEventQuery(e) != hipSuccess) {
+                ++dev.coef_fence_waits;
+                MXEC_HIP(hipEventSynchronize(e));
+            }
+            dev.coef_free.push_back(e);
+        }
+        (void)hipGetLastError();
+        dev.coef_fences[h].clear();
+        for (auto i = dev.coef_index.begin(); i != dev.coef_index.end();)
+            i = i->second.second + 1 < next ? dev.coef_index.erase(i) : std::next(i);
+        for (auto i = dev.patterns.begin(); i != dev.patterns.end();)
+            i = i->second.gen + 1 < next ? dev.patterns.erase(i) : std::next(i);
+        dev.coef_gen = next;
         dev.coef_used = 0;
-        ++dev.coef_epoch;
+        ++dev.coef_recycles;
     }
-    const uint32_t o = uint32_t(dev.coef_used);
+    const uint32_t o = uint32_t(size_t(dev.coef_gen & 1) * dev.coef_half + dev.coef_used);
     // Synchronous copy: the table is on the device before any stream can see
     // the key in the index.
     MXEC_HIP(hipMemcpy(static_cast<uint32_t*>(dev.coef.p) + o, table.data(), table.size() * 4,
                        hipMemcpyHostToDevice));
     dev.coef_used += (table.size() + 3) & ~size_t(3);
-    dev.coef_index.emplace(key, o);
+    dev.coef_index.emplace(key, std::make_pair(o, dev.coef_gen));
+    coef_note_use(dev.coef_gen);
     *off = o;
     return MXEC_OK;
+}
+
+int coef_fence(Device& dev, const CoefUse& use, hipStream_t s, bool* live) {
+    *live = true;
+    if (!use.any()) return MXEC_OK;
+    std::lock_guard<std::mutex> g(dev.coef_mu);
+    // Generation lo's half is reused by generation lo + 2.
+    if (dev.coef_gen > use.lo + 1) {
+        *live = false;
+        ++dev.coef_relaunches;
+        return MXEC_OK;
+    }
+    for (uint64_t gen = use.lo; gen <= use.hi; ++gen) {
+        const int h = int(gen & 1);
+        if (dev.coef_fences[h].size() >= 64) coef_prune(dev, h);
+        hipEvent_t e = nullptr;
+        if (!dev.coef_free.empty()) {
+            e = dev.coef_free.back();
+            dev.coef_free.pop_back();
+        } else {
+            MXEC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        if (hipEventRecord(e, s) != hipSuccess) {
+            dev.coef_free.push_back(e);
+            return set_error(MXEC_E_DEVICE, "coefficient fence: hipEventRecord failed");
+        }
+        dev.coef_fences[h].push_back(e);
+    }
+    return MXEC_OK;
+}
+
+void coef_release(Device& dev) {
+    std::lock_guard<std::mutex> g(dev.coef_mu);
+    for (auto& v : dev.coef_fences) {
+        for (hipEvent_t e : v) (void)hipEventDestroy(e);
+        v.clear();
+    }
+    for (hipEvent_t e : dev.coef_free) (void)hipEventDestroy(e);
+    dev.coef_free.clear();
 }
 
 namespace {
@@ -380,13 +455,10 @@ std::unordered_map<hipStream_t, const Device*>& aff_streams() {
 }
 }  // namespace
 
-bool affinity_on() {
-    const char* e = getenv("MXEC_DEBUG_AFFINITY");
-    return e && *e && std::strcmp(e, "0") != 0;
-}
+bool affinity_on(const Device& d) { return d.kn && d.kn->debug_affinity; }
 
 void affinity_tag(hipStream_t s, const Device* d) {
-    if (!s || !affinity_on()) return;
+    if (!s || !d || !affinity_on(*d)) return;
     std::lock_guard<std::mutex> g(g_aff_mu);
     aff_streams()[s] = d;
 }
@@ -401,7 +473,7 @@ void affinity_untag(hipStream_t s) {
 
 int affinity_check(const Device& d, const Slot* slot, hipStream_t s, const char* where, const DescArena* arena,
                    const void* const* ptrs, size_t n_ptrs) {
-    if (!affinity_on()) return MXEC_OK;
+    if (!affinity_on(d)) return MXEC_OK;
     g_aff_checks.fetch_add(1);
     std::string bad;
     int cur = -1;
@@ -434,7 +506,6 @@ int affinity_check(const Device& d, const Slot* slot, hipStream_t s, const char*
 }
 
 void affinity_report() {
-    if (!affinity_on()) return;
     fprintf(stderr, "maxio_ec affinity: %llu checks, %llu violations\n",
             static_cast<unsigned long long>(g_aff_checks.load()), static_cast<unsigned long long>(g_aff_bad.load()));
 }

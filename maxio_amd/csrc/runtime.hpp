@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/maxio_ec.h"
+#include "knobs.hpp"
 
 namespace mxec {
 
@@ -181,23 +182,37 @@ struct GridTuner {
 struct Device {
     int id = 0;
     int n_cus = 256;
+    const Knobs* kn = nullptr;  // the context's settings (read at mxec_open)
     GridTuner tuner;
     std::vector<std::unique_ptr<Slot>> slots;
     std::atomic<unsigned> next_slot{0};
     // Coefficient tables (gf256.hpp coef_tables) for every matrix in use,
-    // keyed by matrix identity; uploaded once, read by every launch.
+    // keyed by matrix identity; uploaded once, read by every launch.  The
+    // arena is two halves (kCoefArenaDwords each, or MXEC_TEST_COEF_ARENA_KB):
+    // generation g fills half g & 1; when it is full, generation g + 1 takes
+    // the other half, after waiting for the events that fence the launches
+    // which read that half's tables (generation g - 1) -- no device-wide
+    // wait, other streams keep running.  A launch whose tables came from a
+    // generation recycled before its fence was registered is queued again
+    // (with_stable_coef, ops.hpp).
     std::mutex coef_mu;
     DevBuf coef;
+    size_t coef_half = 0;     // dwords per half (set on first use)
+    size_t coef_used = 0;     // dwords used in the current half
+    uint64_t coef_gen = 0;    // current generation
+    // key -> (dword offset, generation)
+    std::map<std::vector<uint8_t>, std::pair<uint32_t, uint64_t>> coef_index;
+    std::vector<hipEvent_t> coef_fences[2];  // after launches that read half h
+    std::vector<hipEvent_t> coef_free;       // spare fence events
+    uint64_t coef_recycles = 0, coef_relaunches = 0, coef_fence_waits = 0;
     // CRC32 / CRC32C constant tables (sums.cpp), uploaded on first use.
     std::mutex sums_mu;
     DevBuf crc_tables;
     DevBuf aes_te;  // AES T-tables (gcm.cpp)
-    size_t coef_used = 0;  // dwords
-    uint64_t coef_epoch = 0;  // bumped whenever the arena is recycled
-    std::map<std::vector<uint8_t>, uint32_t> coef_index;
-    // Erasure pattern -> (decode plan, table offset), resolved once per device
-    // and dropped with the arena (ops.cpp decode_plan).  Key: presence bitmask
-    // over k+m <= 256 shards, plus (k, m, data_only).
+    // Erasure pattern -> (decode plan, table offset, generation), resolved
+    // once per device and dropped with its generation's half (ops.cpp
+    // decode_plan).  Key: presence bitmask over k+m <= 256 shards, plus
+    // (k, m, data_only).
     struct PatternKey {
         std::array<uint64_t, 4> mask{};
         uint32_t kmf = 0;
@@ -209,7 +224,12 @@ struct Device {
                           a.mask[2] * 0x165667B19E3779F9ull ^ a.mask[3] ^ uint64_t(a.kmf) << 40);
         }
     };
-    std::unordered_map<PatternKey, std::pair<std::shared_ptr<const void>, uint32_t>, PatternHash> patterns;
+    struct PatternVal {
+        std::shared_ptr<const void> plan;
+        uint32_t off;
+        uint64_t gen;
+    };
+    std::unordered_map<PatternKey, PatternVal, PatternHash> patterns;
     // Host-batch pipeline state (pipeline.cpp): streams, pinned rings, pools;
     // created on first use and kept, one batch at a time per device.
     std::mutex pipe_mu;
@@ -221,6 +241,7 @@ struct Device {
 };
 
 struct Ctx {
+    Knobs knobs;  // read once by mxec_open; every device points at it
     std::vector<std::unique_ptr<Device>> devs;
     std::atomic<unsigned> rr{0};
     // Worker threads of the *_async entry points (async.cpp), created on
@@ -230,17 +251,50 @@ struct Ctx {
 };
 void async_shutdown(Ctx& c);
 
-// Descriptor tables of many launches in flight at once (host pipeline): one
-// pinned + device region, bump-allocated, never reused until reset().
+// Descriptor tables of many launches in flight at once (host pipeline):
+// pinned + device blocks, bump-allocated, never reused until reserve().  The
+// first block is sized by the caller's estimate; a wave that needs more (a
+// piece-major wave's tables grow with pieces x classes) chains further
+// blocks instead of failing, and keeps them for later waves.  Growing costs
+// a hipMalloc / hipHostMalloc (no device-wide wait); only re-sizing the
+// first block frees memory.
 struct DescArena {
     const Device* owner = nullptr;
-    PinnedBuf host;
-    DevBuf dev;
-    size_t used = 0;
+    struct Block {
+        PinnedBuf host;
+        DevBuf dev;
+    };
+    std::vector<std::unique_ptr<Block>> blocks;
+    size_t cur = 0;   // block being filled
+    size_t used = 0;  // bytes used in it
+    uint64_t grown = 0;  // blocks chained beyond the first, over the arena's life (stats)
+    // Start a wave: the first block holds at least `bytes`; everything is free.
     int reserve(size_t bytes) {
-        MXEC_TRY(host.ensure(bytes));
-        MXEC_TRY(dev.ensure(bytes));
+        if (blocks.empty()) blocks.emplace_back(new Block());
+        Block& b = *blocks[0];
+        MXEC_TRY(b.host.ensure(bytes));
+        MXEC_TRY(b.dev.ensure(bytes));
+        cur = 0;
         used = 0;
+        return 0;
+    }
+    // n bytes (a multiple of 256) of host staging and their device twin.
+    int take(size_t n, char** h, char** d) {
+        if (blocks.empty()) MXEC_TRY(reserve(size_t(1) << 20));
+        while (used + n > blocks[cur]->host.cap || used + n > blocks[cur]->dev.cap) {
+            ++cur;
+            used = 0;
+            if (cur == blocks.size()) {
+                const size_t cap = std::max(n, blocks[0]->host.cap);
+                blocks.emplace_back(new Block());
+                MXEC_TRY(blocks[cur]->host.ensure(cap));
+                MXEC_TRY(blocks[cur]->dev.ensure(cap));
+                ++grown;
+            }
+        }
+        *h = static_cast<char*>(blocks[cur]->host.p) + used;
+        *d = static_cast<char*>(blocks[cur]->dev.p) + used;
+        used += n;
         return 0;
     }
 };
@@ -270,13 +324,34 @@ private:
     std::vector<char> tmp_;
 };
 
-// Device offset (in dwords) of a coefficient table, uploading it on first use.
+// Dwords per half of the coefficient arena (64 MiB of tables).
+constexpr size_t kCoefArenaDwords = size_t(16) << 20;
+
+// Device offset (in dwords) of a coefficient table, uploading it on first
+// use; records the table's generation with coef_note_use.
 int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<uint32_t>& table,
                 uint32_t* off);
 
+// The generations of the tables one batch collected (with_stable_coef):
+// coef_offset and the memoised lookups note every table's generation in the
+// calling thread's current CoefUse, if one is set.
+struct CoefUse {
+    uint64_t lo = UINT64_MAX, hi = 0;
+    bool any() const { return lo != UINT64_MAX; }
+};
+void coef_note_use(uint64_t gen);
+CoefUse* coef_use_swap(CoefUse* u);  // sets the thread's current CoefUse, returns the previous
+// After a batch's launches are queued on `s`: if every table it used is
+// still live, fence them with an event on `s` (a later recycle of their half
+// waits for it) and return true; false if one of their halves was recycled
+// in the meantime (the batch must be queued again).
+int coef_fence(Device& dev, const CoefUse& use, hipStream_t s, bool* live);
+// Release the arena's events (context close).
+void coef_release(Device& dev);
+
 Device* pick_device(Ctx* ctx, int dev_index);
 
-// MXEC_DEBUG_AFFINITY=1 (tests; read per call): every launch and copy checks
+// MXEC_DEBUG_AFFINITY=1 (tests; read at mxec_open, per context): every launch and copy checks
 // that the HIP current device, the stream, the slot, the descriptor arena and
 // the data pointers all belong to the device doing the work.  Internal
 // streams are tagged with their (logical) device when created, so on
@@ -284,12 +359,12 @@ Device* pick_device(Ctx* ctx, int dev_index);
 // where physical ids cannot tell them apart -- a stream, slot or arena of
 // another logical device is still caught.  A violation fails the call with
 // MXEC_E_DEVICE; mxec_close prints the running totals to stderr.
-bool affinity_on();
+bool affinity_on(const Device& d);
 void affinity_tag(hipStream_t s, const Device* d);
 void affinity_untag(hipStream_t s);  // before the stream is destroyed
 int affinity_check(const Device& d, const Slot* slot, hipStream_t s, const char* where,
                    const DescArena* arena = nullptr, const void* const* ptrs = nullptr, size_t n_ptrs = 0);
-void affinity_report();
+void affinity_report();  // the process's totals (mxec_close of a context with the checks on)
 
 }  // namespace mxec
 

@@ -149,13 +149,15 @@ __device__ __forceinline__ void load_kw(const u32x4* kwl, u32x4 (&v)[16]) {
     for (int q = 0; q < 16; ++q) v[q] = kwl[q * ROW];
 }
 
+#ifdef MXEC_LAB
 // 64 rounds reading K + W from LDS: all 16 reads issued up front so their
-// latency overlaps the first rounds.
+// latency overlaps the first rounds (the split form's two-buffer ring, lab).
 __device__ __forceinline__ void compress_kw(uint32_t (&st)[8], const u32x4* kwl) {
     u32x4 v[16];
     load_kw(kwl, v);
     compress_regs(st, v);
 }
+#endif
 
 __constant__ uint32_t kK256[64] = {
     0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
@@ -342,10 +344,12 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
     if (wave == 0) {
         __syncthreads();
         if constexpr (NB == 2) {
+#ifdef MXEC_LAB
             for (uint64_t b = 0; b < nmax; ++b) {
                 if (b < nfull) compress_kw(st, &kw[b & 1][0][lane]);
                 __syncthreads();
             }
+#endif
         } else {
             // Blocks 0 and 1 were written before the first barrier; block
             // b+1 before the barrier that opens block b.  Two register sets
@@ -430,8 +434,10 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
 constexpr int kQuadRow = 66;  // u32x4 per K + W row: 64 producer lanes, zeros, ones
 
 #define QDPP(x, ctrl) uint32_t(__builtin_amdgcn_update_dpp(0, int(x), (ctrl), 0xF, 0xF, true))
+#ifdef MXEC_LAB
 constexpr int kQuadFromE = 0xA2;   // quad_perm [2, 0, 2, 2]: lane A reads lane E, the rest a zero lane
 constexpr int kQuadFromA = 0xA9;   // quad_perm [1, 2, 2, 2]: lane E reads lane A, the rest a zero lane
+#endif
 constexpr int kQuadBcastA = 0x55;  // quad_perm [1, 1, 1, 1]
 constexpr int kPairBcastA = 0xF5;  // quad_perm [1, 1, 3, 3]: each message's lane A to its lane E
 
@@ -440,6 +446,7 @@ struct QuadLane {
     uint32_t ma;             // all ones in lane A (selector ~(a ^ b); negated d), else 0
 };
 
+#ifdef MXEC_LAB
 // One block.  s[0..3] = (e, f, g, h) in lane E, (a, b, c, d) in lane A, zero
 // in the zero lanes; v = the block's K + W rows as this lane reads them.
 __device__ __forceinline__ void compress_quad(uint32_t (&s)[4], const u32x4 (&v)[16], const QuadLane& q) {
@@ -463,6 +470,7 @@ __device__ __forceinline__ void compress_quad(uint32_t (&s)[4], const u32x4 (&v)
     s[2] += x[2];
     s[3] += x[1];
 }
+#endif
 
 // Lag variant (the auto quad form; MXEC_SHA_FORM=lag pins it).  Above, lane A's
 // a' = T1 + T2 needs lane E's T1 of the same round, so a DPP add sits on
@@ -623,16 +631,22 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     for (uint64_t b = 0; b < nmax; b += 2) {
         load_kw<kQuadRow>(kcol + rb * BUF, nxt);
         if (b < nfull) {
-            if constexpr (LAG) compress_lag(s, cur, q);
-            else compress_quad(s, cur, q);
+#ifdef MXEC_LAB
+            if constexpr (!LAG) compress_quad(s, cur, q);
+            else
+#endif
+            compress_lag(s, cur, q);
         }
         __syncthreads();
         rb = rb == 2 ? 0 : rb + 1;
         if (b + 1 >= nmax) break;
         load_kw<kQuadRow>(kcol + rb * BUF, cur);
         if (b + 1 < nfull) {
-            if constexpr (LAG) compress_lag(s, nxt, q);
-            else compress_quad(s, nxt, q);
+#ifdef MXEC_LAB
+            if constexpr (!LAG) compress_quad(s, nxt, q);
+            else
+#endif
+            compress_lag(s, nxt, q);
         }
         __syncthreads();
         rb = rb == 2 ? 0 : rb + 1;
@@ -882,14 +896,17 @@ __global__ __launch_bounds__(256) void sha256_stream_kernel(const uint8_t* const
 // profiles/r2_sha_stream_lab_sizes.jsonl).
 constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 
-// MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read
-// per launch), default 3.
 // The quad form the auto choice takes (up to kShaLagMsgs per CU): 4 =
 // same-round, 5 = lag, 6 = lag with two messages per quad.  6 against 5 on
 // config 3's 10 240 x 1 MiB: 20.72 vs 20.89 ms; at 16 000 messages (past 5's
 // 48 per CU) 20.93 ms against the split form's 27.5 (profiles/r3/sha_lag/).
+// Forms 4 and 5 and the split form's two-buffer ring exist in lab builds
+// only (`make lab`, -DMXEC_LAB).
 constexpr int kShaQuadAuto = 6;
 
+#ifdef MXEC_LAB
+// MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read
+// per launch), default 3.
 int split_bufs() {
     const char* e = getenv("MXEC_SHA_SPLIT_BUFS");
     return e && atoi(e) == 2 ? 2 : 3;
@@ -900,32 +917,41 @@ uint32_t sha_prio() {
     const char* e = getenv("MXEC_SHA_PRIO");
     return e ? uint32_t(atoi(e)) : 3u;
 }
+#else
+constexpr int split_bufs() { return 3; }
+constexpr uint32_t sha_prio() { return 3u; }
+#endif
 
 hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const uint32_t blocks = (a.n + 63) / 64;
     int form = a.force;
     if (form == 0) {
-        // MXEC_SHA_FORM=one|split|quad|lag|lagpair pins the form (tests, lab).
         // Auto: the lag pair form while its workgroups fit one per CU, then
-        // split, then one wave per 64 messages.
+        // split, then one wave per 64 messages.  (The host pins a form
+        // through a.force: MXEC_SHA_FORM, read into the context's knobs.)
         const uint64_t n_cus = a.n_cus ? a.n_cus : 256;
+#ifdef MXEC_LAB
+        // Lab builds: MXEC_SHA_FORM=quad|lag selects the lab quad forms.
         const char* env = getenv("MXEC_SHA_FORM");
-        if (env && !strcmp(env, "one")) form = 1;
-        else if (env && !strcmp(env, "split")) form = 2;
-        else if (env && !strcmp(env, "quad")) form = 4;
+        if (env && !strcmp(env, "quad")) form = 4;
         else if (env && !strcmp(env, "lag")) form = 5;
-        else if (env && !strcmp(env, "lagpair")) form = 6;
-        else form = a.n <= kShaLagMsgs * n_cus ? kShaQuadAuto : a.n <= kSplitMaxMessages ? 2 : 1;
+        else
+#endif
+        form = a.n <= kShaLagMsgs * n_cus ? kShaQuadAuto : a.n <= kSplitMaxMessages ? 2 : 1;
     }
     if (a.piece.state && form != 4 && form != 5 && form != 6) return hipErrorInvalidValue;  // piece mode: quad forms
-    if (form == 4 || form == 5) {  // 4: the same-round quad (lab A/B), 5: the lag quad
+#ifdef MXEC_LAB
+    if (form == 4 || form == 5) {  // 4: the same-round quad, 5: the lag quad (lab A/B)
         const dim3 grid((a.n + kShaQuadMsgs - 1) / kShaQuadMsgs);
         hipLaunchKernelGGL(form == 5 ? sha256_quad_kernel<true> : sha256_quad_kernel<false>, grid, dim3(256), 0, s,
                            a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
         return hipGetLastError();
     }
-    if (form == 6) {  // the lag quad, two messages per quad (lab)
+#else
+    if (form == 4 || form == 5) return hipErrorInvalidValue;
+#endif
+    if (form == 6) {  // the lag quad, two messages per quad (the auto form)
         hipLaunchKernelGGL((sha256_quad_kernel<true, true>), dim3((a.n + 63) / 64), dim3(192), 0, s, a.ptrs, a.lens,
                            a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
         return hipGetLastError();
@@ -938,10 +964,13 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const bool split = form == 2;
+#ifdef MXEC_LAB
     if (split && split_bufs() == 2)
         hipLaunchKernelGGL(sha256_split_kernel<2>, dim3(blocks), dim3(128), 0, s, a.ptrs, a.lens,
                            a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
-    else if (split)
+    else
+#endif
+    if (split)
         hipLaunchKernelGGL(sha256_split_kernel<3>, dim3(blocks), dim3(128), 0, s, a.ptrs, a.lens,
                            a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio());
     else

@@ -966,9 +966,8 @@ int mxec_get_object_chunked(mxec_ctx* ctx, const char* ec_dir, uint64_t offset, 
         // Windows of at most kGetWindow bytes of chunks (at least one chunk): one
         // hash round trip per window, and a slot's device staging stays bounded
         // however large the object.
-        // MXEC_GET_WINDOW (bytes) overrides the window (tests).
-        const char* we = getenv("MXEC_GET_WINDOW");
-        const uint64_t kGetWindow = we && *we ? std::max<uint64_t>(1, strtoull(we, nullptr, 10)) : uint64_t(1) << 30;
+        // MXEC_GET_WINDOW (bytes, read at mxec_open) overrides the window (tests).
+        const uint64_t kGetWindow = ctx->c.knobs.get_window;
         std::vector<LoadedChunk> batch;
         pos = 0;
         left = r->remaining;

@@ -136,6 +136,11 @@ def device_count() -> int:
     return int(N.lib().mxec_device_count())
 
 
+def version() -> str:
+    """mxec_version(): '... (gfx950)', or '... (gfx950, lab build)' for `make lab`."""
+    return N.lib().mxec_version().decode()
+
+
 class Context:
     """An ``mxec_ctx``: every visible MI355X (or the ones in device_mask)."""
 
@@ -171,6 +176,14 @@ class Context:
         b, m = ctypes.c_uint64(0), ctypes.c_uint64(0)
         _check(self._lib.mxec_ctx_combiner_stats(self._h, dev, ctypes.byref(b), ctypes.byref(m)))
         return {"batches": b.value, "messages": m.value}
+
+    def coef_stats(self, dev: int = 0) -> dict:
+        """Coefficient-table arena of device `dev`: recycles of its halves,
+        batches queued again after a recycle, recycles that waited for a
+        fenced launch (mxec_ctx_coef_stats)."""
+        r, q, w = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(self._lib.mxec_ctx_coef_stats(self._h, dev, ctypes.byref(r), ctypes.byref(q), ctypes.byref(w)))
+        return {"recycles": r.value, "relaunches": q.value, "fence_waits": w.value}
 
     def rs_grid(self, k: int, m: int, shard_size: int, dev: int = 0) -> int:
         """Workgroups per CU large uniform RS launches of this shape run at on

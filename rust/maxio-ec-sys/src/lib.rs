@@ -136,6 +136,8 @@ extern "C" {
     pub fn mxec_ctx_device_id(ctx: *const MxecCtx, i: c_int) -> c_int;
     pub fn mxec_ctx_combiner_stats(ctx: *mut MxecCtx, i: c_int, launches: *mut u64, messages: *mut u64) -> c_int;
     pub fn mxec_ctx_rs_grid(ctx: *mut MxecCtx, dev: c_int, k: c_int, m: c_int, shard_size: u64) -> c_int;
+    pub fn mxec_ctx_coef_stats(ctx: *mut MxecCtx, dev: c_int, recycles: *mut u64, relaunches: *mut u64,
+                               fence_waits: *mut u64) -> c_int;
     pub fn mxec_host_alloc(ctx: *mut MxecCtx, bytes: usize) -> *mut c_void;
     pub fn mxec_host_free(ctx: *mut MxecCtx, p: *mut c_void);
     pub fn mxec_rs_check(k: c_int, m: c_int) -> c_int;

@@ -49,3 +49,49 @@ def ctx():
     c = maxio_amd.Context(streams_per_device=2)
     yield c
     c.close()
+
+
+def open_ctx(streams=2, device_mask=0, **env):
+    """A context opened with MXEC_* settings: the library reads its knobs
+    once, at mxec_open (maxio_amd/csrc/knobs.cpp), so a test that changes
+    one opens its own context.  Values None / "" unset the variable."""
+    import maxio_amd
+
+    saved = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            if v is None or v == "":
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+        return maxio_amd.Context(device_mask=device_mask, streams_per_device=streams)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="session")
+def ctx_with():
+    """Session cache of open_ctx contexts, one per distinct setting:
+    ctx_with(streams=2, MXEC_X="1")."""
+    cache = {}
+
+    def get(streams=2, device_mask=0, **env):
+        key = (streams, device_mask, tuple(sorted((k, str(v)) for k, v in env.items())))
+        if key not in cache:
+            cache[key] = open_ctx(streams, device_mask, **env)
+        return cache[key]
+
+    yield get
+    for c in cache.values():
+        c.close()
+
+
+def lab_build() -> bool:
+    """True when the loaded library is the lab build (make lab; MXEC_LIB)."""
+    import maxio_amd
+
+    return "lab build" in maxio_amd.version()

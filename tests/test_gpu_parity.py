@@ -374,23 +374,30 @@ def test_short_last_chunk_device_encode_and_rebuild(ctx, last):
     assert np.array_equal(got[:, 2], host[:, 2])
 
 
-# MXEC_SHA_FORM pins the SHA-256 kernel (lag: the default quad form, four
-# lanes per message behind a producer wave with the a-side two rounds behind
-# the e-side; lagpair: the lag form with two messages per quad (lab); quad:
-# the same-round quad form; split: producer/consumer waves;
-# one: one wave per 64 messages).
-SHA_FORMS = ["lag", "lagpair", "quad", "split", "one"]
+# MXEC_SHA_FORM pins the SHA-256 kernel (read at mxec_open, so each form has
+# its own context).  Shipping forms: lagpair (the auto form up to 64
+# messages per CU: the lag quad, four lanes per message behind a producer
+# wave, the a-side two rounds behind the e-side, two messages per quad),
+# split (producer/consumer waves) and one (one wave per 64 messages).  Lab
+# builds (make lab, MXEC_LIB) add lag (one message per quad) and quad (the
+# same-round quad form).
+SHA_FORMS = ["lagpair", "split", "one", "lag", "quad"]
+LAB_SHA_FORMS = {"lag", "quad"}
 
 
-def _pin_sha_form(monkeypatch, form):
-    monkeypatch.setenv("MXEC_SHA_FORM", form)
+def _form_ctx(ctx_with, form):
+    from conftest import lab_build
+
+    if form in LAB_SHA_FORMS and not lab_build():
+        pytest.skip(f"SHA form {form!r} exists in lab builds only")
+    return ctx_with(MXEC_SHA_FORM=form)
 
 
 @pytest.mark.parametrize("form", SHA_FORMS)
-def test_sha256_every_kernel_form(ctx, form, monkeypatch):
+def test_sha256_every_kernel_form(ctx_with, form):
     """Every SHA-256 kernel form on mixed lengths (multi-block, tails 0..63,
     unaligned starts)."""
-    _pin_sha_form(monkeypatch, form)
+    ctx = _form_ctx(ctx_with, form)
     rng = np.random.default_rng(13)
     lens = list(rng.integers(0, 5000, 300)) + [0, 55, 56, 64, 4096, 100_003]
     blob = rng.integers(0, 256, int(sum(lens)) + 64, dtype=np.uint8).tobytes()
@@ -405,14 +412,14 @@ def test_sha256_every_kernel_form(ctx, form, monkeypatch):
 
 @pytest.mark.parametrize("form", SHA_FORMS)
 @pytest.mark.parametrize("shift", [0, 16, 3])
-def test_sha256_device_messages_ring_edges(ctx, form, shift, monkeypatch):
+def test_sha256_device_messages_ring_edges(ctx_with, form, shift):
     """Device-resident messages straight into the kernel (no staging copy),
     16-byte aligned (shift 0/16: the split form's prefetch-ring path) or not
     (shift 3: its byte-load path): lone messages of 0..9 full blocks (every
     ring phase and tail count), a wave whose lanes end at different blocks,
     empty messages (their lanes borrow a donor lane's address) and a batch
     past one workgroup."""
-    _pin_sha_form(monkeypatch, form)
+    ctx = _form_ctx(ctx_with, form)
     torch = _torch()
     rng = np.random.default_rng(21 + shift)
     cases = [[64 * b + t] for b in range(10) for t in (0, 37)]

@@ -66,14 +66,14 @@ class Batch:
 
 
 @pytest.mark.parametrize("multi", ["1", "0"])
-def test_mixed_encode_then_reconstruct_one_call_each(ctx, multi, monkeypatch):
+def test_mixed_encode_then_reconstruct_one_call_each(ctx_with, multi):
     """Encode every class in one call (digests too), erase 1..m seeded
     shards per object (data and parity) and silently corrupt a present shard
     of every third object, then one verified reconstruct call: every object
     equals its encoded state, the corrupted shards were caught.  multi=1: the
     r = 1..4 groups of each call run as one multi-r launch (rs_apply_multi,
     the default); 0: one grouped launch per r."""
-    monkeypatch.setenv("MXEC_RS_MULTI", multi)
+    ctx = ctx_with(MXEC_RS_MULTI=multi)  # read at mxec_open
     torch = _torch()
     rng = np.random.default_rng(SEED)
     b = Batch(torch, _classes(rng) + [(4, 2, 10 << 20, 1, [10 << 20] * 3 + [777])])

@@ -67,7 +67,7 @@ def test_batch_host_pinned_buffers(ctx):
 
 
 @pytest.mark.parametrize("piece_mb", ["1", "2", "0"])
-def test_batch_host_digests_in_pieces(ctx, piece_mb, monkeypatch):
+def test_batch_host_digests_in_pieces(ctx_with, piece_mb):
     """With digests the wave runs piece-major (MXEC_PIPE_PIECE_MB, default
     1; 0 = the group form):
     every chunk is hashed piece by piece, its chain carried in a device
@@ -76,7 +76,7 @@ def test_batch_host_digests_in_pieces(ctx, piece_mb, monkeypatch):
     (the first one included), one byte into a piece, empty, and objects of
     one piece beside them: parity and every digest equal to the oracle and
     hashlib."""
-    monkeypatch.setenv("MXEC_PIPE_PIECE_MB", piece_mb)
+    ctx = ctx_with(MXEC_PIPE_PIECE_MB=piece_mb)
     rng = np.random.default_rng(40 + int(piece_mb))
     M = 1 << 20
     specs = [(4, 2, 3 * M + 100, None), (4, 2, 3 * M + 100, 2 * M + 17), (8, 4, 2 * M, M),
@@ -91,17 +91,18 @@ def test_batch_host_digests_in_pieces(ctx, piece_mb, monkeypatch):
 
 
 @pytest.mark.parametrize("ramp_kb,copy2d", [("", ""), ("0", "1"), ("256", "1"), ("64", "1"), ("64", "0")])
-def test_batch_host_pinned_pieces_2d(ctx, ramp_kb, copy2d, monkeypatch):
+def test_batch_host_pinned_pieces_2d(ctx_with, ramp_kb, copy2d):
     """Page-locked bodies in pieces, defaults (uniform pieces, 1D copies)
-    and the lab knobs: the same piece of an object's k chunks (and of its m
-    parity chunks) as one 2D copy (MXEC_PIPE_COPY2D=1), a ramp of pieces
-    from MXEC_PIPE_RAMP_KB up to 1 MiB;
+    and the lab knobs (lab builds only): the same piece of an object's k
+    chunks (and of its m parity chunks) as one 2D copy (MXEC_PIPE_COPY2D=1),
+    a ramp of pieces from MXEC_PIPE_RAMP_KB up to 1 MiB;
     shards off the piece grid.  Parity and digests equal to the oracle."""
+    from conftest import lab_build
+
     torch = pytest.importorskip("torch")
-    if ramp_kb:
-        monkeypatch.setenv("MXEC_PIPE_RAMP_KB", ramp_kb)
-    if copy2d:
-        monkeypatch.setenv("MXEC_PIPE_COPY2D", copy2d)
+    if (ramp_kb or copy2d) and not lab_build():
+        pytest.skip("MXEC_PIPE_RAMP_KB / MXEC_PIPE_COPY2D exist in lab builds only")
+    ctx = ctx_with(MXEC_PIPE_RAMP_KB=ramp_kb, MXEC_PIPE_COPY2D=copy2d)
     k, m, s, n = 4, 2, 3 * (1 << 20) + 128, 6
     host = torch.randint(0, 256, (n, k, s), dtype=torch.uint8).pin_memory()
     par = torch.zeros((n, m, s), dtype=torch.uint8).pin_memory()
@@ -241,13 +242,13 @@ def test_reconstruct_batch_host_mixed(ctx, verify):
 
 
 @pytest.mark.parametrize("piece_mb", ["1", "2", "0"])
-def test_reconstruct_batch_host_verify_in_pieces(ctx, piece_mb, monkeypatch):
+def test_reconstruct_batch_host_verify_in_pieces(ctx_with, piece_mb):
     """With verification the present shards go up and are hashed piece by
     piece (MXEC_PIPE_PIECE_MB; 0 = one launch after the whole upload):
     shards over several pieces and off the piece grid, short and empty last
     chunks, a corrupt present shard caught as an erasure, an object that
     fails (buffers untouched), the rest bit-exact."""
-    monkeypatch.setenv("MXEC_PIPE_PIECE_MB", piece_mb)
+    ctx = ctx_with(MXEC_PIPE_PIECE_MB=piece_mb)
     rng = np.random.default_rng(50 + int(piece_mb))
     M = 1 << 20
     specs = [(4, 2, 3 * M + 100, None, {1}, {4}), (4, 2, 3 * M + 100, 2 * M + 17, {0, 5}, set()),
@@ -340,3 +341,31 @@ def test_reconstruct_batch_host_every_pattern(ctx, k, m, s, verify):
         for i in range(k + m):
             g = o * (k + m) + i
             assert np.array_equal(bufs[g][:lens[g]], originals[o][i]), (sorted(pats[o]), i)
+
+
+def test_batch_host_pieces_descriptor_tables_outgrow_first_block(ctx):
+    """a piece-major wave's descriptor tables grow with pieces x
+    shape classes (each piece re-issues one RS launch per (k, m, S) class and
+    one hash launch), past the first block the wave reserves from its
+    object count.  150 objects of distinct 64 MiB-class shard sizes (150
+    classes x 64 one-MiB pieces: ~3 MB of tables against a ~2.1 MB first
+    block) must encode like any other batch (the arena chains another
+    block) instead of failing with MXEC_E_OOM.  k = 1: the crate's parity
+    is a copy of the data (matrix [[1]]), so the check is cheap."""
+    import hashlib
+
+    n, M = 150, 1 << 20
+    rng = np.random.default_rng(77)
+    data = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(n)]
+    sizes = [64 * M + 4096 * o for o in range(n)]
+    outs = [np.full(s, 0xEE, np.uint8) for s in sizes]
+    objs = [(1, 1, s) for s in sizes]
+    digests = np.zeros(n * 2 * 32, np.uint8)
+    status = ctx.encode_batch_host(objs, [d.ctypes.data for d in data], [o.ctypes.data for o in outs],
+                                   data_len=[4096] * n, digests=digests)
+    assert (status == 0).all()
+    for o in range(n):
+        assert np.array_equal(outs[o][:4096], data[o]) and not outs[o][4096:].any(), o
+        assert digests[o * 64:o * 64 + 32].tobytes() == hashlib.sha256(data[o].tobytes()).digest(), o
+    for o in range(0, n, 15):  # parity digests over the full (zero-padded) shard
+        assert digests[o * 64 + 32:o * 64 + 64].tobytes() == hashlib.sha256(outs[o].tobytes()).digest(), o

@@ -261,7 +261,7 @@ def _drain_raw(ctx, ec, off, ln):
 @pytest.mark.parametrize("window", [None, "1", "300"])
 @pytest.mark.parametrize("damage", ["none", "missing", "corrupt", "short", "missing+corrupt",
                                     "missing+parity", "too_many", "no_parity_corrupt"])
-def test_one_shot_get_matches_streaming_reader(ctx, tmp_path, damage, window, monkeypatch):
+def test_one_shot_get_matches_streaming_reader(ctx_with, tmp_path, damage, window):
     """The one-shot GET reads whole chunks straight into the caller's buffer
     and, with a chunk known bad before hashing, verifies and rebuilds in one
     mxec_reconstruct call; the streaming reader goes chunk buffer by chunk
@@ -270,8 +270,7 @@ def test_one_shot_get_matches_streaming_reader(ctx, tmp_path, damage, window, mo
     window at its default, one chunk (window 1) and two chunks (300)."""
     import numpy as np
 
-    if window is not None:
-        monkeypatch.setenv("MXEC_GET_WINDOW", window)
+    ctx = ctx_with(MXEC_GET_WINDOW=window)  # read at mxec_open; None: the default
 
     body = np.random.default_rng(9).integers(0, 256, 1000, dtype=np.uint8).tobytes()
     ec = tmp_path / "o.ec"
