@@ -306,9 +306,11 @@ class Reconstruct:
         shards = [d.tobytes() for d in data] + [p.tobytes() for p in parity]
         shards[1] = shards[5] = None
         sizes = [S] * (k + m)
-        return (lambda i: oracle.try_reconstruct_data_chunk(shards, k, m, S, dig, sizes, 1)), k * S, (
-            "try_reconstruct_data_chunk restated (oracle): SHA-256 (scalar) of the 10 present 1 MiB "
-            "shards + crate reconstruct of 2, per object")
+        ni = oracle.have_sha_ni()
+        self.cpu_sha_ni = ni
+        return (lambda i: oracle.try_reconstruct_data_chunk(shards, k, m, S, dig, sizes, 1, sha_ni=True)), k * S, (
+            f"try_reconstruct_data_chunk restated (oracle): SHA-256 ({'SHA-NI, as sha2 0.10.9 selects' if ni else 'scalar: no SHA-NI on this host'}) "
+            "of the 10 present 1 MiB shards + crate reconstruct (64 KiB MUL_TABLE) of 2, per object")
 
     def drop(self):
         del self.obj, self.dig, self.ref
@@ -367,7 +369,9 @@ class ReconstructStream:
         return all(p.spot_check() for p in self.parts)
 
     def cpu_work(self):
-        return self.parts[0].cpu_work()
+        spec = self.parts[0].cpu_work()
+        self.cpu_sha_ni = self.parts[0].cpu_sha_ni
+        return spec
 
     def drop(self):
         self.pool.shutdown()
@@ -1076,6 +1080,17 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
         "rs_decode": hbm_block(float(n) * (k + 2) * S, ms_rs, "rs_apply_fast<R=2> (decode 8 -> 2, no verify)",
                                cal3, "rs_pattern_same_buffers_GBps"),
     }
+    # the reference's CPU path for the same work, 1 core and all cores
+    # (SHA-NI as sha2 0.10.9 selects it on x86-64)
+    work, per_call, what = r.cpu_work()
+    v1, n1, el1 = cpu_leg(work, per_call, 4.0, 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 64)
+    va, na, ela = cpu_leg(work, per_call, 3.0, threads)
+    out["config3"]["cpu_baseline"] = {"value": round(v1, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                                      "sha_ni": r.cpu_sha_ni, "sample": f"{n1} calls in {el1:.1f}s: {what}"}
+    out["config3"]["cpu_baseline_all_cores"] = {"value": round(va, 4), "unit": "GiB/s", "cores": threads,
+                                                "kind": "port", "sha_ni": r.cpu_sha_ni,
+                                                "sample": f"{na} calls in {ela:.1f}s on {threads} threads"}
     del dig
     r.drop()
     del r
@@ -1384,7 +1399,14 @@ def gpu_numa_node(torch, d: int):
         return None
 
 
-def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
+def _leg_times(ts: list) -> dict:
+    """Every timed batch of a leg, its median (the reported rate) and max."""
+    med = statistics.median(ts)
+    return {"s_per_batch": round(med, 4), "s_max": round(max(ts), 4),
+            "max_over_median": round(max(ts) / med, 3), "s_each": [round(t, 4) for t in ts]}
+
+
+def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: bool = False) -> dict:
     """mxec_encode_batch_host from mxec_host_alloc (page-locked) memory: the
     PUT path as MaxIO sees it -- request bodies in host memory, parity and
     digests back in host memory (filesystem.rs:1107-1135) -- over every
@@ -1392,8 +1414,13 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
     the GET side, mxec_reconstruct_batch_host over the same objects with two
     erasures each, without and with verification.
     Payload GiB/s (k * chunk_size per object) over all ranks at the median
-    of `reps` timed batches (each batch's time listed), next to the box's raw
-    pinned copy rates and the bounds they set."""
+    of `reps` timed batches (each batch's time and the max listed), next to
+    the box's raw pinned copy rates and the bounds they set.  get_only: the
+    verified GET leg alone (one untimed PUT with digests first) -- the bench
+    runs it again after the device-resident extras, so a process that has
+    allocated and freed tens of GB of HBM is measured too.
+    BENCH_GET_STAMPS=1 adds each timed GET batch's CLOCK_MONOTONIC start and
+    end (ns) for lining the legs up with a rocprofv3 trace."""
     import numpy as np
 
     k, m, S = 4, 2, 10 << 20
@@ -1422,11 +1449,13 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
     # The same bytes at the measured simultaneous 2:1 rates (pcie_rates).
     duplex_s = max(n * k * S / (rates["duplex_2to1_up_GBps"] * 1e9), n * m * S / (rates["duplex_2to1_down_GBps"] * 1e9))
     dig_all = None
-    for sha in (False, True):
+    for sha in ((True,) if get_only else (False, True)):
         dig = np.zeros(n * (k + m) * 32, np.uint8) if sha else None
         if sha:
             dig_all = dig
         ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm: pools, tables
+        if get_only:
+            break
         ts = []
         for _ in range(reps):
             barrier()
@@ -1436,9 +1465,8 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
         el = statistics.median(ts)
         payload = reduce_sum(float(n * k * S))
         key = "rs_sha256" if sha else "rs_only"
-        res[key] = {"s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
-                    "frac_of_pcie_bound": round(bound_s / el, 4),
-                    "frac_of_duplex_bound": round(duplex_s / el, 4), "s_each": [round(t, 4) for t in ts]}
+        res[key] = dict(_leg_times(ts), GiBps_payload=round(payload / GIB / el, 2),
+                        frac_of_pcie_bound=round(bound_s / el, 4), frac_of_duplex_bound=round(duplex_s / el, 4))
     # GET side (chunk_reader.rs:157-226 from the shard files in host memory):
     # mxec_reconstruct_batch_host over the same objects with two seeded
     # erasures each -- the 4 present shards go up, the 2 rebuilt ones come
@@ -1456,25 +1484,33 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5) -> dict:
     get_down_s = n * 2 * S / (rates["d2h_GBps"] * 1e9)
     get_duplex_s = max(n * (k + m - 2) * S / (rates["duplex_2to1_up_GBps"] * 1e9),
                        n * 2 * S / (rates["duplex_2to1_down_GBps"] * 1e9))
-    for verify in (False, True):
+    stamps = os.environ.get("BENCH_GET_STAMPS") == "1"
+    for verify in ((True,) if get_only else (False, True)):
         exp = dig_all if verify else None
         pr = present0.copy()
         rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)  # warm
         assert rc == 0, rc
-        ts = []
+        ts, marks = [], []
         for _ in range(reps):
             pr = present0.copy()
             barrier()
             t0 = time.perf_counter()
+            m0 = time.monotonic_ns()
             rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)
+            marks.append((m0, time.monotonic_ns()))
             ts.append(reduce_max(time.perf_counter() - t0))
             assert rc == 0, rc
         el = statistics.median(ts)
         payload = reduce_sum(float(n * k * S))
-        res["get_verify_sha256" if verify else "get_rs_only"] = {
-            "s_per_batch": round(el, 4), "GiBps_payload": round(payload / GIB / el, 2),
-            "frac_of_pcie_bound": round(max(get_up_s, get_down_s) / el, 4),
-            "frac_of_duplex_bound": round(get_duplex_s / el, 4), "s_each": [round(t, 4) for t in ts]}
+        res["get_verify_sha256" if verify else "get_rs_only"] = dict(
+            _leg_times(ts), GiBps_payload=round(payload / GIB / el, 2),
+            frac_of_pcie_bound=round(max(get_up_s, get_down_s) / el, 4),
+            frac_of_duplex_bound=round(get_duplex_s / el, 4))
+        if stamps:
+            res["get_verify_sha256" if verify else "get_rs_only"]["monotonic_ns"] = marks
+    if get_only:
+        del data, par
+        return res
     if plan.rank == 0:
         # the rebuilt shards of one object, scribbled first, come back exact
         o = n // 3
@@ -1633,6 +1669,7 @@ def main() -> int:
         achieved = w.alg_bytes / (ms_launch * 1e-3) / 1e9
         w.kernel = "crc_tiles_kernel + crc_finish_kernel (CRC32C alone)"
     cpu_spec = w.cpu_work() if (rank == 0 and one_gpu and args.cpu_seconds > 0) else None
+    cpu_sha_ni = getattr(w, "cpu_sha_ni", None)  # set by cpu_work when the baseline hashes
     alg_bytes, w_name, w_kernel, w_bound, w_payload = w.alg_bytes, w.name, w.kernel, w.bound, w.payload
     is_stream = isinstance(w, ReconstructStream)
     stream_dims = (len(w.parts), w.parts[0].n) if is_stream else None
@@ -1642,13 +1679,18 @@ def main() -> int:
     del w
     lanes = []
     torch.cuda.empty_cache()
-    # The host legs first: after the extras' 60+ GB of device buffers were
-    # allocated and freed, a box's first process measured its GET legs 20 %
-    # slower with 0.9 s batches; each leg is timed on its own.
+    # The host legs first, on a process that has not yet run the extras;
+    # the verified GET runs again after them (extra.e2e_get_after_extras).
     if not args.no_e2e and args.config == "2":
         extra["e2e_host"] = e2e_host_leg(ctx, torch, plan, 128 if D == 1 and world == 1 else 64)
     if rank == 0 and with_extra:
         extra.update(extras(ctx, torch, dev, stream, args.steps, cal))
+        if not args.no_e2e:
+            # The verified GET again, now that the process has allocated and
+            # freed the extras' tens of GB of HBM (a long-lived MaxIO server's
+            # shape): its batches' max against their median.
+            torch.cuda.empty_cache()
+            extra["e2e_get_after_extras"] = e2e_host_leg(ctx, torch, plan, 128, get_only=True)
     if cal is not None:
         extra["calibration"] = cal
     cpu = cpu_all = None
@@ -1657,6 +1699,8 @@ def main() -> int:
         v, n, el = cpu_leg(work, per_call, args.cpu_seconds, 1)
         cpu = {"value": round(v, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
                "sample": f"{n} calls in {el:.1f}s, 1 thread: {what}"}
+        if cpu_sha_ni is not None:
+            cpu["sha_ni"] = cpu_sha_ni
         # The GPU box grants 16 host cores (OMP_NUM_THREADS) while
         # os.cpu_count() shows the whole machine.
         nc = os.cpu_count() or 1
@@ -1665,6 +1709,8 @@ def main() -> int:
         cpu_all = {"value": round(v, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
                    "sample": f"{n} calls in {el:.1f}s on {threads} threads "
                              f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, os.cpu_count()={nc})"}
+        if cpu_sha_ni is not None:
+            cpu_all["sha_ni"] = cpu_sha_ni
 
     if rank == 0:
         tag = {"2": ("k4m2", grid_bpc), "ns": ("k8m4", grid_bpc), "4a": ("k10m4", grid_bpc),

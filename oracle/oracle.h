@@ -96,6 +96,11 @@ int orc_have_sha_ni(void);
 int orc_compute_parity(int k, int m, size_t chunk_size,
                        const uint8_t* const* data, const size_t* data_len,
                        uint8_t* const* parity, uint8_t* sha_out);
+/* The same with the digests by orc_sha256_fast (SHA-NI, as sha2 0.10.9 on
+ * x86-64) when use_sha_ni: the timed CPU baseline's form. */
+int orc_compute_parity_ex(int k, int m, size_t chunk_size,
+                          const uint8_t* const* data, const size_t* data_len,
+                          uint8_t* const* parity, uint8_t* sha_out, int use_sha_ni);
 
 /* --- chunk_reader.rs:157-226 try_reconstruct_data_chunk, minus file I/O --- */
 /* shards[i] / shard_len[i]: bytes "read from disk" for shard i, or NULL when
@@ -108,6 +113,12 @@ int orc_try_reconstruct_data_chunk(int k, int m, size_t shard_size,
                                    const uint8_t* expected_sha,
                                    const uint64_t* chunk_sizes, int target,
                                    uint8_t* out, int* n_present);
+int orc_try_reconstruct_data_chunk_ex(int k, int m, size_t shard_size,
+                                      const uint8_t* const* shards,
+                                      const size_t* shard_len,
+                                      const uint8_t* expected_sha,
+                                      const uint64_t* chunk_sizes, int target,
+                                      uint8_t* out, int* n_present, int use_sha_ni);
 
 /* --- PUT body digests (body_oracle.c; filesystem.rs:28-63, 700-777) ------ */
 uint32_t orc_crc32(const uint8_t* p, size_t n);                      /* crc32fast::hash */

@@ -63,12 +63,13 @@ def lib() -> ctypes.CDLL:
                                          ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_md5.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.orc_sha1.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
-        L.orc_compute_parity.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
-                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                         ctypes.c_void_p]
-        L.orc_try_reconstruct_data_chunk.argtypes = [
+        L.orc_compute_parity_ex.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int]
+        L.orc_have_sha_ni.argtypes = []
+        L.orc_try_reconstruct_data_chunk_ex.argtypes = [
             ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
-            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -269,23 +270,31 @@ def put_checksum_b64(algo: str, data) -> str:
     return base64.b64encode(raw).decode()
 
 
-def compute_parity(data: Sequence, m: int, chunk_size: int):
-    """filesystem.rs:1084-1145 minus I/O: (parity shards, k+m digests, rc)."""
+def have_sha_ni() -> bool:
+    """Whether this host has the x86 SHA extensions (sha2 0.10.9's backend)."""
+    return bool(lib().orc_have_sha_ni())
+
+
+def compute_parity(data: Sequence, m: int, chunk_size: int, sha_ni: bool = False):
+    """filesystem.rs:1084-1145 minus I/O: (parity shards, k+m digests, rc).
+    sha_ni: digests by the SHA-NI form (the timed CPU baseline; sha2 0.10.9
+    auto-selects it on x86-64), else the scalar restatement (the checker)."""
     arrs = [_arr(d) for d in data]
     k = len(arrs)
     parity = [np.zeros(chunk_size, np.uint8) for _ in range(max(m, 0))]
     lens = (ctypes.c_size_t * max(1, k))(*[a.size for a in arrs])
     dig = np.zeros((k + max(m, 0)) * 32 or 32, np.uint8)
     src = [a if a.size else np.zeros(1, np.uint8) for a in arrs]
-    rc = lib().orc_compute_parity(k, m, chunk_size, _pp(src), lens, _pp(parity), dig.ctypes.data)
+    rc = lib().orc_compute_parity_ex(k, m, chunk_size, _pp(src), lens, _pp(parity), dig.ctypes.data, int(sha_ni))
     digests = [dig[32 * i: 32 * i + 32].tobytes() for i in range(k + max(m, 0))]
     return parity, digests, int(rc)
 
 
 def try_reconstruct_data_chunk(shards: Sequence[Optional[object]], k: int, m: int,
                                shard_size: int, expected: Sequence[bytes],
-                               chunk_sizes: Sequence[int], target: int):
-    """chunk_reader.rs:157-226 minus I/O: (bytes or None, rc, n_present)."""
+                               chunk_sizes: Sequence[int], target: int, sha_ni: bool = False):
+    """chunk_reader.rs:157-226 minus I/O: (bytes or None, rc, n_present).
+    sha_ni as compute_parity."""
     total = k + m
     arrs = [None if s is None else _arr(s) for s in shards]
     keep = [a if (a is not None and a.size) else np.zeros(1, np.uint8) for a in arrs]
@@ -296,8 +305,8 @@ def try_reconstruct_data_chunk(shards: Sequence[Optional[object]], k: int, m: in
     sizes = (ctypes.c_uint64 * total)(*chunk_sizes)
     out = np.zeros(max(1, shard_size), np.uint8)
     npres = ctypes.c_int(0)
-    rc = lib().orc_try_reconstruct_data_chunk(k, m, shard_size, ptrs, lens, exp.ctypes.data,
-                                              sizes, target, out.ctypes.data, ctypes.byref(npres))
+    rc = lib().orc_try_reconstruct_data_chunk_ex(k, m, shard_size, ptrs, lens, exp.ctypes.data,
+                                                 sizes, target, out.ctypes.data, ctypes.byref(npres), int(sha_ni))
     if rc:
         return None, int(rc), npres.value
     return out[: chunk_sizes[target]].tobytes(), 0, npres.value

@@ -299,9 +299,16 @@ out:
  * data chunk to chunk_size (:1108-1113), zeroed parity (:1116-1118),
  * ReedSolomon::new + encode (:1121-1124), sha256 of each full parity shard
  * (:1131).  Data digests are write_chunk's (:1070) over unpadded bytes. */
-int orc_compute_parity(int k, int m, size_t chunk_size,
-                       const uint8_t* const* data, const size_t* data_len,
-                       uint8_t* const* parity, uint8_t* sha_out) {
+/* The digest function of the composite calls: the scalar restatement (the
+ * checker) or, for the timed CPU baseline, the SHA-NI form sha2 0.10.9
+ * auto-selects on x86-64 (orc_sha256_fast; scalar where the host lacks it). */
+static void sha_scalar(const uint8_t* p, size_t n, uint8_t out[32]) { orc_sha256(p, n, out); }
+static void sha_ni(const uint8_t* p, size_t n, uint8_t out[32]) { (void)orc_sha256_fast(p, n, out); }
+
+int orc_compute_parity_ex(int k, int m, size_t chunk_size,
+                          const uint8_t* const* data, const size_t* data_len,
+                          uint8_t* const* parity, uint8_t* sha_out, int use_sha_ni) {
+    void (*sha)(const uint8_t*, size_t, uint8_t*) = use_sha_ni ? sha_ni : sha_scalar;
     if (k + m > 255) return ORC_E_TOO_MANY_SHARDS_255;
     int rc = orc_rs_check(k, m);
     if (rc) return rc;
@@ -310,7 +317,7 @@ int orc_compute_parity(int k, int m, size_t chunk_size,
         if (data_len[j] > chunk_size) { rc = ORC_E_INVALID_ARG; break; }
         shards[j] = (uint8_t*)calloc(chunk_size ? chunk_size : 1, 1);
         memcpy(shards[j], data[j], data_len[j]);
-        if (sha_out) orc_sha256(data[j], data_len[j], sha_out + 32 * j);
+        if (sha_out) sha(data[j], data_len[j], sha_out + 32 * j);
     }
     if (rc == ORC_OK) {
         for (int i = 0; i < m; ++i) {
@@ -319,23 +326,30 @@ int orc_compute_parity(int k, int m, size_t chunk_size,
         }
         rc = orc_rs_encode(k, m, chunk_size, shards);
         if (rc == ORC_OK && sha_out)
-            for (int i = 0; i < m; ++i) orc_sha256(parity[i], chunk_size, sha_out + 32 * (k + i));
+            for (int i = 0; i < m; ++i) sha(parity[i], chunk_size, sha_out + 32 * (k + i));
     }
     for (int j = 0; j < k; ++j) free(shards[j]);
     free(shards);
     return rc;
 }
 
+int orc_compute_parity(int k, int m, size_t chunk_size,
+                       const uint8_t* const* data, const size_t* data_len,
+                       uint8_t* const* parity, uint8_t* sha_out) {
+    return orc_compute_parity_ex(k, m, chunk_size, data, data_len, parity, sha_out, 0);
+}
+
 /* chunk_reader.rs:157-226 without the disk: every shard is hashed and
  * compared to the manifest digest (:176-196); mismatches / missing files
  * become None; present ones are padded to shard_size; present < k is an
  * error (:199-208); reconstruct (:211); return target truncated (:216-222). */
-int orc_try_reconstruct_data_chunk(int k, int m, size_t shard_size,
-                                   const uint8_t* const* shards,
-                                   const size_t* shard_len,
-                                   const uint8_t* expected_sha,
-                                   const uint64_t* chunk_sizes, int target,
-                                   uint8_t* out, int* n_present) {
+int orc_try_reconstruct_data_chunk_ex(int k, int m, size_t shard_size,
+                                      const uint8_t* const* shards,
+                                      const size_t* shard_len,
+                                      const uint8_t* expected_sha,
+                                      const uint64_t* chunk_sizes, int target,
+                                      uint8_t* out, int* n_present, int use_sha_ni) {
+    void (*sha)(const uint8_t*, size_t, uint8_t*) = use_sha_ni ? sha_ni : sha_scalar;
     int rc = orc_rs_check(k, m);
     if (rc) return rc;
     if (target < 0 || target >= k + m) return ORC_E_INVALID_INDEX;
@@ -347,7 +361,7 @@ int orc_try_reconstruct_data_chunk(int k, int m, size_t shard_size,
         bufs[i] = (uint8_t*)calloc(shard_size ? shard_size : 1, 1);
         if (!shards[i]) continue;
         uint8_t d[32];
-        orc_sha256(shards[i], shard_len[i], d);
+        sha(shards[i], shard_len[i], d);
         if (memcmp(d, expected_sha + 32 * i, 32) != 0) continue;
         /* Vec::resize(shard_size): pad, or truncate if longer */
         size_t n = shard_len[i] < shard_size ? shard_len[i] : shard_size;
@@ -370,4 +384,14 @@ int orc_try_reconstruct_data_chunk(int k, int m, size_t shard_size,
     free(bufs);
     free(present);
     return rc;
+}
+
+int orc_try_reconstruct_data_chunk(int k, int m, size_t shard_size,
+                                   const uint8_t* const* shards,
+                                   const size_t* shard_len,
+                                   const uint8_t* expected_sha,
+                                   const uint64_t* chunk_sizes, int target,
+                                   uint8_t* out, int* n_present) {
+    return orc_try_reconstruct_data_chunk_ex(k, m, shard_size, shards, shard_len, expected_sha, chunk_sizes,
+                                             target, out, n_present, 0);
 }

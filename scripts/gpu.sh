@@ -14,8 +14,12 @@
 #   ranks2    the torch.distributed.run path with two ranks on the one GPU
 #             (BENCH_GPU_OF_RANK=0, gloo for the timing collectives)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench command
+#   trace     rocprofv3 --kernel-trace --memory-copy-trace of the default bench
+#             with BENCH_GET_STAMPS=1; tools/get_trace_summary.py lines the
+#             timed GET batches up with the trace -> get_trace_summary.json
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (one run each) of rs_apply_fast
-#             for configs 2 and ns, summarised with the grid they ran at
+#             for configs 2 and ns, summarised with the grid they ran at (the
+#             grid fixed through the lab build's MXEC_RS_BPC: make lab first)
 #   clock     GRBM_GUI_ACTIVE / GRBM_COUNT pass (one run per config) of configs
 #             3 (SHA-256 split form + decode) and 2 / ns (RS encode):
 #             effective clock per kernel (tools/clock_summary.py)
@@ -65,13 +69,22 @@ for st in "${STEPS[@]}"; do
       find /tmp/prof -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
       find /tmp/prof -name "*kernel_trace.csv" -exec cp {} "$O/kernel_trace.csv" \;
       cat "$O/prof_bench.json" ;;
+    trace)
+      ( cd /tmp && BENCH_GET_STAMPS=1 timeout -k 10 900 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/trace \
+          -o run --output-format csv -- python3 "$R/bench.py" $BENCH_ARGS > "$O/trace_bench.json" \
+          2> "$O/trace_bench.err" ) || { tail -20 "$O/trace_bench.err"; exit 1; }
+      kt=$(find /tmp/trace -name "*kernel_trace.csv" -print -quit); mt=$(find /tmp/trace -name "*memory_copy_trace.csv" -print -quit)
+      python tools/get_trace_summary.py "$kt" "$mt" "$O/trace_bench.json" --out "$O/get_trace_summary.json" > /dev/null \
+        || exit 1
+      gzip -c "$kt" > "$O/kernel_trace.csv.gz"; gzip -c "$mt" > "$O/memory_copy_trace.csv.gz"
+      cat "$O/trace_bench.json" ;;
     pmc)
       # each (config, grid) with the grid fixed (MXEC_RS_BPC also turns the
       # grid tuner off), counters only on rs_apply_fast, one run per counter
       for cb in 2:1024 2:512 ns:512 ns:256; do
         cfg=${cb%%:*}; bpc=${cb##*:}
         for c in FETCH_SIZE WRITE_SIZE; do
-          ( cd /tmp && MXEC_RS_BPC=$bpc timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast \
+          ( cd /tmp && MXEC_LIB="$R/maxio_amd/lib/libmaxio_ec_lab.so" MXEC_RS_BPC=$bpc timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast \
               -d "/tmp/pmc/${cfg}_${bpc}_$c" -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 2 \
               --warmup 1 --cpu-seconds 0 --no-extra --no-e2e > "$O/pmc_${cfg}_${bpc}_$c.log" 2>&1 ) \
               || { tail -5 "$O/pmc_${cfg}_${bpc}_$c.log"; exit 1; }
