@@ -29,6 +29,11 @@
 #include <vector>
 
 #include "../../include/maxio_ec.h"
+#ifdef MXEC_LAB
+#include <chrono>
+#include <cstdio>
+#include <string>
+#endif
 #include "deal.hpp"
 #include "kernels.hpp"
 #include "ops.hpp"
@@ -187,6 +192,66 @@ struct PipeRes {
     }
 };
 
+#ifdef MXEC_LAB
+// MXEC_PIPE_TRACE=1 (lab builds): where a host reconstruct wave's time goes
+// -- timing events on the copy and compute streams and host clocks around
+// every wait, one stderr JSON line per wave (tools: the GET-stall study).
+struct PipeTrace {
+    bool on = false;
+    std::chrono::steady_clock::time_point h0;
+    hipEvent_t e0 = nullptr;
+    std::vector<std::pair<std::string, hipEvent_t>> ev;
+    std::vector<std::pair<std::string, double>> host;
+    void start(hipStream_t s) {
+        const char* e = getenv("MXEC_PIPE_TRACE");
+        on = e && *e == '1';
+        if (!on) return;
+        h0 = std::chrono::steady_clock::now();
+        (void)hipEventCreate(&e0);
+        (void)hipEventRecord(e0, s);
+    }
+    void mark(const char* what, hipStream_t s) {
+        if (!on) return;
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        (void)hipEventRecord(e, s);
+        ev.emplace_back(what, e);
+    }
+    void now(const char* what) {
+        if (!on) return;
+        host.emplace_back(what, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
+    }
+    void report(const char* tag) {
+        if (!on) return;
+        now("end");
+        std::string out = std::string("{\"pipe_trace\": \"") + tag + "\", \"gpu_ms\": [";
+        for (size_t i = 0; i < ev.size(); ++i) {
+            float ms = -1;
+            (void)hipEventSynchronize(ev[i].second);
+            (void)hipEventElapsedTime(&ms, e0, ev[i].second);
+            char b[96];
+            snprintf(b, sizeof b, "%s[\"%s\", %.3f]", i ? ", " : "", ev[i].first.c_str(), ms);
+            out += b;
+            (void)hipEventDestroy(ev[i].second);
+        }
+        out += "], \"host_ms\": [";
+        for (size_t i = 0; i < host.size(); ++i) {
+            char b[96];
+            snprintf(b, sizeof b, "%s[\"%s\", %.3f]", i ? ", " : "", host[i].first.c_str(), host[i].second);
+            out += b;
+        }
+        out += "]}";
+        fprintf(stderr, "%s\n", out.c_str());
+        (void)hipEventDestroy(e0);
+        ev.clear();
+        host.clear();
+    }
+};
+#define PTRACE(x) tr_.x
+#else
+#define PTRACE(x) ((void)0)
+#endif
+
 class DevicePipeline {
 public:
     DevicePipeline(Device& d, PipeRes& r)
@@ -252,6 +317,7 @@ private:
     int rec_wave(std::vector<RecObj>& objs, size_t o0, size_t o1, bool data_only) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         hipStream_t cs = cs_[0];
+        PTRACE(start(h2d_));
         // Groups: consecutive objects up to kGroupBytes of present input.
         std::vector<std::pair<size_t, size_t>> groups;
         for (size_t g0 = o0; g0 < o1;) {
@@ -297,6 +363,7 @@ private:
             // verdicts come back after the last piece, then the rebuild as
             // below (nothing is written to the caller's buffers before).
             MXEC_TRY(verify_in_pieces(objs, o0, o1, ok, exp, msgs, P));
+            PTRACE(now("verified"));
         } else {
             MXEC_TRY(upload_and_verify(objs, o0, o1, groups, ok, exp, verify, cs, &up));
         }
@@ -355,6 +422,8 @@ private:
             hipEvent_t rs_done;
             MXEC_TRY(new_event(&rs_done));
             MXEC_HIP(hipEventRecord(rs_done, cs));
+            PTRACE(mark("rs", cs));
+            PTRACE(now("rs_queued"));
             MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
             for (size_t o = q0; o < q1; ++o) {
                 RecObj& h = objs[o];
@@ -369,7 +438,11 @@ private:
             }
             MXEC_TRY(flush_down());
         }
-        return flush();
+        PTRACE(mark("d2h", d2h_));
+        PTRACE(now("down_queued"));
+        const int frc = flush();
+        PTRACE(report("rec_wave"));
+        return frc;
     }
 
     // Piece-major upload of every present shard (and the expected digests),
@@ -416,10 +489,13 @@ private:
             hipEvent_t up;
             MXEC_TRY(new_event(&up));
             MXEC_HIP(hipEventRecord(up, h2d_));
+            PTRACE(mark("up", h2d_));
             MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
             if (!sp.empty())
                 MXEC_TRY(run_sha_pieces(d_, slot_, cs, sp, sl, ss, st, state, pc > 0, nullptr, &arena_, exp, ok));
+            PTRACE(mark("sha", cs));
         }
+        PTRACE(now("pieces_queued"));
         MXEC_TRY(flags_.ensure(msgs));
         MXEC_HIP(hipMemcpyAsync(flags_.p, ok, msgs, hipMemcpyDeviceToHost, cs));
         MXEC_HIP(hipStreamSynchronize(cs));
@@ -502,6 +578,9 @@ private:
     DescArena& arena_;
     DevBuf& pool_;
     DevBuf& scratch_;  // the wave's digests, message order
+#ifdef MXEC_LAB
+    PipeTrace tr_;
+#endif
     DevBuf& state_;    // chain states of a piece-major verification
     PinnedBuf& flags_;
     Slot& slot_;
