@@ -770,7 +770,11 @@ def probe_lib():
                      ("mxprobe_rs_pattern_strided", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
-                                                     ctypes.c_void_p])):
+                                                     ctypes.c_void_p]),
+                     ("mxprobe_rs_float4_strided", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                    ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                    ctypes.c_void_p])):
         getattr(lib, fn).argtypes = args
         getattr(lib, fn).restype = ctypes.c_int
     return lib

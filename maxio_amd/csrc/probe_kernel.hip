@@ -133,6 +133,29 @@ __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__
     }
 }
 
+// The RS access pattern at the float4 copy's granularity: one 16-byte column
+// of one object per lane (XOR for the GF math), plain loads and stores, one
+// workgroup per 256 columns -- the schedule with the least state per lane
+// (the placement lab's second denominator).
+template <int R>
+__global__ __launch_bounds__(256) void probe_rs_float4(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                       uint32_t k, uint64_t cols, uint64_t n_obj, uint64_t dstride,
+                                                       uint64_t pstride, uint64_t sstride) {
+    const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (g >= cols * n_obj) return;
+    const uint64_t o = g / cols, c = (g - o * cols) * 16;
+    u32x4 acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
+    for (uint32_t j = 0; j < k; ++j) {
+        const u32x4 x = *reinterpret_cast<const u32x4*>(data + o * dstride + j * sstride + c);
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] ^= x * (i + j + 1u);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) *reinterpret_cast<u32x4*>(par + o * pstride + i * sstride + c) = acc[i];
+}
+
 int g_stream_wpc = 16;  // workgroups per CU of the plain stream probes (mxprobe_set_stream_wpc)
 
 int cus() {
@@ -224,6 +247,26 @@ extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32
 extern "C" int mxprobe_rs_pattern(const void* data, void* parity, uint32_t k, uint32_t m, uint64_t S, uint64_t n_obj,
                                   void* stream) {
     return mxprobe_rs_pattern_strided(data, parity, k, m, S, n_obj, uint64_t(k) * S, uint64_t(m) * S, S, stream);
+}
+
+// probe_rs_float4 over the same strided layout (m in {1, 2, 4}, S % 16 == 0).
+extern "C" int mxprobe_rs_float4_strided(const void* data, void* parity, uint32_t k, uint32_t m, uint64_t S,
+                                         uint64_t n_obj, uint64_t data_obj_stride, uint64_t parity_obj_stride,
+                                         uint64_t shard_stride, void* stream) {
+    if (k == 0 || S == 0 || (S % 16) || ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
+        return int(hipErrorInvalidValue);
+    const uint64_t cols = S / 16, blocks = (cols * n_obj + 255) / 256;
+    if (blocks >= (uint64_t(1) << 32)) return int(hipErrorInvalidValue);
+    const auto* in = static_cast<const uint8_t*>(data);
+    auto* out = static_cast<uint8_t*>(parity);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 g{uint32_t(blocks), 1, 1}, b{256, 1, 1};
+    const uint64_t ds = data_obj_stride, ps = parity_obj_stride, ss = shard_stride;
+    if (m == 1) hipLaunchKernelGGL(probe_rs_float4<1>, g, b, 0, s, in, out, k, cols, n_obj, ds, ps, ss);
+    else if (m == 2) hipLaunchKernelGGL(probe_rs_float4<2>, g, b, 0, s, in, out, k, cols, n_obj, ds, ps, ss);
+    else if (m == 4) hipLaunchKernelGGL(probe_rs_float4<4>, g, b, 0, s, in, out, k, cols, n_obj, ds, ps, ss);
+    else return int(hipErrorInvalidValue);
+    return int(hipGetLastError());
 }
 
 // The RS pattern at m = 2 with store policy `policy` (store_p above), for the

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Is the RS kernel's rate a property of where its batch lands?  Allocates
+`--allocs` object-major batches of configs[1]'s shape ([n][k+m][S + pad],
+4+2 x 10 MiB, the bench's layout) one after another (most of the card), and
+on each, in one process, times with HIP events (median of --reps):
+
+* rs:         the shipping encode (mxec_encode_strided_device), for every
+              grid in --grids (workgroups per CU; the lab build's MXEC_RS_BPC)
+* pattern:    the RS kernel's own tile / load schedule with XOR math
+              (libmaxio_probe mxprobe_rs_pattern_strided)
+* f4pattern:  the same bytes at the float4 copy's granularity (one 16-byte
+              column per lane, plain loads / stores: mxprobe_rs_float4_strided)
+* f4copy:     the guide's float4 copy, first half of the buffer onto the
+              second half (the bench's `float4_copy_on_buffers`)
+
+One JSON line per allocation.  Lab tool (needs `make lab`: the default is
+MXEC_LIB = the lab build, for MXEC_RS_BPC).
+
+  python tools/placement_lab.py [--objects 256] [--allocs 8] [--grids 1024,512] [--reps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("MXEC_LIB", os.path.join(ROOT, "maxio_amd", "lib", "libmaxio_ec_lab.so"))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--objects", type=int, default=256)
+    ap.add_argument("--allocs", type=int, default=8)
+    ap.add_argument("--grids", default="1024,512")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--check", action="store_true", help="oracle-check object 0 after the rs timings")
+    a = ap.parse_args()
+    import torch
+
+    import bench
+    import maxio_amd
+
+    k, m, S, n = 4, 2, 10 << 20, a.objects
+    pad = (2 << 20) + (64 << 10)
+    ss = S + pad
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(device=dev)
+    sh = st.cuda_stream
+    probe = bench.probe_lib()
+    ctx = maxio_amd.Context(device_mask=1, streams_per_device=2)
+    alg = n * (k + m) * S
+
+    def tbps(ms):
+        return round(alg / (ms * 1e-3) / 1e12, 4)
+
+    bufs = []
+    for ai in range(a.allocs):
+        try:
+            obj = torch.empty((n, k + m, ss), dtype=torch.uint8, device=dev)
+        except RuntimeError as e:  # out of memory: stop here
+            print(json.dumps({"alloc": ai, "stopped": str(e)[:120]}), flush=True)
+            break
+        bufs.append(obj)
+        obj[:, :k, :S].random_(0, 256)
+        torch.cuda.synchronize()
+        d0, p0, ost = obj.data_ptr(), obj[:, k:].data_ptr(), (k + m) * ss
+        row = {"alloc": ai, "objects": n, "base_mod_2MiB": d0 % (2 << 20)}
+        for g in a.grids.split(","):
+            os.environ["MXEC_RS_BPC"] = g
+            ms = bench.event_ms(torch, st, lambda: ctx.encode_strided_device(
+                k, m, S, n, d0, ost, ss, p0, ost, ss, stream=sh), a.reps, warm=2)
+            row[f"rs_bpc{g}_TBps"] = tbps(ms)
+        os.environ.pop("MXEC_RS_BPC", None)
+        if a.check:
+            h = obj[0].cpu().numpy()
+            want = bench._oracle().encode(list(h[:k, :S]), m, S)
+            row["rs_check"] = all((h[k + i, :S] == want[i]).all() for i in range(m))
+        row["pattern_TBps"] = tbps(bench.event_ms(torch, st, lambda: probe.mxprobe_rs_pattern_strided(
+            d0, p0, k, m, S, n, ost, ost, ss, sh), a.reps))
+        row["f4pattern_TBps"] = tbps(bench.event_ms(torch, st, lambda: probe.mxprobe_rs_float4_strided(
+            d0, p0, k, m, S, n, ost, ost, ss, sh), a.reps))
+        half = (obj.numel() // 2) & ~15
+        ms = bench.event_ms(torch, st, lambda: probe.mxprobe_copy_float4(d0 + half, d0, half, sh), a.reps)
+        row["f4copy_TBps"] = round(2 * half / (ms * 1e-3) / 1e12, 4)
+        for key in [x for x in row if x.startswith("rs_bpc")]:
+            row[key.replace("_TBps", "_of_f4copy")] = round(row[key] / row["f4copy_TBps"], 4)
+        print(json.dumps(row), flush=True)
+    ctx.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
