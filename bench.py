@@ -80,6 +80,13 @@ SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415, "quad": 1780}
 # x 4 cycles per block at the clock the chip holds.
 SHA_CONSUMER_VALU_PER_BLOCK = {"split": 905, "quad": 607}
 SHA_QUAD_MSGS_PER_CU = 64  # the lag form, two messages per quad
+# The hardware floor of ONE message's chain, whatever the form: a round's
+# e' (and a') depends on the previous one through Σ's rotates, their XOR3 and
+# one three-way add (Ch / Maj and the h + d + K + W sums run beside it), so a
+# round cannot take less than the dependent latencies of v_alignbit_b32 ->
+# v_bitop3_b32 -> v_add3_u32 measured for one wave alone on its SIMD
+# (tools/valu_lab.cpp, profiles/r1_lab_valu_issue.jsonl, chains = 1).
+SHA_ROUND_DEP_CYCLES = 10.77 + 8.63 + 8.63
 # Chip INT32 issue ceiling for those instructions (v_alignbit / v_bitop3 /
 # v_add3 / v_add / v_perm): CUs x 4 SIMDs x lanes per cycle x 2.4 GHz, lanes
 # per cycle measured with tools/valu_lab chip (profiles/r2_lab_valu_chip.jsonl).
@@ -935,6 +942,14 @@ def sha_chain_block(form: str, us_per_block: float):
         d.update({"clock_GHz_measured": clk, "clock_source": src,
                   "floor_us_per_block": round(cyc / (clk * 1e3), 4),
                   "frac": round(cyc / (clk * 1e3) / us_per_block, 4)})
+    # against the hardware rather than the form's own instruction count
+    hz = (clk or CLOCK_GHZ) * 1e3
+    hw = 64 * SHA_ROUND_DEP_CYCLES / hz
+    d["hw_chain_floor"] = {
+        "path": "per round: v_alignbit_b32 -> v_bitop3_b32 (XOR3) -> v_add3_u32, one wave's dependent latencies "
+                "10.77 + 8.63 + 8.63 cycles (profiles/r1_lab_valu_issue.jsonl); 64 rounds per block",
+        "cycles_per_block": round(64 * SHA_ROUND_DEP_CYCLES, 1), "clock_GHz": clk or CLOCK_GHZ,
+        "floor_us_per_block": round(hw, 4), "frac": round(hw / us_per_block, 4)}
     return d
 
 
@@ -957,7 +972,9 @@ def config3_roofline(form: str, nmsg: int, sha_GBps: float, ms_sha: float, S: in
                        "form_lane_ops_per_block": SHA_VALU_PER_BLOCK[form],
                        "valu_peak_lane_ops_per_s": n_cus * 4 * VALU_LANES_PER_SIMD_CYCLE * CLOCK_GHZ * 1e9}}
     if chain:
-        f = chain.get("frac", chain["frac_at_2.4GHz"])
+        # `frac` is against the hardware's chain floor (hw_chain_floor); the
+        # form's own 4-cycle issue floor stays in chain.frac
+        f = chain["hw_chain_floor"]["frac"]
         d.update({"bound": "valu-chain", "peak": round(sha_GBps / f, 1), "frac": f, "chain": chain})
     else:
         d.update({"bound": "valu", "peak": round(vb, 1), "frac": round(sha_GBps / vb, 4)})
