@@ -1711,7 +1711,15 @@ def main() -> int:
             # freed the extras' tens of GB of HBM (a long-lived MaxIO server's
             # shape): its batches' max against their median.
             torch.cuda.empty_cache()
+            # BENCH_GET_AFTER_SLEEP (s, lab): idle this long first -- the GET
+            # stall study times the leg with and without a pause
+            # after the extras' frees.
+            pause = float(os.environ.get("BENCH_GET_AFTER_SLEEP", "0"))
+            if pause > 0:
+                time.sleep(pause)
             extra["e2e_get_after_extras"] = e2e_host_leg(ctx, torch, plan, 128, get_only=True)
+            if pause > 0:
+                extra["e2e_get_after_extras"]["slept_s_before"] = pause
     if cal is not None:
         extra["calibration"] = cal
     cpu = cpu_all = None
