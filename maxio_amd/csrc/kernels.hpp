@@ -217,4 +217,14 @@ struct GcmArgs {
 };
 hipError_t launch_gcm_frames(const GcmArgs& a, bool decrypt, int n_cus, hipStream_t s);
 
+// ---- host <-> device copies by CU waves (copy_kernel.hip) ---------------------
+// One block of a copy batch: len bytes from src to dst (one side host memory
+// mapped into the GPU's address space, the other HBM).  The table itself may
+// sit in mapped host memory.
+struct alignas(16) CopyBlk {
+    uint64_t dst, src, len, pad;
+};
+constexpr uint64_t kCopyBlock = uint64_t(256) << 10;  // bytes per block (at most)
+hipError_t launch_copy_blocks(const CopyBlk* blks, uint64_t n, bool to_host, uint32_t grid, hipStream_t s);
+
 }  // namespace mxec

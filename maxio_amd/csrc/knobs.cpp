@@ -13,6 +13,7 @@ const char* const kKnobNames[] = {
     "MXEC_TEST_LOGICAL_DEVICES", "MXEC_TEST_RS_GRID", "MXEC_TEST_COEF_ARENA_KB", "MXEC_DEBUG_AFFINITY",
     "MXEC_HOST_NUMA",            "MXEC_SPIN_WAIT",    "MXEC_RS_TUNE",            "MXEC_RS_MULTI",
     "MXEC_SHA_FORM",             "MXEC_DESC_UPLOAD",  "MXEC_PIPE_PIECE_MB",      "MXEC_GET_WINDOW",
+    "MXEC_PIPE_COPY",
     "MXEC_GATHER_US",            "MXEC_GATHER_MAX_US", "MXEC_GATHER_IDLE_US",    "MXEC_COMBINE_BELOW",
     "MXEC_COMBINE_STREAMS",      "MXEC_COMBINE_PRIORITY", "MXEC_COMBINE_LOG",    nullptr};
 
@@ -65,6 +66,7 @@ Knobs read_knobs() {
     if (const char* u = env("MXEC_DESC_UPLOAD")) k.desc_upload = !std::strcmp(u, "inline") ? 0 : !std::strcmp(u, "stream") ? 2 : 1;
     const long piece = env_long("MXEC_PIPE_PIECE_MB", 1);
     k.pipe_piece = piece <= 0 ? 0 : uint64_t(std::min(piece, 1L << 20)) << 20;
+    if (const char* c = env("MXEC_PIPE_COPY")) k.pipe_copy = !std::strcmp(c, "waves") ? 1 : 0;
     if (const char* w = env("MXEC_GET_WINDOW")) k.get_window = std::max<uint64_t>(1, std::strtoull(w, nullptr, 10));
     k.gather_us = env_long("MXEC_GATHER_US", k.gather_us);
     k.gather_max_us = env_long("MXEC_GATHER_MAX_US", k.gather_max_us);

@@ -424,6 +424,7 @@ private:
             MXEC_HIP(hipEventRecord(rs_done, cs));
             PTRACE(mark("rs", cs));
             PTRACE(now("rs_queued"));
+            MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
             for (size_t o = q0; o < q1; ++o) {
                 RecObj& h = objs[o];
@@ -438,6 +439,7 @@ private:
             }
             MXEC_TRY(flush_down());
         }
+        MXEC_TRY(issue_down());
         PTRACE(mark("d2h", d2h_));
         PTRACE(now("down_queued"));
         const int frc = flush();
@@ -488,6 +490,7 @@ private:
             MXEC_TRY(flush_up());
             hipEvent_t up;
             MXEC_TRY(new_event(&up));
+            MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up, h2d_));
             PTRACE(mark("up", h2d_));
             MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
@@ -533,6 +536,7 @@ private:
             }
             MXEC_TRY(flush_up());
             MXEC_TRY(new_event(&up[q]));
+            MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up[q], h2d_));
         }
         if (verify) {
@@ -593,11 +597,46 @@ private:
         return MXEC_OK;
     }
 
+    // MXEC_PIPE_COPY=waves: copies from / to mxec_host_alloc memory go as
+    // CU-wave copy launches (copy_kernel.hip) instead of SDMA DMAs; they are
+    // collected here and issued as one launch at the next point the stream
+    // is waited on or marked (issue_up / issue_down).
+    bool wave_copy(const void* host, uint64_t len) const {
+        return d_.kn && d_.kn->pipe_copy == 1 && pinned_mapped(host, len);
+    }
+    static void add_blocks(std::vector<CopyBlk>& v, uint8_t* dst, const uint8_t* src, uint64_t len) {
+        for (uint64_t o = 0; o < len; o += kCopyBlock)
+            v.push_back(CopyBlk{reinterpret_cast<uint64_t>(dst + o), reinterpret_cast<uint64_t>(src + o),
+                                std::min(kCopyBlock, len - o), 0});
+    }
+    // The block table goes into the arena's page-locked host half, which the
+    // kernel reads in place (no table upload through the copy engines).
+    int issue_blocks(std::vector<CopyBlk>& v, bool to_host, hipStream_t s) {
+        if (v.empty()) return MXEC_OK;
+        const size_t bytes = (v.size() * sizeof(CopyBlk) + 255) & ~size_t(255);
+        char* h = nullptr;
+        char* d = nullptr;
+        MXEC_TRY(arena_.take(bytes, &h, &d));
+        std::memcpy(h, v.data(), v.size() * sizeof(CopyBlk));
+        const uint32_t grid = kCopyGrid;
+        MXEC_HIP(launch_copy_blocks(reinterpret_cast<const CopyBlk*>(h), v.size(), to_host, grid, s));
+        v.clear();
+        return MXEC_OK;
+    }
+    int issue_up() { return issue_blocks(up_blks_, false, h2d_); }
+    int issue_down() { return issue_blocks(down_blks_, true, d2h_); }
+    std::vector<CopyBlk> up_blks_, down_blks_;
+    static constexpr uint32_t kCopyGrid = 128;  // workgroups per copy launch
+
     int upload(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
         if (affinity_on(d_)) {
             const void* p = dst;
             MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload", &arena_, &p, 1));
+        }
+        if (wave_copy(src, len)) {
+            add_blocks(up_blks_, dst, src, len);
+            return MXEC_OK;
         }
         if (is_pinned(src, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, h2d_));
@@ -727,6 +766,10 @@ private:
             const void* p = src;
             MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download", &arena_, &p, 1));
         }
+        if (wave_copy(dst, len)) {
+            add_blocks(down_blks_, dst, src, len);
+            return MXEC_OK;
+        }
         if (is_pinned(dst, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, d2h_));
             return MXEC_OK;
@@ -744,6 +787,7 @@ private:
     }
 
     int flush() {
+        MXEC_TRY(issue_down());
         MXEC_HIP(hipStreamSynchronize(d2h_));
         for (auto& p : pend_) std::memcpy(p.dst, out_.ptr(p.ring), p.len);
         pend_.clear();
@@ -804,6 +848,7 @@ private:
             hipEvent_t up, rs_done;
             MXEC_TRY(new_event(&up));
             MXEC_TRY(new_event(&rs_done));
+            MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up, h2d_));
             MXEC_HIP(hipStreamWaitEvent(rs_s, up, 0));
             // Parity of this piece: RS is bytewise, so bytes [off, off + P) of
@@ -859,6 +904,7 @@ private:
                 MXEC_TRY(run_sha_pieces(d_, slot, sha_s, sp, sl, ss, st, state, pc > 0, digests, &arena_));
             }
             // This piece of every parity chunk goes down.
+            MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
             for (size_t o = o0; o < o1; ++o) {
                 const HostObj& h = objs[o];
@@ -872,6 +918,7 @@ private:
         if (nm) {
             MXEC_TRY(new_event(&sha_done));
             MXEC_HIP(hipEventRecord(sha_done, sha_s));
+            MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, sha_done, 0));
             uint64_t msg0 = 0;
             for (size_t o = o0; o < o1; ++o) {
@@ -931,6 +978,7 @@ private:
             hipEvent_t up;
             MXEC_TRY(new_event(&up));
             MXEC_TRY(new_event(&done[g]));
+            MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up, h2d_));
             MXEC_HIP(hipStreamWaitEvent(rs_s, up, 0));
             std::map<std::tuple<int, int, uint64_t>, std::vector<size_t>> classes;
@@ -987,6 +1035,7 @@ private:
         }
         // Phase 3: parity back group by group as RS finishes, digests last.
         for (size_t g = 0; g < groups.size(); ++g) {
+            MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, done[g], 0));
             for (size_t o = groups[g].first; o < groups[g].second; ++o) {
                 const HostObj& h = objs[o];
@@ -999,6 +1048,7 @@ private:
             MXEC_TRY(flush_down());  // before the next group's wait
         }
         if (sha_done) {
+            MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, sha_done, 0));
             uint64_t msg0 = 0;
             for (size_t o = o0; o < o1; ++o) {

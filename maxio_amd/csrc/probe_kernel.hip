@@ -156,6 +156,23 @@ __global__ __launch_bounds__(256) void probe_rs_float4(const uint8_t* __restrict
     for (int i = 0; i < R; ++i) *reinterpret_cast<u32x4*>(par + o * pstride + i * sstride + c) = acc[i];
 }
 
+// Host <-> device copy by CU waves instead of the SDMA engines: each lane
+// moves 16-byte vectors, four in flight, grid-stride over the range (the
+// host side is page-locked memory mapped into the GPU's address space).
+__global__ __launch_bounds__(256) void probe_copy_waves(const u32x4* __restrict__ s, u32x4* __restrict__ d, uint64_t n) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const u32x4 a = __builtin_nontemporal_load(s + i), b = __builtin_nontemporal_load(s + i + stride);
+        const u32x4 c = __builtin_nontemporal_load(s + i + 2 * stride), e = __builtin_nontemporal_load(s + i + 3 * stride);
+        __builtin_nontemporal_store(a, d + i);
+        __builtin_nontemporal_store(b, d + i + stride);
+        __builtin_nontemporal_store(c, d + i + 2 * stride);
+        __builtin_nontemporal_store(e, d + i + 3 * stride);
+    }
+    for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
 int g_stream_wpc = 16;  // workgroups per CU of the plain stream probes (mxprobe_set_stream_wpc)
 
 int cus() {
@@ -289,6 +306,16 @@ extern "C" int mxprobe_rs_pattern_policy(const void* data, void* parity, uint32_
         case 3: hipLaunchKernelGGL((probe_pattern<2, 3>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
         default: hipLaunchKernelGGL((probe_pattern<2, 4>), g, b, 0, s, in, out, k, S, n_obj, os, os, ss); break;
     }
+    return int(hipGetLastError());
+}
+
+// probe_copy_waves over `bytes` (multiple of 16) with `blocks` workgroups of
+// 256 lanes: host -> device or device -> host by CU loads / stores.
+extern "C" int mxprobe_copy_waves(void* dst, const void* src, uint64_t bytes, int blocks, void* stream) {
+    if ((bytes & 15) || blocks < 1 || ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15))
+        return int(hipErrorInvalidValue);
+    hipLaunchKernelGGL(probe_copy_waves, dim3(uint32_t(blocks)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), bytes / 16);
     return int(hipGetLastError());
 }
 

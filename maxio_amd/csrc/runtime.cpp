@@ -126,6 +126,16 @@ bool pinned_range(const void* p, uint64_t len) {
     return hip_says_pinned(p) && hip_says_pinned(static_cast<const uint8_t*>(p) + len - 1);
 }
 
+bool pinned_mapped(const void* p, uint64_t len) {
+    if (!p || !len) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(g_pinned_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return a - it->first < it->second && len <= it->second - (a - it->first);
+}
+
 int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
     if (slot.owner) {
         const void* b = dev_base;

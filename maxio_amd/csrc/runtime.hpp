@@ -153,6 +153,10 @@ void pinned_register(const void* p, size_t n);
 void pinned_unregister(const void* p);
 // True when every byte of [p, p + len) is page-locked host memory.
 bool pinned_range(const void* p, uint64_t len);
+// True when [p, p + len) lies in one mxec_host_alloc allocation: page-locked
+// and mapped into every GPU's address space at its host address, so kernels
+// may load and store it directly (copy_kernel.hip).
+bool pinned_mapped(const void* p, uint64_t len);
 
 // Online choice between two grid sizes for the large uniform RS launches
 // of one shape (ops.cpp rs_grid_pick): which of them runs faster depends on
