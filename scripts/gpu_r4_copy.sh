@@ -17,4 +17,9 @@ BENCH_GET_AFTER_SLEEP=10 MXEC_LIB=$LAB MXEC_PIPE_TRACE=1 timeout -k 10 400 pytho
   > "$O/bench_sleep10.json" 2> "$O/bench_sleep10.err" || { tail -20 "$O/bench_sleep10.err"; exit 1; }
 timeout -k 10 300 python tools/host_copy_lab.py > "$O/host_copy_lab.jsonl" 2> "$O/host_copy_lab.err" \
   || { tail -20 "$O/host_copy_lab.err"; exit 1; }
+# back-to-back processes: the headline right after a process that freed ~64 GB,
+# then again after a 30 s pause (is "slow mode" the driver clearing freed VRAM?)
+timeout -k 10 200 python bench.py --no-extra --no-e2e --cpu-seconds 0 > "$O/bench_b2b_1.json" 2> "$O/bench_b2b_1.err" || exit 1
+sleep 30
+timeout -k 10 200 python bench.py --no-extra --no-e2e --cpu-seconds 0 > "$O/bench_b2b_2.json" 2> "$O/bench_b2b_2.err" || exit 1
 echo done
