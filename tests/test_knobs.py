@@ -72,3 +72,14 @@ def test_product_library_has_only_default_kernel_instantiations():
     sha = {k for k in ks if "sha256_" in k}
     assert not any("sha256_quad_kernel<true, false>" in k or "sha256_quad_kernel<false" in k for k in sha), sha
     assert not any("sha256_split_kernel<2>" in k for k in sha), sha
+
+
+def test_entry_point_count_matches_the_docs():
+    """DESIGN.md and INTEGRATION.md state how many functions the header
+    declares (the counts had drifted apart)."""
+    hdr = open(os.path.join(ROOT, "include", "maxio_ec.h")).read()
+    n = len(set(re.findall(r"\b(mxec_[a-z_0-9]+)\s*\(", hdr)))
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    integ = open(DOC).read()
+    assert f"{n} entry points" in design and f"{n} functions" in design, n
+    assert f"header's {n} functions" in integ, n
