@@ -168,9 +168,29 @@ struct PipeRes {
         if (ready) return MXEC_OK;
         desc_slot.owner = &dev;
         arena.owner = &dev;
-        MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
-        MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
-        for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        if (dev.kn && dev.kn->pipe_copy == 1) {
+            // Wave copies (MXEC_PIPE_COPY=waves): the copy streams get a few
+            // CUs spread over the chip and the compute streams the rest, so
+            // copy waves never share a SIMD with a latency-bound SHA-256
+            // chain (the chains slowed 50 % beside unmasked copy waves).
+            const int n = dev.n_cus > 0 ? dev.n_cus : 256;
+            int copy_cus = 32;
+#ifdef MXEC_LAB
+            if (const char* e = getenv("MXEC_PIPE_COPY_CUS")) copy_cus = atoi(e);  // lab
+#endif
+            copy_cus = std::max(1, std::min(copy_cus, n / 2));
+            const int every = n / copy_cus;
+            std::vector<uint32_t> cm(size_t((n + 31) / 32), 0u), rm(cm.size(), 0u);
+            for (int i = 0; i < n; ++i)
+                ((i % every == every - 1 && i / every < copy_cus) ? cm : rm)[size_t(i / 32)] |= 1u << (i % 32);
+            MXEC_HIP(hipExtStreamCreateWithCUMask(&h2d, uint32_t(cm.size()), cm.data()));
+            MXEC_HIP(hipExtStreamCreateWithCUMask(&d2h, uint32_t(cm.size()), cm.data()));
+            for (auto& s : cs) MXEC_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(rm.size()), rm.data()));
+        } else {
+            MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+            MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+            for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        }
         affinity_tag(h2d, &dev);
         affinity_tag(d2h, &dev);
         for (auto s : cs) affinity_tag(s, &dev);

@@ -405,10 +405,10 @@ def test_host_alloc_buffers_copy_modes(ctx_with, copy):
     ref_d, ref_p = data.copy(), par.copy()
     present = np.ones((n, k + m), np.uint8)
     for o in range(n):
-        for i in rng.choice(k + m, 2, replace=False):
+        for i in rng.choice(k + m, 1 if o == 2 else 2, replace=False):
             present[o, i] = 0
             (data[o, i] if i < k else par[o, i - k])[:] = 0x5A
-    # one present shard silently corrupted in object 2: caught, rebuilt
+    # object 2 (one erasure): a present shard silently corrupted, caught, rebuilt
     c = int(np.flatnonzero(present[2])[0])
     (data[2, c] if c < k else par[2, c - k])[77] ^= 1
     sptr, slen = [], []
