@@ -168,6 +168,21 @@ struct PipeRes {
         if (ready) return MXEC_OK;
         desc_slot.owner = &dev;
         arena.owner = &dev;
+#ifdef MXEC_LAB
+        // MXEC_PIPE_COPY_PRIO (lab, waves mode): 1 = the copy streams at the
+        // highest priority, 2 = the compute streams at it (a hardware queue
+        // of their own either way), no CU masks.
+        const char* pe = getenv("MXEC_PIPE_COPY_PRIO");
+        const int prio_mode = dev.kn && dev.kn->pipe_copy == 1 && pe ? atoi(pe) : 0;
+        if (prio_mode == 1 || prio_mode == 2) {
+            int least = 0, greatest = 0;
+            MXEC_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            const int pc = prio_mode == 1 ? greatest : least, pk = prio_mode == 2 ? greatest : least;
+            MXEC_HIP(hipStreamCreateWithPriority(&h2d, hipStreamNonBlocking, pc));
+            MXEC_HIP(hipStreamCreateWithPriority(&d2h, hipStreamNonBlocking, pc));
+            for (auto& s : cs) MXEC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pk));
+        } else
+#endif
         if (dev.kn && dev.kn->pipe_copy == 1) {
             // Wave copies (MXEC_PIPE_COPY=waves): the copy streams get a few
             // CUs spread over the chip and the compute streams the rest, so
@@ -638,7 +653,10 @@ private:
         char* d = nullptr;
         MXEC_TRY(arena_.take(bytes, &h, &d));
         std::memcpy(h, v.data(), v.size() * sizeof(CopyBlk));
-        const uint32_t grid = kCopyGrid;
+        uint32_t grid = kCopyGrid;
+#ifdef MXEC_LAB
+        if (const char* e = getenv("MXEC_PIPE_COPY_GRID")) grid = uint32_t(atoi(e));  // lab
+#endif
         MXEC_HIP(launch_copy_blocks(reinterpret_cast<const CopyBlk*>(h), v.size(), to_host, grid, s));
         v.clear();
         return MXEC_OK;
