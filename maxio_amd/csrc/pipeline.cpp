@@ -173,7 +173,7 @@ struct PipeRes {
         // highest priority, 2 = the compute streams at it (a hardware queue
         // of their own either way), no CU masks.
         const char* pe = getenv("MXEC_PIPE_COPY_PRIO");
-        const int prio_mode = dev.kn && dev.kn->pipe_copy == 1 && pe ? atoi(pe) : 0;
+        const int prio_mode = dev.kn && dev.kn->pipe_copy != 0 && pe ? atoi(pe) : 0;
         if (prio_mode == 1 || prio_mode == 2) {
             int least = 0, greatest = 0;
             MXEC_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -183,7 +183,7 @@ struct PipeRes {
             for (auto& s : cs) MXEC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pk));
         } else
 #endif
-        if (dev.kn && dev.kn->pipe_copy == 1) {
+        if (dev.kn && dev.kn->pipe_copy != 0) {
             // Wave copies (MXEC_PIPE_COPY=waves): the copy streams get a few
             // CUs spread over the chip and the compute streams the rest, so
             // copy waves never share a SIMD with a latency-bound SHA-256
@@ -636,8 +636,10 @@ private:
     // CU-wave copy launches (copy_kernel.hip) instead of SDMA DMAs; they are
     // collected here and issued as one launch at the next point the stream
     // is waited on or marked (issue_up / issue_down).
-    bool wave_copy(const void* host, uint64_t len) const {
-        return d_.kn && d_.kn->pipe_copy == 1 && pinned_mapped(host, len);
+    bool wave_copy(const void* host, uint64_t len, bool up) const {
+        if (!d_.kn || d_.kn->pipe_copy == 0) return false;
+        if (d_.kn->pipe_copy == 1 && !up) return false;  // waves: uploads only
+        return pinned_mapped(host, len);
     }
     static void add_blocks(std::vector<CopyBlk>& v, uint8_t* dst, const uint8_t* src, uint64_t len) {
         for (uint64_t o = 0; o < len; o += kCopyBlock)
@@ -672,7 +674,7 @@ private:
             const void* p = dst;
             MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload", &arena_, &p, 1));
         }
-        if (wave_copy(src, len)) {
+        if (wave_copy(src, len, true)) {
             add_blocks(up_blks_, dst, src, len);
             return MXEC_OK;
         }
@@ -804,7 +806,7 @@ private:
             const void* p = src;
             MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download", &arena_, &p, 1));
         }
-        if (wave_copy(dst, len)) {
+        if (wave_copy(dst, len, false)) {
             add_blocks(down_blks_, dst, src, len);
             return MXEC_OK;
         }
