@@ -67,7 +67,7 @@ Knobs read_knobs() {
     const long piece = env_long("MXEC_PIPE_PIECE_MB", 1);
     k.pipe_piece = piece <= 0 ? 0 : uint64_t(std::min(piece, 1L << 20)) << 20;
     if (const char* c = env("MXEC_PIPE_COPY"))
-        k.pipe_copy = !std::strcmp(c, "waves") ? 1 : !std::strcmp(c, "waves2") ? 2 : 0;
+        k.pipe_copy = !std::strcmp(c, "sdma") ? 0 : !std::strcmp(c, "waves") ? 1 : 2;
     if (const char* w = env("MXEC_GET_WINDOW")) k.get_window = std::max<uint64_t>(1, std::strtoull(w, nullptr, 10));
     k.gather_us = env_long("MXEC_GATHER_US", k.gather_us);
     k.gather_max_us = env_long("MXEC_GATHER_MAX_US", k.gather_max_us);

@@ -26,8 +26,9 @@ struct Knobs {
     int sha_form = 0;              // MXEC_SHA_FORM: 0 auto, 1 one, 2 split, 3 stream, 6 lagpair
     int desc_upload = 1;           // MXEC_DESC_UPLOAD: 0 inline, 1 auto, 2 side stream
     uint64_t pipe_piece = uint64_t(1) << 20;  // MXEC_PIPE_PIECE_MB (0: whole chunks)
-    int pipe_copy = 0;             // MXEC_PIPE_COPY: 0 sdma (hipMemcpyAsync); 1 waves: uploads by
-                                   //   copy_kernel.hip; 2 waves2: both directions
+    int pipe_copy = 2;             // MXEC_PIPE_COPY: 0 sdma (hipMemcpyAsync); 1 waves (copy_kernel.hip
+                                   //   for every host batch); 2 auto: reconstruct batches by waves,
+                                   //   encode batches by SDMA
     uint64_t get_window = uint64_t(1) << 30;  // MXEC_GET_WINDOW: bytes of chunks per GET window
     long gather_us = 100;          // MXEC_GATHER_US
     long gather_max_us = 2000;     // MXEC_GATHER_MAX_US

@@ -168,12 +168,29 @@ struct PipeRes {
         if (ready) return MXEC_OK;
         desc_slot.owner = &dev;
         arena.owner = &dev;
+        MXEC_TRY(create_streams(dev));
+        affinity_tag(h2d, &dev);
+        affinity_tag(d2h, &dev);
+        for (auto s : cs) affinity_tag(s, &dev);
+        MXEC_TRY(in.init());
+        MXEC_TRY(out.init());
+        ready = true;
+        return MXEC_OK;
+    }
+    // With wave copies possible (MXEC_PIPE_COPY waves / auto), the copy
+    // streams get 32 CUs spread over the chip and the compute streams the
+    // rest, so copy waves never share a SIMD with a latency-bound SHA-256
+    // chain; with SDMA only, plain streams.
+    int create_streams(const Device& dev) {
+        const bool waves = dev.kn && dev.kn->pipe_copy != 0;
+        int copy_cus = waves ? 32 : 0;
 #ifdef MXEC_LAB
-        // MXEC_PIPE_COPY_PRIO (lab, waves mode): 1 = the copy streams at the
-        // highest priority, 2 = the compute streams at it (a hardware queue
-        // of their own either way), no CU masks.
+        // Lab: MXEC_PIPE_COPY_CUS (0: no masks); MXEC_PIPE_COPY_PRIO 1 = the
+        // copy streams at the highest priority, 2 = the compute streams at
+        // it (a hardware queue of their own either way), no masks.
+        if (const char* e = getenv("MXEC_PIPE_COPY_CUS"); e && waves) copy_cus = atoi(e);
         const char* pe = getenv("MXEC_PIPE_COPY_PRIO");
-        const int prio_mode = dev.kn && dev.kn->pipe_copy != 0 && pe ? atoi(pe) : 0;
+        const int prio_mode = waves && pe ? atoi(pe) : 0;
         if (prio_mode == 1 || prio_mode == 2) {
             int least = 0, greatest = 0;
             MXEC_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -181,19 +198,12 @@ struct PipeRes {
             MXEC_HIP(hipStreamCreateWithPriority(&h2d, hipStreamNonBlocking, pc));
             MXEC_HIP(hipStreamCreateWithPriority(&d2h, hipStreamNonBlocking, pc));
             for (auto& s : cs) MXEC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pk));
-        } else
+            return MXEC_OK;
+        }
 #endif
-        if (dev.kn && dev.kn->pipe_copy != 0) {
-            // Wave copies (MXEC_PIPE_COPY=waves): the copy streams get a few
-            // CUs spread over the chip and the compute streams the rest, so
-            // copy waves never share a SIMD with a latency-bound SHA-256
-            // chain (the chains slowed 50 % beside unmasked copy waves).
-            const int n = dev.n_cus > 0 ? dev.n_cus : 256;
-            int copy_cus = 32;
-#ifdef MXEC_LAB
-            if (const char* e = getenv("MXEC_PIPE_COPY_CUS")) copy_cus = atoi(e);  // lab
-#endif
-            copy_cus = std::max(1, std::min(copy_cus, n / 2));
+        const int n = dev.n_cus > 0 ? dev.n_cus : 256;
+        copy_cus = std::min(copy_cus, n / 2);
+        if (copy_cus > 0) {
             const int every = n / copy_cus;
             std::vector<uint32_t> cm(size_t((n + 31) / 32), 0u), rm(cm.size(), 0u);
             for (int i = 0; i < n; ++i)
@@ -201,17 +211,11 @@ struct PipeRes {
             MXEC_HIP(hipExtStreamCreateWithCUMask(&h2d, uint32_t(cm.size()), cm.data()));
             MXEC_HIP(hipExtStreamCreateWithCUMask(&d2h, uint32_t(cm.size()), cm.data()));
             for (auto& s : cs) MXEC_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(rm.size()), rm.data()));
-        } else {
-            MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
-            MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
-            for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            return MXEC_OK;
         }
-        affinity_tag(h2d, &dev);
-        affinity_tag(d2h, &dev);
-        for (auto s : cs) affinity_tag(s, &dev);
-        MXEC_TRY(in.init());
-        MXEC_TRY(out.init());
-        ready = true;
+        MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+        MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+        for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         return MXEC_OK;
     }
     ~PipeRes() {
@@ -296,7 +300,15 @@ public:
         for (auto e : events_) (void)hipEventDestroy(e);
     }
 
+    // MXEC_PIPE_COPY (knobs.hpp): sdma; waves (every host batch); auto (the
+    // default) -- host reconstruct batches by waves, host encode batches by
+    // SDMA.  Measured (profiles/r4/get_stall/): the verified GET 0.263 s by
+    // waves against 0.268 by SDMA, and 0.263 against [0.33, 0.92, 0.33,
+    // 0.92, 0.27] s after the bench's extras (SDMA copies collapse for
+    // seconds there); the PUT with digests 0.264 by waves against 0.218 by
+    // SDMA (copy waves beside the SHA-256 chains slow the chains).
     int run(std::vector<HostObj>& objs) {
+        waves_now_ = d_.kn && d_.kn->pipe_copy == 1;  // encode: waves only when asked for
         size_t o = 0;
         while (o < objs.size()) {  // waves that fit the pool
             uint64_t need = 0, desc = 1 << 20;
@@ -317,6 +329,7 @@ public:
 
     // Host reconstruct batch: waves that fit the pool, as run().
     int run_rec(std::vector<RecObj>& objs, bool data_only) {
+        waves_now_ = d_.kn && d_.kn->pipe_copy != 0;  // reconstruct: waves by default (auto)
         size_t o = 0;
         while (o < objs.size()) {
             uint64_t need = 0, desc = 1 << 20;
@@ -632,15 +645,13 @@ private:
         return MXEC_OK;
     }
 
-    // MXEC_PIPE_COPY=waves: copies from / to mxec_host_alloc memory go as
-    // CU-wave copy launches (copy_kernel.hip) instead of SDMA DMAs; they are
-    // collected here and issued as one launch at the next point the stream
-    // is waited on or marked (issue_up / issue_down).
-    bool wave_copy(const void* host, uint64_t len, bool up) const {
-        if (!d_.kn || d_.kn->pipe_copy == 0) return false;
-        if (d_.kn->pipe_copy == 1 && !up) return false;  // waves: uploads only
-        return pinned_mapped(host, len);
-    }
+    // Wave copies (MXEC_PIPE_COPY, run / run_rec): copies from / to
+    // mxec_host_alloc memory go as CU-wave copy launches (copy_kernel.hip)
+    // instead of SDMA DMAs; they are collected here and issued as one launch
+    // at the next point the stream is waited on or marked (issue_up /
+    // issue_down).
+    bool wave_copy(const void* host, uint64_t len) const { return waves_now_ && pinned_mapped(host, len); }
+    bool waves_now_ = false;  // this call's copies of mxec_host_alloc memory go by waves
     static void add_blocks(std::vector<CopyBlk>& v, uint8_t* dst, const uint8_t* src, uint64_t len) {
         for (uint64_t o = 0; o < len; o += kCopyBlock)
             v.push_back(CopyBlk{reinterpret_cast<uint64_t>(dst + o), reinterpret_cast<uint64_t>(src + o),
@@ -666,7 +677,10 @@ private:
     int issue_up() { return issue_blocks(up_blks_, false, h2d_); }
     int issue_down() { return issue_blocks(down_blks_, true, d2h_); }
     std::vector<CopyBlk> up_blks_, down_blks_;
-    static constexpr uint32_t kCopyGrid = 128;  // workgroups per copy launch
+    // Workgroups per copy launch: few, so the copy's host loads in flight do
+    // not queue ahead of the SHA-256 chains' HBM loads (128 slowed the chains
+    // 5x; 16 moves 57 GB/s alone and left the verified GET's chains alone).
+    static constexpr uint32_t kCopyGrid = 16;
 
     int upload(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
@@ -674,7 +688,7 @@ private:
             const void* p = dst;
             MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload", &arena_, &p, 1));
         }
-        if (wave_copy(src, len, true)) {
+        if (wave_copy(src, len)) {
             add_blocks(up_blks_, dst, src, len);
             return MXEC_OK;
         }
@@ -806,7 +820,7 @@ private:
             const void* p = src;
             MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download", &arena_, &p, 1));
         }
-        if (wave_copy(dst, len, false)) {
+        if (wave_copy(dst, len)) {
             add_blocks(down_blks_, dst, src, len);
             return MXEC_OK;
         }

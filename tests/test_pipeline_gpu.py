@@ -371,11 +371,12 @@ def test_batch_host_pieces_descriptor_tables_outgrow_first_block(ctx):
         assert digests[o * 64 + 32:o * 64 + 64].tobytes() == hashlib.sha256(outs[o].tobytes()).digest(), o
 
 
-@pytest.mark.parametrize("copy", ["waves", "sdma"])
+@pytest.mark.parametrize("copy", ["auto", "waves", "sdma"])
 def test_host_alloc_buffers_copy_modes(ctx_with, copy):
     """mxec_host_alloc buffers (mapped into the GPU's address space) through
-    the host batch calls with MXEC_PIPE_COPY=waves (CU-wave copy kernels,
-    copy_kernel.hip) and =sdma: a PUT with digests in pieces, shards off the
+    the host batch calls with MXEC_PIPE_COPY=auto (the default: the GET by
+    CU-wave copy kernels, copy_kernel.hip, the PUT by SDMA), =waves (both by
+    waves) and =sdma: a PUT with digests in pieces, shards off the
     piece grid and short last chunks, then a verified GET with two erasures
     per object and one corrupted present shard -- parity, digests and the
     rebuilt shards equal to the oracle / the originals in both modes."""
