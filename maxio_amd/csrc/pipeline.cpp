@@ -177,18 +177,15 @@ struct PipeRes {
         ready = true;
         return MXEC_OK;
     }
-    // With wave copies possible (MXEC_PIPE_COPY waves / auto), the copy
-    // streams get 32 CUs spread over the chip and the compute streams the
-    // rest, so copy waves never share a SIMD with a latency-bound SHA-256
-    // chain; with SDMA only, plain streams.
+    // Plain non-blocking streams.  Lab builds can put the copy streams on a
+    // few masked CUs and the compute streams on the rest
+    // (MXEC_PIPE_COPY_CUS = n; measured no different from unmasked at the
+    // wave copies' 16 workgroups, profiles/r4/get_stall/) or at different
+    // priorities (MXEC_PIPE_COPY_PRIO 1 = copies highest, 2 = compute).
     int create_streams(const Device& dev) {
-        const bool waves = dev.kn && dev.kn->pipe_copy != 0;
-        int copy_cus = waves ? 32 : 0;
 #ifdef MXEC_LAB
-        // Lab: MXEC_PIPE_COPY_CUS (0: no masks); MXEC_PIPE_COPY_PRIO 1 = the
-        // copy streams at the highest priority, 2 = the compute streams at
-        // it (a hardware queue of their own either way), no masks.
-        if (const char* e = getenv("MXEC_PIPE_COPY_CUS"); e && waves) copy_cus = atoi(e);
+        const bool waves = dev.kn && dev.kn->pipe_copy != 0;
+        const char* ce = getenv("MXEC_PIPE_COPY_CUS");
         const char* pe = getenv("MXEC_PIPE_COPY_PRIO");
         const int prio_mode = waves && pe ? atoi(pe) : 0;
         if (prio_mode == 1 || prio_mode == 2) {
@@ -200,9 +197,8 @@ struct PipeRes {
             for (auto& s : cs) MXEC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pk));
             return MXEC_OK;
         }
-#endif
         const int n = dev.n_cus > 0 ? dev.n_cus : 256;
-        copy_cus = std::min(copy_cus, n / 2);
+        const int copy_cus = waves && ce ? std::min(atoi(ce), n / 2) : 0;
         if (copy_cus > 0) {
             const int every = n / copy_cus;
             std::vector<uint32_t> cm(size_t((n + 31) / 32), 0u), rm(cm.size(), 0u);
@@ -213,6 +209,9 @@ struct PipeRes {
             for (auto& s : cs) MXEC_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(rm.size()), rm.data()));
             return MXEC_OK;
         }
+#else
+        (void)dev;
+#endif
         MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
         MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
         for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
