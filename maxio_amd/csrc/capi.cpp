@@ -22,6 +22,12 @@ using namespace mxec;
 
 namespace {
 
+// MXEC_PIPE_COPY (knobs.hpp): whether a host-pointer call's copies of
+// mxec_host_alloc memory may go by CU-wave copy kernels -- the reconstruct /
+// hash (GET) paths under auto and waves, the encode (PUT) path under waves
+// only (pipeline.cpp has the measurements behind the split).
+bool copy_waves_get(const Device& d) { return d.kn && d.kn->pipe_copy != 0; }
+bool copy_waves_put(const Device& d) { return d.kn && d.kn->pipe_copy == 1; }
 
 // One object of a device-resident reconstruct batch (device shard pointers).
 struct BatchObj {
@@ -362,7 +368,7 @@ int mxec_sha256_batch(mxec_ctx* ctx, const uint8_t* const* bufs, const size_t* l
             ptrs[i] = base + off[i];
             l[i] = lens[i];
         }
-        MXEC_TRY(upload_segments(slot, s, base, segs));
+        MXEC_TRY(upload_segments(slot, s, base, segs, copy_waves_get(*ds.d)));
         MXEC_TRY(slot_wait(slot, s));  // uploads done: the combiner hashes on its own stream
         return sha256_combined(*ds.d, slot, s, ptrs, l, &out[0][0]);
     });
@@ -395,7 +401,7 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* c
             in[size_t(j)] = base + sa * uint64_t(j);
             if (len[size_t(j)]) up.push_back({sa * uint64_t(j), data[j], len[size_t(j)]});
         }
-        MXEC_TRY(upload_segments(slot, s, base, up));
+        MXEC_TRY(upload_segments(slot, s, base, up, copy_waves_put(*ds.d)));
         for (int i = 0; i < m; ++i) out[size_t(i)] = base + sa * uint64_t(k + i);
         uint32_t off = 0;
         MXEC_TRY(with_stable_coef(
@@ -406,7 +412,7 @@ int mxec_encode(mxec_ctx* ctx, int k, int m, size_t shard_size, const uint8_t* c
             }));
         std::vector<DownloadSeg> down;
         for (int i = 0; i < m; ++i) down.push_back({sa * uint64_t(k + i), parity[i], shard_size});
-        MXEC_TRY(download_segments(slot, s, base, down));
+        MXEC_TRY(download_segments(slot, s, base, down, copy_waves_put(*ds.d)));
         if (sha256_out) {
             // write_chunk / compute_and_write_parity digests (filesystem.rs:1070,
             // :1131), combined with every concurrent caller's verification work.
@@ -451,7 +457,7 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
             sl.push_back(len[size_t(i)]);
             si.push_back(i);
         }
-        MXEC_TRY(upload_segments(slot, s, base, up));
+        MXEC_TRY(upload_segments(slot, s, base, up, copy_waves_get(*ds.d)));
         if (expected_sha256 && !sp.empty()) {
             // chunk_reader.rs:176-196: hash every present shard; mismatch -> erasure.
             MXEC_TRY(slot_wait(slot, s));
@@ -498,7 +504,7 @@ int mxec_reconstruct(mxec_ctx* ctx, int k, int m, size_t shard_size, uint8_t* co
             for (size_t t = 0; t < out.size(); ++t)
                 if (out_len[t]) down.push_back({sa * uint64_t(plan->missing[t]), shards[plan->missing[t]], out_len[t]});
             // plan->missing is ascending, so are the offsets.
-            MXEC_TRY(download_segments(slot, s, base, down));
+            MXEC_TRY(download_segments(slot, s, base, down, copy_waves_get(*ds.d)));
             for (int e : plan->missing) present[size_t(e)] = 1;
         } else {
             // Nothing to rebuild: the uploads may still be reading the

@@ -1,6 +1,8 @@
 // runtime.cpp — device buffers, descriptor rings, coefficient arena.
 #include "runtime.hpp"
 
+#include "kernels.hpp"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -136,12 +138,43 @@ bool pinned_mapped(const void* p, uint64_t len) {
     return a - it->first < it->second && len <= it->second - (a - it->first);
 }
 
-int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs) {
+namespace {
+// The segments as CU-wave copy blocks, the table read in place from the
+// slot's descriptor ring (copy_kernel.hip; 16 workgroups, as pipeline.cpp).
+int wave_copy_segments(Slot& slot, hipStream_t s, const std::vector<CopyBlk>& blks, bool to_host) {
+    if (blks.empty()) return MXEC_OK;
+    DescWriter w(slot);
+    const size_t o = w.add(sizeof(CopyBlk) * blks.size());
+    std::memcpy(w.data() + o, blks.data(), sizeof(CopyBlk) * blks.size());
+    char* hb = nullptr;
+    MXEC_TRY(w.commit_host(&hb));
+    MXEC_HIP(launch_copy_blocks(reinterpret_cast<const CopyBlk*>(hb + o), blks.size(), to_host, 16, s));
+    return w.finish(s);
+}
+void add_blocks(std::vector<CopyBlk>& v, uint64_t dst, uint64_t src, uint64_t len) {
+    for (uint64_t o = 0; o < len; o += kCopyBlock) v.push_back(CopyBlk{dst + o, src + o, std::min(kCopyBlock, len - o), 0});
+}
+}  // namespace
+
+int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs, bool waves) {
     if (slot.owner) {
         const void* b = dev_base;
         MXEC_TRY(affinity_check(*slot.owner, &slot, s, "upload_segments", nullptr, &b, 1));
     }
     if (segs.empty()) return MXEC_OK;
+    if (waves) {
+        bool mapped = true;
+        for (const auto& g : segs) mapped = mapped && (g.len == 0 || pinned_mapped(g.src, g.len));
+        if (mapped) {
+            std::vector<CopyBlk> blks;
+            for (const auto& g : segs)
+                if (g.len)
+                    add_blocks(blks, reinterpret_cast<uint64_t>(dev_base + g.dst_off), reinterpret_cast<uint64_t>(g.src),
+                               g.len);
+            slot.borrowed = s;  // the kernel reads the caller's buffers: wait before returning
+            return wave_copy_segments(slot, s, blks, false);
+        }
+    }
     bool all_pinned = true;
     for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.src, g.len));
     if (all_pinned) {  // DMA straight from the caller's page-locked buffers
@@ -193,12 +226,26 @@ int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vec
     return MXEC_OK;
 }
 
-int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs) {
+int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs,
+                      bool waves) {
     if (slot.owner) {
         const void* b = dev_base;
         MXEC_TRY(affinity_check(*slot.owner, &slot, s, "download_segments", nullptr, &b, 1));
     }
     if (segs.empty()) return slot_wait(slot, s);
+    if (waves) {
+        bool mapped = true;
+        for (const auto& g : segs) mapped = mapped && (g.len == 0 || pinned_mapped(g.dst, g.len));
+        if (mapped) {
+            std::vector<CopyBlk> blks;
+            for (const auto& g : segs)
+                if (g.len)
+                    add_blocks(blks, reinterpret_cast<uint64_t>(g.dst), reinterpret_cast<uint64_t>(dev_base + g.src_off),
+                               g.len);
+            MXEC_TRY(wave_copy_segments(slot, s, blks, true));
+            return slot_wait(slot, s);
+        }
+    }
     bool all_pinned = true;
     for (const auto& g : segs) all_pinned = all_pinned && (g.len == 0 || pinned_range(g.dst, g.len));
     if (all_pinned) {  // DMA straight into the caller's page-locked buffers
@@ -321,6 +368,21 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
         MXEC_HIP(hipStreamWaitEvent(stream, buf_->uploaded, 0));
     }
     *dev_base = static_cast<char*>(buf_->dev.p);
+    return MXEC_OK;
+}
+
+int DescWriter::commit_host(char** host_base) {
+    if (arena_) return set_error(MXEC_E_INVALID_ARG, "commit_host: slot ring only");
+    buf_ = &slot_.ring[slot_.ring_next];
+    slot_.ring_next = (slot_.ring_next + 1) % Slot::kRing;
+    if (!buf_->done) MXEC_HIP(hipEventCreateWithFlags(&buf_->done, hipEventDisableTiming));
+    if (buf_->pending) {
+        MXEC_HIP(hipEventSynchronize(buf_->done));
+        buf_->pending = false;
+    }
+    MXEC_TRY(buf_->host.grow(tmp_.empty() ? 16 : tmp_.size()));
+    std::memcpy(buf_->host.p, tmp_.data(), tmp_.size());
+    *host_base = static_cast<char*>(buf_->host.p);
     return MXEC_OK;
 }
 

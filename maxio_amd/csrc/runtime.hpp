@@ -133,7 +133,11 @@ constexpr uint64_t kStagePiece = uint64_t(8) << 20;
 // call must wait on `s` before it returns to its caller (slot_wait, or the
 // DevScope destructor on an early error return).  Segments must be sorted by
 // dst_off and not overlap.
-int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs);
+// waves: segments wholly inside mxec_host_alloc memory may move by a CU-wave
+// copy kernel (copy_kernel.hip) instead of SDMA (the host reconstruct and
+// hash paths, MXEC_PIPE_COPY auto / waves; pipeline.cpp has the measurements).
+int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vector<UploadSeg>& segs,
+                    bool waves = false);
 // One device -> host download segment: len bytes from src_off to dst.
 struct DownloadSeg {
     uint64_t src_off;
@@ -143,7 +147,8 @@ struct DownloadSeg {
 // The reverse of upload_segments, through the same pinned pair; returns when
 // every byte has landed (waits for everything enqueued on `s` before it,
 // too).  Segments sorted by src_off, not overlapping.
-int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs);
+int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const std::vector<DownloadSeg>& segs,
+                      bool waves = false);
 
 // Page-locked host ranges.  mxec_host_alloc registers its allocations so the
 // copy paths recognise them without a hipPointerGetAttributes call per
@@ -314,6 +319,10 @@ public:
     char* data() { return tmp_.data(); }
     // Upload; dev_base receives the device base to add offsets to.
     int commit(hipStream_t stream, char** dev_base);
+    // No upload: the tables stay in the ring entry's page-locked host buffer
+    // (mapped into the GPU's address space), which kernels read in place;
+    // host_base receives that buffer.  Slot ring only.
+    int commit_host(char** host_base);
     // Device scratch of `bytes` that lives as long as this launch's tables
     // (the ring entry is not reused before finish()'s event): after commit,
     // slot ring only (not with an arena).

@@ -424,3 +424,45 @@ def test_host_alloc_buffers_copy_modes(ctx_with, copy):
             assert np.array_equal(data[o, j, :dl[j]], ref_d[o, j, :dl[j]]), (copy, o, j)
         assert np.array_equal(par[o], ref_p[o]), (copy, o)
     assert hashlib.sha256(data[n - 1, 0].tobytes()).digest() == dig[(n - 1) * (k + m) * 32:][:32].tobytes()
+
+
+@pytest.mark.parametrize("copy", ["auto", "sdma"])
+def test_single_request_calls_on_host_alloc_buffers(ctx_with, copy):
+    """The single-request entry points with mxec_host_alloc buffers: under
+    MXEC_PIPE_COPY=auto the hash and reconstruct calls move them by CU-wave
+    copy kernels (runtime.cpp upload_segments / download_segments), under
+    sdma by DMAs.  mxec_sha256_batch against hashlib (odd lengths and
+    offsets); mxec_reconstruct with verification, two erasures and one
+    corrupted shard, rebuilt in place in the caller's page-locked shards."""
+    import ctypes
+    import hashlib
+
+    import maxio_amd.ec as E
+
+    ctx = ctx_with(MXEC_PIPE_COPY=copy)
+    rng = np.random.default_rng(93)
+    blob = ctx.host_array(3 << 20)
+    blob[:] = rng.integers(0, 256, blob.size, dtype=np.uint8)
+    cuts = [(0, 0), (5, 1000), (4096, 1 << 20), (17, (1 << 20) + 333), (2 << 20, 64)]
+    got = ctx.sha256([blob[o:o + n] for o, n in cuts])
+    assert got == [hashlib.sha256(blob[o:o + n].tobytes()).digest() for o, n in cuts]
+    k, m, S = 8, 4, (1 << 20) + 48
+    sh = ctx.host_array((k + m) * S).reshape(k + m, S)
+    sh[:k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    par, dig = ctx.encode([sh[j] for j in range(k)], m, S)
+    for i in range(m):
+        sh[k + i] = par[i]
+    ref = sh.copy()
+    present = np.ones(k + m, np.uint8)
+    for i in (1, 9):
+        present[i] = 0
+        sh[i] = 0x33
+    sh[4, 100] ^= 0x10  # silent corruption: caught by the digest, rebuilt
+    exp = np.frombuffer(b"".join(dig), np.uint8).copy()
+    npres = ctypes.c_int(0)
+    lens = (ctypes.c_size_t * (k + m))(*([S] * (k + m)))
+    rc = ctx._lib.mxec_reconstruct(ctx.handle, k, m, S, E._pp([sh[i].ctypes.data for i in range(k + m)]), lens,
+                                   exp.ctypes.data_as(E.N.U8P), present.ctypes.data_as(E.N.U8P), 0,
+                                   ctypes.byref(npres))
+    assert rc == 0 and present.all() and npres.value == k + m - 3
+    assert np.array_equal(sh, ref)
