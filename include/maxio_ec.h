@@ -121,7 +121,8 @@ int mxec_ctx_coef_stats(mxec_ctx* ctx, int dev, uint64_t* recycles, uint64_t* re
 /* Page-locked host memory for request bodies and GET buffers (the Axum body
  * MaxIO hands to a PUT, the buffer a GET fills).  Every host-pointer entry
  * point accepts any host memory; when a buffer comes from here, its bytes
- * move by DMA straight to and from the device instead of through the
+ * move straight to and from the device (by DMA, or by the GPU's own waves
+ * over PCIe, INTEGRATION.md MXEC_PIPE_COPY) instead of through the
  * library's pinned staging copy.  NULL on failure; free with
  * mxec_host_free. */
 void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes);

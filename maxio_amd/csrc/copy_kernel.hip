@@ -1,6 +1,7 @@
 // copy_kernel.hip — host <-> device copies by CU waves, for the host
-// pipeline (pipeline.cpp) when its copies must not queue behind other users
-// of the SDMA engines (MXEC_PIPE_COPY=waves).
+// pipeline (pipeline.cpp) and the single-request calls when their copies
+// must not queue behind other users of the SDMA engines (MXEC_PIPE_COPY:
+// reconstruct batches under the default `auto`, every batch under `waves`).
 //
 // The caller's page-locked buffers from mxec_host_alloc are mapped into the
 // GPU's address space at their host address, so a wave can load from /
