@@ -17,6 +17,12 @@ One JSON line per allocation.  Lab tool (needs `make lab`: the default is
 MXEC_LIB = the lab build, for MXEC_RS_BPC).
 
   python tools/placement_lab.py [--objects 256] [--allocs 8] [--grids 1024,512] [--reps 5]
+                                [--free-each --spacer-mib 0,4096,...]
+
+--free-each drops each batch before the next (full configs[1] batches, 74 GB,
+fit three at a time otherwise); --spacer-mib allocates a spacer of that many
+MiB (one value per allocation, cycled) ahead of each batch, so successive
+batches land at different places.
 """
 from __future__ import annotations
 
@@ -37,7 +43,10 @@ def main() -> int:
     ap.add_argument("--grids", default="1024,512")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--check", action="store_true", help="oracle-check object 0 after the rs timings")
+    ap.add_argument("--free-each", action="store_true", help="free each batch before allocating the next")
+    ap.add_argument("--spacer-mib", default="", help="comma list: MiB allocated ahead of each batch (cycled)")
     a = ap.parse_args()
+    spacers = [int(x) for x in a.spacer_mib.split(",") if x]
     import torch
 
     import bench
@@ -58,7 +67,13 @@ def main() -> int:
 
     bufs = []
     for ai in range(a.allocs):
+        if a.free_each:
+            bufs.clear()
+            torch.cuda.empty_cache()
+        spacer_mib = spacers[ai % len(spacers)] if spacers else 0
         try:
+            if spacer_mib:
+                bufs.append(torch.empty(spacer_mib << 20, dtype=torch.uint8, device=dev))
             obj = torch.empty((n, k + m, ss), dtype=torch.uint8, device=dev)
         except RuntimeError as e:  # out of memory: stop here
             print(json.dumps({"alloc": ai, "stopped": str(e)[:120]}), flush=True)
@@ -67,7 +82,8 @@ def main() -> int:
         obj[:, :k, :S].random_(0, 256)
         torch.cuda.synchronize()
         d0, p0, ost = obj.data_ptr(), obj[:, k:].data_ptr(), (k + m) * ss
-        row = {"alloc": ai, "objects": n, "base_mod_2MiB": d0 % (2 << 20)}
+        row = {"alloc": ai, "objects": n, "base_mod_2MiB": d0 % (2 << 20), "spacer_mib": spacer_mib,
+               "va_GiB": round(d0 / 2**30, 1)}
         for g in a.grids.split(","):
             os.environ["MXEC_RS_BPC"] = g
             ms = bench.event_ms(torch, st, lambda: ctx.encode_strided_device(
