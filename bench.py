@@ -789,7 +789,7 @@ def probe_lib():
 
 def event_ms(torch, stream, fn, reps: int, warm: int = 1) -> float:
     """Average HIP-event time of fn() on `stream` after `warm` untimed calls
-    (5 for RS launches: the grid tuner times launches 2-5 of a shape)."""
+    (7 for RS launches: the grid tuner times launches 2-7 of a shape)."""
     for _ in range(warm):
         fn()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
@@ -1037,7 +1037,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     # -- north star: encode k=8 m=4, 1 MiB, 4096 objects -------------------
     w = make_workload("ns", torch, ctx, dev, sh, 0, 0)
     torch.cuda.synchronize()
-    ms = event_ms(torch, stream, w.step, max(5, steps // 2), warm=5)
+    ms = event_ms(torch, stream, w.step, max(5, steps // 2), warm=7)
     ok = w.spot_check()
     same = pattern_on_buffers(torch, stream, w)
     f4_ns = float4_copy_on_buffers(torch, stream, w)
@@ -1062,7 +1062,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
     torch.cuda.empty_cache()
     # -- config 3: reconstruct 8+4, 2 erasures + verify, 1024 objects --------
     r = Reconstruct(torch, ctx, dev, sh, 1024, SEED)
-    ms_call = event_ms(torch, stream, r.step, 5, warm=5)
+    ms_call = event_ms(torch, stream, r.step, 5, warm=7)
     ok = r.spot_check()
     k, m, S, n = r.k, r.m, r.S, r.n
     present_ptrs, present_lens = [], []
@@ -1154,7 +1154,7 @@ def extras(ctx, torch, dev, stream, steps: int, cal: dict) -> dict:
                "RS encode k=4 m=2, 10 MiB chunks, 1024 objects, data [n][k][S] and parity [n][m][S] as two "
                "allocations (no pad)", SEED + 3, separate=True)
     torch.cuda.synchronize()
-    ms = event_ms(torch, stream, w.step, max(5, steps // 4), warm=5)
+    ms = event_ms(torch, stream, w.step, max(5, steps // 4), warm=7)
     ok = w.spot_check()
     same = pattern_on_buffers(torch, stream, w)
     f4 = float4_copy_on_buffers(torch, stream, w)  # over the data allocation
@@ -1563,8 +1563,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
-    # 5: the RS grid tuner times launches 2-5 of a shape (ops.cpp rs_grid_pick)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 7: the RS grid tuner times launches 2-7 of a shape (ops.cpp rs_grid_pick)
+    ap.add_argument("--warmup", type=int, default=7)
     ap.add_argument("--config", default="2", choices=["2", "3", "3c", "ns", "4a", "4b", "5", "sums", "frames"])
     ap.add_argument("--workers", type=int, default=8, help="config 3c: concurrent batches")
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")

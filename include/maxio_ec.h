@@ -105,7 +105,7 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages);
 /* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
  * (k inputs, m outputs, shard_size) at: the grid tuner times the first
- * launches of a shape at two grid sizes and keeps the faster one (which of
+ * launches of a shape at three grid sizes and keeps the fastest (which of
  * them wins depends on the box and on where the batch sits in HBM).  0 while
  * the shape is still being tuned; the default grid for shapes never launched
  * or too small to tune.  Diagnostics (the bench reports it). */

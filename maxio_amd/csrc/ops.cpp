@@ -205,9 +205,17 @@ bool tuning_on(const Device& dev) {
     return true;
 }
 
+// The candidate with the best time per GB (ties: the lower index).
+int tuner_best(const GridTuner::State& st) {
+    int b = 0;
+    for (int c = 1; c < GridTuner::kCands; ++c)
+        if (st.best_ms_per_gb[c] < st.best_ms_per_gb[b]) b = c;
+    return b;
+}
+
 // Reads every finished trial of a shape into its best times; decides once
-// both candidates have two samples (launches 2-5 of the shape alternate the
-// two grids; the sixth waits for them if they are still running).
+// every candidate has two samples (launches 2-7 of the shape cycle through
+// the three grids).
 void tuner_poll(GridTuner::State& st) {
     for (size_t i = 0; i < st.pending.size();) {
         GridTuner::Trial& t = st.pending[i];
@@ -226,8 +234,9 @@ void tuner_poll(GridTuner::State& st) {
         (void)hipEventDestroy(t.b);
         st.pending.erase(st.pending.begin() + long(i));
     }
-    if (st.decided < 0 && st.samples[0] >= 2 && st.samples[1] >= 2)
-        st.decided = st.best_ms_per_gb[1] < st.best_ms_per_gb[0] ? 1 : 0;
+    bool all = true;
+    for (int c = 0; c < GridTuner::kCands; ++c) all = all && st.samples[c] >= 2;
+    if (st.decided < 0 && all) st.decided = tuner_best(st);
 }
 }  // namespace
 
@@ -242,24 +251,26 @@ int rs_grid_pick(Device& dev, int k, int r, uint64_t shard_size, double gb, uint
     GridTuner::State& st = dev.tuner.states[key];
     if (!st.cands[0]) {
         st.cands[0] = rs_default_variant(uint32_t(r)).blocks_per_cu;
-        st.cands[1] = st.cands[0] / 2;  // r <= 2: 1024 / 512; r = 3, 4: 512 / 256
+        st.cands[1] = st.cands[0] / 2;  // r <= 2: 1024 / 512 / 256; r = 3, 4: 512 / 256 / 128
+        st.cands[2] = st.cands[0] / 4;
     }
     tuner_poll(st);
     if (st.decided >= 0) {
         *bpc = uint32_t(st.cands[st.decided]);
         return MXEC_OK;
     }
-    if (st.launches >= 5) {
-        // Launches 2-5 were the trials (two per grid) and some still run (a
+    constexpr int kTrials = 2 * GridTuner::kCands;
+    if (st.launches > kTrials) {
+        // Launches 2-7 were the trials (two per grid) and some still run (a
         // caller that queues far ahead): the default grid until their events
         // complete -- never a host wait inside an enqueue-only call.
-        if (st.pending.empty()) st.decided = st.best_ms_per_gb[1] < st.best_ms_per_gb[0] ? 1 : 0;
+        if (st.pending.empty()) st.decided = tuner_best(st);
         *bpc = uint32_t(st.cands[st.decided >= 0 ? st.decided : 0]);
         return MXEC_OK;
     }
     const int l = st.launches++;
     if (l == 0) return MXEC_OK;  // first launch of a shape: cold, untimed
-    trial->cand = (l - 1) & 1;
+    trial->cand = (l - 1) % GridTuner::kCands;
     trial->gb = gb;
     MXEC_HIP(hipEventCreate(&trial->a));
     if (hipEventCreate(&trial->b) != hipSuccess) {

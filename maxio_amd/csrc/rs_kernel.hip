@@ -617,6 +617,12 @@ RsVariant rs_default_variant(uint32_t r_total) {
         const int b = atoi(e);
         if (b > 0 && b <= 4096) v.blocks_per_cu = b;
     }
+    // MXEC_RS_VECS = 1 | 2 | 4 (4 only for R <= 4): vectors per lane of
+    // uniform launches (the tile is 4 KiB x V per shard).
+    if (const char* e = getenv("MXEC_RS_VECS")) {
+        const int vv = atoi(e);
+        if (vv == 1 || vv == 2 || (vv == 4 && r_total <= 4)) v.vecs = vv;
+    }
 #endif
     return v;
 }

@@ -163,24 +163,27 @@ bool pinned_range(const void* p, uint64_t len);
 // may load and store it directly (copy_kernel.hip).
 bool pinned_mapped(const void* p, uint64_t len);
 
-// Online choice between two grid sizes for the large uniform RS launches
-// of one shape (ops.cpp rs_grid_pick): which of them runs faster depends on
-// the box and on where the batch sits in HBM (profiles/r3/grid_ab/: 512
-// workgroups per CU 3.6 % ahead of 1024 on one box, 0.8 % behind on
-// another), so the first launches of a shape alternate between the two,
-// timed with events on the caller's stream, and the faster one is kept for
-// the context's life.
+// Online choice among three grid sizes (the default, half and a quarter of
+// it) for the large uniform RS launches of one shape (ops.cpp
+// rs_grid_pick): which runs fastest depends on the box and on where the
+// batch sits in HBM (profiles/r3/grid_ab/: 512 workgroups per CU 3.6 % ahead
+// of 1024 on one box, 0.8 % behind on another; profiles/r4/placement_full/:
+// on configs[1] batches that 1024 runs at 6.06-6.07 TB/s, 256 runs at 6.24,
+// and where 1024 is fast 256 trails it by ~1 %), so the first launches of a
+// shape cycle through the three, timed with events on the caller's stream,
+// and the fastest is kept for the context's life.
 struct GridTuner {
+    static constexpr int kCands = 3;
     struct Trial {
         hipEvent_t a = nullptr, b = nullptr;
         int cand = 0;
         double gb = 0;  // bytes of the launch, in GB
     };
     struct State {
-        int cands[2] = {0, 0};
+        int cands[kCands] = {0, 0, 0};
         int launches = 0;
-        int samples[2] = {0, 0};
-        double best_ms_per_gb[2] = {1e30, 1e30};
+        int samples[kCands] = {0, 0, 0};
+        double best_ms_per_gb[kCands] = {1e30, 1e30, 1e30};
         int decided = -1;
         std::vector<Trial> pending;
     };

@@ -625,8 +625,8 @@ def test_put_data_chunk_write_error_wins(ctx, tmp_path):
 
 
 def test_grid_tuner_decides_and_stays_exact():
-    """The RS grid tuner (ops.cpp rs_grid_pick): launches 2-5 of a large
-    uniform shape alternate two grid sizes, the sixth keeps the faster; every
+    """The RS grid tuner (ops.cpp rs_grid_pick): launches 2-7 of a large
+    uniform shape cycle through three grid sizes, the eighth keeps the fastest; every
     launch's parity is bit-exact (the grid never changes the bytes).  A fresh
     context so the shape's tuning starts here."""
     torch = _torch()
@@ -639,7 +639,7 @@ def test_grid_tuner_decides_and_stays_exact():
         torch.cuda.synchronize()
         assert c.rs_grid(k, m, s) == 1024  # never launched: the default
         ref = None
-        for it in range(8):
+        for it in range(10):
             obj[:, k:].zero_()
             torch.cuda.synchronize()
             c.encode_strided_device(k, m, s, n, obj.data_ptr(), (k + m) * s, s, obj[:, k:].data_ptr(), (k + m) * s, s)
@@ -651,4 +651,4 @@ def test_grid_tuner_decides_and_stays_exact():
                 assert all(np.array_equal(h[k + i], want[i]) for i in range(m))
             else:
                 assert torch.equal(obj[:, k:], ref), it
-        assert c.rs_grid(k, m, s) in (1024, 512)
+        assert c.rs_grid(k, m, s) in (1024, 512, 256)

@@ -45,6 +45,15 @@ def main() -> int:
     ap.add_argument("--check", action="store_true", help="oracle-check object 0 after the rs timings")
     ap.add_argument("--free-each", action="store_true", help="free each batch before allocating the next")
     ap.add_argument("--spacer-mib", default="", help="comma list: MiB allocated ahead of each batch (cycled)")
+    ap.add_argument("--variants", default="",
+                    help="semicolon list of name=ENV:val,ENV:val (lab RS knobs, e.g. "
+                         "'v2=MXEC_RS_VECS:2;st=MXEC_RS_STORE_NT:0'), each timed like a grid")
+    ap.add_argument("--pads-kib", default="",
+                    help="comma list of other shard pads (KiB): on every allocation, time rs (first grid) "
+                         "with the shards S + pad apart inside the same buffer (the largest pad sizes it)")
+    ap.add_argument("--revisit", type=int, default=0,
+                    help="after the last allocation, time rs (first grid) and f4copy on every kept batch again, "
+                         "this many passes (is a slow batch slow for good, or only when it came first?)")
     a = ap.parse_args()
     spacers = [int(x) for x in a.spacer_mib.split(",") if x]
     import torch
@@ -54,7 +63,8 @@ def main() -> int:
 
     k, m, S, n = 4, 2, 10 << 20, a.objects
     pad = (2 << 20) + (64 << 10)
-    ss = S + pad
+    pads = [int(x) << 10 for x in a.pads_kib.split(",") if x]
+    ss = S + max([pad] + pads)
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
     sh = st.cuda_stream
@@ -66,9 +76,11 @@ def main() -> int:
         return round(alg / (ms * 1e-3) / 1e12, 4)
 
     bufs = []
+    kept = []  # (alloc index, batch) for --revisit
     for ai in range(a.allocs):
         if a.free_each:
             bufs.clear()
+            kept.clear()
             torch.cuda.empty_cache()
         spacer_mib = spacers[ai % len(spacers)] if spacers else 0
         try:
@@ -79,6 +91,7 @@ def main() -> int:
             print(json.dumps({"alloc": ai, "stopped": str(e)[:120]}), flush=True)
             break
         bufs.append(obj)
+        kept.append((ai, obj))
         obj[:, :k, :S].random_(0, 256)
         torch.cuda.synchronize()
         d0, p0, ost = obj.data_ptr(), obj[:, k:].data_ptr(), (k + m) * ss
@@ -90,6 +103,23 @@ def main() -> int:
                 k, m, S, n, d0, ost, ss, p0, ost, ss, stream=sh), a.reps, warm=2)
             row[f"rs_bpc{g}_TBps"] = tbps(ms)
         os.environ.pop("MXEC_RS_BPC", None)
+        for spec in [x for x in a.variants.split(";") if x]:
+            name, _, kv = spec.partition("=")
+            env = dict(p.split(":", 1) for p in kv.split(",") if p)
+            os.environ.update(env)
+            ms = bench.event_ms(torch, st, lambda: ctx.encode_strided_device(
+                k, m, S, n, d0, ost, ss, p0, ost, ss, stream=sh), a.reps, warm=2)
+            for key in env:
+                os.environ.pop(key, None)
+            row[f"rs_{name}_TBps"] = tbps(ms)
+        g0 = a.grids.split(",")[0]
+        for pk in pads:
+            s2 = S + pk
+            os.environ["MXEC_RS_BPC"] = g0
+            ms = bench.event_ms(torch, st, lambda: ctx.encode_strided_device(
+                k, m, S, n, d0, (k + m) * s2, s2, d0 + k * s2, (k + m) * s2, s2, stream=sh), a.reps, warm=2)
+            os.environ.pop("MXEC_RS_BPC", None)
+            row[f"rs_pad{pk >> 10}k_TBps"] = tbps(ms)
         if a.check:
             h = obj[0].cpu().numpy()
             want = bench._oracle().encode(list(h[:k, :S]), m, S)
@@ -101,9 +131,23 @@ def main() -> int:
         half = (obj.numel() // 2) & ~15
         ms = bench.event_ms(torch, st, lambda: probe.mxprobe_copy_float4(d0 + half, d0, half, sh), a.reps)
         row["f4copy_TBps"] = round(2 * half / (ms * 1e-3) / 1e12, 4)
-        for key in [x for x in row if x.startswith("rs_bpc")]:
+        for key in [x for x in row if x.startswith("rs_") and x.endswith("_TBps")]:
             row[key.replace("_TBps", "_of_f4copy")] = round(row[key] / row["f4copy_TBps"], 4)
         print(json.dumps(row), flush=True)
+    g0 = a.grids.split(",")[0]
+    for rp in range(a.revisit):
+        for ai, obj in kept:
+            d0, p0, ost = obj.data_ptr(), obj[:, k:].data_ptr(), (k + m) * ss
+            os.environ["MXEC_RS_BPC"] = g0
+            row = {"revisit": rp, "alloc": ai}
+            row[f"rs_bpc{g0}_TBps"] = tbps(bench.event_ms(torch, st, lambda: ctx.encode_strided_device(
+                k, m, S, n, d0, ost, ss, p0, ost, ss, stream=sh), a.reps, warm=2))
+            os.environ.pop("MXEC_RS_BPC", None)
+            half = (obj.numel() // 2) & ~15
+            ms = bench.event_ms(torch, st, lambda: probe.mxprobe_copy_float4(d0 + half, d0, half, sh), a.reps)
+            row["f4copy_TBps"] = round(2 * half / (ms * 1e-3) / 1e12, 4)
+            row[f"rs_bpc{g0}_of_f4copy"] = round(row[f"rs_bpc{g0}_TBps"] / row["f4copy_TBps"], 4)
+            print(json.dumps(row), flush=True)
     ctx.close()
     return 0
 
