@@ -54,6 +54,14 @@ struct ShaCombiner {
     std::vector<Req*> pending;
     bool gathering = false;  // a leader is collecting its batch
     size_t last_batch = 1;   // requests in the previous launch
+    // A caller that only ever arrives alone (one thread verifying one GET
+    // after another) stops paying the lone leader's gather window: after
+    // kLoneStreak launches in a row that carried one request each, with no
+    // arrival while another request was pending or in flight, a leader
+    // launches at once.  The first overlapping arrival ends the streak.
+    static constexpr int kLoneStreak = 8;
+    int lone_launches = 0;
+    bool overlap = false;    // an arrival found company since the last launch
     size_t pending_msgs = 0;   // messages of `pending`
     size_t inflight_msgs = 0;  // messages of the launches running now
     size_t lane_limit = 0;     // a second lane opens only below this (see below)
@@ -238,6 +246,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
     me.after_launch = after_launch;
     for (uint64_t l : lens) me.longest = std::max(me.longest, l);  // outside the lock
     std::unique_lock<std::mutex> lk(c->mu);
+    if (!c->pending.empty() || c->inflight_msgs > 0 || c->gathering) c->overlap = true;
     c->pending.push_back(&me);
     c->pending_msgs += ptrs.size();
     if (c->gathering) c->cv_gather.notify_one();  // the gathering leader may be waiting for us
@@ -259,7 +268,8 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // the previous size is forgotten as soon as fewer come.
         const size_t want = c->last_batch;
         const Knobs& kn = knobs_of(d);
-        const long wait_us = want > 1 ? kn.gather_max_us : kn.gather_us;
+        const long wait_us = want > 1 ? kn.gather_max_us
+                             : c->lone_launches >= ShaCombiner::kLoneStreak ? 0 : kn.gather_us;
         const auto t0 = std::chrono::steady_clock::now();
         if (c->pending.size() < std::max<size_t>(want, 2) && wait_us > 0)
             c->cv_gather.wait_for(lk, std::chrono::microseconds(wait_us),
@@ -308,6 +318,8 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         c->pending_msgs = 0;
         c->inflight_msgs += batch_msgs;
         c->last_batch = batch.size();
+        c->lone_launches = batch.size() == 1 && !c->overlap ? c->lone_launches + 1 : 0;
+        c->overlap = false;
         c->gathering = false;
         Slot* slot_run = c->free_slots.back();
         c->free_slots.pop_back();

@@ -511,6 +511,38 @@ def test_concurrent_small_sha_requests_are_combined(ctx):
         c.close()
 
 
+def test_combiner_after_a_lone_streak_still_combines():
+    """A context that first serves lone requests one after another (past the
+    combiner's lone streak, where a leader stops waiting for company) still
+    gets every digest right, and concurrent callers arriving afterwards
+    still share launches (combiner.cpp kLoneStreak)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    c = maxio_amd.Context(streams_per_device=12)
+    try:
+        rng = np.random.default_rng(77)
+        lone = [rng.integers(0, 256, 5000 + 97 * i, dtype=np.uint8).tobytes() for i in range(12)]
+        for b in lone:
+            assert c.sha256([b]) == [hashlib.sha256(b).digest()]
+        before = c.combiner_stats()
+        assert before["batches"] == len(lone)
+
+        def job(t):
+            bufs = [np.random.default_rng(500 + t).integers(0, 256, 3000 + t, dtype=np.uint8).tobytes()
+                    for _ in range(1 + t % 3)]
+            for _ in range(4):
+                if c.sha256(bufs) != [hashlib.sha256(b).digest() for b in bufs]:
+                    return False
+            return True
+
+        with ThreadPoolExecutor(12) as pool:
+            assert all(pool.map(job, range(48)))
+        after = c.combiner_stats()
+        assert after["batches"] - before["batches"] < 4 * 48  # some requests rode in another's launch
+    finally:
+        c.close()
+
+
 def test_pinned_host_buffers_take_the_direct_dma_path(ctx, tmp_path):
     """Buffers from mxec_host_alloc (Context.host_array) move by DMA straight
     to and from the device: same results as pageable buffers for hashing,
