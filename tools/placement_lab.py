@@ -48,6 +48,9 @@ def main() -> int:
     ap.add_argument("--variants", default="",
                     help="semicolon list of name=ENV:val,ENV:val (lab RS knobs, e.g. "
                          "'v2=MXEC_RS_VECS:2;st=MXEC_RS_STORE_NT:0'), each timed like a grid")
+    ap.add_argument("--shape", default="4,2,10", help="k,m,chunk MiB (default configs[1]: 4,2,10)")
+    ap.add_argument("--base-pad-kib", type=int, default=-1,
+                    help="the batch's own shard pad (default: 2112 KiB at chunks >= 4 MiB, else 0, as bench.py)")
     ap.add_argument("--pads-kib", default="",
                     help="comma list of other shard pads (KiB): on every allocation, time rs (first grid) "
                          "with the shards S + pad apart inside the same buffer (the largest pad sizes it)")
@@ -61,8 +64,9 @@ def main() -> int:
     import bench
     import maxio_amd
 
-    k, m, S, n = 4, 2, 10 << 20, a.objects
-    pad = (2 << 20) + (64 << 10)
+    k, m, smib = (int(x) for x in a.shape.split(","))
+    S, n = smib << 20, a.objects
+    pad = (a.base_pad_kib << 10) if a.base_pad_kib >= 0 else ((2 << 20) + (64 << 10) if S >= (4 << 20) else 0)
     pads = [int(x) << 10 for x in a.pads_kib.split(",") if x]
     ss = S + max([pad] + pads)
     dev = torch.device("cuda", 0)
