@@ -18,7 +18,8 @@
 #             with BENCH_GET_STAMPS=1; tools/get_trace_summary.py lines the
 #             timed GET batches up with the trace -> get_trace_summary.json
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (one run each) of rs_apply_fast
-#             for configs 2 and ns, summarised with the grid they ran at (the
+#             for configs 2 and ns at every grid the tuner can pick (2: 1024 /
+#             512 / 256, ns: 512 / 256 / 128), summarised with the grid (the
 #             grid fixed through the lab build's MXEC_RS_BPC: make lab first)
 #   clock     GRBM_GUI_ACTIVE / GRBM_COUNT pass (one run per config) of configs
 #             3 (SHA-256 split form + decode) and 2 / ns (RS encode):
@@ -81,7 +82,7 @@ for st in "${STEPS[@]}"; do
     pmc)
       # each (config, grid) with the grid fixed (MXEC_RS_BPC also turns the
       # grid tuner off), counters only on rs_apply_fast, one run per counter
-      for cb in 2:1024 2:512 ns:512 ns:256; do
+      for cb in 2:1024 2:512 2:256 ns:512 ns:256 ns:128; do
         cfg=${cb%%:*}; bpc=${cb##*:}
         for c in FETCH_SIZE WRITE_SIZE; do
           ( cd /tmp && MXEC_LIB="$R/maxio_amd/lib/libmaxio_ec_lab.so" MXEC_RS_BPC=$bpc timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply_fast \
@@ -93,13 +94,13 @@ for st in "${STEPS[@]}"; do
       done
       # configs[1]: 1024 x 4+2 x 10 MiB = 655 360 tiles of 16 KiB;
       # north star: 4096 x 8+4 x 1 MiB = 262 144 tiles.
-      for cb in 2:1024 2:512; do
+      for cb in 2:1024 2:512 2:256; do
         bpc=${cb##*:}
         python tools/pmc_summary.py "$O/pmc_2_${bpc}_FETCH_SIZE.csv" "$O/pmc_2_${bpc}_WRITE_SIZE.csv" \
           "rs_apply_fast<2, 4, true, false" 64424509440 --blocks-per-cu $bpc --tiles 655360 \
           --what "config 2, rs_apply_fast<2,4,nt> at $bpc WG/CU" --out "$O/pmc_k4m2_bpc${bpc}_traffic.json" || exit 1
       done
-      for cb in ns:512 ns:256; do
+      for cb in ns:512 ns:256 ns:128; do
         bpc=${cb##*:}
         python tools/pmc_summary.py "$O/pmc_ns_${bpc}_FETCH_SIZE.csv" "$O/pmc_ns_${bpc}_WRITE_SIZE.csv" \
           "rs_apply_fast<4, 4, true, false" 51539607552 --blocks-per-cu $bpc --tiles 262144 \
