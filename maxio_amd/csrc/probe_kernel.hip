@@ -133,6 +133,50 @@ __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__
     }
 }
 
+// The RS tile schedule split into its halves (the placement lab's
+// diagnosis): READ only loads the k data shards of every tile (folded into a
+// sink store that never fires), WRITE only stores the R parity shards.
+template <int R, bool READ, bool WRITE>
+__global__ __launch_bounds__(256) void probe_pattern_part(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                          uint32_t k, uint64_t S, uint64_t n_obj, uint64_t ostride,
+                                                          uint64_t sstride, u32x4* __restrict__ sink) {
+    constexpr uint64_t kTile = 256 * 16 * 4;
+    const uint64_t tpo = S / kTile, n_tiles = tpo * n_obj;
+    u32x4 any = {0, 0, 0, 0};
+    for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint64_t o = t / tpo, base = (t - o * tpo) * kTile + threadIdx.x * 16;
+        u32x4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+        if constexpr (READ) {
+            for (uint32_t j = 0; j < k; j += 4) {
+                u32x4 x[4][4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        x[jj][v] = __builtin_nontemporal_load(
+                            reinterpret_cast<const u32x4*>(data + o * ostride + (j + jj) * sstride + base + v * 4096));
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[v] ^= (x[0][v] ^ x[1][v]) + (x[2][v] ^ x[3][v]);
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[v] = u32x4{uint32_t(t), uint32_t(v), 0x5A5A5A5Au, 0xA5A5A5A5u};
+        }
+        if constexpr (WRITE) {
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    store_p<0>(reinterpret_cast<u32x4*>(par + o * ostride + i * sstride + base + v * 4096),
+                               acc[v] + uint32_t(i));
+        } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) any ^= acc[v];
+        }
+    }
+    if (!WRITE && any.x == 0x12345678u && any.y == 0x9abcdef0u) sink[0] = any;
+}
+
 // The RS access pattern at the float4 copy's granularity: one 16-byte column
 // of one object per lane (XOR for the GF math), plain loads and stores, one
 // workgroup per 256 columns -- the schedule with the least state per lane
@@ -264,6 +308,30 @@ extern "C" int mxprobe_rs_pattern_strided(const void* data, void* parity, uint32
 extern "C" int mxprobe_rs_pattern(const void* data, void* parity, uint32_t k, uint32_t m, uint64_t S, uint64_t n_obj,
                                   void* stream) {
     return mxprobe_rs_pattern_strided(data, parity, k, m, S, n_obj, uint64_t(k) * S, uint64_t(m) * S, S, stream);
+}
+
+// The halves of the RS pattern over an object-major batch (one buffer,
+// object stride `obj_stride`, shard stride `shard_stride`, m = 2, k a
+// multiple of 4, S a multiple of 16 KiB): part 0 reads the k data shards
+// only, part 1 writes the m parity shards only, part 2 both (the pattern).
+// Grid as the RS kernel at m <= 2 (1024 per CU).  sink: 16 bytes of device
+// memory (never written in practice).
+extern "C" int mxprobe_rs_pattern_part(const void* data, void* parity, uint32_t k, uint64_t S, uint64_t n_obj,
+                                       uint64_t obj_stride, uint64_t shard_stride, int part, void* sink,
+                                       void* stream) {
+    if (k == 0 || (k & 3) || S == 0 || (S % 16384) || part < 0 || part > 2 ||
+        ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity) |
+          reinterpret_cast<uintptr_t>(sink)) & 15))
+        return int(hipErrorInvalidValue);
+    const dim3 g(uint32_t(cus() * 1024)), b(256);
+    const auto* in = static_cast<const uint8_t*>(data);
+    auto* out = static_cast<uint8_t*>(parity);
+    auto* sk = static_cast<u32x4*>(sink);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (part == 0) hipLaunchKernelGGL((probe_pattern_part<2, true, false>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
+    else if (part == 1) hipLaunchKernelGGL((probe_pattern_part<2, false, true>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
+    else hipLaunchKernelGGL((probe_pattern_part<2, true, true>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
+    return int(hipGetLastError());
 }
 
 // probe_rs_float4 over the same strided layout (m in {1, 2, 4}, S % 16 == 0).

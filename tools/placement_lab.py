@@ -27,6 +27,7 @@ batches land at different places.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -54,6 +55,9 @@ def main() -> int:
     ap.add_argument("--pads-kib", default="",
                     help="comma list of other shard pads (KiB): on every allocation, time rs (first grid) "
                          "with the shards S + pad apart inside the same buffer (the largest pad sizes it)")
+    ap.add_argument("--parts", action="store_true",
+                    help="also time the RS pattern's halves on each batch (m = 2): reads of the k data shards "
+                         "only, writes of the parity only, both; and a plain read stream of the same bytes")
     ap.add_argument("--revisit", type=int, default=0,
                     help="after the last allocation, time rs (first grid) and f4copy on every kept batch again, "
                          "this many passes (is a slow batch slow for good, or only when it came first?)")
@@ -132,6 +136,19 @@ def main() -> int:
             d0, p0, k, m, S, n, ost, ost, ss, sh), a.reps))
         row["f4pattern_TBps"] = tbps(bench.event_ms(torch, st, lambda: probe.mxprobe_rs_float4_strided(
             d0, p0, k, m, S, n, ost, ost, ss, sh), a.reps))
+        if a.parts:
+            sink = torch.zeros(16, dtype=torch.uint8, device=dev)
+            probe.mxprobe_rs_pattern_part.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+            probe.mxprobe_rs_pattern_part.restype = ctypes.c_int
+            for part, name, nbytes in ((0, "reads", k * S * n), (1, "writes", m * S * n), (2, "both", (k + m) * S * n)):
+                ms = bench.event_ms(torch, st, lambda: probe.mxprobe_rs_pattern_part(
+                    d0, p0, k, S, n, ost, ss, part, sink.data_ptr(), sh), a.reps)
+                row[f"part_{name}_TBps"] = round(nbytes / (ms * 1e-3) / 1e12, 4)
+            rb = (obj.numel() * k // (k + m)) & ~15
+            ms = bench.event_ms(torch, st, lambda: probe.mxprobe_read(d0, rb, sink.data_ptr(), sh), a.reps)
+            row["read_stream_TBps"] = round(rb / (ms * 1e-3) / 1e12, 4)
         half = (obj.numel() // 2) & ~15
         ms = bench.event_ms(torch, st, lambda: probe.mxprobe_copy_float4(d0 + half, d0, half, sh), a.reps)
         row["f4copy_TBps"] = round(2 * half / (ms * 1e-3) / 1e12, 4)
