@@ -177,6 +177,57 @@ __global__ __launch_bounds__(256) void probe_pattern_part(const uint8_t* __restr
     if (!WRITE && any.x == 0x12345678u && any.y == 0x9abcdef0u) sink[0] = any;
 }
 
+// The RS pattern (k = 4, m = 2) in time-divided phases: every workgroup
+// reads G tiles' data shards (parity kept in registers) only while the
+// chip-wide 100 MHz clock is in the first `rwin` ticks of each `period`, and
+// stores the parity only in the rest, so HBM sees read bursts and write
+// bursts instead of a steady 2:1 mix (is the mixing penalty avoidable?).
+// period == 0: no gating (the same kernel, unphased).  Lab probe only.
+__device__ __forceinline__ uint64_t rt_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+template <int G>
+__global__ __launch_bounds__(256) void probe_phased(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                    uint64_t S, uint64_t n_obj, uint64_t ostride, uint64_t sstride,
+                                                    uint32_t period, uint32_t rwin) {
+    constexpr uint64_t kTile = 256 * 16 * 4;
+    const uint64_t tpo = S / kTile, n_tiles = tpo * n_obj;
+    for (uint64_t t0 = uint64_t(blockIdx.x) * G; t0 < n_tiles; t0 += uint64_t(gridDim.x) * G) {
+        if (period) {
+            while (rt_ticks() % period >= rwin) __builtin_amdgcn_s_sleep(1);
+        }
+        u32x4 out[G][2][4];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint64_t t = t0 + g < n_tiles ? t0 + g : t0;
+            const uint64_t o = t / tpo, base = (t - o * tpo) * kTile + threadIdx.x * 16;
+            u32x4 x[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    x[j][v] = __builtin_nontemporal_load(
+                        reinterpret_cast<const u32x4*>(data + o * ostride + j * sstride + base + v * 4096));
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                out[g][0][v] = (x[0][v] ^ x[1][v]) + (x[2][v] ^ x[3][v]);
+                out[g][1][v] = (x[0][v] + x[1][v]) ^ (x[2][v] + x[3][v]);
+            }
+        }
+        if (period) {
+            while (rt_ticks() % period < rwin) __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            if (t0 + g >= n_tiles) break;
+            const uint64_t t = t0 + g, o = t / tpo, base = (t - o * tpo) * kTile + threadIdx.x * 16;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    store_p<0>(reinterpret_cast<u32x4*>(par + o * ostride + i * sstride + base + v * 4096), out[g][i][v]);
+        }
+    }
+}
+
 // The RS access pattern at the float4 copy's granularity: one 16-byte column
 // of one object per lane (XOR for the GF math), plain loads and stores, one
 // workgroup per 256 columns -- the schedule with the least state per lane
@@ -331,6 +382,25 @@ extern "C" int mxprobe_rs_pattern_part(const void* data, void* parity, uint32_t 
     if (part == 0) hipLaunchKernelGGL((probe_pattern_part<2, true, false>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
     else if (part == 1) hipLaunchKernelGGL((probe_pattern_part<2, false, true>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
     else hipLaunchKernelGGL((probe_pattern_part<2, true, true>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
+    return int(hipGetLastError());
+}
+
+// probe_phased over an object-major k = 4, m = 2 batch: `wpc` workgroups per
+// CU, G in {1, 2, 4} tiles per phase, period / rwin in 10 ns ticks (period 0:
+// ungated).
+extern "C" int mxprobe_rs_phased(const void* data, void* parity, uint64_t S, uint64_t n_obj, uint64_t obj_stride,
+                                 uint64_t shard_stride, int G, int wpc, uint32_t period, uint32_t rwin, void* stream) {
+    if (S == 0 || (S % 16384) || wpc < 1 || wpc > 4096 || (period && rwin >= period) ||
+        ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15))
+        return int(hipErrorInvalidValue);
+    const dim3 g(uint32_t(cus() * wpc)), b(256);
+    const auto* in = static_cast<const uint8_t*>(data);
+    auto* out = static_cast<uint8_t*>(parity);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (G == 1) hipLaunchKernelGGL(probe_phased<1>, g, b, 0, s, in, out, S, n_obj, obj_stride, shard_stride, period, rwin);
+    else if (G == 2) hipLaunchKernelGGL(probe_phased<2>, g, b, 0, s, in, out, S, n_obj, obj_stride, shard_stride, period, rwin);
+    else if (G == 4) hipLaunchKernelGGL(probe_phased<4>, g, b, 0, s, in, out, S, n_obj, obj_stride, shard_stride, period, rwin);
+    else return int(hipErrorInvalidValue);
     return int(hipGetLastError());
 }
 
