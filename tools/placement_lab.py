@@ -19,6 +19,9 @@ MXEC_LIB = the lab build, for MXEC_RS_BPC).
   python tools/placement_lab.py [--objects 256] [--allocs 8] [--grids 1024,512] [--reps 5]
                                 [--free-each --spacer-mib 0,4096,...]
 
+--pads-kib sizes the batch for its largest pad, and the other columns
+(rs_bpc*, variants, pattern, f4pattern, parts) then run at that stride too;
+the rs_pad*k columns are the encode at each listed pad in the same buffer.
 --free-each drops each batch before the next (full configs[1] batches, 74 GB,
 fit three at a time otherwise); --spacer-mib allocates a spacer of that many
 MiB (one value per allocation, cycled) ahead of each batch, so successive
