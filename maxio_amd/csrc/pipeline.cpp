@@ -169,6 +169,7 @@ struct PipeRes {
         desc_slot.owner = &dev;
         arena.owner = &dev;
         MXEC_TRY(create_streams(dev));
+        arena.upload = h2d;  // table copies ride the upload stream (DescArena)
         affinity_tag(h2d, &dev);
         affinity_tag(d2h, &dev);
         for (auto s : cs) affinity_tag(s, &dev);
@@ -886,6 +887,7 @@ private:
         const uint64_t npieces = grid.count(longest);
         hipStream_t rs_s = cs_[0], sha_s = cs_[1];
         hipEvent_t sha_done = nullptr;
+        PTRACE(start(h2d_));
         for (uint64_t pc = 0; pc < npieces; ++pc) {
             const uint64_t off = grid.start(pc), pw = grid.width(pc);
             for (size_t o = o0; o < o1; ++o) {
@@ -903,6 +905,8 @@ private:
             MXEC_TRY(new_event(&rs_done));
             MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up, h2d_));
+            PTRACE(mark("up", h2d_));
+            PTRACE(now("up_queued"));
             MXEC_HIP(hipStreamWaitEvent(rs_s, up, 0));
             // Parity of this piece: RS is bytewise, so bytes [off, off + P) of
             // the parity come from the same bytes of the data (short data
@@ -955,7 +959,9 @@ private:
             if (!sp.empty()) {
                 MXEC_HIP(hipStreamWaitEvent(sha_s, rs_done, 0));
                 MXEC_TRY(run_sha_pieces(d_, slot, sha_s, sp, sl, ss, st, state, pc > 0, digests, &arena_));
+                PTRACE(mark("sha", sha_s));
             }
+            PTRACE(mark("rs", rs_s));
             // This piece of every parity chunk goes down.
             MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
@@ -967,6 +973,8 @@ private:
                     MXEC_TRY(queue_down(h.parity[i] + off, ob + uint64_t(h.k + i) * h.slot(), std::min(pw, h.S - off)));
             }
             MXEC_TRY(flush_down());
+            PTRACE(mark("down", d2h_));
+            PTRACE(now("piece_queued"));
         }
         if (nm) {
             MXEC_TRY(new_event(&sha_done));
@@ -982,7 +990,9 @@ private:
             }
             MXEC_TRY(flush_down());
         }
-        return flush();
+        const int frc = flush();
+        PTRACE(report("wave_pieces"));
+        return frc;
     }
 
     int wave(std::vector<HostObj>& objs, size_t o0, size_t o1) {

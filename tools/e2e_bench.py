@@ -42,6 +42,10 @@ def main() -> int:
     ap.add_argument("--m", type=int, default=2)
     ap.add_argument("--chunk-size", type=int, default=10 << 20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--alloc", choices=["torch", "mxec"], default="torch",
+                    help="page-locked buffers from torch pin_memory (SDMA always) or mxec_host_alloc "
+                         "(mapped: MXEC_PIPE_COPY decides SDMA or CU-wave copies)")
+    ap.add_argument("--modes", default="pinned,pageable")
     args = ap.parse_args()
 
     import torch
@@ -81,8 +85,13 @@ def main() -> int:
     del hb, db, hb2, db2
 
     objs = [(k, m, S)] * n
-    for mode in ("pinned", "pageable"):
-        if mode == "pinned":
+    out["alloc"] = args.alloc
+    out["MXEC_PIPE_COPY"] = os.environ.get("MXEC_PIPE_COPY", "auto")
+    for mode in args.modes.split(","):
+        if mode == "pinned" and args.alloc == "mxec":
+            data = ctx.host_array(n * k * S).reshape(n, k, S)
+            par = ctx.host_array(n * m * S).reshape(n, m, S)
+        elif mode == "pinned":
             data_t = torch.empty((n, k, S), dtype=torch.uint8).pin_memory()
             par_t = torch.empty((n, m, S), dtype=torch.uint8).pin_memory()
             data, par = data_t.numpy(), par_t.numpy()
