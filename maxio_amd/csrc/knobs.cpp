@@ -66,6 +66,7 @@ Knobs read_knobs() {
     if (const char* u = env("MXEC_DESC_UPLOAD")) k.desc_upload = !std::strcmp(u, "inline") ? 0 : !std::strcmp(u, "stream") ? 2 : 1;
     const long piece = env_long("MXEC_PIPE_PIECE_MB", 1);
     k.pipe_piece = piece <= 0 ? 0 : uint64_t(std::min(piece, 1L << 20)) << 20;
+    k.pipe_piece_auto = env("MXEC_PIPE_PIECE_MB") == nullptr;
     if (const char* c = env("MXEC_PIPE_COPY"))
         k.pipe_copy = !std::strcmp(c, "sdma") ? 0 : !std::strcmp(c, "waves") ? 1 : 2;
     if (const char* w = env("MXEC_GET_WINDOW")) k.get_window = std::max<uint64_t>(1, std::strtoull(w, nullptr, 10));

@@ -26,6 +26,7 @@ struct Knobs {
     int sha_form = 0;              // MXEC_SHA_FORM: 0 auto, 1 one, 2 split, 3 stream, 6 lagpair
     int desc_upload = 1;           // MXEC_DESC_UPLOAD: 0 inline, 1 auto, 2 side stream
     uint64_t pipe_piece = uint64_t(1) << 20;  // MXEC_PIPE_PIECE_MB (0: whole chunks)
+    bool pipe_piece_auto = true;   // MXEC_PIPE_PIECE_MB unset: 1, 2 or 4 MiB per wave (pipeline.cpp)
     int pipe_copy = 2;             // MXEC_PIPE_COPY: 0 sdma (hipMemcpyAsync); 1 waves (copy_kernel.hip
                                    //   for every host batch); 2 auto: reconstruct batches by waves,
                                    //   encode batches by SDMA

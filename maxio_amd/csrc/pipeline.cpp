@@ -169,7 +169,6 @@ struct PipeRes {
         desc_slot.owner = &dev;
         arena.owner = &dev;
         MXEC_TRY(create_streams(dev));
-        arena.upload = h2d;  // table copies ride the upload stream (DescArena)
         affinity_tag(h2d, &dev);
         affinity_tag(d2h, &dev);
         for (auto s : cs) affinity_tag(s, &dev);
@@ -401,7 +400,14 @@ private:
         for (size_t o = o0; o < o1; ++o)
             if (objs[o].expected)
                 for (int i = 0; i < objs[o].k + objs[o].m; ++i) vmsgs += objs[o].present[i] ? 1 : 0;
-        const uint64_t P = piece_bytes();
+        uint64_t up_bytes = 0, longest_msg = 0;
+        for (size_t o = o0; o < o1; ++o)
+            for (int i = 0; i < objs[o].k + objs[o].m; ++i)
+                if (objs[o].present[i]) {
+                    up_bytes += objs[o].len[i];
+                    if (objs[o].expected) longest_msg = std::max(longest_msg, objs[o].len[i]);
+                }
+        const uint64_t P = piece_bytes(up_bytes, longest_msg);
         std::vector<hipEvent_t> up;  // per group (group form): its upload is done
         if (verify && P && vmsgs && vmsgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256)) {
             // Piece-major upload + verification (the PUT wave's scheme, see
@@ -859,7 +865,26 @@ private:
     // down, piece after piece, so every chain starts after the first piece
     // (~9 ms) and the wave ends near one chain's length.  Taken when the
     // wave's messages fit the lag quad form (64 per CU).
-    uint64_t piece_bytes() const { return d_.kn ? d_.kn->pipe_piece : uint64_t(1) << 20; }  // MXEC_PIPE_PIECE_MB
+    //
+    // Piece size (MXEC_PIPE_PIECE_MB; unset = per wave): small pieces start
+    // the chains early, but each piece of each chunk is its own copy, and
+    // 1 MiB copies move ~33 GB/s where 4 MiB ones move ~43 (PUT with digests,
+    // 512 x 4+2 x 10 MiB: 0.645 s at 1 MiB, 0.557 at 2, 0.503 at 4; 128
+    // objects: 0.218 / 0.227 / 0.246 s, profiles/r4/e2e_pieces/).  So a wave
+    // takes the smallest piece whose upload, at that piece's copy rate, still
+    // fits inside the longest chain (the wave's floor either way), else 4 MiB.
+    uint64_t piece_bytes(uint64_t upload_bytes, uint64_t longest) const {
+        if (!d_.kn) return uint64_t(1) << 20;
+        if (!d_.kn->pipe_piece_auto) return d_.kn->pipe_piece;
+        const double chain_s = double(longest / 64) * kShaLagUsPerBlock * 1e-6;
+        static constexpr struct {
+            uint64_t bytes;
+            double gbps;  // sustained H2D rate of copies this size, measured (above)
+        } kSteps[] = {{uint64_t(1) << 20, 33.0}, {uint64_t(2) << 20, 38.0}};
+        for (const auto& s : kSteps)
+            if (double(upload_bytes) / (s.gbps * 1e9) <= chain_s) return s.bytes;
+        return uint64_t(4) << 20;
+    }
 
     int wave_pieces(std::vector<HostObj>& objs, size_t o0, size_t o1, uint64_t P) {
         Slot& slot = slot_;
@@ -997,10 +1022,14 @@ private:
 
     int wave(std::vector<HostObj>& objs, size_t o0, size_t o1) {
         {
-            uint64_t msgs = 0;
-            for (size_t o = o0; o < o1; ++o)
-                if (objs[o].dig) msgs += uint64_t(objs[o].k + objs[o].m);
-            const uint64_t P = piece_bytes();
+            uint64_t msgs = 0, up_bytes = 0, longest_msg = 0;
+            for (size_t o = o0; o < o1; ++o) {
+                for (int j = 0; j < objs[o].k; ++j) up_bytes += std::min<uint64_t>(objs[o].dlen[j], objs[o].S);
+                if (!objs[o].dig) continue;
+                msgs += uint64_t(objs[o].k + objs[o].m);
+                longest_msg = std::max(longest_msg, objs[o].S);
+            }
+            const uint64_t P = piece_bytes(up_bytes, longest_msg);
             if (P && msgs && msgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256))
                 return wave_pieces(objs, o0, o1, P);
         }

@@ -333,15 +333,7 @@ int DescWriter::commit(hipStream_t stream, char** dev_base) {
         char* d = nullptr;
         MXEC_TRY(arena_->take(n, &h, &d));
         std::memcpy(h, tmp_.data(), tmp_.size());
-        if (arena_->upload && arena_->upload != stream) {
-            hipEvent_t e = nullptr;
-            if (arena_->next_event(&e)) return set_error(MXEC_E_DEVICE, "hipEventCreate failed");
-            MXEC_HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, arena_->upload));
-            MXEC_HIP(hipEventRecord(e, arena_->upload));
-            MXEC_HIP(hipStreamWaitEvent(stream, e, 0));
-        } else {
-            MXEC_HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream));
-        }
+        MXEC_HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream));
         *dev_base = d;
         return MXEC_OK;
     }

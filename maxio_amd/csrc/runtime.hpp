@@ -272,17 +272,6 @@ void async_shutdown(Ctx& c);
 // first block frees memory.
 struct DescArena {
     const Device* owner = nullptr;
-    // Copy stream for the tables (the host pipeline's H2D stream), or null:
-    // copy on the launch stream.  A table copy queued on a compute stream
-    // waits there for that stream's previous kernel, and copies of different
-    // streams can share a copy engine's queue in submission order, so the
-    // next piece's uploads queued behind it waited for the previous SHA-256
-    // piece (PUT with digests at 512 objects: 60 ms per piece instead of the
-    // upload's 37).  On the copy stream it waits only for earlier copies; the
-    // launch stream waits for it through an event.
-    hipStream_t upload = nullptr;
-    std::vector<hipEvent_t> events;  // one per table copy of the current wave
-    size_t events_used = 0;
     struct Block {
         PinnedBuf host;
         DevBuf dev;
@@ -299,21 +288,7 @@ struct DescArena {
         MXEC_TRY(b.dev.ensure(bytes));
         cur = 0;
         used = 0;
-        events_used = 0;  // the previous wave's launches are done (the wave ended with a sync)
         return 0;
-    }
-    // An event for the next table copy (reused wave after wave).
-    int next_event(hipEvent_t* e) {
-        if (events_used == events.size()) {
-            hipEvent_t n = nullptr;
-            if (hipEventCreateWithFlags(&n, hipEventDisableTiming) != hipSuccess) return MXEC_E_DEVICE;
-            events.push_back(n);
-        }
-        *e = events[events_used++];
-        return 0;
-    }
-    ~DescArena() {
-        for (auto e : events) (void)hipEventDestroy(e);
     }
     // n bytes (a multiple of 256) of host staging and their device twin.
     int take(size_t n, char** h, char** d) {
