@@ -66,10 +66,10 @@ def test_batch_host_pinned_buffers(ctx):
     _check(objs, chunks_of, digests)
 
 
-@pytest.mark.parametrize("piece_mb", ["1", "2", "0"])
+@pytest.mark.parametrize("piece_mb", ["1", "2", "4", "0", ""])
 def test_batch_host_digests_in_pieces(ctx_with, piece_mb):
-    """With digests the wave runs piece-major (MXEC_PIPE_PIECE_MB, default
-    1; 0 = the group form):
+    """With digests the wave runs piece-major (MXEC_PIPE_PIECE_MB; unset
+    ("") = chosen per wave among 1 / 2 / 4 MiB; 0 = the group form):
     every chunk is hashed piece by piece, its chain carried in a device
     state slot from launch to launch.  Shards over several pieces and off
     the piece grid, last chunks that end mid-piece, on a piece boundary
@@ -77,7 +77,7 @@ def test_batch_host_digests_in_pieces(ctx_with, piece_mb):
     one piece beside them: parity and every digest equal to the oracle and
     hashlib."""
     ctx = ctx_with(MXEC_PIPE_PIECE_MB=piece_mb)
-    rng = np.random.default_rng(40 + int(piece_mb))
+    rng = np.random.default_rng(40 + int(piece_mb or 9))
     M = 1 << 20
     specs = [(4, 2, 3 * M + 100, None), (4, 2, 3 * M + 100, 2 * M + 17), (8, 4, 2 * M, M),
              (10, 4, M + 64, M + 1), (4, 2, 3 * M + 100, 0), (1, 2, 5 * M + 3, None),
@@ -241,7 +241,7 @@ def test_reconstruct_batch_host_mixed(ctx, verify):
         g += k + m
 
 
-@pytest.mark.parametrize("piece_mb", ["1", "2", "0"])
+@pytest.mark.parametrize("piece_mb", ["1", "2", "4", "0", ""])
 def test_reconstruct_batch_host_verify_in_pieces(ctx_with, piece_mb):
     """With verification the present shards go up and are hashed piece by
     piece (MXEC_PIPE_PIECE_MB; 0 = one launch after the whole upload):
@@ -249,7 +249,7 @@ def test_reconstruct_batch_host_verify_in_pieces(ctx_with, piece_mb):
     chunks, a corrupt present shard caught as an erasure, an object that
     fails (buffers untouched), the rest bit-exact."""
     ctx = ctx_with(MXEC_PIPE_PIECE_MB=piece_mb)
-    rng = np.random.default_rng(50 + int(piece_mb))
+    rng = np.random.default_rng(50 + int(piece_mb or 9))
     M = 1 << 20
     specs = [(4, 2, 3 * M + 100, None, {1}, {4}), (4, 2, 3 * M + 100, 2 * M + 17, {0, 5}, set()),
              (8, 4, 2 * M, M, {3}, {9}), (4, 2, 3 * M + 100, 0, {2}, {0}),
