@@ -1427,6 +1427,47 @@ def _leg_times(ts: list) -> dict:
             "max_over_median": round(max(ts) / med, 3), "s_each": [round(t, 4) for t in ts]}
 
 
+def e2e_put_large(ctx, n: int = 512, reps: int = 3) -> dict:
+    """PUT with every chunk's SHA-256 from page-locked host memory at a
+    large batch (one GPU): n x 4+2 x 10 MiB through mxec_encode_batch_host,
+    where the upload (not one chunk's chain) is the bound and the per-wave
+    piece size goes to 4 MiB (pipeline.cpp piece_bytes).  Median of `reps`
+    batches after a warm one, next to the same batch without digests; one
+    object's parity and digests checked against the oracle."""
+    import hashlib
+
+    import numpy as np
+
+    k, m, S = 4, 2, 10 << 20
+    data = ctx.host_array(n * k * S).reshape(n, k, S)
+    par = ctx.host_array(n * m * S).reshape(n, m, S)
+    _fill_random(data, 17)
+    dptr = [data[o, j].ctypes.data for o in range(n) for j in range(k)]
+    pptr = [par[o, i].ctypes.data for o in range(n) for i in range(m)]
+    objs = [(k, m, S)] * n
+    res = {"workload": f"PUT compute from page-locked host memory, {n} x 4+2 x 10 MiB per batch, one GPU"}
+    for sha in (False, True):
+        dig = np.zeros(n * (k + m) * 32, np.uint8) if sha else None
+        ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ctx.encode_batch_host(objs, dptr, pptr, digests=dig)
+            ts.append(time.perf_counter() - t0)
+        el = statistics.median(ts)
+        res["rs_sha256" if sha else "rs_only"] = dict(_leg_times(ts), GiBps_payload=round(n * k * S / GIB / el, 2))
+        if sha:
+            o = n // 2
+            want = _oracle().encode(list(data[o]), m, S)
+            res["spot_check_vs_oracle"] = bool(
+                all(np.array_equal(par[o, i], want[i]) for i in range(m)) and
+                all(bytes(dig[(o * (k + m) + j) * 32:(o * (k + m) + j + 1) * 32]) ==
+                    hashlib.sha256((data[o, j] if j < k else par[o, j - k]).tobytes()).digest()
+                    for j in range(k + m)))
+    del data, par
+    return res
+
+
 def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: bool = False) -> dict:
     """mxec_encode_batch_host from mxec_host_alloc (page-locked) memory: the
     PUT path as MaxIO sees it -- request bodies in host memory, parity and
@@ -1704,6 +1745,8 @@ def main() -> int:
     # the verified GET runs again after them (extra.e2e_get_after_extras).
     if not args.no_e2e and args.config == "2":
         extra["e2e_host"] = e2e_host_leg(ctx, torch, plan, 128 if D == 1 and world == 1 else 64)
+        if D == 1 and world == 1 and with_extra:
+            extra["e2e_put_512"] = e2e_put_large(ctx)
     if rank == 0 and with_extra:
         extra.update(extras(ctx, torch, dev, stream, args.steps, cal))
         if not args.no_e2e:
