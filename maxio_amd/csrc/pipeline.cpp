@@ -717,15 +717,20 @@ private:
     // host and on the device -- go as one DMA: an object's k data chunks are
     // usually contiguous in the request body and always in its device image
     // (and its m parity chunks likewise), so 4+2 objects take 2 copies
-    // instead of 6.  With MXEC_PIPE_COPY2D=1 (lab), copies of one width at
-    // one pitch on each side (the same piece of an object's k chunks in the
-    // piece-major waves) go as one 2D copy when the host side is
-    // page-locked.  Off by default: within one process it won 1-2 %, but in
-    // default bench lines the GET group form (2D runs of whole 10 MiB
-    // shards) fell from 0.113 to 0.150-0.266 s and one process's PUT with
-    // digests ran 0.317 s against 0.210 in the next (profiles/r3/pieces/).
-    // queue_up / queue_down collect; flush_up / flush_down issue (before an
-    // event is recorded on the copy stream).
+    // instead of 6.  In the PUT's piece-major waves (SDMA copies), copies of
+    // one width at one pitch on each side -- the same piece of an object's k
+    // data chunks, of its m parity chunks -- go as one 2D copy when the host
+    // side is page-locked -- when the wave is upload-bound (pieces above
+    // 1 MiB): PUT with digests 0.516 -> 0.457 s at 512 objects, 0.301 ->
+    // 0.283 at 256 (profiles/r4/e2e_pieces/copy2d/).  At 1 MiB pieces (a
+    // chain-bound wave, 128 objects) 2D copies won 2 % in the e2e tool but
+    // the default bench line's leg ran 0.300 s against 0.219 with 1D copies
+    // (`copy2d/bench_2d_at_1MiB_*.json`), as in round 3, so they stay 1D
+    // there.  Nowhere else: in round 3 the GET group form's 2D runs of
+    // whole 10 MiB shards fell from 0.113 to 0.150-0.266 s
+    // (profiles/r3/pieces/).  MXEC_PIPE_COPY2D=0/1 (lab builds) forces it
+    // off / on everywhere.  queue_up / queue_down collect; flush_up /
+    // flush_down issue (before an event is recorded on the copy stream).
     struct Run {
         uint8_t* dst = nullptr;
         const uint8_t* src = nullptr;
@@ -733,15 +738,14 @@ private:
         uint64_t rows = 0;
         uint64_t dpitch = 0, spitch = 0;
     };
-    static bool copy2d_on() {  // lab builds only (read per call); default off, see below
+    bool copy2d_on() const {
 #ifdef MXEC_LAB
-        const char* e = getenv("MXEC_PIPE_COPY2D");
-        return e && atoi(e) != 0;
-#else
-        return false;
+        if (const char* e = getenv("MXEC_PIPE_COPY2D")) return atoi(e) != 0;  // lab override
 #endif
+        return pieces2d_;
     }
-    static bool extend(Run& r, uint8_t* dst, const uint8_t* src, uint64_t len) {
+    bool pieces2d_ = false;  // set while a PUT piece-major wave queues its copies
+    bool extend(Run& r, uint8_t* dst, const uint8_t* src, uint64_t len) const {
         if (!r.len) return false;
         if (r.rows == 1 && r.dst + r.len == dst && r.src + r.len == src) {
             r.len += len;
@@ -912,6 +916,11 @@ private:
         const uint64_t npieces = grid.count(longest);
         hipStream_t rs_s = cs_[0], sha_s = cs_[1];
         hipEvent_t sha_done = nullptr;
+        struct TwoD {  // 2D piece copies for this wave's SDMA copies (queue_up)
+            bool& f;
+            TwoD(bool& flag, bool on) : f(flag) { f = on; }
+            ~TwoD() { f = false; }
+        } twod(pieces2d_, !waves_now_ && P > (uint64_t(1) << 20));
         PTRACE(start(h2d_));
         for (uint64_t pc = 0; pc < npieces; ++pc) {
             const uint64_t off = grid.start(pc), pw = grid.width(pc);
