@@ -46,6 +46,9 @@ def main() -> int:
                     help="page-locked buffers from torch pin_memory (SDMA always) or mxec_host_alloc "
                          "(mapped: MXEC_PIPE_COPY decides SDMA or CU-wave copies)")
     ap.add_argument("--modes", default="pinned,pageable")
+    ap.add_argument("--get", action="store_true",
+                    help="also time the GET side: mxec_reconstruct_batch_host over the same objects with two "
+                         "erased shards each, without and with verification of the present shards")
     args = ap.parse_args()
 
     import torch
@@ -101,8 +104,11 @@ def main() -> int:
         fill(data, 7)
         dptr = [data[o, j].ctypes.data for o in range(n) for j in range(k)]
         pptr = [par[o, i].ctypes.data for o in range(n) for i in range(m)]
+        dig_keep = None
         for sha in (True, False):
             dig = np.zeros(n * (k + m) * 32, np.uint8) if sha else None
+            if sha:
+                dig_keep = dig
             ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm (pool, tables)
             t0 = time.perf_counter()
             for _ in range(args.reps):
@@ -110,6 +116,26 @@ def main() -> int:
             el = (time.perf_counter() - t0) / args.reps
             key = f"{mode}_{'rs_sha' if sha else 'rs_only'}"
             out[key] = {"s": round(el, 4), "GiBps_payload": round(n * k * S / GIB / el, 2)}
+        if args.get:
+            sptr = []
+            for o in range(n):
+                sptr += [data[o, j].ctypes.data for j in range(k)] + [par[o, i].ctypes.data for i in range(m)]
+            rng = np.random.default_rng(11)
+            present0 = np.ones(n * (k + m), np.uint8)
+            for o in range(n):
+                for i in rng.choice(k + m, 2, replace=False):
+                    present0[o * (k + m) + i] = 0
+            for verify in (False, True):
+                exp = dig_keep if verify else None
+                rc, _ = ctx.reconstruct_batch_host(objs, sptr, present0.copy(), expected=exp)  # warm
+                assert rc == 0, rc
+                t0 = time.perf_counter()
+                for _ in range(args.reps):
+                    rc, _ = ctx.reconstruct_batch_host(objs, sptr, present0.copy(), expected=exp)
+                    assert rc == 0, rc
+                el = (time.perf_counter() - t0) / args.reps
+                out[f"{mode}_get_{'verify' if verify else 'rs_only'}"] = {
+                    "s": round(el, 4), "GiBps_payload": round(n * k * S / GIB / el, 2)}
         # spot check one object against the oracle
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
