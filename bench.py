@@ -1204,7 +1204,7 @@ class Plan:
                      each (LOCAL_RANK), --gpus must equal WORLD_SIZE
           "logical"  BENCH_REHEARSE_LOGICAL=1 and fewer visible GPUs than
                      --gpus: a labelled rehearsal on N logical devices of one
-                     card (MXEC_TEST_LOGICAL_DEVICES), never an N-GPU number
+                     card (mxec_open_test logical_devices), never an N-GPU number
     """
 
     def __init__(self, mode, n_gpus, torch_devs, world=1, rank=0, logical=1, rehearsal=None):
@@ -1248,7 +1248,7 @@ def plan_devices(gpus: int, env, visible: int) -> Plan:
         if gpus > 8:
             raise BenchRefusal(f"--gpus {gpus}: logical rehearsals go up to 8 devices")
         return Plan("logical", gpus, [0] * gpus, logical=gpus,
-                    rehearsal=(f"{gpus} logical devices of ONE card (MXEC_TEST_LOGICAL_DEVICES={gpus}): "
+                    rehearsal=(f"{gpus} logical devices of ONE card (mxec_open_test logical_devices={gpus}): "
                                "exercises the multi-device path, not an N-GPU measurement"))
     raise BenchRefusal(f"--gpus {gpus} asks for {gpus} GPUs but {visible} HIP device(s) are visible; run it on a "
                        f"node with {gpus} GPUs (or set BENCH_REHEARSE_LOGICAL=1 for a labelled rehearsal on "
@@ -1301,6 +1301,40 @@ def gather_objects(obj) -> list:
 def sync_all(torch, devs) -> None:
     for d in sorted(set(devs)):
         torch.cuda.synchronize(d)
+
+
+def tune_before_timing(torch, lanes, devs, max_launches: int = 12) -> dict:
+    """Run the workload until the library's RS grid tuner has decided, before
+    the warmup and the timed steps.  The tuner times launches 2-7 of a large
+    uniform shape at three grids and keeps the fastest (ops.cpp
+    rs_grid_pick); without this, a short --warmup would leave its trial
+    launches (half and quarter grids) inside the timed region.  Each launch
+    is waited on, so the trials' events complete and the next call reads
+    them.  Workloads without one large uniform shape run 7 launches (their
+    tuner shapes, if any, see as many)."""
+    t0 = time.perf_counter()
+    n = 0
+    decided = True
+    grid = None
+    for w, stream, tdev in lanes:
+        shape = (w.k, w.m, w.S) if isinstance(w, Encode) else None
+        with torch.cuda.device(tdev):
+            for i in range(max_launches):
+                if shape is not None and i > 0 and w.ctx.rs_grid(*shape):
+                    break
+                if shape is None and i >= 7:
+                    break
+                w.step()
+                torch.cuda.synchronize(tdev)
+                n += 1
+        if shape is not None:
+            g = w.ctx.rs_grid(*shape)
+            decided = decided and g > 0
+            grid = g if grid is None else grid
+    sync_all(torch, devs)
+    return {"decided": decided, "launches": n, "grid_before_timing": grid,
+            "seconds": round(time.perf_counter() - t0, 3),
+            "what": "launches run before --warmup until the RS grid tuner decided (one sync each)"}
 
 
 def run_steps(torch, lanes, steps: int, events: bool):
@@ -1464,6 +1498,8 @@ def e2e_put_large(ctx, n: int = 512, reps: int = 3) -> dict:
                 all(bytes(dig[(o * (k + m) + j) * 32:(o * (k + m) + j + 1) * 32]) ==
                     hashlib.sha256((data[o, j] if j < k else par[o, j - k]).tobytes()).digest()
                     for j in range(k + m)))
+    ctx.host_free(data)
+    ctx.host_free(par)
     del data, par
     return res
 
@@ -1571,6 +1607,8 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
         if stamps:
             res["get_verify_sha256" if verify else "get_rs_only"]["monotonic_ns"] = marks
     if get_only:
+        ctx.host_free(data)
+        ctx.host_free(par)
         del data, par
         return res
     if plan.rank == 0:
@@ -1593,6 +1631,8 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
         o = n // 2
         want = _oracle().encode(list(data[o]), m, S)
         res["spot_check_vs_oracle"] = all(np.array_equal(par[o, i], want[i]) for i in range(m))
+    ctx.host_free(data)
+    ctx.host_free(par)
     del data, par
     return res
 
@@ -1603,9 +1643,11 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    # 7: the RS grid tuner times launches 2-7 of a shape (ops.cpp rs_grid_pick)
-    ap.add_argument("--warmup", type=int, default=7)
+    # The driver's own command is --steps 20 --warmup 5; the RS grid tuner's
+    # trial launches run before the warmup (tune_before_timing), so the grid
+    # never changes inside the timed region whatever --warmup is.
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="2", choices=["2", "3", "3c", "ns", "4a", "4b", "5", "sums", "frames"])
     ap.add_argument("--workers", type=int, default=8, help="config 3c: concurrent batches")
     ap.add_argument("--objects", type=int, default=0, help="objects per GPU (0 = config default)")
@@ -1623,8 +1665,6 @@ def main() -> int:
     except BenchRefusal as e:
         print(f"bench.py: {e}", file=sys.stderr, flush=True)
         return 2
-    if plan.logical > 1:
-        os.environ["MXEC_TEST_LOGICAL_DEVICES"] = str(plan.logical)
     if plan.mode == "ranks":
         import torch.distributed as dist
 
@@ -1650,7 +1690,8 @@ def main() -> int:
     # slot per concurrent batch.
     with_extra = args.config == "2" and one_gpu and not args.no_extra
     ctx = maxio_amd.Context(device_mask=plan.device_mask,
-                            streams_per_device=max(2, args.workers if args.config == "3c" or with_extra else 2))
+                            streams_per_device=max(2, args.workers if args.config == "3c" or with_extra else 2),
+                            test={"logical_devices": plan.logical} if plan.logical > 1 else None)
     if len(ctx.device_ids()) != D:
         print(f"bench.py: the context opened {len(ctx.device_ids())} device(s), the plan needs {D}",
               file=sys.stderr, flush=True)
@@ -1669,6 +1710,7 @@ def main() -> int:
     w, stream, dev = lanes[0]
     sh = stream.cuda_stream
 
+    tuning = tune_before_timing(torch, lanes, plan.torch_devs)
     run_steps(torch, lanes, args.warmup, events=False)
     sync_all(torch, plan.torch_devs)
     spot_local = all(bool(l[0].spot_check()) for l in lanes)
@@ -1685,8 +1727,12 @@ def main() -> int:
     if getattr(w, "wall_timed", False):  # work on the workers' streams, not `stream`
         ms_dev = [elapsed * 1e3 / args.steps] * D
 
-    # The grid the RS grid tuner settled on for the encode shape (0: still tuning).
+    # The grid the RS grid tuner settled on for the encode shape (0: still
+    # tuning), and whether it was the same grid before the timed steps.
     grid_bpc = w.ctx.rs_grid(w.k, w.m, w.S) if isinstance(w, Encode) else None
+    if isinstance(w, Encode):
+        tuning["grid_after_timing"] = grid_bpc
+        tuning["same_grid_over_timed_steps"] = grid_bpc == tuning.get("grid_before_timing")
     payload_local = float(sum(l[0].payload for l in lanes))
     value = reduce_sum(payload_local) * args.steps / GIB / elapsed  # weak scaling: every GPU of every rank
     per_dev = [{"gpu": plan.torch_devs[i] if plan.mode != "logical" else f"logical {i} of card 0",
@@ -1836,6 +1882,8 @@ def main() -> int:
             },
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "tuner_decided_before_timing": tuning["decided"],
+            "tuning": tuning,
             "spot_check_vs_oracle": spot_ok,
             "extra": extra or None,
         }
@@ -1857,6 +1905,13 @@ def main() -> int:
                                     traffic=None)
         print(json.dumps(line), flush=True)
     ctx.close()
+    if os.environ.get("BENCH_DUMP_MAPS") == "1":
+        # The loaded DSOs' address ranges, so a fault during process teardown
+        # (after this point: static destructors, __cxa_finalize) resolves to
+        # a library and an offset.
+        with open("/proc/self/maps") as f:
+            maps = [l.rstrip("\n") for l in f if " r-xp " in l or ".so" in l]
+        print("BENCH_MAPS_BEGIN\n" + "\n".join(maps) + "\nBENCH_MAPS_END", file=sys.stderr, flush=True)
     if plan.mode == "ranks":
         import torch.distributed as dist
 

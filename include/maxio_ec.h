@@ -95,6 +95,18 @@ int mxec_device_count(void);
  * streams_per_device: HIP streams (and staging rings) per device, >= 1.
  * Returns NULL if no device can be opened (see mxec_last_error). */
 mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device);
+/* TEST-ONLY open: as mxec_open, plus settings that exist to drive code paths
+ * on a one-GPU test box.  They are never read from the environment, so a
+ * production host cannot turn them on by accident.
+ *   logical_devices:  open every selected GPU this many times (1..8), each
+ *                     copy a separate device with its own streams, arenas,
+ *                     combiner and pipeline (the multi-device paths);
+ *   rs_grid_cap:      cap every RS launch at this many workgroups (0: off),
+ *                     so each workgroup walks many tiles of its grid-stride loop;
+ *   coef_arena_bytes: bytes per half of each device's coefficient-table arena
+ *                     (0: 64 MiB), small enough that tests recycle it. */
+mxec_ctx* mxec_open_test(uint32_t device_mask, int streams_per_device, int logical_devices, uint32_t rs_grid_cap,
+                         uint64_t coef_arena_bytes);
 void mxec_close(mxec_ctx* ctx);
 int mxec_ctx_device_count(const mxec_ctx* ctx);
 /* HIP device id of the ctx's i-th device. */
@@ -103,6 +115,12 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
  * the device's combiner (concurrent small requests share one launch) and the
  * messages they hashed. */
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages);
+/* Copies the host-batch pipeline (mxec_{encode,reconstruct}_batch_host) has
+ * issued on ctx device `dev` since the context opened: 1D SDMA DMAs, 2D SDMA
+ * DMAs (the PUT's piece copies) and the rows they moved, CU-wave copy blocks.
+ * Any pointer may be NULL.  Diagnostics (tests). */
+int mxec_ctx_copy_stats(mxec_ctx* ctx, int dev, uint64_t* copies_1d, uint64_t* copies_2d, uint64_t* rows_2d,
+                        uint64_t* wave_blocks);
 /* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
  * (k inputs, m outputs, shard_size) at: the grid tuner times the first
  * launches of a shape at three grid sizes and keeps the fastest (which of

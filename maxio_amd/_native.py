@@ -95,10 +95,12 @@ _SIGS = {
     "mxec_last_error": (ctypes.c_char_p, []),
     "mxec_device_count": (INT, []),
     "mxec_open": (P, [ctypes.c_uint32, INT]),
+    "mxec_open_test": (P, [ctypes.c_uint32, INT, INT, ctypes.c_uint32, ctypes.c_uint64]),
     "mxec_close": (None, [P]),
     "mxec_ctx_device_count": (INT, [P]),
     "mxec_ctx_device_id": (INT, [P, INT]),
     "mxec_ctx_combiner_stats": (INT, [P, INT, U64P, U64P]),
+    "mxec_ctx_copy_stats": (INT, [P, INT, U64P, U64P, U64P, U64P]),
     "mxec_ctx_rs_grid": (INT, [P, INT, INT, INT, U64]),
     "mxec_ctx_coef_stats": (INT, [P, INT, U64P, U64P, U64P]),
     "mxec_host_alloc": (P, [P, ctypes.c_size_t]),

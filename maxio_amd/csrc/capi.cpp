@@ -150,7 +150,12 @@ int mxec_device_count(void) {
     return n;
 }
 
-mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
+namespace {
+// The one open path.  `logical` > 1 (mxec_open_test only) opens every
+// selected device that many times, each copy with its own slots, streams,
+// arenas, combiner and pipeline, so the multi-device paths (per-device
+// workers, round robin, error aggregation) run on a one-GPU box.
+mxec_ctx* open_ctx(uint32_t device_mask, int streams_per_device, const Knobs& kn) {
     try {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -158,13 +163,6 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
             return nullptr;
         }
         if (streams_per_device < 1) streams_per_device = 1;
-        // Every documented setting, read once (knobs.hpp).
-        // MXEC_TEST_LOGICAL_DEVICES=L (tests and bench rehearsals only): open
-        // every selected device L times, each copy with its own slots,
-        // streams, arenas, combiner and pipeline, so the multi-device paths
-        // (per-device workers, round robin, error aggregation) run on a
-        // one-GPU box.  Never meant for production: it warns on stderr.
-        Knobs kn = read_knobs();
         const int logical = kn.test_logical_devices;
         auto* ctx = new mxec_ctx();
         ctx->c.knobs = kn;
@@ -214,6 +212,30 @@ mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
         return nullptr;
     }
 }
+}  // namespace
+
+// Every documented setting is read once, here (knobs.hpp).
+mxec_ctx* mxec_open(uint32_t device_mask, int streams_per_device) {
+    return open_ctx(device_mask, streams_per_device, read_knobs());
+}
+
+// Test-only settings come as arguments, never from the environment, so no
+// variable a production host may carry can make one card pose as several
+// devices, cap the RS grid or shrink the coefficient arena.
+mxec_ctx* mxec_open_test(uint32_t device_mask, int streams_per_device, int logical_devices, uint32_t rs_grid_cap,
+                         uint64_t coef_arena_bytes) {
+    Knobs kn = read_knobs();
+    if (logical_devices < 1 || logical_devices > 8 || coef_arena_bytes > (uint64_t(64) << 20) ||
+        rs_grid_cap > (1u << 30)) {
+        set_error(MXEC_E_INVALID_ARG, "mxec_open_test: logical_devices 1..8, rs_grid_cap <= 2^30, "
+                                      "coef_arena_bytes <= 64 MiB");
+        return nullptr;
+    }
+    kn.test_logical_devices = logical_devices;
+    kn.test_rs_grid = rs_grid_cap;
+    kn.test_coef_arena = coef_arena_bytes & ~uint64_t(3);
+    return open_ctx(device_mask, streams_per_device, kn);
+}
 
 void mxec_close(mxec_ctx* ctx) {
     if (!ctx) return;
@@ -234,6 +256,18 @@ int mxec_ctx_device_count(const mxec_ctx* ctx) { return ctx ? int(ctx->c.devs.si
 int mxec_ctx_device_id(const mxec_ctx* ctx, int i) {
     if (!ctx || i < 0 || i >= int(ctx->c.devs.size())) return -1;
     return ctx->c.devs[size_t(i)]->id;
+}
+
+int mxec_ctx_copy_stats(mxec_ctx* ctx, int dev, uint64_t* copies_1d, uint64_t* copies_2d, uint64_t* rows_2d,
+                        uint64_t* wave_blocks) {
+    if (!ctx || dev < 0 || dev >= int(ctx->c.devs.size()))
+        return set_error(MXEC_E_INVALID_ARG, "mxec_ctx_copy_stats: no such device");
+    const Device& d = *ctx->c.devs[size_t(dev)];
+    if (copies_1d) *copies_1d = d.copies_1d.load();
+    if (copies_2d) *copies_2d = d.copies_2d.load();
+    if (rows_2d) *rows_2d = d.copies_2d_rows.load();
+    if (wave_blocks) *wave_blocks = d.copy_wave_blocks.load();
+    return MXEC_OK;
 }
 
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages) {

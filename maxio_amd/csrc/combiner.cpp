@@ -1,7 +1,8 @@
 // combiner.cpp — cross-request coalescing of SHA-256 verification.
 //
-// SHA-256 of one message is a serial chain (~1.8 us per 64-byte block on one
-// lane, sha256_kernel.hip), so a launch over 8 chunks of one GET takes as
+// SHA-256 of one message is a serial chain (1.27 us per 64-byte block in the
+// lag pair form, ~1.8 in the split form: kernels.hpp kShaLagUsPerBlock /
+// kShaSplitUsPerBlock, sha256_kernel.hip), so a launch over 8 chunks of one GET takes as
 // long as a launch over thousands: per-request launches leave the GPU nearly
 // idle and, past GPU_MAX_HW_QUEUES streams, even queue behind each other.
 // Concurrent callers on one device (MaxIO's tokio workers serving GETs, chunk
@@ -263,8 +264,8 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // are pending as the previous launch carried, so a steady stream of
         // concurrent callers keeps landing in few launches instead of a lone
         // first request and the rest; a lone leader waits a short window.  A
-        // launch lasts >= 1.8 us per 64-byte block of its longest message (29
-        // ms per 1 MiB chunk), so the wait costs a few percent at most, and
+        // launch lasts >= kShaLagUsPerBlock (1.27 us) per 64-byte block of its
+        // longest message (~21 ms per 1 MiB chunk), so the wait costs a few percent at most, and
         // the previous size is forgotten as soon as fewer come.
         const size_t want = c->last_batch;
         const Knobs& kn = knobs_of(d);
@@ -280,11 +281,12 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // 10 240-chunk verifications (config 3c) settled into two launches of
         // four (split form, 640 groups each) instead of one of 81 920
         // messages, which takes the stream form.  Only when the launch will
-        // be long next to the idle window: a chain takes ~1.8 us per 64-byte
-        // block of the longest pending message, and the extension is taken
+        // be long next to the idle window: a chain takes kShaLagUsPerBlock or
+        // kShaSplitUsPerBlock per 64-byte block of the longest pending message
+        // (launch_us below), and the extension is taken
         // only while one idle window costs at most 2 % of that, so small
-        // latency-bound verifications (64 KiB chunks: a ~1.8 ms launch) do
-        // not pay it, while 1 MiB chunks (~29 ms) still gather.
+        // latency-bound verifications (64 KiB chunks: a ~1.3 ms launch) do
+        // not pay it, while 1 MiB chunks (~21-28 ms) still gather.
         // (Stopping at the stream form's size instead split config 3c's
         // eight batches into launches of five and three: 585 vs 970 GiB/s.)
         // For such long launches the idle window grows to 2 % of the launch

@@ -9,8 +9,10 @@
 // copies into blocks of at most kCopyBlock bytes; a grid-stride loop walks
 // the blocks, each lane moving 16-byte vectors with four in flight (plain
 // loads of host memory; nontemporal stores into HBM, nontemporal loads of
-// HBM and plain stores into host memory for the download).  Blocks whose
-// ends or pointers are not 16-byte aligned take a byte loop.
+// HBM and plain stores into host memory for the download).  A block whose
+// two ends sit at the same offset modulo 16 moves its ragged head and tail
+// bytewise and the rest as vectors; the host sends segments whose ends
+// differ modulo 16 by SDMA (copy_phase_ok), so the byte loop is a fallback.
 #include "kernels.hpp"
 
 namespace mxec {
@@ -25,10 +27,16 @@ __global__ __launch_bounds__(kThreads) void copy_blocks(const CopyBlk* __restric
         const CopyBlk k = blks[b];
         const uint8_t* src = reinterpret_cast<const uint8_t*>(k.src);
         uint8_t* dst = reinterpret_cast<uint8_t*>(k.dst);
-        if (((k.src | k.dst | k.len) & 15) == 0) {
-            const u32x4* s = reinterpret_cast<const u32x4*>(src);
-            u32x4* d = reinterpret_cast<u32x4*>(dst);
-            const uint64_t nv = k.len / 16;
+        if (((k.src ^ k.dst) & 15) == 0) {
+            // Same phase modulo 16 on both sides: the ragged head and tail
+            // (< 16 bytes each) by single lanes, the aligned middle as
+            // 16-byte vectors -- a short last chunk or a caller pointer at an
+            // odd offset costs two bytes' loops, not a byte loop over the block.
+            const uint64_t head = std::min<uint64_t>((16 - (k.src & 15)) & 15, k.len);
+            if (threadIdx.x < head) dst[threadIdx.x] = src[threadIdx.x];
+            const u32x4* s = reinterpret_cast<const u32x4*>(src + head);
+            u32x4* d = reinterpret_cast<u32x4*>(dst + head);
+            const uint64_t nv = (k.len - head) / 16;
             uint64_t i = threadIdx.x;
             for (; i + 3 * kThreads < nv; i += 4 * kThreads) {
                 u32x4 v[4];
@@ -46,7 +54,11 @@ __global__ __launch_bounds__(kThreads) void copy_blocks(const CopyBlk* __restric
                 if (kToHost) d[i] = v;
                 else __builtin_nontemporal_store(v, d + i);
             }
+            const uint64_t done = head + nv * 16;
+            if (threadIdx.x < k.len - done) dst[done + threadIdx.x] = src[done + threadIdx.x];
         } else {
+            // Different phases (the host side sends such segments by SDMA
+            // instead, copy_phase_ok; kept for completeness).
             for (uint64_t i = threadIdx.x; i < k.len; i += kThreads) dst[i] = src[i];
         }
     }

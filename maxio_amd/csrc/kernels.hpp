@@ -52,7 +52,7 @@ struct RsArgs {
     // tuner, ops.cpp); 0 = rs_default_variant's.
     uint32_t blocks_per_cu = 0;
     // Every launch form: at most this many workgroups (0: no cap).  Tests
-    // (MXEC_TEST_RS_GRID) shrink the grid so each workgroup walks many tiles.
+    // (mxec_open_test rs_grid_cap) shrink the grid so each workgroup walks many tiles.
     uint32_t max_blocks = 0;
 };
 constexpr uint32_t kMultiR = 4;
@@ -226,5 +226,10 @@ struct alignas(16) CopyBlk {
 };
 constexpr uint64_t kCopyBlock = uint64_t(256) << 10;  // bytes per block (at most)
 hipError_t launch_copy_blocks(const CopyBlk* blks, uint64_t n, bool to_host, uint32_t grid, hipStream_t s);
+// Whether a host <-> device segment suits the wave copy: both ends at the
+// same offset modulo 16 (then only its head and tail bytes go bytewise).
+inline bool copy_phase_ok(const void* host, const void* dev) {
+    return ((reinterpret_cast<uintptr_t>(host) ^ reinterpret_cast<uintptr_t>(dev)) & 15) == 0;
+}
 
 }  // namespace mxec

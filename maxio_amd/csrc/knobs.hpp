@@ -12,11 +12,12 @@
 namespace mxec {
 
 struct Knobs {
-    // --- test-only (warn on stderr when set) -------------------------------
-    int test_logical_devices = 1;  // MXEC_TEST_LOGICAL_DEVICES: open each GPU N times (N <= 8)
-    uint32_t test_rs_grid = 0;     // MXEC_TEST_RS_GRID: cap on workgroups per RS launch (uniform,
-                                   //   grouped, multi-r, edge): every workgroup walks many tiles
-    uint64_t test_coef_arena = 0;  // MXEC_TEST_COEF_ARENA_KB: coefficient-table arena per half (bytes)
+    // --- test-only: set by mxec_open_test's arguments, never by the environment
+    int test_logical_devices = 1;  // open each GPU N times (N <= 8)
+    uint32_t test_rs_grid = 0;     // cap on workgroups per RS launch (uniform, grouped, multi-r,
+                                   //   edge): every workgroup walks many tiles
+    uint64_t test_coef_arena = 0;  // coefficient-table arena per half (bytes)
+    // --- debugging ------------------------------------------------------------
     bool debug_affinity = false;   // MXEC_DEBUG_AFFINITY: device-affinity checks on every launch
     // --- production ----------------------------------------------------------
     bool host_numa = false;        // MXEC_HOST_NUMA: mxec_host_alloc on the GPUs' NUMA node

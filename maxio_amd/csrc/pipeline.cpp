@@ -656,7 +656,9 @@ private:
     // instead of SDMA DMAs; they are collected here and issued as one launch
     // at the next point the stream is waited on or marked (issue_up /
     // issue_down).
-    bool wave_copy(const void* host, uint64_t len) const { return waves_now_ && pinned_mapped(host, len); }
+    bool wave_copy(const void* host, const void* dev, uint64_t len) const {
+        return waves_now_ && copy_phase_ok(host, dev) && pinned_mapped(host, len);
+    }
     bool waves_now_ = false;  // this call's copies of mxec_host_alloc memory go by waves
     static void add_blocks(std::vector<CopyBlk>& v, uint8_t* dst, const uint8_t* src, uint64_t len) {
         for (uint64_t o = 0; o < len; o += kCopyBlock)
@@ -677,6 +679,7 @@ private:
         if (const char* e = getenv("MXEC_PIPE_COPY_GRID")) grid = uint32_t(atoi(e));  // lab
 #endif
         MXEC_HIP(launch_copy_blocks(reinterpret_cast<const CopyBlk*>(h), v.size(), to_host, grid, s));
+        d_.copy_wave_blocks += v.size();
         v.clear();
         return MXEC_OK;
     }
@@ -694,12 +697,13 @@ private:
             const void* p = dst;
             MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload", &arena_, &p, 1));
         }
-        if (wave_copy(src, len)) {
+        if (wave_copy(src, dst, len)) {
             add_blocks(up_blks_, dst, src, len);
             return MXEC_OK;
         }
         if (is_pinned(src, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, h2d_));
+            ++d_.copies_1d;
             return MXEC_OK;
         }
         for (uint64_t off = 0; off < len; off += kRingBuf) {
@@ -708,6 +712,7 @@ private:
             MXEC_TRY(in_.take(&r));
             std::memcpy(in_.ptr(r), src + off, n);
             MXEC_HIP(hipMemcpyAsync(dst + off, in_.ptr(r), n, hipMemcpyHostToDevice, h2d_));
+            ++d_.copies_1d;
             MXEC_TRY(in_.mark(r, h2d_));
         }
         return MXEC_OK;
@@ -782,6 +787,8 @@ private:
                 MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload 2d", &arena_, &p, 1));
             }
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyHostToDevice, h2d_));
+            ++d_.copies_2d;
+            d_.copies_2d_rows += r.rows;
             return MXEC_OK;
         }
         for (uint64_t i = 0; i < r.rows; ++i) MXEC_TRY(upload(r.dst + i * r.dpitch, r.src + i * r.spitch, r.len));
@@ -805,6 +812,8 @@ private:
                 MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download 2d", &arena_, &p, 1));
             }
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyDeviceToHost, d2h_));
+            ++d_.copies_2d;
+            d_.copies_2d_rows += r.rows;
             return MXEC_OK;
         }
         for (uint64_t i = 0; i < r.rows; ++i) MXEC_TRY(download(r.dst + i * r.dpitch, r.src + i * r.spitch, r.len));
@@ -830,12 +839,13 @@ private:
             const void* p = src;
             MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download", &arena_, &p, 1));
         }
-        if (wave_copy(dst, len)) {
+        if (wave_copy(dst, src, len)) {
             add_blocks(down_blks_, dst, src, len);
             return MXEC_OK;
         }
         if (is_pinned(dst, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, d2h_));
+            ++d_.copies_1d;
             return MXEC_OK;
         }
         for (uint64_t off = 0; off < len; off += kRingBuf) {
@@ -844,6 +854,7 @@ private:
             int r;
             MXEC_TRY(out_.take(&r));
             MXEC_HIP(hipMemcpyAsync(out_.ptr(r), src + off, n, hipMemcpyDeviceToHost, d2h_));
+            ++d_.copies_1d;
             MXEC_TRY(out_.mark(r, d2h_));
             pend_.push_back(Pending{r, dst + off, n});
         }

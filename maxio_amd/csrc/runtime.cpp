@@ -100,27 +100,39 @@ bool hip_says_pinned(const void* p) {
     return at.type == hipMemoryTypeHost;
 }
 
-std::mutex g_pinned_mu;
-std::map<uintptr_t, size_t> g_pinned;  // base -> bytes (mxec_host_alloc)
+// base -> bytes (mxec_host_alloc).  Never destroyed: a caller may free its
+// page-locked buffers from its own exit handlers, after this library's
+// static destructors would have run.
+struct PinnedSet {
+    std::mutex mu;
+    std::map<uintptr_t, size_t> map;
+};
+PinnedSet& pinned_set() {
+    static PinnedSet* p = new PinnedSet();
+    return *p;
+}
 }  // namespace
 
 void pinned_register(const void* p, size_t n) {
-    std::lock_guard<std::mutex> g(g_pinned_mu);
-    g_pinned[reinterpret_cast<uintptr_t>(p)] = n;
+    PinnedSet& ps = pinned_set();
+    std::lock_guard<std::mutex> g(ps.mu);
+    ps.map[reinterpret_cast<uintptr_t>(p)] = n;
 }
 
 void pinned_unregister(const void* p) {
-    std::lock_guard<std::mutex> g(g_pinned_mu);
-    g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+    PinnedSet& ps = pinned_set();
+    std::lock_guard<std::mutex> g(ps.mu);
+    ps.map.erase(reinterpret_cast<uintptr_t>(p));
 }
 
 bool pinned_range(const void* p, uint64_t len) {
     if (!p || !len) return false;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     {
-        std::lock_guard<std::mutex> g(g_pinned_mu);
-        auto it = g_pinned.upper_bound(a);
-        if (it != g_pinned.begin()) {
+        PinnedSet& ps = pinned_set();
+        std::lock_guard<std::mutex> g(ps.mu);
+        auto it = ps.map.upper_bound(a);
+        if (it != ps.map.begin()) {
             --it;
             if (a - it->first < it->second) return len <= it->second - (a - it->first);
         }
@@ -131,9 +143,10 @@ bool pinned_range(const void* p, uint64_t len) {
 bool pinned_mapped(const void* p, uint64_t len) {
     if (!p || !len) return false;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    std::lock_guard<std::mutex> g(g_pinned_mu);
-    auto it = g_pinned.upper_bound(a);
-    if (it == g_pinned.begin()) return false;
+    PinnedSet& ps = pinned_set();
+    std::lock_guard<std::mutex> g(ps.mu);
+    auto it = ps.map.upper_bound(a);
+    if (it == ps.map.begin()) return false;
     --it;
     return a - it->first < it->second && len <= it->second - (a - it->first);
 }
@@ -164,7 +177,8 @@ int upload_segments(Slot& slot, hipStream_t s, uint8_t* dev_base, const std::vec
     if (segs.empty()) return MXEC_OK;
     if (waves) {
         bool mapped = true;
-        for (const auto& g : segs) mapped = mapped && (g.len == 0 || pinned_mapped(g.src, g.len));
+        for (const auto& g : segs)
+            mapped = mapped && (g.len == 0 || (pinned_mapped(g.src, g.len) && copy_phase_ok(g.src, dev_base + g.dst_off)));
         if (mapped) {
             std::vector<CopyBlk> blks;
             for (const auto& g : segs)
@@ -235,7 +249,8 @@ int download_segments(Slot& slot, hipStream_t s, const uint8_t* dev_base, const 
     if (segs.empty()) return slot_wait(slot, s);
     if (waves) {
         bool mapped = true;
-        for (const auto& g : segs) mapped = mapped && (g.len == 0 || pinned_mapped(g.dst, g.len));
+        for (const auto& g : segs)
+            mapped = mapped && (g.len == 0 || (pinned_mapped(g.dst, g.len) && copy_phase_ok(g.dst, dev_base + g.src_off)));
         if (mapped) {
             std::vector<CopyBlk> blks;
             for (const auto& g : segs)

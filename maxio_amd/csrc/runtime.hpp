@@ -200,7 +200,7 @@ struct Device {
     std::atomic<unsigned> next_slot{0};
     // Coefficient tables (gf256.hpp coef_tables) for every matrix in use,
     // keyed by matrix identity; uploaded once, read by every launch.  The
-    // arena is two halves (kCoefArenaDwords each, or MXEC_TEST_COEF_ARENA_KB):
+    // arena is two halves (kCoefArenaDwords each, or mxec_open_test coef_arena_bytes):
     // generation g fills half g & 1; when it is full, generation g + 1 takes
     // the other half, after waiting for the events that fence the launches
     // which read that half's tables (generation g - 1) -- no device-wide
@@ -246,6 +246,9 @@ struct Device {
     // created on first use and kept, one batch at a time per device.
     std::mutex pipe_mu;
     std::shared_ptr<void> pipe;
+    // Copies the host pipeline issued (mxec_ctx_copy_stats): 1D SDMA DMAs,
+    // 2D SDMA DMAs and their rows, CU-wave copy blocks (copy_kernel.hip).
+    std::atomic<uint64_t> copies_1d{0}, copies_2d{0}, copies_2d_rows{0}, copy_wave_blocks{0};
     // SHA-256 combiner (combiner.cpp): one launch for the verification work
     // of every concurrent caller on this device.
     std::mutex comb_mu;
@@ -371,7 +374,7 @@ Device* pick_device(Ctx* ctx, int dev_index);
 // that the HIP current device, the stream, the slot, the descriptor arena and
 // the data pointers all belong to the device doing the work.  Internal
 // streams are tagged with their (logical) device when created, so on
-// MXEC_TEST_LOGICAL_DEVICES runs -- one card presented as several devices,
+// mxec_open_test logical-device runs -- one card presented as several devices,
 // where physical ids cannot tell them apart -- a stream, slot or arena of
 // another logical device is still caught.  A violation fails the call with
 // MXEC_E_DEVICE; mxec_close prints the running totals to stderr.

@@ -144,9 +144,22 @@ def version() -> str:
 class Context:
     """An ``mxec_ctx``: every visible MI355X (or the ones in device_mask)."""
 
-    def __init__(self, device_mask: int = 0, streams_per_device: int = 2):
+    def __init__(self, device_mask: int = 0, streams_per_device: int = 2, test: Optional[dict] = None):
+        """``test`` (tests and bench rehearsals only) opens through
+        mxec_open_test: ``logical_devices`` (open each GPU N times),
+        ``rs_grid`` (cap every RS launch at N workgroups), ``coef_arena_kb``
+        (KiB per half of the coefficient arena)."""
         self._lib = N.lib()
-        self._h = self._lib.mxec_open(device_mask, streams_per_device)
+        self._host = {}  # mxec_host_alloc arrays: id(buffer) -> (pointer, finalizer)
+        if test:
+            unknown = set(test) - {"logical_devices", "rs_grid", "coef_arena_kb"}
+            if unknown:
+                raise ValueError(f"unknown test options {sorted(unknown)}")
+            self._h = self._lib.mxec_open_test(
+                device_mask, streams_per_device, int(test.get("logical_devices", 1)),
+                int(test.get("rs_grid", 0)), int(test.get("coef_arena_kb", 0)) << 10)
+        else:
+            self._h = self._lib.mxec_open(device_mask, streams_per_device)
         if not self._h:
             raise RSError(-32, self._lib.mxec_last_error().decode())
 
@@ -185,6 +198,13 @@ class Context:
         _check(self._lib.mxec_ctx_coef_stats(self._h, dev, ctypes.byref(r), ctypes.byref(q), ctypes.byref(w)))
         return {"recycles": r.value, "relaunches": q.value, "fence_waits": w.value}
 
+    def copy_stats(self, dev: int = 0) -> dict:
+        """Copies the host-batch pipeline issued on device `dev` since the
+        context opened (mxec_ctx_copy_stats)."""
+        v = [ctypes.c_uint64(0) for _ in range(4)]
+        _check(self._lib.mxec_ctx_copy_stats(self._h, dev, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("copies_1d", "copies_2d", "rows_2d", "wave_blocks"), (x.value for x in v)))
+
     def rs_grid(self, k: int, m: int, shard_size: int, dev: int = 0) -> int:
         """Workgroups per CU large uniform RS launches of this shape run at on
         device `dev` (the grid tuner's pick; 0 while still tuning)."""
@@ -195,18 +215,30 @@ class Context:
 
     def host_array(self, n: int) -> np.ndarray:
         """A uint8 array of n bytes in page-locked memory (mxec_host_alloc):
-        uploads from it and downloads into it skip the staging copy.  The
-        memory is freed when the array is garbage collected."""
+        uploads from it and downloads into it skip the staging copy.  Free it
+        with host_free(); otherwise it is freed when the array is garbage
+        collected -- but never from an interpreter-exit callback (the HIP
+        runtime may be tearing down by then): memory still held at exit goes
+        back with the process."""
         p = self._lib.mxec_host_alloc(self._h, max(1, n))
         if not p:
             raise MemoryError("mxec_host_alloc failed")
         buf = (ctypes.c_uint8 * max(1, n)).from_address(p)
         a = np.frombuffer(buf, dtype=np.uint8, count=n)
-        lib, h = self._lib, self._h
         import weakref
 
-        weakref.finalize(buf, lib.mxec_host_free, h, p)
+        fin = weakref.finalize(buf, self._lib.mxec_host_free, None, p)
+        fin.atexit = False
+        self._host = {q: f for q, f in self._host.items() if f.alive}
+        self._host[p] = fin
         return a
+
+    def host_free(self, a: np.ndarray) -> None:
+        """Free a host_array now (the array must not be used afterwards)."""
+        fin = self._host.pop(a.ctypes.data, None)
+        if fin is None:
+            raise ValueError("not a host_array of this context (or already freed)")
+        fin()
 
     def device_ids(self) -> list[int]:
         n = self._lib.mxec_ctx_device_count(self._h)

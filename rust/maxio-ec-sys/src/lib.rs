@@ -131,10 +131,15 @@ extern "C" {
     pub fn mxec_last_error() -> *const c_char;
     pub fn mxec_device_count() -> c_int;
     pub fn mxec_open(device_mask: u32, streams_per_device: c_int) -> *mut MxecCtx;
+    /// Test-only open (tests drive the multi-device and grid-stride paths with it).
+    pub fn mxec_open_test(device_mask: u32, streams_per_device: c_int, logical_devices: c_int, rs_grid_cap: u32,
+                          coef_arena_bytes: u64) -> *mut MxecCtx;
     pub fn mxec_close(ctx: *mut MxecCtx);
     pub fn mxec_ctx_device_count(ctx: *const MxecCtx) -> c_int;
     pub fn mxec_ctx_device_id(ctx: *const MxecCtx, i: c_int) -> c_int;
     pub fn mxec_ctx_combiner_stats(ctx: *mut MxecCtx, i: c_int, launches: *mut u64, messages: *mut u64) -> c_int;
+    pub fn mxec_ctx_copy_stats(ctx: *mut MxecCtx, dev: c_int, copies_1d: *mut u64, copies_2d: *mut u64,
+                               rows_2d: *mut u64, wave_blocks: *mut u64) -> c_int;
     pub fn mxec_ctx_rs_grid(ctx: *mut MxecCtx, dev: c_int, k: c_int, m: c_int, shard_size: u64) -> c_int;
     pub fn mxec_ctx_coef_stats(ctx: *mut MxecCtx, dev: c_int, recycles: *mut u64, relaunches: *mut u64,
                                fence_waits: *mut u64) -> c_int;

@@ -6,7 +6,8 @@
 # Steps (each under its own time limit; the first failure ends the call):
 #   tests     full `pytest -m gpu` (one process) -> pytest_gpu.log
 #   smoke     __graft_entry__.smoke()
-#   bench     the driver's default command: python bench.py -> bench.json
+#   bench     the driver's command: python bench.py (defaults --gpus 1 --steps 20
+#             --warmup 5) -> bench.json
 #   refuse2   python bench.py --gpus 2 on a one-GPU box: must exit 2, no line
 #   rehearse  BENCH_REHEARSE_LOGICAL=1 bench.py --gpus 2 (labelled in-process
 #             multi-device rehearsal on two logical devices of the one card)
@@ -15,7 +16,8 @@
 #             (BENCH_GPU_OF_RANK=0, gloo for the timing collectives)
 #   prof      rocprofv3 --kernel-trace --stats of the default bench command
 #   trace     rocprofv3 --kernel-trace --memory-copy-trace of the default bench
-#             with BENCH_GET_STAMPS=1; tools/get_trace_summary.py lines the
+#             with BENCH_GET_STAMPS=1 and BENCH_DUMP_MAPS=1 (the DSO map on
+#             stderr before teardown); tools/get_trace_summary.py lines the
 #             timed GET batches up with the trace -> get_trace_summary.json
 #   pmc       FETCH_SIZE / WRITE_SIZE passes (one run each) of rs_apply_fast
 #             for configs 2 and ns at every grid the tuner can pick (2: 1024 /
@@ -69,9 +71,11 @@ for st in "${STEPS[@]}"; do
           -- python3 "$R/bench.py" $BENCH_ARGS > "$O/prof_bench.json" 2> "$O/prof_bench.err" ) || { tail -20 "$O/prof_bench.err"; exit 1; }
       find /tmp/prof -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats.csv" \;
       find /tmp/prof -name "*kernel_trace.csv" -exec cp {} "$O/kernel_trace.csv" \;
+      python tools/headline_timed.py "$O/kernel_trace.csv" "$O/prof_bench.json" --out "$O/headline_timed.json" || exit 1
+      gzip -f "$O/kernel_trace.csv"
       cat "$O/prof_bench.json" ;;
     trace)
-      ( cd /tmp && BENCH_GET_STAMPS=1 timeout -k 10 900 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/trace \
+      ( cd /tmp && BENCH_GET_STAMPS=1 BENCH_DUMP_MAPS=1 timeout -k 10 900 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/trace \
           -o run --output-format csv -- python3 "$R/bench.py" $BENCH_ARGS > "$O/trace_bench.json" \
           2> "$O/trace_bench.err" ) || { tail -20 "$O/trace_bench.err"; exit 1; }
       kt=$(find /tmp/trace -name "*kernel_trace.csv" -print -quit); mt=$(find /tmp/trace -name "*memory_copy_trace.csv" -print -quit)

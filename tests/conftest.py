@@ -51,12 +51,19 @@ def ctx():
     c.close()
 
 
+TEST_OPTIONS = {"MXEC_TEST_LOGICAL_DEVICES": "logical_devices", "MXEC_TEST_RS_GRID": "rs_grid",
+                "MXEC_TEST_COEF_ARENA_KB": "coef_arena_kb"}
+
+
 def open_ctx(streams=2, device_mask=0, **env):
     """A context opened with MXEC_* settings: the library reads its knobs
     once, at mxec_open (maxio_amd/csrc/knobs.cpp), so a test that changes
-    one opens its own context.  Values None / "" unset the variable."""
+    one opens its own context.  Values None / "" unset the variable.  The
+    MXEC_TEST_* names are not environment variables: they become
+    mxec_open_test arguments (Context(test=...))."""
     import maxio_amd
 
+    test = {TEST_OPTIONS[k]: int(env.pop(k)) for k in list(env) if k in TEST_OPTIONS}
     saved = {k: os.environ.get(k) for k in env}
     try:
         for k, v in env.items():
@@ -64,7 +71,7 @@ def open_ctx(streams=2, device_mask=0, **env):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = str(v)
-        return maxio_amd.Context(device_mask=device_mask, streams_per_device=streams)
+        return maxio_amd.Context(device_mask=device_mask, streams_per_device=streams, test=test or None)
     finally:
         for k, v in saved.items():
             if v is None:

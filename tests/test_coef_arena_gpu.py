@@ -5,7 +5,7 @@ Every RS launch reads its matrix from a per-device table arena of two
 halves; when the current half is full, the next generation takes the other
 half after waiting only for the events that fence the launches which read
 it (no device-wide wait).  A test-only arena of a few KiB
-(MXEC_TEST_COEF_ARENA_KB, read at mxec_open) makes that happen every few
+(mxec_open_test coef_arena_bytes) makes that happen every few
 batches:
 
 * four host threads, each on its own stream, rebuild batches whose seeded

@@ -7,7 +7,7 @@ object checked (not a sample):
   chunks, encoded then reconstructed with 1..m seeded erasures in one stream,
   per class (the bench's layout) and as one mixed-shape launch;
 * configs[3] — 10+4 at 1 MiB, one object per device, on eight logical
-  devices of one GPU (MXEC_TEST_LOGICAL_DEVICES=8, each with its own streams,
+  devices of one GPU (mxec_open_test logical_devices=8, each with its own streams,
   arenas and pipeline, as MaxIO's one process would open eight MI355X), and
   the literal reading k=64 m=4.
 
@@ -152,10 +152,8 @@ def ctx8(monkeypatch, capfd):
     on (MXEC_DEBUG_AFFINITY: every launch and copy asserts that its stream,
     slot, arena and pointers belong to the launching logical device); the
     totals printed at close must show checks and no violation."""
-    monkeypatch.setenv("MXEC_TEST_LOGICAL_DEVICES", "8")
     monkeypatch.setenv("MXEC_DEBUG_AFFINITY", "1")
-    c = maxio_amd.Context(device_mask=1, streams_per_device=1)
-    monkeypatch.delenv("MXEC_TEST_LOGICAL_DEVICES")
+    c = maxio_amd.Context(device_mask=1, streams_per_device=1, test={"logical_devices": 8})
     assert c.device_ids() == [0] * 8
     yield c
     c.close()

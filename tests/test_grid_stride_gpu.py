@@ -5,7 +5,7 @@ rs_apply_multi, rs_apply_edge).  At BASELINE sizes most bytes are carried by
 iterations >= 2 (configs[1]: 655 360 tiles over <= 262 144 workgroups), and
 the grouped kernels prefetch the NEXT iteration's tile record
 (`next = tiles[tile + gridDim.x]`).  Here the context caps every RS launch at
-a handful of workgroups (MXEC_TEST_RS_GRID, read at mxec_open), so each
+a handful of workgroups (mxec_open_test rs_grid_cap), so each
 workgroup walks dozens of tiles across object boundaries, and EVERY object's
 outputs are compared with the oracle:
 

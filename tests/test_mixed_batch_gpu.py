@@ -269,10 +269,8 @@ def ctx8(monkeypatch, capfd):
     totals printed at close must show checks and no violation."""
     import maxio_amd
 
-    monkeypatch.setenv("MXEC_TEST_LOGICAL_DEVICES", "8")
     monkeypatch.setenv("MXEC_DEBUG_AFFINITY", "1")
-    c = maxio_amd.Context(device_mask=1, streams_per_device=1)
-    monkeypatch.delenv("MXEC_TEST_LOGICAL_DEVICES")
+    c = maxio_amd.Context(device_mask=1, streams_per_device=1, test={"logical_devices": 8})
     assert c.device_ids() == [0] * 8
     yield c
     c.close()

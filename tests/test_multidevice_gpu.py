@@ -1,5 +1,5 @@
 """GPU: the in-process multi-device paths of one mxec_ctx, run on a one-GPU
-box by opening device 0 as two logical devices (MXEC_TEST_LOGICAL_DEVICES=2, each
+box by opening device 0 as two logical devices (mxec_open_test logical_devices=2, each
 with its own slots, streams, coefficient arena, combiner and pipeline):
 
 * mxec_encode_batch_host deals objects to per-device workers (o mod D,
@@ -29,9 +29,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture()
 def ctx2(monkeypatch):
-    monkeypatch.setenv("MXEC_TEST_LOGICAL_DEVICES", "2")
-    c = maxio_amd.Context(device_mask=1, streams_per_device=3)
-    monkeypatch.delenv("MXEC_TEST_LOGICAL_DEVICES")
+    c = maxio_amd.Context(device_mask=1, streams_per_device=3, test={"logical_devices": 2})
     assert c.device_ids() == [0, 0]
     yield c
     c.close()

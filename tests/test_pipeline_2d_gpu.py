@@ -1,0 +1,143 @@
+"""GPU: the host pipeline's default copy forms on mxec_host_alloc buffers,
+object for object against the oracle (reference: the PUT's parity and
+digests, filesystem.rs:1107-1135; the GET's rebuild, chunk_reader.rs:157-226).
+
+* PUT with digests in 2 / 4 MiB pieces (MXEC_PIPE_PIECE_MB, product knob) and
+  with the piece size chosen per wave at a batch large enough to be
+  upload-bound: the same piece of an object's k data chunks goes up as one
+  2D SDMA copy (pipeline.cpp flush_up), its m parity pieces come down as
+  one (flush_down).  mxec_ctx_copy_stats proves the 2D copies ran.  Shards
+  off the piece grid; a short and an empty last data chunk break the 2D run
+  in the middle of the batch.  EVERY object's parity and all k+m digests
+  equal oracle.compute_parity.
+* The GET's CU-wave copies (MXEC_PIPE_COPY auto) with ragged lengths and
+  with caller pointers at odd offsets: a segment whose host and device ends
+  sit at different offsets modulo 16 goes by SDMA instead (copy_phase_ok),
+  one at the same offset moves its head / tail bytewise and the rest as
+  vectors (copy_kernel.hip).  Rebuilt shards equal the originals.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+M = 1 << 20
+
+
+def _random(ctx, shape, seed):
+    a = ctx.host_array(int(np.prod(shape))).reshape(shape)
+    rng = np.random.default_rng(seed)
+    flat = a.reshape(-1)
+    step = 256 * M
+    for o in range(0, flat.size, step):
+        n = min(step, flat.size - o)
+        flat[o:o + n] = np.frombuffer(rng.bytes(n), np.uint8)
+    return a
+
+
+def _put_and_check(ctx, n, S, seed, short=None):
+    """n x 4+2 objects of shard size S from host_array memory, PUT with
+    digests; `short` maps object -> length of its last data chunk.  Returns
+    the copy-statistics delta."""
+    k, m = 4, 2
+    short = short or {}
+    data = _random(ctx, (n, k, S), seed)
+    par = ctx.host_array(n * m * S).reshape(n, m, S)
+    par[:] = 0xEE
+    dlen = []
+    for o in range(n):
+        dlen += [S] * (k - 1) + [short.get(o, S)]
+    objs = [(k, m, S)] * n
+    dptr = [data[o, j].ctypes.data for o in range(n) for j in range(k)]
+    pptr = [par[o, i].ctypes.data for o in range(n) for i in range(m)]
+    dig = np.zeros(n * (k + m) * 32, np.uint8)
+    before = ctx.copy_stats()
+    status = ctx.encode_batch_host(objs, dptr, pptr, data_len=dlen, digests=dig)
+    after = ctx.copy_stats()
+    assert (status == 0).all()
+
+    def check(o):
+        chunks = [data[o, j, :dlen[o * k + j]] for j in range(k)]
+        # SHA-NI digests for the big batch (pinned to the scalar form and
+        # FIPS 180-4 in tests/test_oracle.py); the oracle releases the GIL.
+        want, want_dig, rc = oracle.compute_parity(chunks, m, S, sha_ni=n >= 100)
+        assert rc == 0
+        for i in range(m):
+            assert np.array_equal(par[o, i], want[i]), (o, i)
+        got = [dig[(o * (k + m) + t) * 32:(o * (k + m) + t + 1) * 32].tobytes() for t in range(k + m)]
+        assert got == want_dig, o
+
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(8) as ex:
+        list(ex.map(check, range(n)))
+    ctx.host_free(data)
+    ctx.host_free(par)
+    return {key: after[key] - before[key] for key in after}
+
+
+@pytest.mark.parametrize("piece_mb", ["2", "4"])
+def test_put_2d_piece_copies_forced_piece(ctx_with, piece_mb):
+    """24 objects, 5 MiB + 4160-byte shards (two or three pieces per chunk,
+    the last off the grid); object 7's last data chunk ends mid-piece
+    (3 MiB + 11), object 13's is empty."""
+    ctx = ctx_with(MXEC_PIPE_PIECE_MB=piece_mb)
+    S = 5 * M + 4160
+    d = _put_and_check(ctx, 24, S, 501 + int(piece_mb), short={7: 3 * M + 11, 13: 0})
+    assert d["copies_2d"] > 0 and d["rows_2d"] >= 2 * d["copies_2d"], d
+
+
+def test_put_2d_piece_copies_default_upload_bound(ctx):
+    """The default piece choice at a batch whose upload outlasts one chunk's
+    chain (200 x 4+2 x 5 MiB: ~4.2 GB up against a ~105 ms chain), so the
+    wave takes 2 or 4 MiB pieces and 2D copies; two ragged objects."""
+    S = 5 * M + 4160
+    d = _put_and_check(ctx, 200, S, 777, short={0: S - 1, 99: 2 * M + 5, 150: 0})
+    assert d["copies_2d"] > 0, d
+
+
+@pytest.mark.parametrize("copy", ["auto", "waves"])
+@pytest.mark.parametrize("offset", [0, 3, 16 + 5])
+def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset):
+    """Verified GET of 6 x 4+2 objects whose shards start `offset` bytes into
+    page-locked memory and whose last data chunk is S - 3333 bytes: every
+    rebuilt shard equals the original; aligned callers take the wave copies
+    (wave_blocks counted), phase-mismatched ones fall back to SDMA."""
+    ctx = ctx_with(MXEC_PIPE_COPY=copy)
+    k, m, n = 4, 2, 6
+    S = 2 * M + 4096 + 48
+    rng = np.random.default_rng(900 + offset)
+    slot = S + 64
+    buf = ctx.host_array(n * (k + m) * slot + 64)
+    buf[:] = np.frombuffer(rng.bytes(buf.size), np.uint8)
+    shard = [[buf[offset + (o * (k + m) + i) * slot:][:S] for i in range(k + m)] for o in range(n)]
+    dl = [S] * (k - 1) + [S - 3333]
+    objs = [(k, m, S)] * n
+    dig = np.zeros(n * (k + m) * 32, np.uint8)
+    st = ctx.encode_batch_host(objs, [shard[o][j].ctypes.data for o in range(n) for j in range(k)],
+                               [shard[o][k + i].ctypes.data for o in range(n) for i in range(m)],
+                               data_len=dl * n, digests=dig)
+    assert (st == 0).all()
+    ref = [[shard[o][i][:dl[i] if i < k else S].copy() for i in range(k + m)] for o in range(n)]
+    present = np.ones((n, k + m), np.uint8)
+    for o in range(n):
+        for i in rng.choice(k + m, 2, replace=False):
+            present[o, i] = 0
+            shard[o][i][:] = 0x5A
+    before = ctx.copy_stats()
+    pr = present.reshape(-1).copy()
+    rc, st = ctx.reconstruct_batch_host(objs, [shard[o][i].ctypes.data for o in range(n) for i in range(k + m)],
+                                        pr, shard_len=(dl + [S] * m) * n, expected=dig)
+    after = ctx.copy_stats()
+    assert rc == 0 and not st.any() and pr.all()
+    for o in range(n):
+        for i in range(k + m):
+            L = dl[i] if i < k else S
+            assert np.array_equal(shard[o][i][:L], ref[o][i]), (copy, offset, o, i)
+    if offset % 16 == 0:
+        assert after["wave_blocks"] > before["wave_blocks"], (before, after)
+    ctx.host_free(buf)
