@@ -32,8 +32,8 @@ int encode_coef(Device& dev, int k, int m, uint32_t* off) {
         std::lock_guard<std::mutex> g(dev.coef_mu);
         auto it = dev.coef_index.find(key);
         if (it != dev.coef_index.end()) {
-            *off = it->second.first;
-            coef_note_use(it->second.second);
+            *off = it->second.off;
+            coef_note_use(it->second.gen, it->second.seq);
             return MXEC_OK;
         }
     }
@@ -73,7 +73,7 @@ int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_onl
         if (it != dev.patterns.end()) {
             *plan = std::static_pointer_cast<const DecodePlan>(it->second.plan);
             *off = it->second.off;
-            if (!(*plan)->missing.empty()) coef_note_use(it->second.gen);
+            if (!(*plan)->missing.empty()) coef_note_use(it->second.gen, it->second.seq);
             return MXEC_OK;
         }
     }
@@ -86,14 +86,14 @@ int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_onl
         const int rc = decode_coef(dev, *p, data_only, &o);
         coef_use_swap(outer);
         MXEC_TRY(rc);
-        coef_note_use(mine.lo);
+        coef_note_use(mine.lo, mine.seq);
     }
     {
         std::lock_guard<std::mutex> g(dev.coef_mu);
         // Only remember the offset while its generation is live (a recycle
         // may have come between the upload and here).
         const uint64_t gen = mine.any() ? mine.lo : dev.coef_gen;
-        if (gen + 1 >= dev.coef_gen) dev.patterns.emplace(key, Device::PatternVal{p, o, gen});
+        if (gen + 1 >= dev.coef_gen) dev.patterns.emplace(key, Device::PatternVal{p, o, gen, mine.seq});
     }
     *plan = p;
     *off = o;

@@ -182,8 +182,9 @@ inline std::string too_few_msg(int present, int k, int total) {
 
 // Coefficient-table offsets are valid while their generation's half of the
 // device's table arena is not reused (runtime.hpp Device::coef_*): `collect`
-// takes a batch's offsets (noting each table's generation), `launch`
-// enqueues the kernels that read them on `s`; then, under the arena's lock,
+// takes a batch's offsets (noting each table's generation and upload),
+// `s` waits on the GPU for any of those tables still being uploaded,
+// `launch` enqueues the kernels that read them on `s`; then, under the arena's lock,
 // either every generation used is still live and an event on `s` fences the
 // batch (a later recycle of those halves waits for it), or one was recycled
 // between `collect` and here, and the pair runs again.  A launch queued with
@@ -197,6 +198,7 @@ int with_stable_coef(Device& d, hipStream_t s, C&& collect, L&& launch) {
         CoefUse use;
         CoefUse* outer = coef_use_swap(&use);
         int rc = collect();
+        if (rc == MXEC_OK) rc = coef_wait_uploads(d, use, s);  // tables still on their way up
         if (rc == MXEC_OK) rc = launch();
         coef_use_swap(outer);
         MXEC_TRY(rc);

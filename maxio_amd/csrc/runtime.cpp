@@ -431,10 +431,11 @@ void coef_prune(Device& dev, int h) {
 }
 }  // namespace
 
-void coef_note_use(uint64_t gen) {
+void coef_note_use(uint64_t gen, uint64_t seq) {
     if (!t_coef_use) return;
     t_coef_use->lo = std::min(t_coef_use->lo, gen);
     t_coef_use->hi = std::max(t_coef_use->hi, gen);
+    t_coef_use->seq = std::max(t_coef_use->seq, seq);
 }
 
 CoefUse* coef_use_swap(CoefUse* u) {
@@ -443,54 +444,139 @@ CoefUse* coef_use_swap(CoefUse* u) {
     return p;
 }
 
-int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<uint32_t>& table,
-                uint32_t* off) {
-    std::lock_guard<std::mutex> g(dev.coef_mu);
-    auto it = dev.coef_index.find(key);
-    if (it != dev.coef_index.end()) {
-        *off = it->second.first;
-        coef_note_use(it->second.second);
+namespace {
+// An event from the spare list (or a new one).  Under coef_mu.
+int coef_take_event(Device& dev, hipEvent_t* e) {
+    if (!dev.coef_free.empty()) {
+        *e = dev.coef_free.back();
+        dev.coef_free.pop_back();
         return MXEC_OK;
     }
-    if (!dev.coef.p) {
-        const uint64_t test = dev.kn ? dev.kn->test_coef_arena : 0;
-        dev.coef_half = test ? size_t(test / 4) : kCoefArenaDwords;
-        MXEC_TRY(dev.coef.ensure(dev.coef_half * 2 * 4));
-        dev.coef_used = 0;
+    MXEC_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return MXEC_OK;
+}
+
+// First use of the device's arena: the device halves, the table stream and
+// its event.  Under coef_mu.
+int coef_init(Device& dev) {
+    const uint64_t test = dev.kn ? dev.kn->test_coef_arena : 0;
+    dev.coef_half = test ? size_t(test / 4) : kCoefArenaDwords;
+    MXEC_TRY(dev.coef.ensure(dev.coef_half * 2 * 4));
+    dev.coef_used = 0;
+    dev.coef_mirror_chunk = std::min(dev.coef_half * 2, size_t(1) << 18);  // <= 1 MiB
+    dev.coef_mirror.resize((dev.coef_half * 2 + dev.coef_mirror_chunk - 1) / dev.coef_mirror_chunk);
+    if (!dev.coef_stream) {
+        MXEC_HIP(hipStreamCreateWithFlags(&dev.coef_stream, hipStreamNonBlocking));
+        affinity_tag(dev.coef_stream, &dev);
     }
-    if (table.size() > dev.coef_half)
-        return set_error(MXEC_E_INVALID_ARG, "coefficient table larger than the arena");
-    if (dev.coef_used + table.size() > dev.coef_half) {
+    if (!dev.coef_uploaded) MXEC_HIP(hipEventCreateWithFlags(&dev.coef_uploaded, hipEventDisableTiming));
+    return MXEC_OK;
+}
+
+// Queue dwords [o, o + n) of the arena's mirror up to the device.  Under
+// coef_mu; nothing here waits for the device.
+int coef_upload(Device& dev, uint32_t o, const std::vector<uint32_t>& table) {
+    const size_t C = dev.coef_mirror_chunk;
+    for (size_t done = 0; done < table.size();) {
+        const size_t at = size_t(o) + done, c = at / C, in = at % C;
+        const size_t n = std::min(table.size() - done, C - in);
+        PinnedBuf& chunk = dev.coef_mirror[c];
+        if (!chunk.p) MXEC_TRY(chunk.ensure(C * 4));
+        uint32_t* h = static_cast<uint32_t*>(chunk.p) + in;
+        std::memcpy(h, table.data() + done, n * 4);
+        MXEC_HIP(hipMemcpyAsync(static_cast<uint32_t*>(dev.coef.p) + at, h, n * 4, hipMemcpyHostToDevice,
+                                dev.coef_stream));
+        done += n;
+    }
+    MXEC_HIP(hipEventRecord(dev.coef_uploaded, dev.coef_stream));
+    ++dev.coef_seq;
+    ++dev.coef_uploads;
+    return MXEC_OK;
+}
+}  // namespace
+
+int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<uint32_t>& table,
+                uint32_t* off) {
+    std::unique_lock<std::mutex> lk(dev.coef_mu);
+    for (;;) {
+        auto it = dev.coef_index.find(key);
+        if (it != dev.coef_index.end()) {
+            *off = it->second.off;
+            coef_note_use(it->second.gen, it->second.seq);
+            return MXEC_OK;
+        }
+        if (!dev.coef.p) MXEC_TRY(coef_init(dev));
+        if (table.size() > dev.coef_half)
+            return set_error(MXEC_E_INVALID_ARG, "coefficient table larger than the arena");
+        if (dev.coef_recycling) {  // another thread is waiting out a recycle's fences
+            dev.coef_cv.wait(lk);
+            continue;
+        }
+        if (dev.coef_used + table.size() <= dev.coef_half) break;
         // This half is full: the next generation takes the other half, whose
-        // tables (two generations old) may still be read by fenced launches.
+        // tables (two generations old) may still be read by fenced launches
+        // or, for the newest of them, still be on their way up.  Wait for
+        // those outside the lock, then look again.
         const uint64_t next = dev.coef_gen + 1;
         const int h = int(next & 1);
-        for (hipEvent_t e : dev.coef_fences[h]) {
-            if (hipEventQuery(e) != hipSuccess) {
-                ++dev.coef_fence_waits;
-                MXEC_HIP(hipEventSynchronize(e));
-            }
-            dev.coef_free.push_back(e);
-        }
+        std::vector<hipEvent_t> busy;
+        for (hipEvent_t e : dev.coef_fences[h])
+            if (hipEventQuery(e) != hipSuccess) busy.push_back(e);
         (void)hipGetLastError();
+        if (!busy.empty()) {
+            ++dev.coef_fence_waits;
+            dev.coef_recycling = true;
+            lk.unlock();
+            int rc = MXEC_OK;
+            for (hipEvent_t e : busy)
+                if (hipEventSynchronize(e) != hipSuccess) rc = set_error(MXEC_E_DEVICE, "coefficient fence wait failed");
+            lk.lock();
+            dev.coef_recycling = false;
+            dev.coef_cv.notify_all();
+            MXEC_TRY(rc);
+            continue;  // fences added meanwhile are waited for too
+        }
+        for (hipEvent_t e : dev.coef_fences[h]) dev.coef_free.push_back(e);
         dev.coef_fences[h].clear();
+        // The generation being closed: its last upload fences its half, so
+        // that half's mirror is not rewritten before the copies read it.
+        hipEvent_t last = nullptr;
+        MXEC_TRY(coef_take_event(dev, &last));
+        if (hipEventRecord(last, dev.coef_stream) != hipSuccess) {
+            dev.coef_free.push_back(last);
+            return set_error(MXEC_E_DEVICE, "coefficient upload fence: hipEventRecord failed");
+        }
+        dev.coef_fences[dev.coef_gen & 1].push_back(last);
         for (auto i = dev.coef_index.begin(); i != dev.coef_index.end();)
-            i = i->second.second + 1 < next ? dev.coef_index.erase(i) : std::next(i);
+            i = i->second.gen + 1 < next ? dev.coef_index.erase(i) : std::next(i);
         for (auto i = dev.patterns.begin(); i != dev.patterns.end();)
             i = i->second.gen + 1 < next ? dev.patterns.erase(i) : std::next(i);
         dev.coef_gen = next;
         dev.coef_used = 0;
         ++dev.coef_recycles;
+        break;
     }
     const uint32_t o = uint32_t(size_t(dev.coef_gen & 1) * dev.coef_half + dev.coef_used);
-    // Synchronous copy: the table is on the device before any stream can see
-    // the key in the index.
-    MXEC_HIP(hipMemcpy(static_cast<uint32_t*>(dev.coef.p) + o, table.data(), table.size() * 4,
-                       hipMemcpyHostToDevice));
+    MXEC_TRY(coef_upload(dev, o, table));
     dev.coef_used += (table.size() + 3) & ~size_t(3);
-    dev.coef_index.emplace(key, std::make_pair(o, dev.coef_gen));
-    coef_note_use(dev.coef_gen);
+    dev.coef_index.emplace(key, Device::CoefEntry{o, dev.coef_gen, dev.coef_seq});
+    coef_note_use(dev.coef_gen, dev.coef_seq);
     *off = o;
+    return MXEC_OK;
+}
+
+int coef_wait_uploads(Device& dev, const CoefUse& use, hipStream_t s) {
+    if (use.seq == 0) return MXEC_OK;
+    std::lock_guard<std::mutex> g(dev.coef_mu);
+    if (use.seq <= dev.coef_done) return MXEC_OK;
+    if (hipEventQuery(dev.coef_uploaded) == hipSuccess) {
+        dev.coef_done = dev.coef_seq;  // the newest upload landed, and every one before it
+        return MXEC_OK;
+    }
+    (void)hipGetLastError();
+    // The wait is captured at this call: later re-records of the event do not
+    // move it (it may wait for a few newer uploads too, which is harmless).
+    MXEC_HIP(hipStreamWaitEvent(s, dev.coef_uploaded, 0));
     return MXEC_OK;
 }
 
@@ -525,12 +611,21 @@ int coef_fence(Device& dev, const CoefUse& use, hipStream_t s, bool* live) {
 
 void coef_release(Device& dev) {
     std::lock_guard<std::mutex> g(dev.coef_mu);
+    if (dev.coef_stream) (void)hipStreamSynchronize(dev.coef_stream);
     for (auto& v : dev.coef_fences) {
         for (hipEvent_t e : v) (void)hipEventDestroy(e);
         v.clear();
     }
     for (hipEvent_t e : dev.coef_free) (void)hipEventDestroy(e);
     dev.coef_free.clear();
+    if (dev.coef_uploaded) (void)hipEventDestroy(dev.coef_uploaded);
+    dev.coef_uploaded = nullptr;
+    if (dev.coef_stream) {
+        affinity_untag(dev.coef_stream);
+        (void)hipStreamDestroy(dev.coef_stream);
+    }
+    dev.coef_stream = nullptr;
+    dev.coef_mirror.clear();
 }
 
 namespace {

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -207,16 +208,38 @@ struct Device {
     // wait, other streams keep running.  A launch whose tables came from a
     // generation recycled before its fence was registered is queued again
     // (with_stable_coef, ops.hpp).
+    //
+    // New tables go up asynchronously: the host writes them into a page-locked
+    // mirror of the arena (1 MiB chunks, allocated on first touch) and
+    // hipMemcpyAsync moves them on the device's own table stream, whose
+    // event every launch that reads a not-yet-landed table waits on
+    // (coef_wait_uploads; a GPU-side wait, not a host one).  A half's mirror
+    // is rewritten only after a recycle, which waits for the last upload of
+    // the generation it replaces (its event sits among that half's fences).
+    // A recycle that must wait for fences releases coef_mu while it waits
+    // (coef_recycling holds other allocations back; lookups of live tables
+    // go on): no thread holds the lock across a device wait.
     std::mutex coef_mu;
+    std::condition_variable coef_cv;  // a recycle's fence wait finished
+    bool coef_recycling = false;
     DevBuf coef;
     size_t coef_half = 0;     // dwords per half (set on first use)
     size_t coef_used = 0;     // dwords used in the current half
     uint64_t coef_gen = 0;    // current generation
-    // key -> (dword offset, generation)
-    std::map<std::vector<uint8_t>, std::pair<uint32_t, uint64_t>> coef_index;
-    std::vector<hipEvent_t> coef_fences[2];  // after launches that read half h
+    struct CoefEntry {
+        uint32_t off;  // dword offset
+        uint64_t gen;  // generation
+        uint64_t seq;  // upload sequence number (coef_seq when it was queued)
+    };
+    std::map<std::vector<uint8_t>, CoefEntry> coef_index;
+    std::vector<hipEvent_t> coef_fences[2];  // after launches that read half h (and its last upload)
     std::vector<hipEvent_t> coef_free;       // spare fence events
-    uint64_t coef_recycles = 0, coef_relaunches = 0, coef_fence_waits = 0;
+    std::vector<PinnedBuf> coef_mirror;      // page-locked image of the arena, in chunks
+    size_t coef_mirror_chunk = 0;            // dwords per mirror chunk
+    hipStream_t coef_stream = nullptr;       // the table uploads, in order
+    hipEvent_t coef_uploaded = nullptr;      // recorded after the newest upload
+    uint64_t coef_seq = 0, coef_done = 0;    // uploads queued / known landed
+    uint64_t coef_recycles = 0, coef_relaunches = 0, coef_fence_waits = 0, coef_uploads = 0;
     // CRC32 / CRC32C constant tables (sums.cpp), uploaded on first use.
     std::mutex sums_mu;
     DevBuf crc_tables;
@@ -240,6 +263,7 @@ struct Device {
         std::shared_ptr<const void> plan;
         uint32_t off;
         uint64_t gen;
+        uint64_t seq;  // the table's upload (Device::CoefEntry)
     };
     std::unordered_map<PatternKey, PatternVal, PatternHash> patterns;
     // Host-batch pipeline state (pipeline.cpp): streams, pinned rings, pools;
@@ -356,9 +380,13 @@ int coef_offset(Device& dev, const std::vector<uint8_t>& key, const std::vector<
 // calling thread's current CoefUse, if one is set.
 struct CoefUse {
     uint64_t lo = UINT64_MAX, hi = 0;
+    uint64_t seq = 0;  // newest table upload the batch reads (0: none)
     bool any() const { return lo != UINT64_MAX; }
 };
-void coef_note_use(uint64_t gen);
+void coef_note_use(uint64_t gen, uint64_t seq);
+// Before a batch's launches on `s`: if a table it reads may not have landed
+// yet, `s` waits (on the GPU) for the table stream's newest upload.
+int coef_wait_uploads(Device& dev, const CoefUse& use, hipStream_t s);
 CoefUse* coef_use_swap(CoefUse* u);  // sets the thread's current CoefUse, returns the previous
 // After a batch's launches are queued on `s`: if every table it used is
 // still live, fence them with an event on `s` (a later recycle of their half

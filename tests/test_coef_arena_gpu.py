@@ -4,11 +4,13 @@ ops.hpp with_stable_coef).
 Every RS launch reads its matrix from a per-device table arena of two
 halves; when the current half is full, the next generation takes the other
 half after waiting only for the events that fence the launches which read
-it (no device-wide wait).  A test-only arena of a few KiB
+it (no device-wide wait, and not under the arena's lock); new tables go up
+by hipMemcpyAsync on a per-device table stream that the launches wait for
+on the GPU.  A test-only arena of a few KiB
 (mxec_open_test coef_arena_bytes) makes that happen every few
 batches:
 
-* four host threads, each on its own stream, rebuild batches whose seeded
+* four and sixteen host threads, each on its own stream, rebuild batches whose seeded
   erasure patterns are all different (one decode table each) while the
   others do the same: every object bit-exact, the arena recycled many times;
 * the same sequence from one thread, results equal to the oracle's
@@ -56,10 +58,15 @@ def _encoded(torch, n, seed):
     return t
 
 
-def test_recycles_under_four_threads(ctx_with):
-    ctx = ctx_with(streams=4, MXEC_TEST_COEF_ARENA_KB=32)  # 8 192 dwords per half: ~10-20 decode tables
+@pytest.mark.parametrize("n_thr", [4, 16])
+def test_recycles_under_threads(ctx_with, n_thr):
+    """n_thr threads on their own streams: with 16, a storm of distinct
+    erasure patterns where new tables go up asynchronously on the table
+    stream (launches wait for them on the GPU) and recycles wait for their
+    fences outside the arena's lock."""
+    ctx = ctx_with(streams=n_thr, MXEC_TEST_COEF_ARENA_KB=32)  # 8 192 dwords per half: ~10-20 decode tables
     torch = _torch()
-    n_thr, n_obj, rounds = 4, 4, 30
+    n_obj, rounds = 4, 30
     refs = []
     for th in range(n_thr):
         r = _encoded(torch, n_obj, 700 + th)
