@@ -1588,6 +1588,7 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
         pr = present0.copy()
         rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)  # warm
         assert rc == 0, rc
+        c0 = [ctx.copy_stats(i) for i in range(D)]
         ts, marks = [], []
         for _ in range(reps):
             pr = present0.copy()
@@ -1604,6 +1605,11 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
             _leg_times(ts), GiBps_payload=round(payload / GIB / el, 2),
             frac_of_pcie_bound=round(max(get_up_s, get_down_s) / el, 4),
             frac_of_duplex_bound=round(get_duplex_s / el, 4))
+        # Which copy engine the timed batches used (MXEC_PIPE_COPY=auto: SDMA
+        # unless its probe found it slow): the copy counters' difference.
+        c1 = [ctx.copy_stats(i) for i in range(D)]
+        res["get_verify_sha256" if verify else "get_rs_only"]["copies"] = {
+            key: sum(b[key] - a[key] for a, b in zip(c0, c1)) for key in c1[0]}
         if stamps:
             res["get_verify_sha256" if verify else "get_rs_only"]["monotonic_ns"] = marks
     if get_only:

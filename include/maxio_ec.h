@@ -117,10 +117,12 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages);
 /* Copies the host-batch pipeline (mxec_{encode,reconstruct}_batch_host) has
  * issued on ctx device `dev` since the context opened: 1D SDMA DMAs, 2D SDMA
- * DMAs (the PUT's piece copies) and the rows they moved, CU-wave copy blocks.
- * Any pointer may be NULL.  Diagnostics (tests). */
+ * DMAs (the PUT's piece copies) and the rows they moved, CU-wave copy blocks;
+ * and the SDMA health probes MXEC_PIPE_COPY=auto ran before large batches and
+ * how many found SDMA below its floor (those batches copied by waves).  Any
+ * pointer may be NULL.  Diagnostics (tests). */
 int mxec_ctx_copy_stats(mxec_ctx* ctx, int dev, uint64_t* copies_1d, uint64_t* copies_2d, uint64_t* rows_2d,
-                        uint64_t* wave_blocks);
+                        uint64_t* wave_blocks, uint64_t* sdma_probes, uint64_t* sdma_slow);
 /* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
  * (k inputs, m outputs, shard_size) at: the grid tuner times the first
  * launches of a shape at three grid sizes and keeps the fastest (which of

@@ -26,7 +26,9 @@ namespace {
 // mxec_host_alloc memory may go by CU-wave copy kernels -- the reconstruct /
 // hash (GET) paths under auto and waves, the encode (PUT) path under waves
 // only (pipeline.cpp has the measurements behind the split).
-bool copy_waves_get(const Device& d) { return d.kn && d.kn->pipe_copy != 0; }
+bool copy_waves_get(const Device& d) {
+    return d.kn && (d.kn->pipe_copy == 1 || (d.kn->pipe_copy == 2 && d.sdma_slow.load()));
+}
 bool copy_waves_put(const Device& d) { return d.kn && d.kn->pipe_copy == 1; }
 
 // One object of a device-resident reconstruct batch (device shard pointers).
@@ -259,7 +261,7 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i) {
 }
 
 int mxec_ctx_copy_stats(mxec_ctx* ctx, int dev, uint64_t* copies_1d, uint64_t* copies_2d, uint64_t* rows_2d,
-                        uint64_t* wave_blocks) {
+                        uint64_t* wave_blocks, uint64_t* sdma_probes, uint64_t* sdma_slow) {
     if (!ctx || dev < 0 || dev >= int(ctx->c.devs.size()))
         return set_error(MXEC_E_INVALID_ARG, "mxec_ctx_copy_stats: no such device");
     const Device& d = *ctx->c.devs[size_t(dev)];
@@ -267,6 +269,8 @@ int mxec_ctx_copy_stats(mxec_ctx* ctx, int dev, uint64_t* copies_1d, uint64_t* c
     if (copies_2d) *copies_2d = d.copies_2d.load();
     if (rows_2d) *rows_2d = d.copies_2d_rows.load();
     if (wave_blocks) *wave_blocks = d.copy_wave_blocks.load();
+    if (sdma_probes) *sdma_probes = d.sdma_probes.load();
+    if (sdma_slow) *sdma_slow = d.sdma_slow_verdicts.load();
     return MXEC_OK;
 }
 

@@ -163,6 +163,20 @@ struct PipeRes {
     DevBuf chain_state;  // SHA-256 chain states between pieces (host reconstruct)
     PinnedBuf flags;  // verification verdicts read back (host reconstruct)
     Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
+    // SDMA health (MXEC_PIPE_COPY=auto): a few 1 MiB page-locked -> HBM DMAs
+    // timed before a large batch, and the verdict kept for a short while.
+    struct SdmaProbe {
+        PinnedBuf src;
+        DevBuf dst;
+        hipEvent_t a = nullptr, b = nullptr;
+        double gbps = -1;  // last measured rate (-1: never)
+        bool slow = false;
+        std::chrono::steady_clock::time_point at{};
+        ~SdmaProbe() {
+            if (a) (void)hipEventDestroy(a);
+            if (b) (void)hipEventDestroy(b);
+        }
+    } sdma;
     bool ready = false;
     int init(const Device& dev) {
         if (ready) return MXEC_OK;
@@ -294,20 +308,26 @@ class DevicePipeline {
 public:
     DevicePipeline(Device& d, PipeRes& r)
         : d_(d), h2d_(r.h2d), d2h_(r.d2h), cs_(r.cs), in_(r.in), out_(r.out), arena_(r.arena),
-          pool_(r.pool), scratch_(r.digests), state_(r.chain_state), flags_(r.flags), slot_(r.desc_slot) {}
+          pool_(r.pool), scratch_(r.digests), state_(r.chain_state), flags_(r.flags), slot_(r.desc_slot),
+          sdma_(r.sdma) {}
     ~DevicePipeline() {
         for (auto e : events_) (void)hipEventDestroy(e);
     }
 
     // MXEC_PIPE_COPY (knobs.hpp): sdma; waves (every host batch); auto (the
-    // default) -- host reconstruct batches by waves, host encode batches by
-    // SDMA.  Measured (profiles/r4/get_stall/): the verified GET 0.263 s by
-    // waves against 0.268 by SDMA, and 0.263 against [0.33, 0.92, 0.33,
-    // 0.92, 0.27] s after the bench's extras (SDMA copies collapse for
-    // seconds there); the PUT with digests 0.264 by waves against 0.218 by
-    // SDMA (copy waves beside the SHA-256 chains slow the chains).
+    // default) -- SDMA while it runs at its normal rate, CU-wave copies while
+    // it does not (sdma_slow).  Measured (profiles/r4/get_stall/,
+    // e2e_get_modes/): in a healthy process SDMA is the faster engine
+    // (RS-only GET 0.101 s against 0.119 by waves at 128 objects; the PUT
+    // with digests 0.218 against 0.264, copy waves beside the SHA-256 chains
+    // slowing the chains), but after heavy HBM churn SDMA copies collapsed
+    // for seconds to ~7 GB/s ([0.33, 0.92, 0.33, 0.92, 0.27] s verified GETs
+    // against 0.263 by waves).
     int run(std::vector<HostObj>& objs) {
-        waves_now_ = d_.kn && d_.kn->pipe_copy == 1;  // encode: waves only when asked for
+        // encode: SDMA unless waves are asked for, or SDMA is measured slow
+        uint64_t up = 0;
+        for (const auto& h : objs) up += uint64_t(h.k) * h.S;
+        waves_now_ = d_.kn && (d_.kn->pipe_copy == 1 || (d_.kn->pipe_copy == 2 && sdma_slow(up)));
         size_t o = 0;
         while (o < objs.size()) {  // waves that fit the pool
             uint64_t need = 0, desc = 1 << 20;
@@ -328,7 +348,11 @@ public:
 
     // Host reconstruct batch: waves that fit the pool, as run().
     int run_rec(std::vector<RecObj>& objs, bool data_only) {
-        waves_now_ = d_.kn && d_.kn->pipe_copy != 0;  // reconstruct: waves by default (auto)
+        // reconstruct: SDMA unless waves are asked for, or SDMA is measured slow
+        uint64_t up = 0;
+        for (const auto& h : objs)
+            for (int i = 0; i < h.k + h.m; ++i) up += h.present[i] ? h.len[i] : 0;
+        waves_now_ = d_.kn && (d_.kn->pipe_copy == 1 || (d_.kn->pipe_copy == 2 && sdma_slow(up)));
         size_t o = 0;
         while (o < objs.size()) {
             uint64_t need = 0, desc = 1 << 20;
@@ -350,6 +374,51 @@ public:
     }
 
 private:
+    // Whether this call's copies of mxec_host_alloc memory should avoid SDMA:
+    // before a batch of at least kProbeMinBytes, four 1 MiB DMAs from a
+    // page-locked buffer into HBM on the (idle) upload stream are timed; a
+    // rate under MXEC_PIPE_SDMA_FLOOR GB/s (default 30; healthy: ~33-38 for
+    // 1 MiB copies, collapsed: ~7) sends the batch's copies to the wave
+    // kernels.  The verdict stands for kProbeHoldMs (smaller batches and
+    // back-to-back ones reuse it); the probe costs ~0.15 ms.
+    static constexpr uint64_t kProbeMinBytes = uint64_t(64) << 20;
+    static constexpr int kProbeHoldMs = 200;
+    static constexpr uint64_t kProbeBytes = uint64_t(1) << 20;
+    static constexpr int kProbeCopies = 4;
+    bool sdma_slow(uint64_t upload_bytes) {
+        PipeRes::SdmaProbe& pr = sdma_;
+        const auto now = std::chrono::steady_clock::now();
+        const bool fresh = pr.gbps >= 0 && now - pr.at < std::chrono::milliseconds(kProbeHoldMs);
+        if (fresh || upload_bytes < kProbeMinBytes) return pr.slow;
+        if (hipStreamQuery(h2d_) != hipSuccess) {  // still busy with an earlier batch: keep the verdict
+            (void)hipGetLastError();
+            return pr.slow;
+        }
+        if (pr.src.ensure(kProbeBytes) || pr.dst.ensure(kProbeBytes * kProbeCopies)) return pr.slow;
+        if (!pr.a && (hipEventCreate(&pr.a) != hipSuccess || hipEventCreate(&pr.b) != hipSuccess)) {
+            (void)hipGetLastError();
+            return pr.slow;
+        }
+        float ms = 0;
+        bool ok = hipEventRecord(pr.a, h2d_) == hipSuccess;
+        for (int i = 0; ok && i < kProbeCopies; ++i)
+            ok = hipMemcpyAsync(static_cast<uint8_t*>(pr.dst.p) + uint64_t(i) * kProbeBytes, pr.src.p, kProbeBytes,
+                                hipMemcpyHostToDevice, h2d_) == hipSuccess;
+        ok = ok && hipEventRecord(pr.b, h2d_) == hipSuccess && hipEventSynchronize(pr.b) == hipSuccess &&
+             hipEventElapsedTime(&ms, pr.a, pr.b) == hipSuccess && ms > 0;
+        if (!ok) {
+            (void)hipGetLastError();
+            return pr.slow;
+        }
+        pr.gbps = double(kProbeBytes * kProbeCopies) / (double(ms) * 1e6);
+        pr.slow = pr.gbps < double(d_.kn ? d_.kn->pipe_sdma_floor : 30);
+        pr.at = now;
+        ++d_.sdma_probes;
+        d_.sdma_slow_verdicts += pr.slow ? 1 : 0;
+        d_.sdma_slow = pr.slow;
+        return pr.slow;
+    }
+
     // One wave of a host reconstruct batch (try_reconstruct_data_chunk,
     // chunk_reader.rs:157-226, per object): the present shards go up group
     // by group (coalesced, direct from pinned memory), their digests are
@@ -642,6 +711,7 @@ private:
     DevBuf& state_;    // chain states of a piece-major verification
     PinnedBuf& flags_;
     Slot& slot_;
+    PipeRes::SdmaProbe& sdma_;
     std::vector<Pending> pend_;
     std::vector<hipEvent_t> events_;
 

@@ -273,6 +273,11 @@ struct Device {
     // Copies the host pipeline issued (mxec_ctx_copy_stats): 1D SDMA DMAs,
     // 2D SDMA DMAs and their rows, CU-wave copy blocks (copy_kernel.hip).
     std::atomic<uint64_t> copies_1d{0}, copies_2d{0}, copies_2d_rows{0}, copy_wave_blocks{0};
+    // SDMA health probes of the host pipeline (MXEC_PIPE_COPY=auto) and how
+    // many found SDMA slow; the last verdict also steers the single-request
+    // calls' copies of mxec_host_alloc memory.
+    std::atomic<uint64_t> sdma_probes{0}, sdma_slow_verdicts{0};
+    std::atomic<bool> sdma_slow{false};
     // SHA-256 combiner (combiner.cpp): one launch for the verification work
     // of every concurrent caller on this device.
     std::mutex comb_mu;

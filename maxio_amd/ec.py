@@ -201,9 +201,10 @@ class Context:
     def copy_stats(self, dev: int = 0) -> dict:
         """Copies the host-batch pipeline issued on device `dev` since the
         context opened (mxec_ctx_copy_stats)."""
-        v = [ctypes.c_uint64(0) for _ in range(4)]
+        v = [ctypes.c_uint64(0) for _ in range(6)]
         _check(self._lib.mxec_ctx_copy_stats(self._h, dev, *[ctypes.byref(x) for x in v]))
-        return dict(zip(("copies_1d", "copies_2d", "rows_2d", "wave_blocks"), (x.value for x in v)))
+        return dict(zip(("copies_1d", "copies_2d", "rows_2d", "wave_blocks", "sdma_probes", "sdma_slow"),
+                        (x.value for x in v)))
 
     def rs_grid(self, k: int, m: int, shard_size: int, dev: int = 0) -> int:
         """Workgroups per CU large uniform RS launches of this shape run at on

@@ -139,7 +139,8 @@ extern "C" {
     pub fn mxec_ctx_device_id(ctx: *const MxecCtx, i: c_int) -> c_int;
     pub fn mxec_ctx_combiner_stats(ctx: *mut MxecCtx, i: c_int, launches: *mut u64, messages: *mut u64) -> c_int;
     pub fn mxec_ctx_copy_stats(ctx: *mut MxecCtx, dev: c_int, copies_1d: *mut u64, copies_2d: *mut u64,
-                               rows_2d: *mut u64, wave_blocks: *mut u64) -> c_int;
+                               rows_2d: *mut u64, wave_blocks: *mut u64, sdma_probes: *mut u64,
+                               sdma_slow: *mut u64) -> c_int;
     pub fn mxec_ctx_rs_grid(ctx: *mut MxecCtx, dev: c_int, k: c_int, m: c_int, shard_size: u64) -> c_int;
     pub fn mxec_ctx_coef_stats(ctx: *mut MxecCtx, dev: c_int, recycles: *mut u64, relaunches: *mut u64,
                                fence_waits: *mut u64) -> c_int;

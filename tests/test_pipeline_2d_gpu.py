@@ -10,7 +10,8 @@ digests, filesystem.rs:1107-1135; the GET's rebuild, chunk_reader.rs:157-226).
   off the piece grid; a short and an empty last data chunk break the 2D run
   in the middle of the batch.  EVERY object's parity and all k+m digests
   equal oracle.compute_parity.
-* The GET's CU-wave copies (MXEC_PIPE_COPY auto) with ragged lengths and
+* The CU-wave copies (MXEC_PIPE_COPY=waves, or auto while a timed probe
+  finds SDMA below MXEC_PIPE_SDMA_FLOOR) with ragged lengths and
   with caller pointers at odd offsets: a segment whose host and device ends
   sit at different offsets modulo 16 goes by SDMA instead (copy_phase_ok),
   one at the same offset moves its head / tail bytewise and the rest as
@@ -100,15 +101,17 @@ def test_put_2d_piece_copies_default_upload_bound(ctx):
     assert d["copies_2d"] > 0, d
 
 
-@pytest.mark.parametrize("copy", ["auto", "waves"])
+@pytest.mark.parametrize("copy,floor", [("waves", ""), ("auto", "100000")])
 @pytest.mark.parametrize("offset", [0, 3, 16 + 5])
-def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset):
-    """Verified GET of 6 x 4+2 objects whose shards start `offset` bytes into
-    page-locked memory and whose last data chunk is S - 3333 bytes: every
-    rebuilt shard equals the original; aligned callers take the wave copies
-    (wave_blocks counted), phase-mismatched ones fall back to SDMA."""
-    ctx = ctx_with(MXEC_PIPE_COPY=copy)
-    k, m, n = 4, 2, 6
+def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset, floor):
+    """Verified GET of 9 x 4+2 objects (72 MiB up: the auto mode's SDMA probe
+    runs) whose shards start `offset` bytes into page-locked memory and whose
+    last data chunk is S - 3333 bytes, by waves (MXEC_PIPE_COPY=waves, and
+    auto with a floor no SDMA reaches): every rebuilt shard equals the
+    original; aligned callers take the wave copies (wave_blocks counted),
+    phase-mismatched ones fall back to SDMA."""
+    ctx = ctx_with(MXEC_PIPE_COPY=copy, MXEC_PIPE_SDMA_FLOOR=floor)
+    k, m, n = 4, 2, 9
     S = 2 * M + 4096 + 48
     rng = np.random.default_rng(900 + offset)
     slot = S + 64
@@ -140,4 +143,22 @@ def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset):
             assert np.array_equal(shard[o][i][:L], ref[o][i]), (copy, offset, o, i)
     if offset % 16 == 0:
         assert after["wave_blocks"] > before["wave_blocks"], (before, after)
+    if copy == "auto":
+        assert after["sdma_probes"] > before["sdma_probes"] and after["sdma_slow"] > before["sdma_slow"]
     ctx.host_free(buf)
+
+
+@pytest.mark.parametrize("floor,waves", [("0", False), ("100000", True)])
+def test_auto_copy_engine_follows_the_sdma_probe(ctx_with, floor, waves):
+    """MXEC_PIPE_COPY=auto: the probe before a large batch decides the copy
+    engine (floor 0: SDMA always passes; an unreachable floor: every batch by
+    waves); both bit-exact (PUT with digests against the oracle, then a
+    verified GET of the same objects)."""
+    ctx = ctx_with(MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
+    S = 3 * M + 4096 + 48
+    before = ctx.copy_stats()
+    _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333})
+    after = ctx.copy_stats()
+    assert after["sdma_probes"] > before["sdma_probes"], (before, after)
+    assert (after["wave_blocks"] > before["wave_blocks"]) == waves, (before, after)
+    assert (after["sdma_slow"] > before["sdma_slow"]) == waves, (before, after)

@@ -374,9 +374,9 @@ def test_batch_host_pieces_descriptor_tables_outgrow_first_block(ctx):
 @pytest.mark.parametrize("copy", ["auto", "waves", "sdma"])
 def test_host_alloc_buffers_copy_modes(ctx_with, copy):
     """mxec_host_alloc buffers (mapped into the GPU's address space) through
-    the host batch calls with MXEC_PIPE_COPY=auto (the default: the GET by
-    CU-wave copy kernels, copy_kernel.hip, the PUT by SDMA), =waves (both by
-    waves) and =sdma: a PUT with digests in pieces, shards off the
+    the host batch calls with MXEC_PIPE_COPY=auto (the default: SDMA while a
+    timed probe finds it healthy, CU-wave copy kernels, copy_kernel.hip,
+    while not), =waves (both by waves) and =sdma: a PUT with digests in pieces, shards off the
     piece grid and short last chunks, then a verified GET with two erasures
     per object and one corrupted present shard -- parity, digests and the
     rebuilt shards equal to the oracle / the originals in both modes."""
@@ -426,12 +426,13 @@ def test_host_alloc_buffers_copy_modes(ctx_with, copy):
     assert hashlib.sha256(data[n - 1, 0].tobytes()).digest() == dig[(n - 1) * (k + m) * 32:][:32].tobytes()
 
 
-@pytest.mark.parametrize("copy", ["auto", "sdma"])
+@pytest.mark.parametrize("copy", ["waves", "sdma"])
 def test_single_request_calls_on_host_alloc_buffers(ctx_with, copy):
     """The single-request entry points with mxec_host_alloc buffers: under
-    MXEC_PIPE_COPY=auto the hash and reconstruct calls move them by CU-wave
-    copy kernels (runtime.cpp upload_segments / download_segments), under
-    sdma by DMAs.  mxec_sha256_batch against hashlib (odd lengths and
+    MXEC_PIPE_COPY=waves the hash and reconstruct calls move them by CU-wave
+    copy kernels (runtime.cpp upload_segments / download_segments; under
+    auto they do so while the device's last SDMA probe found SDMA slow),
+    under sdma by DMAs.  mxec_sha256_batch against hashlib (odd lengths and
     offsets); mxec_reconstruct with verification, two erasures and one
     corrupted shard, rebuilt in place in the caller's page-locked shards."""
     import ctypes
