@@ -1588,7 +1588,7 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
         pr = present0.copy()
         rc, _ = ctx.reconstruct_batch_host(objs, sptr, pr, expected=exp)  # warm
         assert rc == 0, rc
-        c0 = [ctx.copy_stats(i) for i in range(D)]
+        c0 = [ctx.pipe_stats(i) for i in range(D)]
         ts, marks = [], []
         for _ in range(reps):
             pr = present0.copy()
@@ -1607,7 +1607,7 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
             frac_of_duplex_bound=round(get_duplex_s / el, 4))
         # Which copy engine the timed batches used (MXEC_PIPE_COPY=auto: SDMA
         # unless its probe found it slow): the copy counters' difference.
-        c1 = [ctx.copy_stats(i) for i in range(D)]
+        c1 = [ctx.pipe_stats(i) for i in range(D)]
         res["get_verify_sha256" if verify else "get_rs_only"]["copies"] = {
             key: sum(b[key] - a[key] for a, b in zip(c0, c1)) for key in c1[0]}
         if stamps:

@@ -115,14 +115,24 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i);
  * the device's combiner (concurrent small requests share one launch) and the
  * messages they hashed. */
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages);
-/* Copies the host-batch pipeline (mxec_{encode,reconstruct}_batch_host) has
- * issued on ctx device `dev` since the context opened: 1D SDMA DMAs, 2D SDMA
- * DMAs (the PUT's piece copies) and the rows they moved, CU-wave copy blocks;
- * and the SDMA health probes MXEC_PIPE_COPY=auto ran before large batches and
- * how many found SDMA below its floor (those batches copied by waves).  Any
- * pointer may be NULL.  Diagnostics (tests). */
-int mxec_ctx_copy_stats(mxec_ctx* ctx, int dev, uint64_t* copies_1d, uint64_t* copies_2d, uint64_t* rows_2d,
-                        uint64_t* wave_blocks, uint64_t* sdma_probes, uint64_t* sdma_slow);
+/* Host-batch pipeline (mxec_{encode,reconstruct}_batch_host) counters of ctx
+ * device `dev` since the context opened, into out[0 .. n): the copies it
+ * issued (1D SDMA DMAs, 2D SDMA DMAs -- the PUT's piece copies -- and their
+ * rows, CU-wave copy blocks), the SDMA health probes MXEC_PIPE_COPY=auto ran
+ * before large batches and how many found SDMA below its floor (those
+ * batches copied by waves), and the piece-major verified reconstruct waves
+ * and the verification groups they ran as.  Returns how many counters were
+ * written (min(n, MXEC_PIPE_STAT_COUNT)), or an error.  Diagnostics (tests). */
+#define MXEC_PIPE_STAT_COPIES_1D 0
+#define MXEC_PIPE_STAT_COPIES_2D 1
+#define MXEC_PIPE_STAT_ROWS_2D 2
+#define MXEC_PIPE_STAT_WAVE_BLOCKS 3
+#define MXEC_PIPE_STAT_SDMA_PROBES 4
+#define MXEC_PIPE_STAT_SDMA_SLOW 5
+#define MXEC_PIPE_STAT_VERIFY_WAVES 6
+#define MXEC_PIPE_STAT_VERIFY_GROUPS 7
+#define MXEC_PIPE_STAT_COUNT 8
+int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n);
 /* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
  * (k inputs, m outputs, shard_size) at: the grid tuner times the first
  * launches of a shape at three grid sizes and keeps the fastest (which of

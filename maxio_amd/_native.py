@@ -100,7 +100,7 @@ _SIGS = {
     "mxec_ctx_device_count": (INT, [P]),
     "mxec_ctx_device_id": (INT, [P, INT]),
     "mxec_ctx_combiner_stats": (INT, [P, INT, U64P, U64P]),
-    "mxec_ctx_copy_stats": (INT, [P, INT, U64P, U64P, U64P, U64P, U64P, U64P]),
+    "mxec_ctx_pipe_stats": (INT, [P, INT, U64P, INT]),
     "mxec_ctx_rs_grid": (INT, [P, INT, INT, INT, U64]),
     "mxec_ctx_coef_stats": (INT, [P, INT, U64P, U64P, U64P]),
     "mxec_host_alloc": (P, [P, ctypes.c_size_t]),

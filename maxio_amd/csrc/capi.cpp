@@ -260,18 +260,17 @@ int mxec_ctx_device_id(const mxec_ctx* ctx, int i) {
     return ctx->c.devs[size_t(i)]->id;
 }
 
-int mxec_ctx_copy_stats(mxec_ctx* ctx, int dev, uint64_t* copies_1d, uint64_t* copies_2d, uint64_t* rows_2d,
-                        uint64_t* wave_blocks, uint64_t* sdma_probes, uint64_t* sdma_slow) {
-    if (!ctx || dev < 0 || dev >= int(ctx->c.devs.size()))
-        return set_error(MXEC_E_INVALID_ARG, "mxec_ctx_copy_stats: no such device");
+int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n) {
+    if (!ctx || dev < 0 || dev >= int(ctx->c.devs.size()) || !out || n < 0)
+        return set_error(MXEC_E_INVALID_ARG, "mxec_ctx_pipe_stats: no such device or no output");
     const Device& d = *ctx->c.devs[size_t(dev)];
-    if (copies_1d) *copies_1d = d.copies_1d.load();
-    if (copies_2d) *copies_2d = d.copies_2d.load();
-    if (rows_2d) *rows_2d = d.copies_2d_rows.load();
-    if (wave_blocks) *wave_blocks = d.copy_wave_blocks.load();
-    if (sdma_probes) *sdma_probes = d.sdma_probes.load();
-    if (sdma_slow) *sdma_slow = d.sdma_slow_verdicts.load();
-    return MXEC_OK;
+    const uint64_t v[MXEC_PIPE_STAT_COUNT] = {d.copies_1d.load(),        d.copies_2d.load(),
+                                              d.copies_2d_rows.load(),   d.copy_wave_blocks.load(),
+                                              d.sdma_probes.load(),      d.sdma_slow_verdicts.load(),
+                                              d.verify_waves.load(),     d.verify_groups.load()};
+    const int k = std::min(n, int(MXEC_PIPE_STAT_COUNT));
+    for (int i = 0; i < k; ++i) out[i] = v[i];
+    return k;
 }
 
 int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* messages) {

@@ -431,24 +431,7 @@ private:
     // shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT and none of its buffers is
     // written.
     int rec_wave(std::vector<RecObj>& objs, size_t o0, size_t o1, bool data_only) {
-        uint8_t* base = static_cast<uint8_t*>(pool_.p);
-        hipStream_t cs = cs_[0];
         PTRACE(start(h2d_));
-        // Groups: consecutive objects up to kGroupBytes of present input.
-        std::vector<std::pair<size_t, size_t>> groups;
-        for (size_t g0 = o0; g0 < o1;) {
-            size_t g1 = g0;
-            uint64_t in_bytes = 0;
-            while (g1 < o1) {
-                uint64_t b = 0;
-                for (int i = 0; i < objs[g1].k + objs[g1].m; ++i) b += objs[g1].present[i] ? objs[g1].len[i] : 0;
-                if (g1 > g0 && in_bytes + b > kGroupBytes) break;
-                in_bytes += b;
-                ++g1;
-            }
-            groups.emplace_back(g0, g1);
-            g0 = g1;
-        }
         uint64_t msgs = 0;
         bool verify = false;
         for (size_t o = o0; o < o1; ++o) {
@@ -477,24 +460,138 @@ private:
                     if (objs[o].expected) longest_msg = std::max(longest_msg, objs[o].len[i]);
                 }
         const uint64_t P = piece_bytes(up_bytes, longest_msg);
-        std::vector<hipEvent_t> up;  // per group (group form): its upload is done
         if (verify && P && vmsgs && vmsgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256)) {
             // Piece-major upload + verification (the PUT wave's scheme, see
             // wave_pieces): piece p of every present shard goes up and is
             // hashed, chains carried in state slots, so every chain starts
             // after the first piece instead of after the whole upload; the
-            // verdicts come back after the last piece, then the rebuild as
-            // below (nothing is written to the caller's buffers before).
-            MXEC_TRY(verify_in_pieces(objs, o0, o1, ok, exp, msgs, P));
-            PTRACE(now("verified"));
+            // verdicts come back after the last piece, then the rebuild
+            // (nothing is written to the caller's buffers before).  A large
+            // wave runs as a few verification groups (verify_cuts): group
+            // j + 1's pieces go up and hash (on the other compute stream)
+            // while the host waits for group j's verdicts, rebuilds it and
+            // sends its shards down.
+            const std::vector<size_t> cut = verify_cuts(objs, o0, o1, up_bytes, longest_msg, P);
+            MXEC_TRY(state_.ensure(msgs * 32));
+            MXEC_TRY(flags_.ensure(msgs));
+            std::vector<uint64_t> mbase(cut.size(), 0);
+            for (size_t j = 1; j < cut.size(); ++j) {
+                mbase[j] = mbase[j - 1];
+                for (size_t o = cut[j - 1]; o < cut[j]; ++o) mbase[j] += uint64_t(objs[o].k + objs[o].m);
+            }
+            const size_t G = cut.size() - 1;
+            std::vector<hipEvent_t> verdict(G, nullptr);
+            auto enqueue = [&](size_t j) {
+                return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], cs_[j & 1], &verdict[j]);
+            };
+            MXEC_TRY(enqueue(0));
+            for (size_t j = 0; j < G; ++j) {
+                if (j + 1 < G) MXEC_TRY(enqueue(j + 1));
+                MXEC_TRY(verify_collect(objs, cut[j], cut[j + 1], mbase[j], verdict[j]));
+                PTRACE(now("verified"));
+                for (const auto& q : object_groups(objs, cut[j], cut[j + 1]))
+                    MXEC_TRY(rebuild_down(objs, q.first, q.second, cs_[j & 1], nullptr, data_only));
+            }
+            d_.verify_groups += G;
+            d_.verify_waves += 1;
         } else {
-            MXEC_TRY(upload_and_verify(objs, o0, o1, groups, ok, exp, verify, cs, &up));
+            const auto groups = object_groups(objs, o0, o1);
+            std::vector<hipEvent_t> up;  // per group: its upload is done
+            MXEC_TRY(upload_and_verify(objs, o0, o1, groups, ok, exp, verify, cs_[0], &up));
+            // Per group, rebuild once it is up (without verification, as soon
+            // as it is up), then its shards down.
+            for (size_t q = 0; q < groups.size(); ++q)
+                MXEC_TRY(rebuild_down(objs, groups[q].first, groups[q].second, cs_[0], verify ? nullptr : up[q],
+                                      data_only));
         }
-        // Phase 3: per group, rebuild once it is up, then its shards down.
-        for (size_t q = 0; q < groups.size(); ++q) {
-            const size_t q0 = groups[q].first, q1 = groups[q].second;
-            // without verification a group is rebuilt as soon as it is up
-            if (!verify) MXEC_HIP(hipStreamWaitEvent(cs, up[q], 0));
+        MXEC_TRY(issue_down());
+        PTRACE(mark("d2h", d2h_));
+        PTRACE(now("down_queued"));
+        const int frc = flush();
+        PTRACE(report("rec_wave"));
+        return frc;
+    }
+
+    // Consecutive objects up to kGroupBytes of present input.
+    static std::vector<std::pair<size_t, size_t>> object_groups(const std::vector<RecObj>& objs, size_t o0,
+                                                                size_t o1) {
+        std::vector<std::pair<size_t, size_t>> groups;
+        for (size_t g0 = o0; g0 < o1;) {
+            size_t g1 = g0;
+            uint64_t in_bytes = 0;
+            while (g1 < o1) {
+                uint64_t b = 0;
+                for (int i = 0; i < objs[g1].k + objs[g1].m; ++i) b += objs[g1].present[i] ? objs[g1].len[i] : 0;
+                if (g1 > g0 && in_bytes + b > kGroupBytes) break;
+                in_bytes += b;
+                ++g1;
+            }
+            groups.emplace_back(g0, g1);
+            g0 = g1;
+        }
+        return groups;
+    }
+
+    // Verification groups of a piece-major reconstruct wave: cut points
+    // (first o0, last o1) by upload bytes.  With G groups the last group's
+    // chains start (G-1)/G of the way through the upload, and only the last
+    // group's rebuilt shards go down after the upload has ended, so the wave
+    // lasts about
+    //   max((G-1)/G * T_up + chain, T_up + one piece's hash) + D / G
+    // against max(chain, T_up + piece) + D for one group (T_up: the upload
+    // at the piece copies' rate, chain: the longest message's SHA-256, D:
+    // the rebuilt shards' download).  The smallest G (1..4) within 2 % of
+    // the best is taken.  A wave whose upload is shorter than its chain
+    // stays one group (128 x 4+2 x 10 MiB: 0.26 s either way).
+    std::vector<size_t> verify_cuts(const std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t up_bytes,
+                                    uint64_t longest, uint64_t P) const {
+        uint64_t down_bytes = 0;
+        for (size_t o = o0; o < o1; ++o)
+            for (int i = 0; i < objs[o].k + objs[o].m; ++i) down_bytes += objs[o].present[i] ? 0 : objs[o].len[i];
+        const double up_rate = (P >= (uint64_t(4) << 20) ? 43.0 : P >= (uint64_t(2) << 20) ? 38.0 : 33.0) * 1e9;
+        const double T = double(up_bytes) / up_rate, D = double(down_bytes) / 50e9;
+        const double chain = double(longest / 64) * kShaLagUsPerBlock * 1e-6;
+        const double piece = double(std::min(P, longest) / 64) * kShaLagUsPerBlock * 1e-6;
+        int G = 1;
+#ifdef MXEC_LAB
+        if (const char* e = getenv("MXEC_GET_VGROUPS")) G = std::max(1, std::min(8, atoi(e)));  // lab: force
+        else
+#endif
+        {
+            double est[5] = {0, 0, 0, 0, 0}, best = 1e30;
+            for (int g = 1; g <= 4; ++g) {
+                est[g] = std::max(double(g - 1) / g * T + chain, T + piece) + D / g;
+                best = std::min(best, est[g]);
+            }
+            while (G < 4 && est[G] > best * 1.02) ++G;
+        }
+        std::vector<size_t> cut{o0};
+        const size_t n = o1 - o0;
+        if (G > 1 && n >= size_t(G)) {
+            uint64_t acc = 0;
+            int next = 1;
+            for (size_t o = o0; o < o1 && next < G; ++o) {
+                for (int i = 0; i < objs[o].k + objs[o].m; ++i) acc += objs[o].present[i] ? objs[o].len[i] : 0;
+                if (double(acc) >= double(up_bytes) * next / G && o + 1 < o1) {
+                    cut.push_back(o + 1);
+                    ++next;
+                }
+            }
+        }
+        cut.push_back(o1);
+        return cut;
+    }
+
+    // Objects [q0, q1) of a wave, their present shards up (or verified):
+    // rebuild each object's missing shards from its decode plan (one grouped
+    // launch, run_rs_mixed, on cs after `up` if given), then send them down
+    // to the caller's buffers and mark them present.  An object short of k
+    // shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT and none of its buffers is
+    // written.
+    int rebuild_down(std::vector<RecObj>& objs, size_t q0, size_t q1, hipStream_t cs, hipEvent_t up, bool data_only) {
+        uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        if (up) MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
+        {
             std::vector<std::shared_ptr<const DecodePlan>> plans(q1 - q0);
             std::vector<uint32_t> offs(q1 - q0);
             std::vector<const uint8_t*> in;
@@ -562,35 +659,35 @@ private:
             }
             MXEC_TRY(flush_down());
         }
-        MXEC_TRY(issue_down());
-        PTRACE(mark("d2h", d2h_));
-        PTRACE(now("down_queued"));
-        const int frc = flush();
-        PTRACE(report("rec_wave"));
-        return frc;
+        return MXEC_OK;
     }
 
-    // Piece-major upload of every present shard (and the expected digests),
-    // each piece of the shards to verify hashed as soon as it is up with the
-    // chains carried in device state slots (run_sha_pieces, slot = message
-    // index in the wave, verdict ok[slot]); after the last piece the verdicts
-    // come back and a mismatch becomes an erasure (chunk_reader.rs:176-196).
-    // Leaves cs after every upload.
-    int verify_in_pieces(std::vector<RecObj>& objs, size_t o0, size_t o1, uint8_t* ok, uint8_t* exp, uint64_t msgs,
-                         uint64_t P) {
+    // Piece-major upload of every present shard of objects [o0, o1) (and the
+    // expected digests), each piece of the shards to verify hashed on cs as
+    // soon as it is up with the chains carried in device state slots
+    // (run_sha_pieces, slot = message index in the wave starting at mb,
+    // verdict ok[slot]); after the last piece the verdicts are copied back
+    // and *verdict recorded.  Returns without waiting.
+    int verify_enqueue(std::vector<RecObj>& objs, size_t o0, size_t o1, uint8_t* ok, uint8_t* exp, uint64_t mb,
+                       hipStream_t cs, hipEvent_t* verdict) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
-        hipStream_t cs = cs_[0];
-        MXEC_TRY(state_.ensure(msgs * 32));
         uint32_t* state = static_cast<uint32_t*>(state_.p);
-        uint64_t longest = 0;
-        for (size_t o = o0; o < o1; ++o)
+        uint64_t longest = 0, up_bytes = 0, vlongest = 0, gm = 0;
+        for (size_t o = o0; o < o1; ++o) {
+            gm += uint64_t(objs[o].k + objs[o].m);
             for (int i = 0; i < objs[o].k + objs[o].m; ++i)
-                if (objs[o].present[i]) longest = std::max(longest, objs[o].len[i]);
-        const PieceGrid grid(P);
+                if (objs[o].present[i]) {
+                    longest = std::max(longest, objs[o].len[i]);
+                    up_bytes += objs[o].len[i];
+                    if (objs[o].expected) vlongest = std::max(vlongest, objs[o].len[i]);
+                }
+        }
+        const uint64_t P = piece_bytes(up_bytes, vlongest);
+        const PieceGrid grid(P ? P : (uint64_t(1) << 20));
         const uint64_t npieces = grid.count(longest);
         for (uint64_t pc = 0; pc < npieces; ++pc) {
             const uint64_t off = grid.start(pc), pw = grid.width(pc);
-            uint64_t g = 0;
+            uint64_t g = mb;
             std::vector<const uint8_t*> sp;
             std::vector<uint64_t> sl, st;
             std::vector<uint32_t> ss;
@@ -622,11 +719,18 @@ private:
             PTRACE(mark("sha", cs));
         }
         PTRACE(now("pieces_queued"));
-        MXEC_TRY(flags_.ensure(msgs));
-        MXEC_HIP(hipMemcpyAsync(flags_.p, ok, msgs, hipMemcpyDeviceToHost, cs));
-        MXEC_HIP(hipStreamSynchronize(cs));
+        MXEC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(flags_.p) + mb, ok + mb, gm, hipMemcpyDeviceToHost, cs));
+        MXEC_TRY(new_event(verdict));
+        MXEC_HIP(hipEventRecord(*verdict, cs));
+        return MXEC_OK;
+    }
+
+    // Waits for objects [o0, o1)'s verdicts (verify_enqueue): a mismatch
+    // becomes an erasure (chunk_reader.rs:176-196).
+    int verify_collect(std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t mb, hipEvent_t verdict) {
+        MXEC_HIP(hipEventSynchronize(verdict));
         const auto* okh = static_cast<const uint8_t*>(flags_.p);
-        uint64_t g = 0;
+        uint64_t g = mb;
         for (size_t o = o0; o < o1; ++o) {
             RecObj& h = objs[o];
             for (int i = 0; i < h.k + h.m; ++i, ++g)

@@ -277,6 +277,9 @@ struct Device {
     // many found SDMA slow; the last verdict also steers the single-request
     // calls' copies of mxec_host_alloc memory.
     std::atomic<uint64_t> sdma_probes{0}, sdma_slow_verdicts{0};
+    // Piece-major verified reconstruct waves and the verification groups
+    // they ran as (pipeline.cpp verify_cuts).
+    std::atomic<uint64_t> verify_waves{0}, verify_groups{0};
     std::atomic<bool> sdma_slow{false};
     // SHA-256 combiner (combiner.cpp): one launch for the verification work
     // of every concurrent caller on this device.

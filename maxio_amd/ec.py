@@ -198,13 +198,18 @@ class Context:
         _check(self._lib.mxec_ctx_coef_stats(self._h, dev, ctypes.byref(r), ctypes.byref(q), ctypes.byref(w)))
         return {"recycles": r.value, "relaunches": q.value, "fence_waits": w.value}
 
-    def copy_stats(self, dev: int = 0) -> dict:
-        """Copies the host-batch pipeline issued on device `dev` since the
-        context opened (mxec_ctx_copy_stats)."""
-        v = [ctypes.c_uint64(0) for _ in range(6)]
-        _check(self._lib.mxec_ctx_copy_stats(self._h, dev, *[ctypes.byref(x) for x in v]))
-        return dict(zip(("copies_1d", "copies_2d", "rows_2d", "wave_blocks", "sdma_probes", "sdma_slow"),
-                        (x.value for x in v)))
+    PIPE_STATS = ("copies_1d", "copies_2d", "rows_2d", "wave_blocks", "sdma_probes", "sdma_slow", "verify_waves",
+                  "verify_groups")
+
+    def pipe_stats(self, dev: int = 0) -> dict:
+        """Host-batch pipeline counters of device `dev` since the context
+        opened (mxec_ctx_pipe_stats): copies issued by engine, SDMA probes,
+        verification groups."""
+        v = (ctypes.c_uint64 * len(self.PIPE_STATS))()
+        n = self._lib.mxec_ctx_pipe_stats(self._h, dev, v, len(self.PIPE_STATS))
+        if n < 0:
+            _check(n)
+        return dict(zip(self.PIPE_STATS, list(v)[:n]))
 
     def rs_grid(self, k: int, m: int, shard_size: int, dev: int = 0) -> int:
         """Workgroups per CU large uniform RS launches of this shape run at on

@@ -91,6 +91,17 @@ pub struct MxecMultipartPart {
     pub encrypted: u8,
 }
 
+// ---- mxec_ctx_pipe_stats counter indices ----------------------------------
+pub const MXEC_PIPE_STAT_COPIES_1D: c_int = 0;
+pub const MXEC_PIPE_STAT_COPIES_2D: c_int = 1;
+pub const MXEC_PIPE_STAT_ROWS_2D: c_int = 2;
+pub const MXEC_PIPE_STAT_WAVE_BLOCKS: c_int = 3;
+pub const MXEC_PIPE_STAT_SDMA_PROBES: c_int = 4;
+pub const MXEC_PIPE_STAT_SDMA_SLOW: c_int = 5;
+pub const MXEC_PIPE_STAT_VERIFY_WAVES: c_int = 6;
+pub const MXEC_PIPE_STAT_VERIFY_GROUPS: c_int = 7;
+pub const MXEC_PIPE_STAT_COUNT: c_int = 8;
+
 // ---- return codes (reed_solomon_erasure::Error one for one, then MaxIO's) --
 pub const MXEC_OK: c_int = 0;
 pub const MXEC_E_TOO_FEW_SHARDS: c_int = -1;
@@ -138,9 +149,7 @@ extern "C" {
     pub fn mxec_ctx_device_count(ctx: *const MxecCtx) -> c_int;
     pub fn mxec_ctx_device_id(ctx: *const MxecCtx, i: c_int) -> c_int;
     pub fn mxec_ctx_combiner_stats(ctx: *mut MxecCtx, i: c_int, launches: *mut u64, messages: *mut u64) -> c_int;
-    pub fn mxec_ctx_copy_stats(ctx: *mut MxecCtx, dev: c_int, copies_1d: *mut u64, copies_2d: *mut u64,
-                               rows_2d: *mut u64, wave_blocks: *mut u64, sdma_probes: *mut u64,
-                               sdma_slow: *mut u64) -> c_int;
+    pub fn mxec_ctx_pipe_stats(ctx: *mut MxecCtx, dev: c_int, out: *mut u64, n: c_int) -> c_int;
     pub fn mxec_ctx_rs_grid(ctx: *mut MxecCtx, dev: c_int, k: c_int, m: c_int, shard_size: u64) -> c_int;
     pub fn mxec_ctx_coef_stats(ctx: *mut MxecCtx, dev: c_int, recycles: *mut u64, relaunches: *mut u64,
                                fence_waits: *mut u64) -> c_int;

@@ -6,7 +6,7 @@ digests, filesystem.rs:1107-1135; the GET's rebuild, chunk_reader.rs:157-226).
   with the piece size chosen per wave at a batch large enough to be
   upload-bound: the same piece of an object's k data chunks goes up as one
   2D SDMA copy (pipeline.cpp flush_up), its m parity pieces come down as
-  one (flush_down).  mxec_ctx_copy_stats proves the 2D copies ran.  Shards
+  one (flush_down).  mxec_ctx_pipe_stats proves the 2D copies ran.  Shards
   off the piece grid; a short and an empty last data chunk break the 2D run
   in the middle of the batch.  EVERY object's parity and all k+m digests
   equal oracle.compute_parity.
@@ -56,9 +56,9 @@ def _put_and_check(ctx, n, S, seed, short=None):
     dptr = [data[o, j].ctypes.data for o in range(n) for j in range(k)]
     pptr = [par[o, i].ctypes.data for o in range(n) for i in range(m)]
     dig = np.zeros(n * (k + m) * 32, np.uint8)
-    before = ctx.copy_stats()
+    before = ctx.pipe_stats()
     status = ctx.encode_batch_host(objs, dptr, pptr, data_len=dlen, digests=dig)
-    after = ctx.copy_stats()
+    after = ctx.pipe_stats()
     assert (status == 0).all()
 
     def check(o):
@@ -131,11 +131,11 @@ def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset, floor):
         for i in rng.choice(k + m, 2, replace=False):
             present[o, i] = 0
             shard[o][i][:] = 0x5A
-    before = ctx.copy_stats()
+    before = ctx.pipe_stats()
     pr = present.reshape(-1).copy()
     rc, st = ctx.reconstruct_batch_host(objs, [shard[o][i].ctypes.data for o in range(n) for i in range(k + m)],
                                         pr, shard_len=(dl + [S] * m) * n, expected=dig)
-    after = ctx.copy_stats()
+    after = ctx.pipe_stats()
     assert rc == 0 and not st.any() and pr.all()
     for o in range(n):
         for i in range(k + m):
@@ -156,9 +156,9 @@ def test_auto_copy_engine_follows_the_sdma_probe(ctx_with, floor, waves):
     verified GET of the same objects)."""
     ctx = ctx_with(MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
     S = 3 * M + 4096 + 48
-    before = ctx.copy_stats()
+    before = ctx.pipe_stats()
     _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333})
-    after = ctx.copy_stats()
+    after = ctx.pipe_stats()
     assert after["sdma_probes"] > before["sdma_probes"], (before, after)
     assert (after["wave_blocks"] > before["wave_blocks"]) == waves, (before, after)
     assert (after["sdma_slow"] > before["sdma_slow"]) == waves, (before, after)
