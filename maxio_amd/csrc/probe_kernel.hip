@@ -133,6 +133,62 @@ __global__ __launch_bounds__(256) void probe_pattern(const uint8_t* __restrict__
     }
 }
 
+// The RS pattern (m = 2) with each workgroup's parity held back in LDS over
+// G consecutive tiles of one object and then stored as G x 16 KiB runs per
+// parity shard (do longer store bursts recover the ~12 %
+// the 2:1 read / write mix costs?).  LDS: G x 2 x 16 KiB per workgroup
+// (G = 2: 64 KiB, two workgroups per CU; G = 4: 128 KiB, one).
+template <int G>
+__global__ __launch_bounds__(256) void probe_pattern_lds(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                         uint32_t k, uint64_t S, uint64_t n_obj, uint64_t ostride,
+                                                         uint64_t sstride) {
+    constexpr int R = 2;
+    constexpr uint64_t kTile = 256 * 16 * 4;
+    __shared__ u32x4 held[G][R][4][256];
+    const uint64_t tpo = S / kTile, spo = tpo / G, n_super = spo * n_obj;
+    for (uint64_t t = blockIdx.x; t < n_super; t += gridDim.x) {
+        const uint64_t o = t / spo, t0 = (t - o * spo) * G;
+#pragma unroll 1
+        for (int g = 0; g < G; ++g) {
+            const uint64_t base = (t0 + g) * kTile + threadIdx.x * 16;
+            u32x4 acc[4][R];
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int i = 0; i < R; ++i) acc[v][i] = u32x4{0, 0, 0, 0};
+            for (uint32_t j = 0; j < k; j += 4) {
+                u32x4 x[4][4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        x[jj][v] = __builtin_nontemporal_load(
+                            reinterpret_cast<const u32x4*>(data + o * ostride + (j + jj) * sstride + base + v * 4096));
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+#pragma unroll
+                    for (int i = 0; i < R; ++i) acc[v][i] ^= (x[0][v] ^ x[1][v]) + (x[2][v] ^ x[3][v]) * (i + 1u);
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int i = 0; i < R; ++i) held[g][i][v][threadIdx.x] = acc[v][i];
+        }
+        // Each lane stores back what it computed (same addresses as the plain
+        // pattern), shard after shard, G tiles in a row.
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    __builtin_nontemporal_store(
+                        held[g][i][v][threadIdx.x],
+                        reinterpret_cast<u32x4*>(par + o * ostride + i * sstride + (t0 + g) * kTile +
+                                                 threadIdx.x * 16 + v * 4096));
+    }
+}
+
 // The RS tile schedule split into its halves (the placement lab's
 // diagnosis): READ only loads the k data shards of every tile (folded into a
 // sink store that never fires), WRITE only stores the R parity shards.
@@ -382,6 +438,24 @@ extern "C" int mxprobe_rs_pattern_part(const void* data, void* parity, uint32_t 
     if (part == 0) hipLaunchKernelGGL((probe_pattern_part<2, true, false>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
     else if (part == 1) hipLaunchKernelGGL((probe_pattern_part<2, false, true>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
     else hipLaunchKernelGGL((probe_pattern_part<2, true, true>), g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride, sk);
+    return int(hipGetLastError());
+}
+
+// probe_pattern_lds over an object-major batch (m = 2, k a multiple of 4,
+// S a multiple of G x 16 KiB; parity at data + k * shard_stride of each
+// object), `wpc` workgroups per CU.
+extern "C" int mxprobe_rs_pattern_lds(const void* data, void* parity, uint32_t k, uint64_t S, uint64_t n_obj,
+                                      uint64_t obj_stride, uint64_t shard_stride, int G, int wpc, void* stream) {
+    if (k == 0 || (k & 3) || S == 0 || (G != 2 && G != 4) || (S % (uint64_t(G) * 16384)) || wpc < 1 ||
+        wpc > 4096 || ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity)) & 15) ||
+        static_cast<const uint8_t*>(parity) != static_cast<const uint8_t*>(data) + uint64_t(k) * shard_stride)
+        return int(hipErrorInvalidValue);
+    const dim3 g(uint32_t(cus() * wpc)), b(256);
+    const auto* in = static_cast<const uint8_t*>(data);
+    auto* out = static_cast<uint8_t*>(parity);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (G == 2) hipLaunchKernelGGL(probe_pattern_lds<2>, g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride);
+    else hipLaunchKernelGGL(probe_pattern_lds<4>, g, b, 0, s, in, out, k, S, n_obj, obj_stride, shard_stride);
     return int(hipGetLastError());
 }
 

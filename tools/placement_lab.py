@@ -61,6 +61,9 @@ def main() -> int:
     ap.add_argument("--parts", action="store_true",
                     help="also time the RS pattern's halves on each batch (m = 2): reads of the k data shards "
                          "only, writes of the parity only, both; and a plain read stream of the same bytes")
+    ap.add_argument("--lds", default="",
+                    help="comma list of G:wpc (e.g. 2:512,4:256): the RS pattern with each workgroup's parity held "
+                         "in LDS over G tiles and stored in G x 16 KiB runs (mxprobe_rs_pattern_lds, m = 2)")
     ap.add_argument("--revisit", type=int, default=0,
                     help="after the last allocation, time rs (first grid) and f4copy on every kept batch again, "
                          "this many passes (is a slow batch slow for good, or only when it came first?)")
@@ -139,6 +142,17 @@ def main() -> int:
             d0, p0, k, m, S, n, ost, ost, ss, sh), a.reps))
         row["f4pattern_TBps"] = tbps(bench.event_ms(torch, st, lambda: probe.mxprobe_rs_float4_strided(
             d0, p0, k, m, S, n, ost, ost, ss, sh), a.reps))
+        for spec in [x for x in a.lds.split(",") if x]:
+            G, wpc = (int(x) for x in spec.split(":"))
+            probe.mxprobe_rs_pattern_lds.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                     ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+            probe.mxprobe_rs_pattern_lds.restype = ctypes.c_int
+            rc = probe.mxprobe_rs_pattern_lds(d0, p0, k, S, n, ost, ss, G, wpc, sh)
+            if rc:
+                raise SystemExit(f"mxprobe_rs_pattern_lds rc {rc}")
+            row[f"pattern_lds{G}_wpc{wpc}_TBps"] = tbps(bench.event_ms(torch, st, lambda: probe.mxprobe_rs_pattern_lds(
+                d0, p0, k, S, n, ost, ss, G, wpc, sh), a.reps))
         if a.parts:
             sink = torch.zeros(16, dtype=torch.uint8, device=dev)
             probe.mxprobe_rs_pattern_part.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
@@ -155,7 +169,7 @@ def main() -> int:
         half = (obj.numel() // 2) & ~15
         ms = bench.event_ms(torch, st, lambda: probe.mxprobe_copy_float4(d0 + half, d0, half, sh), a.reps)
         row["f4copy_TBps"] = round(2 * half / (ms * 1e-3) / 1e12, 4)
-        for key in [x for x in row if x.startswith("rs_") and x.endswith("_TBps")]:
+        for key in [x for x in row if x.startswith(("rs_", "pattern")) and x.endswith("_TBps")]:
             row[key.replace("_TBps", "_of_f4copy")] = round(row[key] / row["f4copy_TBps"], 4)
         print(json.dumps(row), flush=True)
     g0 = a.grids.split(",")[0]
