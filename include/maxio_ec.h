@@ -118,20 +118,22 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
 /* Host-batch pipeline (mxec_{encode,reconstruct}_batch_host) counters of ctx
  * device `dev` since the context opened, into out[0 .. n): the copies it
  * issued (1D SDMA DMAs, 2D SDMA DMAs -- the PUT's piece copies -- and their
- * rows, CU-wave copy blocks), the SDMA health probes MXEC_PIPE_COPY=auto ran
- * before large batches and how many found SDMA below its floor (those
- * batches copied by waves), and the piece-major verified reconstruct waves
- * and the verification groups they ran as.  Returns how many counters were
+ * rows, CU-wave copy blocks), the upload brackets MXEC_PIPE_COPY=auto timed
+ * and how many ran below its SDMA floor (the rest of those calls, and the
+ * device's calls for 2 s, copied by waves), the piece-major verified
+ * reconstruct waves and the verification groups they ran as, and the last
+ * timed bracket's SDMA rate in MB/s.  Returns how many counters were
  * written (min(n, MXEC_PIPE_STAT_COUNT)), or an error.  Diagnostics (tests). */
 #define MXEC_PIPE_STAT_COPIES_1D 0
 #define MXEC_PIPE_STAT_COPIES_2D 1
 #define MXEC_PIPE_STAT_ROWS_2D 2
 #define MXEC_PIPE_STAT_WAVE_BLOCKS 3
-#define MXEC_PIPE_STAT_SDMA_PROBES 4
+#define MXEC_PIPE_STAT_SDMA_CHECKS 4
 #define MXEC_PIPE_STAT_SDMA_SLOW 5
 #define MXEC_PIPE_STAT_VERIFY_WAVES 6
 #define MXEC_PIPE_STAT_VERIFY_GROUPS 7
-#define MXEC_PIPE_STAT_COUNT 8
+#define MXEC_PIPE_STAT_SDMA_LAST_MBPS 8
+#define MXEC_PIPE_STAT_COUNT 9
 int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n);
 /* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
  * (k inputs, m outputs, shard_size) at: the grid tuner times the first

@@ -267,7 +267,8 @@ int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n) {
     const uint64_t v[MXEC_PIPE_STAT_COUNT] = {d.copies_1d.load(),        d.copies_2d.load(),
                                               d.copies_2d_rows.load(),   d.copy_wave_blocks.load(),
                                               d.sdma_probes.load(),      d.sdma_slow_verdicts.load(),
-                                              d.verify_waves.load(),     d.verify_groups.load()};
+                                              d.verify_waves.load(),     d.verify_groups.load(),
+                                              d.sdma_last_mbps.load()};
     const int k = std::min(n, int(MXEC_PIPE_STAT_COUNT));
     for (int i = 0; i < k; ++i) out[i] = v[i];
     return k;

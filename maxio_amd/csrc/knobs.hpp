@@ -29,9 +29,9 @@ struct Knobs {
     uint64_t pipe_piece = uint64_t(1) << 20;  // MXEC_PIPE_PIECE_MB (0: whole chunks)
     bool pipe_piece_auto = true;   // MXEC_PIPE_PIECE_MB unset: 1, 2 or 4 MiB per wave (pipeline.cpp)
     int pipe_copy = 2;             // MXEC_PIPE_COPY: 0 sdma (hipMemcpyAsync); 1 waves (copy_kernel.hip
-                                   //   for every host batch); 2 auto: SDMA while a timed probe of it
-                                   //   runs at >= pipe_sdma_floor, waves while it does not
-    long pipe_sdma_floor = 30;     // MXEC_PIPE_SDMA_FLOOR: GB/s (auto's switch point; 0: never waves)
+                                   //   for every host batch); 2 auto: SDMA, its upload rate timed as
+                                   //   it goes; waves after it runs below pipe_sdma_floor
+    long pipe_sdma_floor = 20;     // MXEC_PIPE_SDMA_FLOOR: GB/s (auto's switch point; 0: never waves)
     uint64_t get_window = uint64_t(1) << 30;  // MXEC_GET_WINDOW: bytes of chunks per GET window
     long gather_us = 100;          // MXEC_GATHER_US
     long gather_max_us = 2000;     // MXEC_GATHER_MAX_US

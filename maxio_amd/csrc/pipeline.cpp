@@ -163,20 +163,9 @@ struct PipeRes {
     DevBuf chain_state;  // SHA-256 chain states between pieces (host reconstruct)
     PinnedBuf flags;  // verification verdicts read back (host reconstruct)
     Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
-    // SDMA health (MXEC_PIPE_COPY=auto): a few 1 MiB page-locked -> HBM DMAs
-    // timed before a large batch, and the verdict kept for a short while.
-    struct SdmaProbe {
-        PinnedBuf src;
-        DevBuf dst;
-        hipEvent_t a = nullptr, b = nullptr;
-        double gbps = -1;  // last measured rate (-1: never)
-        bool slow = false;
-        std::chrono::steady_clock::time_point at{};
-        ~SdmaProbe() {
-            if (a) (void)hipEventDestroy(a);
-            if (b) (void)hipEventDestroy(b);
-        }
-    } sdma;
+    // MXEC_PIPE_COPY=auto: calls that start before this instant copy
+    // mxec_host_alloc memory by waves (a recent call measured SDMA slow).
+    std::chrono::steady_clock::time_point waves_until{};
     bool ready = false;
     int init(const Device& dev) {
         if (ready) return MXEC_OK;
@@ -309,14 +298,14 @@ public:
     DevicePipeline(Device& d, PipeRes& r)
         : d_(d), h2d_(r.h2d), d2h_(r.d2h), cs_(r.cs), in_(r.in), out_(r.out), arena_(r.arena),
           pool_(r.pool), scratch_(r.digests), state_(r.chain_state), flags_(r.flags), slot_(r.desc_slot),
-          sdma_(r.sdma) {}
+          res_(r) {}
     ~DevicePipeline() {
         for (auto e : events_) (void)hipEventDestroy(e);
     }
 
     // MXEC_PIPE_COPY (knobs.hpp): sdma; waves (every host batch); auto (the
     // default) -- SDMA while it runs at its normal rate, CU-wave copies while
-    // it does not (sdma_slow).  Measured (profiles/r4/get_stall/,
+    // it does not (watch_open / watch_judge below).  Measured (profiles/r4/get_stall/,
     // e2e_get_modes/): in a healthy process SDMA is the faster engine
     // (RS-only GET 0.101 s against 0.119 by waves at 128 objects; the PUT
     // with digests 0.218 against 0.264, copy waves beside the SHA-256 chains
@@ -324,10 +313,7 @@ public:
     // for seconds to ~7 GB/s ([0.33, 0.92, 0.33, 0.92, 0.27] s verified GETs
     // against 0.263 by waves).
     int run(std::vector<HostObj>& objs) {
-        // encode: SDMA unless waves are asked for, or SDMA is measured slow
-        uint64_t up = 0;
-        for (const auto& h : objs) up += uint64_t(h.k) * h.S;
-        waves_now_ = d_.kn && (d_.kn->pipe_copy == 1 || (d_.kn->pipe_copy == 2 && sdma_slow(up)));
+        start_copy_mode();
         size_t o = 0;
         while (o < objs.size()) {  // waves that fit the pool
             uint64_t need = 0, desc = 1 << 20;
@@ -343,16 +329,12 @@ public:
             MXEC_TRY(wave(objs, o, e));
             o = e;
         }
-        return MXEC_OK;
+        return watch_drain();
     }
 
     // Host reconstruct batch: waves that fit the pool, as run().
     int run_rec(std::vector<RecObj>& objs, bool data_only) {
-        // reconstruct: SDMA unless waves are asked for, or SDMA is measured slow
-        uint64_t up = 0;
-        for (const auto& h : objs)
-            for (int i = 0; i < h.k + h.m; ++i) up += h.present[i] ? h.len[i] : 0;
-        waves_now_ = d_.kn && (d_.kn->pipe_copy == 1 || (d_.kn->pipe_copy == 2 && sdma_slow(up)));
+        start_copy_mode();
         size_t o = 0;
         while (o < objs.size()) {
             uint64_t need = 0, desc = 1 << 20;
@@ -370,53 +352,84 @@ public:
             MXEC_TRY(rec_wave(objs, o, e, data_only));
             o = e;
         }
-        return MXEC_OK;
+        return watch_drain();
     }
 
 private:
-    // Whether this call's copies of mxec_host_alloc memory should avoid SDMA:
-    // before a batch of at least kProbeMinBytes, four 1 MiB DMAs from a
-    // page-locked buffer into HBM on the (idle) upload stream are timed; a
-    // rate under MXEC_PIPE_SDMA_FLOOR GB/s (default 30; healthy: ~33-38 for
-    // 1 MiB copies, collapsed: ~7) sends the batch's copies to the wave
-    // kernels.  The verdict stands for kProbeHoldMs (smaller batches and
-    // back-to-back ones reuse it); the probe costs ~0.15 ms.
-    static constexpr uint64_t kProbeMinBytes = uint64_t(64) << 20;
-    static constexpr int kProbeHoldMs = 200;
-    static constexpr uint64_t kProbeBytes = uint64_t(1) << 20;
-    static constexpr int kProbeCopies = 4;
-    bool sdma_slow(uint64_t upload_bytes) {
-        PipeRes::SdmaProbe& pr = sdma_;
-        const auto now = std::chrono::steady_clock::now();
-        const bool fresh = pr.gbps >= 0 && now - pr.at < std::chrono::milliseconds(kProbeHoldMs);
-        if (fresh || upload_bytes < kProbeMinBytes) return pr.slow;
-        if (hipStreamQuery(h2d_) != hipSuccess) {  // still busy with an earlier batch: keep the verdict
-            (void)hipGetLastError();
-            return pr.slow;
-        }
-        if (pr.src.ensure(kProbeBytes) || pr.dst.ensure(kProbeBytes * kProbeCopies)) return pr.slow;
-        if (!pr.a && (hipEventCreate(&pr.a) != hipSuccess || hipEventCreate(&pr.b) != hipSuccess)) {
-            (void)hipGetLastError();
-            return pr.slow;
-        }
+    // Copy engine under MXEC_PIPE_COPY=auto: SDMA, watched.  The uploads of
+    // each piece (or group) of a wave are bracketed by timing events on the
+    // upload stream (watch_open / watch_close); at most two brackets are in
+    // flight, so the host judges each one about two pieces after issuing it.
+    // A bracket of at least kWatchMinBytes (16 MiB) of direct DMAs (no staging
+    // ring) that ran below MXEC_PIPE_SDMA_FLOOR GB/s (default 20; healthy 1-4 MiB
+    // copies run 33-43, the collapse seen after heavy HBM churn ran ~7)
+    // switches the rest of the call's copies of mxec_host_alloc memory to
+    // the wave kernels, and the device's calls for the next kWavesHoldMs.
+    static constexpr uint64_t kWatchMinBytes = uint64_t(16) << 20;
+    static constexpr int kWavesHoldMs = 2000;
+    struct Bracket {
+        hipEvent_t a, b;
+        uint64_t bytes;
+        bool staged;
+    };
+    std::vector<Bracket> watch_;
+    hipEvent_t watch_a_ = nullptr;
+    bool watch_staged_ = false;
+    uint64_t watch_bytes_ = 0;  // SDMA bytes issued in the open bracket
+    void start_copy_mode() {
+        const int mode = d_.kn ? d_.kn->pipe_copy : 0;
+        waves_now_ = mode == 1 || (mode == 2 && std::chrono::steady_clock::now() < res_.waves_until);
+    }
+    bool watching() const { return d_.kn && d_.kn->pipe_copy == 2 && d_.kn->pipe_sdma_floor > 0 && !waves_now_; }
+    int new_timed_event(hipEvent_t* e) {
+        MXEC_HIP(hipEventCreate(e));
+        events_.push_back(*e);
+        return MXEC_OK;
+    }
+    int watch_open() {
+        if (!watching() || watch_a_) return MXEC_OK;
+        MXEC_TRY(new_timed_event(&watch_a_));
+        MXEC_HIP(hipEventRecord(watch_a_, h2d_));
+        watch_staged_ = false;
+        watch_bytes_ = 0;
+        return MXEC_OK;
+    }
+    // After the bracket's copies are issued (issue_up done).
+    int watch_close() {
+        if (!watch_a_) return MXEC_OK;
+        hipEvent_t b = nullptr;
+        MXEC_TRY(new_timed_event(&b));
+        MXEC_HIP(hipEventRecord(b, h2d_));
+        watch_.push_back(Bracket{watch_a_, b, watch_bytes_, watch_staged_});
+        watch_bytes_ = 0;
+        watch_a_ = nullptr;
+        while (watch_.size() > 2) MXEC_TRY(watch_judge());
+        return MXEC_OK;
+    }
+    int watch_judge() {
+        const Bracket k = watch_.front();
+        watch_.erase(watch_.begin());
+        MXEC_HIP(hipEventSynchronize(k.b));
         float ms = 0;
-        bool ok = hipEventRecord(pr.a, h2d_) == hipSuccess;
-        for (int i = 0; ok && i < kProbeCopies; ++i)
-            ok = hipMemcpyAsync(static_cast<uint8_t*>(pr.dst.p) + uint64_t(i) * kProbeBytes, pr.src.p, kProbeBytes,
-                                hipMemcpyHostToDevice, h2d_) == hipSuccess;
-        ok = ok && hipEventRecord(pr.b, h2d_) == hipSuccess && hipEventSynchronize(pr.b) == hipSuccess &&
-             hipEventElapsedTime(&ms, pr.a, pr.b) == hipSuccess && ms > 0;
-        if (!ok) {
-            (void)hipGetLastError();
-            return pr.slow;
-        }
-        pr.gbps = double(kProbeBytes * kProbeCopies) / (double(ms) * 1e6);
-        pr.slow = pr.gbps < double(d_.kn ? d_.kn->pipe_sdma_floor : 30);
-        pr.at = now;
+        MXEC_HIP(hipEventElapsedTime(&ms, k.a, k.b));
+        if (k.staged || k.bytes < kWatchMinBytes || ms <= 0) return MXEC_OK;
         ++d_.sdma_probes;
-        d_.sdma_slow_verdicts += pr.slow ? 1 : 0;
-        d_.sdma_slow = pr.slow;
-        return pr.slow;
+        const double gbps = double(k.bytes) / (double(ms) * 1e6);
+        d_.sdma_last_mbps = uint64_t(gbps * 1e3);
+        if (!waves_now_ && gbps < double(d_.kn ? d_.kn->pipe_sdma_floor : 20)) {
+            ++d_.sdma_slow_verdicts;
+            waves_now_ = true;  // the rest of this call
+            res_.waves_until = std::chrono::steady_clock::now() + std::chrono::milliseconds(kWavesHoldMs);
+        }
+        d_.sdma_slow = waves_now_;
+        return MXEC_OK;
+    }
+    // End of a call: judge what is left (its copies are done), for the
+    // device's next calls.
+    int watch_drain() {
+        watch_a_ = nullptr;
+        while (!watch_.empty()) MXEC_TRY(watch_judge());
+        return MXEC_OK;
     }
 
     // One wave of a host reconstruct batch (try_reconstruct_data_chunk,
@@ -482,7 +495,7 @@ private:
             const size_t G = cut.size() - 1;
             std::vector<hipEvent_t> verdict(G, nullptr);
             auto enqueue = [&](size_t j) {
-                return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], cs_[j & 1], &verdict[j]);
+                return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], P, cs_[j & 1], &verdict[j]);
             };
             MXEC_TRY(enqueue(0));
             for (size_t j = 0; j < G; ++j) {
@@ -668,24 +681,29 @@ private:
     // (run_sha_pieces, slot = message index in the wave starting at mb,
     // verdict ok[slot]); after the last piece the verdicts are copied back
     // and *verdict recorded.  Returns without waiting.
+    // P: the wave's piece size (piece_bytes over the whole wave: a group's
+    // copies are as large as the wave's, whatever its share of the upload).
+    // Above 1 MiB the same piece of an object's adjacent present shards goes
+    // up as one 2D copy, as in the PUT's upload-bound waves.
     int verify_enqueue(std::vector<RecObj>& objs, size_t o0, size_t o1, uint8_t* ok, uint8_t* exp, uint64_t mb,
-                       hipStream_t cs, hipEvent_t* verdict) {
+                       uint64_t P, hipStream_t cs, hipEvent_t* verdict) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         uint32_t* state = static_cast<uint32_t*>(state_.p);
-        uint64_t longest = 0, up_bytes = 0, vlongest = 0, gm = 0;
+        uint64_t longest = 0, gm = 0;
         for (size_t o = o0; o < o1; ++o) {
             gm += uint64_t(objs[o].k + objs[o].m);
             for (int i = 0; i < objs[o].k + objs[o].m; ++i)
-                if (objs[o].present[i]) {
-                    longest = std::max(longest, objs[o].len[i]);
-                    up_bytes += objs[o].len[i];
-                    if (objs[o].expected) vlongest = std::max(vlongest, objs[o].len[i]);
-                }
+                if (objs[o].present[i]) longest = std::max(longest, objs[o].len[i]);
         }
-        const uint64_t P = piece_bytes(up_bytes, vlongest);
-        const PieceGrid grid(P ? P : (uint64_t(1) << 20));
+        const PieceGrid grid(P);
+        struct TwoD {
+            bool& f;
+            TwoD(bool& flag, bool on) : f(flag) { f = on; }
+            ~TwoD() { f = false; }
+        } twod(pieces2d_, !waves_now_ && P > (uint64_t(1) << 20));
         const uint64_t npieces = grid.count(longest);
         for (uint64_t pc = 0; pc < npieces; ++pc) {
+            MXEC_TRY(watch_open());
             const uint64_t off = grid.start(pc), pw = grid.width(pc);
             uint64_t g = mb;
             std::vector<const uint8_t*> sp;
@@ -712,6 +730,7 @@ private:
             MXEC_TRY(new_event(&up));
             MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_TRY(watch_close());
             PTRACE(mark("up", h2d_));
             MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
             if (!sp.empty())
@@ -750,6 +769,7 @@ private:
         up.assign(groups.size(), nullptr);
         uint64_t g = 0;
         for (size_t q = 0; q < groups.size(); ++q) {
+            MXEC_TRY(watch_open());
             for (size_t o = groups[q].first; o < groups[q].second; ++o) {
                 const RecObj& h = objs[o];
                 for (int i = 0; i < h.k + h.m; ++i) {
@@ -765,6 +785,7 @@ private:
             MXEC_TRY(new_event(&up[q]));
             MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up[q], h2d_));
+            MXEC_TRY(watch_close());
         }
         if (verify) {
             std::vector<const uint8_t*> sp;
@@ -815,7 +836,7 @@ private:
     DevBuf& state_;    // chain states of a piece-major verification
     PinnedBuf& flags_;
     Slot& slot_;
-    PipeRes::SdmaProbe& sdma_;
+    PipeRes& res_;
     std::vector<Pending> pend_;
     std::vector<hipEvent_t> events_;
 
@@ -878,8 +899,10 @@ private:
         if (is_pinned(src, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, h2d_));
             ++d_.copies_1d;
+            watch_bytes_ += len;
             return MXEC_OK;
         }
+        watch_staged_ = true;  // host memcpy through the ring: not an SDMA rate
         for (uint64_t off = 0; off < len; off += kRingBuf) {
             const uint64_t n = std::min(kRingBuf, len - off);
             int r;
@@ -955,13 +978,14 @@ private:
         up_run_ = Run{};
         if (!r.len) return MXEC_OK;
         if (r.rows == 1) return upload(r.dst, r.src, r.len);
-        if (is_pinned(r.src, (r.rows - 1) * r.spitch + r.len)) {
+        if (!waves_now_ && is_pinned(r.src, (r.rows - 1) * r.spitch + r.len)) {
             if (affinity_on(d_)) {
                 const void* p = r.dst;
                 MXEC_TRY(affinity_check(d_, &slot_, h2d_, "pipeline upload 2d", &arena_, &p, 1));
             }
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyHostToDevice, h2d_));
             ++d_.copies_2d;
+            watch_bytes_ += r.len * r.rows;
             d_.copies_2d_rows += r.rows;
             return MXEC_OK;
         }
@@ -980,7 +1004,7 @@ private:
         down_run_ = Run{};
         if (!r.len) return MXEC_OK;
         if (r.rows == 1) return download(r.dst, r.src, r.len);
-        if (is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
+        if (!waves_now_ && is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
             if (affinity_on(d_)) {
                 const void* p = r.src;
                 MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download 2d", &arena_, &p, 1));
@@ -1108,6 +1132,7 @@ private:
         } twod(pieces2d_, !waves_now_ && P > (uint64_t(1) << 20));
         PTRACE(start(h2d_));
         for (uint64_t pc = 0; pc < npieces; ++pc) {
+            MXEC_TRY(watch_open());
             const uint64_t off = grid.start(pc), pw = grid.width(pc);
             for (size_t o = o0; o < o1; ++o) {
                 const HostObj& h = objs[o];
@@ -1124,6 +1149,7 @@ private:
             MXEC_TRY(new_event(&rs_done));
             MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_TRY(watch_close());
             PTRACE(mark("up", h2d_));
             PTRACE(now("up_queued"));
             MXEC_HIP(hipStreamWaitEvent(rs_s, up, 0));
@@ -1251,6 +1277,7 @@ private:
         std::vector<hipEvent_t> done(groups.size());
         hipStream_t rs_s = cs_[0], sha_s = cs_[1];
         for (size_t g = 0; g < groups.size(); ++g) {
+            MXEC_TRY(watch_open());
             const size_t g0 = groups[g].first, g1 = groups[g].second;
             for (size_t o = g0; o < g1; ++o) {
                 const HostObj& h = objs[o];
@@ -1266,6 +1293,7 @@ private:
             MXEC_TRY(new_event(&done[g]));
             MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up, h2d_));
+            MXEC_TRY(watch_close());
             MXEC_HIP(hipStreamWaitEvent(rs_s, up, 0));
             std::map<std::tuple<int, int, uint64_t>, std::vector<size_t>> classes;
             for (size_t o = g0; o < g1; ++o) classes[{objs[o].k, objs[o].m, objs[o].S}].push_back(o);

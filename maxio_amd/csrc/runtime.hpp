@@ -273,10 +273,11 @@ struct Device {
     // Copies the host pipeline issued (mxec_ctx_copy_stats): 1D SDMA DMAs,
     // 2D SDMA DMAs and their rows, CU-wave copy blocks (copy_kernel.hip).
     std::atomic<uint64_t> copies_1d{0}, copies_2d{0}, copies_2d_rows{0}, copy_wave_blocks{0};
-    // SDMA health probes of the host pipeline (MXEC_PIPE_COPY=auto) and how
-    // many found SDMA slow; the last verdict also steers the single-request
-    // calls' copies of mxec_host_alloc memory.
-    std::atomic<uint64_t> sdma_probes{0}, sdma_slow_verdicts{0};
+    // SDMA watch of the host pipeline (MXEC_PIPE_COPY=auto): upload brackets
+    // judged, how many ran below the floor, the last one's rate (MB/s); the
+    // current verdict also steers the single-request calls' copies of
+    // mxec_host_alloc memory.
+    std::atomic<uint64_t> sdma_probes{0}, sdma_slow_verdicts{0}, sdma_last_mbps{0};
     // Piece-major verified reconstruct waves and the verification groups
     // they ran as (pipeline.cpp verify_cuts).
     std::atomic<uint64_t> verify_waves{0}, verify_groups{0};

@@ -198,8 +198,8 @@ class Context:
         _check(self._lib.mxec_ctx_coef_stats(self._h, dev, ctypes.byref(r), ctypes.byref(q), ctypes.byref(w)))
         return {"recycles": r.value, "relaunches": q.value, "fence_waits": w.value}
 
-    PIPE_STATS = ("copies_1d", "copies_2d", "rows_2d", "wave_blocks", "sdma_probes", "sdma_slow", "verify_waves",
-                  "verify_groups")
+    PIPE_STATS = ("copies_1d", "copies_2d", "rows_2d", "wave_blocks", "sdma_checks", "sdma_slow", "verify_waves",
+                  "verify_groups", "sdma_last_mbps")
 
     def pipe_stats(self, dev: int = 0) -> dict:
         """Host-batch pipeline counters of device `dev` since the context

@@ -96,11 +96,12 @@ pub const MXEC_PIPE_STAT_COPIES_1D: c_int = 0;
 pub const MXEC_PIPE_STAT_COPIES_2D: c_int = 1;
 pub const MXEC_PIPE_STAT_ROWS_2D: c_int = 2;
 pub const MXEC_PIPE_STAT_WAVE_BLOCKS: c_int = 3;
-pub const MXEC_PIPE_STAT_SDMA_PROBES: c_int = 4;
+pub const MXEC_PIPE_STAT_SDMA_CHECKS: c_int = 4;
 pub const MXEC_PIPE_STAT_SDMA_SLOW: c_int = 5;
 pub const MXEC_PIPE_STAT_VERIFY_WAVES: c_int = 6;
 pub const MXEC_PIPE_STAT_VERIFY_GROUPS: c_int = 7;
-pub const MXEC_PIPE_STAT_COUNT: c_int = 8;
+pub const MXEC_PIPE_STAT_SDMA_LAST_MBPS: c_int = 8;
+pub const MXEC_PIPE_STAT_COUNT: c_int = 9;
 
 // ---- return codes (reed_solomon_erasure::Error one for one, then MaxIO's) --
 pub const MXEC_OK: c_int = 0;

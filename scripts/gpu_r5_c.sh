@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round 5: the SDMA watch (auto copy engine), verification groups with the
+# wave's piece size and 2D piece copies in the GET, the SHA-256 step lab.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+out=gpurun_out/${1:-r5c}
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_get_groups_gpu.py \
+  tests/test_pipeline_2d_gpu.py tests/test_pipeline_gpu.py tests/test_contract_gpu.py tests/test_storage_gpu.py \
+  > $out/pytest_sel.log 2>&1 || { tail -30 $out/pytest_sel.log; exit 1; }
+tail -1 $out/pytest_sel.log
+timeout -k 10 120 tools/sha_step_lab 2048 > $out/sha_step_lab.jsonl 2>&1 || { cat $out/sha_step_lab.jsonl; exit 1; }
+cat $out/sha_step_lab.jsonl
+for n in 128 512; do
+  timeout -k 10 300 python -u tools/e2e_bench.py --objects $n --reps 3 --alloc mxec --modes pinned --get \
+    > $out/e2e_$n.json 2> $out/e2e_$n.err || { tail -5 $out/e2e_$n.err; exit 1; }
+done
+for g in 1 2 3 4; do
+  MXEC_LIB=$PWD/maxio_amd/lib/libmaxio_ec_lab.so MXEC_GET_VGROUPS=$g timeout -k 10 300 python -u tools/e2e_bench.py \
+    --objects 512 --reps 3 --alloc mxec --modes pinned --get > $out/e2e_512_g$g.json 2> $out/e2e_512_g$g.err \
+    || { tail -5 $out/e2e_512_g$g.err; exit 1; }
+done
+MXEC_LIB=$PWD/maxio_amd/lib/libmaxio_ec_lab.so MXEC_PIPE_COPY2D=0 timeout -k 10 300 python -u tools/e2e_bench.py \
+  --objects 512 --reps 3 --alloc mxec --modes pinned --get > $out/e2e_512_no2d.json 2> $out/e2e_512_no2d.err \
+  || { tail -5 $out/e2e_512_no2d.err; exit 1; }
+timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err \
+  || { tail -20 $out/bench.err; exit 1; }
+echo done

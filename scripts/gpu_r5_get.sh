@@ -24,6 +24,9 @@ MXEC_PIPE_COPY=waves timeout -k 10 300 python -u tools/e2e_bench.py --objects 51
   --get > $out/e2e_512_waves.json 2> $out/e2e_512_waves.err || { tail -5 $out/e2e_512_waves.err; exit 1; }
 timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err \
   || { tail -20 $out/bench.err; exit 1; }
+MXEC_LIB=$PWD/maxio_amd/lib/libmaxio_ec_lab.so timeout -k 10 600 python -u tools/placement_lab.py --objects 1024 \
+  --allocs 5 --free-each --spacer-mib 0,6144,12288,20480,30720 --grids 1024 --lds 2:512,2:1024,4:256,4:512 --reps 5 \
+  > $out/placement_lds.jsonl 2> $out/placement_lds.err || { tail -5 $out/placement_lds.err; exit 1; }
 ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/tc -o run --output-format csv \
     -- python3 -c "import torch; x = torch.ones(1 << 20, device='cuda'); print(float(x.cpu().sum()))" \
     > "$OLDPWD/$out/trace_torch_only.out" 2> "$OLDPWD/$out/trace_torch_only.err" ); echo "torch-only trace exit $?" | tee $out/trace_torch_only.rc
