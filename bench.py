@@ -1454,6 +1454,15 @@ def gpu_numa_node(torch, d: int):
         return None
 
 
+def _copy_delta(c0: list, c1: list) -> dict:
+    """Host-pipeline counters (Context.pipe_stats, one dict per device)
+    accumulated over a leg; sdma_last_mbps is a gauge (the last timed upload
+    bracket's SDMA rate), reported as the lowest over the devices."""
+    out = {key: sum(b[key] - a[key] for a, b in zip(c0, c1)) for key in c1[0] if key != "sdma_last_mbps"}
+    out["sdma_last_mbps"] = min(b.get("sdma_last_mbps", 0) for b in c1)
+    return out
+
+
 def _leg_times(ts: list) -> dict:
     """Every timed batch of a leg, its median (the reported rate) and max."""
     med = statistics.median(ts)
@@ -1483,13 +1492,16 @@ def e2e_put_large(ctx, n: int = 512, reps: int = 3) -> dict:
     for sha in (False, True):
         dig = np.zeros(n * (k + m) * 32, np.uint8) if sha else None
         ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm
+        c0 = ctx.pipe_stats()
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
             ctx.encode_batch_host(objs, dptr, pptr, digests=dig)
             ts.append(time.perf_counter() - t0)
         el = statistics.median(ts)
-        res["rs_sha256" if sha else "rs_only"] = dict(_leg_times(ts), GiBps_payload=round(n * k * S / GIB / el, 2))
+        c1 = ctx.pipe_stats()
+        res["rs_sha256" if sha else "rs_only"] = dict(_leg_times(ts), GiBps_payload=round(n * k * S / GIB / el, 2),
+                                                      copies=_copy_delta([c0], [c1]))
         if sha:
             o = n // 2
             want = _oracle().encode(list(data[o]), m, S)
@@ -1554,6 +1566,7 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
         ctx.encode_batch_host(objs, dptr, pptr, digests=dig)  # warm: pools, tables
         if get_only:
             break
+        c0 = [ctx.pipe_stats(i) for i in range(D)]
         ts = []
         for _ in range(reps):
             barrier()
@@ -1563,8 +1576,10 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
         el = statistics.median(ts)
         payload = reduce_sum(float(n * k * S))
         key = "rs_sha256" if sha else "rs_only"
+        c1 = [ctx.pipe_stats(i) for i in range(D)]
         res[key] = dict(_leg_times(ts), GiBps_payload=round(payload / GIB / el, 2),
-                        frac_of_pcie_bound=round(bound_s / el, 4), frac_of_duplex_bound=round(duplex_s / el, 4))
+                        frac_of_pcie_bound=round(bound_s / el, 4), frac_of_duplex_bound=round(duplex_s / el, 4),
+                        copies=_copy_delta(c0, c1))
     # GET side (chunk_reader.rs:157-226 from the shard files in host memory):
     # mxec_reconstruct_batch_host over the same objects with two seeded
     # erasures each -- the 4 present shards go up, the 2 rebuilt ones come
@@ -1608,8 +1623,7 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
         # Which copy engine the timed batches used (MXEC_PIPE_COPY=auto: SDMA
         # unless its probe found it slow): the copy counters' difference.
         c1 = [ctx.pipe_stats(i) for i in range(D)]
-        res["get_verify_sha256" if verify else "get_rs_only"]["copies"] = {
-            key: sum(b[key] - a[key] for a, b in zip(c0, c1)) for key in c1[0]}
+        res["get_verify_sha256" if verify else "get_rs_only"]["copies"] = _copy_delta(c0, c1)
         if stamps:
             res["get_verify_sha256" if verify else "get_rs_only"]["monotonic_ns"] = marks
     if get_only:
