@@ -104,11 +104,11 @@ def test_put_2d_piece_copies_default_upload_bound(ctx):
 @pytest.mark.parametrize("copy,floor", [("waves", ""), ("auto", "100000")])
 @pytest.mark.parametrize("offset", [0, 3, 16 + 5])
 def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset, floor):
-    """Verified GET of 9 x 4+2 objects whose shards start `offset` bytes into page-locked memory and whose
-    last data chunk is S - 3333 bytes, by waves (MXEC_PIPE_COPY=waves, and
-    auto with a floor no SDMA reaches): every rebuilt shard equals the
-    original; aligned callers take the wave copies (wave_blocks counted),
-    phase-mismatched ones fall back to SDMA."""
+    """Verified GET of 9 x 4+2 objects whose shards start `offset` bytes
+    into page-locked memory and whose last data chunk is S - 3333 bytes, by
+    waves (MXEC_PIPE_COPY=waves, and auto with a floor no SDMA reaches):
+    every rebuilt shard equals the original; aligned callers take the wave
+    copies (wave_blocks counted), phase-mismatched ones fall back to SDMA."""
     ctx = ctx_with(MXEC_PIPE_COPY=copy, MXEC_PIPE_SDMA_FLOOR=floor)
     k, m, n = 4, 2, 9
     S = 2 * M + 4096 + 48
@@ -143,7 +143,7 @@ def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset, floor):
     if offset % 16 == 0:
         assert after["wave_blocks"] > before["wave_blocks"], (before, after)
     if copy == "auto":  # the watch switched (in this call, or an earlier one within 2 s)
-        assert after["sdma_slow"] > 0, (start, after)
+        assert after["sdma_slow"] > 0, (before, after)
     ctx.host_free(buf)
 
 
