@@ -148,16 +148,23 @@ def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset, floor):
 
 
 @pytest.mark.parametrize("floor,waves", [("0", False), ("", False), ("100000", True)])
-def test_auto_copy_engine_follows_the_sdma_watch(ctx_with, floor, waves):
+def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
     """MXEC_PIPE_COPY=auto: each piece's uploads are timed as they go (floor
     0: not watched; the default floor: a healthy SDMA passes; an
     unreachable floor: the first judged piece switches the rest of the call
     to waves); parity and digests against the oracle either way."""
-    ctx = ctx_with(MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
+    from conftest import open_ctx
+
+    # a context of its own: a cached one may still hold an earlier call's
+    # verdict (waves for 2 s after a slow bracket)
+    ctx = open_ctx(2, 0, MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
     S = 3 * M + 4096 + 48
-    before = ctx.pipe_stats()
-    _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333})
-    after = ctx.pipe_stats()
+    try:
+        before = ctx.pipe_stats()
+        _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333})
+        after = ctx.pipe_stats()
+    finally:
+        ctx.close()
     assert (after["sdma_checks"] > before["sdma_checks"]) == (floor != "0"), (before, after)
     assert (after["wave_blocks"] > before["wave_blocks"]) == waves, (before, after)
     assert (after["sdma_slow"] > before["sdma_slow"]) == waves, (before, after)

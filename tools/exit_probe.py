@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Which step of a libmaxio_ec process trips rocprofv3's exit-time fault?
+
+Under `rocprofv3 --kernel-trace --memory-copy-trace`, `bench.py` printed its
+line and then died with SIGSEGV inside libhsa-runtime64.so, called from
+librocprofiler-sdk.so during the profiler tool's own __cxa_finalize
+(profiles/r5/trace_bench_exit_crash.err, resolved with BENCH_DUMP_MAPS=1); a
+torch-only program under the same options exits 0.  This runs one small
+piece of the library's work and exits, so a series of runs under the
+profiler narrows the trigger:
+
+  python tools/exit_probe.py <what> [--no-close]
+    what: open          mxec_open / mxec_close only
+          device        + one device-resident encode (a kernel launch)
+          host_pinned   + one mxec_encode_batch_host from mxec_host_alloc memory
+          host_pageable + one mxec_encode_batch_host from pageable memory
+          hash          + one mxec_sha256_batch (host pointers)
+  --no-close leaves the context open at exit (no stream / event teardown).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["open", "device", "host_pinned", "host_pageable", "hash"])
+    ap.add_argument("--no-close", action="store_true")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import maxio_amd
+
+    torch.cuda.set_device(0)
+    ctx = maxio_amd.Context(device_mask=1, streams_per_device=2)
+    k, m, S, n = 4, 2, 1 << 20, 16
+    if a.what == "device":
+        t = torch.randint(0, 256, (n, k + m, S), dtype=torch.uint8, device="cuda")
+        ctx.encode_strided_device(k, m, S, n, t.data_ptr(), (k + m) * S, S, t[:, k:].data_ptr(), (k + m) * S, S)
+        torch.cuda.synchronize()
+    elif a.what in ("host_pinned", "host_pageable"):
+        if a.what == "host_pinned":
+            data = ctx.host_array(n * k * S).reshape(n, k, S)
+            par = ctx.host_array(n * m * S).reshape(n, m, S)
+        else:
+            data = np.zeros((n, k, S), np.uint8)
+            par = np.zeros((n, m, S), np.uint8)
+        data[:] = 7
+        dig = np.zeros(n * (k + m) * 32, np.uint8)
+        ctx.encode_batch_host([(k, m, S)] * n, [data[o, j].ctypes.data for o in range(n) for j in range(k)],
+                              [par[o, i].ctypes.data for o in range(n) for i in range(m)], digests=dig)
+        if a.what == "host_pinned":
+            ctx.host_free(data)
+            ctx.host_free(par)
+    elif a.what == "hash":
+        ctx.sha256([bytes(range(256)) * 4096] * 8)
+    if not a.no_close:
+        ctx.close()
+    print(f"exit_probe {a.what} close={not a.no_close}: done", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
