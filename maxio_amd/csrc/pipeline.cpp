@@ -358,13 +358,17 @@ public:
 private:
     // Copy engine under MXEC_PIPE_COPY=auto: SDMA, watched.  The uploads of
     // each piece (or group) of a wave are bracketed by timing events on the
-    // upload stream (watch_open / watch_close); at most two brackets are in
-    // flight, so the host judges each one about two pieces after issuing it.
-    // A bracket of at least kWatchMinBytes (16 MiB) of direct DMAs (no staging
-    // ring) that ran below MXEC_PIPE_SDMA_FLOOR GB/s (default 20; healthy 1-4 MiB
-    // copies run 33-43, the collapse seen after heavy HBM churn ran ~7)
-    // switches the rest of the call's copies of mxec_host_alloc memory to
-    // the wave kernels, and the device's calls for the next kWavesHoldMs.
+    // upload stream (watch_open / watch_close).  The host never waits for a
+    // bracket (pacing the enqueue loop two brackets deep held back the group
+    // form's downloads: RS-only PUT at 128 objects 0.188 s against 0.112):
+    // brackets are judged when the host finds them complete, at the latest
+    // when the call has synchronised (watch_drain).  A bracket of at least
+    // kWatchMinBytes (16 MiB) of direct DMAs (no staging ring) that ran
+    // below MXEC_PIPE_SDMA_FLOOR GB/s (default 20; healthy 1-4 MiB copies run
+    // 33-43, the collapse seen after heavy HBM churn ran ~7) switches the
+    // rest of the call's copies of mxec_host_alloc memory (if any are still
+    // to be issued) and the device's calls for the next kWavesHoldMs to the
+    // wave kernels.
     static constexpr uint64_t kWatchMinBytes = uint64_t(16) << 20;
     static constexpr int kWavesHoldMs = 2000;
     struct Bracket {
@@ -403,7 +407,13 @@ private:
         watch_.push_back(Bracket{watch_a_, b, watch_bytes_, watch_staged_});
         watch_bytes_ = 0;
         watch_a_ = nullptr;
-        while (watch_.size() > 2) MXEC_TRY(watch_judge());
+        while (!watch_.empty()) {  // the finished ones, oldest first, without waiting
+            if (hipEventQuery(watch_.front().b) != hipSuccess) {
+                (void)hipGetLastError();
+                break;
+            }
+            MXEC_TRY(watch_judge());
+        }
         return MXEC_OK;
     }
     int watch_judge() {

@@ -178,7 +178,9 @@ __device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], u32x4* dst) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int t = 4 * q + u;
+#ifndef MXEC_LAB_SHA_NOSCHED
             if (t >= 16) SHA_W(t);
+#endif
             o[u] = w[t & 15] + kK256[t];
         }
         dst[q * ROW] = u32x4{o[0], o[1], o[2], o[3]};

@@ -149,10 +149,10 @@ def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset, floor):
 
 @pytest.mark.parametrize("floor,waves", [("0", False), ("", False), ("100000", True)])
 def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
-    """MXEC_PIPE_COPY=auto: each piece's uploads are timed as they go (floor
-    0: not watched; the default floor: a healthy SDMA passes; an
-    unreachable floor: the first judged piece switches the rest of the call
-    to waves); parity and digests against the oracle either way."""
+    """MXEC_PIPE_COPY=auto: each piece's uploads are timed (floor 0: not
+    watched; the default floor: a healthy SDMA passes; an unreachable floor:
+    the call's brackets are judged slow, and the device's next calls copy by
+    waves); parity and digests against the oracle either way."""
     from conftest import open_ctx
 
     # a context of its own: a cached one may still hold an earlier call's
@@ -160,13 +160,15 @@ def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
     ctx = open_ctx(2, 0, MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
     S = 3 * M + 4096 + 48
     try:
-        before = ctx.pipe_stats()
+        s0 = ctx.pipe_stats()
         _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333})
-        after = ctx.pipe_stats()
+        s1 = ctx.pipe_stats()
+        _put_and_check(ctx, 8, S, 1400 + len(floor))  # within the 2 s hold of a slow verdict
+        s2 = ctx.pipe_stats()
     finally:
         ctx.close()
-    assert (after["sdma_checks"] > before["sdma_checks"]) == (floor != "0"), (before, after)
-    assert (after["wave_blocks"] > before["wave_blocks"]) == waves, (before, after)
-    assert (after["sdma_slow"] > before["sdma_slow"]) == waves, (before, after)
+    assert (s1["sdma_checks"] > s0["sdma_checks"]) == (floor != "0"), (s0, s1)
+    assert (s1["sdma_slow"] > s0["sdma_slow"]) == waves, (s0, s1)
+    assert (s2["wave_blocks"] > s1["wave_blocks"]) == waves, (s1, s2)
     if floor == "":
-        assert after["sdma_last_mbps"] > 20000, after  # a healthy box's 1 MiB piece copies
+        assert s1["sdma_last_mbps"] > 20000, s1  # a healthy box's 1 MiB piece copies
