@@ -187,6 +187,52 @@ __device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], u32x4* dst) {
     }
 }
 
+// Producer with two lanes per message (the lag pair form's producer waves):
+// lane L = lane & 1 of the pair computes the schedule words of parity L --
+// W[2s + L] at pair step s = 8 .. 31 -- so a producer wave issues ~350 VALU
+// per block instead of the one-lane form's ~570 and, at two producer waves
+// per workgroup, stays well ahead of the consumers (whose ~600 VALU per
+// block are the chain; with one producer wave the two were neck and neck and
+// the barriers cost the difference).  W[t] = σ1(W[t-2]) + W[t-7] +
+// σ0(W[t-15]) + W[t-16]: t - 2 and t - 16 have the lane's own parity, t - 7
+// and t - 15 the other's.  Own words sit in A[k] = W[2k + L]; the other
+// parity in B, lane 0: B[k] = W[2k + 1], lane 1: B[k] = W[2k + 2], so that
+//   W[2s + L] = A[s] + σ1(A[s - 1]) + B[s - 4] + σ0(B[s])   (indices mod 8)
+// reads the same registers in both lanes.  After step s the pair swaps one
+// word by DPP: lane 0 sends its W[2s], lane 1 its W[2s - 1] (the value of
+// the step before: a v_cndmask picks which), and both store what arrives in
+// B[s - 1].  Each lane writes K + W of its own words into the message's LDS
+// column (rows of four words: components L and L + 2).  kown[k] = K[2k + L].
+#define QDPP_SWAP(x) uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0xB1, 0xF, 0xF, true))  // quad_perm [1,0,3,2]
+
+template <int ROW>
+__device__ __forceinline__ void schedule_kw_pair(const uint32_t (&w)[16], bool odd, const uint32_t (&kown)[32],
+                                                 uint32_t* col) {
+    uint32_t A[8], B[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        A[k] = odd ? w[2 * k + 1] : w[2 * k];
+        B[k] = k < 7 ? (odd ? w[2 * k + 2] : w[2 * k + 1]) : w[15];  // lane 1's B[7] (W[16]) arrives at step 8
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        col[q * ROW * 4] = A[2 * q] + kown[2 * q];
+        col[q * ROW * 4 + 2] = A[2 * q + 1] + kown[2 * q + 1];
+    }
+#pragma unroll
+    for (int s = 8; s < 32; ++s) {
+        const uint32_t x = A[s & 7] + SHA_s1(A[(s - 1) & 7]) + B[(s - 4) & 7] + SHA_s0(B[s & 7]);
+        const uint32_t prev = A[(s - 1) & 7];
+        A[s & 7] = x;
+        if (s < 31) B[(s - 1) & 7] = QDPP_SWAP(odd ? prev : x);
+        if (s & 1) {  // row (s - 1) / 2 has both of this lane's words
+            const int q = s >> 1;
+            col[q * ROW * 4] = prev + kown[s - 1];
+            col[q * ROW * 4 + 2] = x + kown[s];
+        }
+    }
+}
+
 __device__ __forceinline__ void message_words(const uint8_t* p, bool aligned, uint32_t (&w)[16]) {
     if (aligned) {
         u32x4 blk[4];
@@ -214,13 +260,33 @@ __device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a <
 // Blocks 0 .. NB-2 are written before a first barrier, block b + NB - 1
 // before the barrier that opens block b: 1 + nmax barriers in all, which the
 // consumer waves match.
-template <int NB, int ROW>
+// PAIR2: two lanes per message (schedule_kw_pair; lane & 1 = the parity,
+// `col` = the message's LDS column); otherwise one lane per message in column
+// `lane` (schedule_kw).
+// With PAIR2 a producer wave holds half of the workgroup's messages, so the
+// workgroup-wide facts come from the caller: `wg_donor`, a message of nmax
+// blocks (the re-read target of lanes without blocks), and `wg_aligned`,
+// whether every message of the workgroup is 16-byte aligned.
+template <int NB, int ROW, bool PAIR2 = false>
 __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live, const uint8_t* p,
-                                            uint64_t nfull, uint64_t nmax, bool aligned) {
+                                            uint64_t nfull, uint64_t nmax, bool aligned, uint32_t col = 0,
+                                            const uint8_t* wg_donor = nullptr, bool wg_aligned = true) {
     constexpr int AHEAD = NB - 1;  // blocks the producer runs ahead of the consumer
     constexpr int BUF = 16 * ROW;  // u32x4 per buffer
     uint32_t w[16];
-    if (__all(!live || nfull == 0 || aligned)) {
+    const bool odd = (lane & 1) != 0;
+    uint32_t kown[32];  // K[2k + parity] (PAIR2)
+    if constexpr (PAIR2) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) kown[k] = odd ? kK256[2 * k + 1] : kK256[2 * k];
+    }
+    auto schedule = [&](uint32_t buf) {
+        if constexpr (PAIR2)
+            schedule_kw_pair<ROW>(w, odd, kown, reinterpret_cast<uint32_t*>(kw + buf * BUF + col) + (odd ? 1 : 0));
+        else
+            schedule_kw<ROW>(w, kw + buf * BUF + lane);
+    };
+    if (PAIR2 ? wg_aligned : __all(!live || nfull == 0 || aligned)) {
         // Every message 16-byte aligned: the raw bytes of the next
         // kShaPrefetch blocks stay in flight across the barriers in a
         // register ring indexed at compile time (the loop is unrolled by the
@@ -234,10 +300,12 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
         // the next use drain every load in flight (it cannot count the ones
         // that may have been skipped).  Blocks at or past nmax are scheduled
         // into buffers nobody reads as a real block.
-        const uint64_t donor_mask = __ballot(nfull == nmax);
-        const int donor = __ffsll((unsigned long long)donor_mask) - 1;
-        const uint8_t* dp = reinterpret_cast<const uint8_t*>(
-            __shfl(reinterpret_cast<uintptr_t>(p), donor));
+        const uint8_t* dp = wg_donor;
+        if constexpr (!PAIR2) {
+            const uint64_t donor_mask = __ballot(nfull == nmax);
+            const int donor = __ffsll((unsigned long long)donor_mask) - 1;
+            dp = reinterpret_cast<const uint8_t*>(__shfl(reinterpret_cast<uintptr_t>(p), donor));
+        }
         const bool own = live && nfull > 0;
         const uint8_t* ps = own ? p : dp;
         const uint64_t last = (own ? nfull : nmax) - 1;  // nmax > 0 when the loop runs
@@ -251,7 +319,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
 #pragma unroll
             for (int j = 0; j < AHEAD; ++j) {
                 block_words(blk[j], w);
-                schedule_kw<ROW>(w, kw + j * BUF + lane);
+                schedule(uint32_t(j));
             }
         }
         __syncthreads();
@@ -268,7 +336,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
                 // consumes: lanes compress only blocks below their nfull).
                 block_words(ring[j], w);
                 load_block(ps + 64 * min_u64(b + AHEAD + kShaPrefetch, last), ring[j]);
-                schedule_kw<ROW>(w, kw + wb * BUF + lane);
+                schedule(wb);
                 wb = wb + 1 == NB ? 0 : wb + 1;
                 __syncthreads();
             }
@@ -277,7 +345,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
         for (int j = 0; j < kShaPrefetch - 1; ++j) {  // the ring already holds these blocks
             if (b0 + j < nmax) {
                 block_words(ring[j], w);
-                schedule_kw<ROW>(w, kw + wb * BUF + lane);
+                schedule(wb);
                 wb = wb + 1 == NB ? 0 : wb + 1;
                 __syncthreads();
             }
@@ -288,14 +356,14 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
         for (int j = 0; j < AHEAD; ++j)
             if (uint64_t(j) < nfull) {
                 message_words(p + 64 * j, aligned, w);
-                schedule_kw<ROW>(w, kw + j * BUF + lane);
+                schedule(uint32_t(j));
             }
         __syncthreads();
         uint32_t wb = AHEAD % NB;
         for (uint64_t b = 0; b < nmax; ++b) {
             if (b + AHEAD < nfull) {
                 message_words(p + 64 * (b + AHEAD), aligned, w);
-                schedule_kw<ROW>(w, kw + wb * BUF + lane);
+                schedule(wb);
             }
             wb = wb + 1 == NB ? 0 : wb + 1;
             __syncthreads();
@@ -552,7 +620,10 @@ __device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[
 // lag form needs no zero lanes, so lanes 4j+2 / 4j+3 run a second message's
 // E and A sides -- and a workgroup is the producer wave (64 messages) plus two
 // consumer waves of 32: 64 messages per workgroup of three waves.
-template <bool LAG, bool PAIR = false>
+// P2 (PAIR only; the auto form): two producer waves of 32 messages, two
+// lanes per message (schedule_kw_pair), waves 0-1; consumers waves 2-3: a
+// workgroup of four waves, one per SIMD.
+template <bool LAG, bool PAIR = false, bool P2 = false>
 __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* __restrict__ ptrs,
                                                          const uint64_t* __restrict__ lens,
                                                          uint8_t* __restrict__ digests,
@@ -561,6 +632,8 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
                                                          uint8_t* __restrict__ ok, uint32_t n, uint32_t prio,
                                                          ShaPiece pc) {
     static_assert(LAG || !PAIR, "two messages per quad needs the lag form (no zero lanes)");
+    static_assert(PAIR || !P2, "two producer waves serve the two-messages-per-quad consumers");
+    constexpr uint32_t PW = P2 ? 2 : 1;  // producer waves
     constexpr int NB = 3, BUF = 16 * kQuadRow;
     constexpr uint32_t MSGS = PAIR ? 64 : kShaQuadMsgs;  // messages per workgroup
     sha_priority(prio);
@@ -585,13 +658,29 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     }
     nmax = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(nmax >> 32))) << 32) |
            __builtin_amdgcn_readfirstlane(uint32_t(nmax));
-    if (wave == 0) {
+    if constexpr (P2) {
+        if (wave < PW) {  // producer wave `wave`: messages 32 * wave + lane / 2, two lanes each
+            // The workgroup-wide donor and alignment, from the one-lane-per-
+            // message view (pi = base + lane) every wave holds.
+            const uint64_t dmask = __ballot(plive && pfull == nmax);
+            const int dl = dmask ? __ffsll((unsigned long long)dmask) - 1 : 0;
+            const uint8_t* wdonor = reinterpret_cast<const uint8_t*>(__shfl(reinterpret_cast<uintptr_t>(pp), dl));
+            const bool waligned = __all(!plive || pfull == 0 || (reinterpret_cast<uintptr_t>(pp) & 15) == 0);
+            const uint32_t mi = wave * 32 + (lane >> 1), qi = base + mi;
+            const bool qlive = qi < n;
+            const uint8_t* qp = qlive ? ptrs[qi] : nullptr;
+            const uint64_t qfull = qlive ? lens[qi] / 64 : 0;
+            kw_producer<NB, kQuadRow, true>(&kw[0][0][0], lane, qlive, qp, qfull, nmax,
+                                            (reinterpret_cast<uintptr_t>(qp) & 15) == 0, mi, wdonor, waligned);
+            return;
+        }
+    } else if (wave == 0) {
         kw_producer<NB, kQuadRow>(&kw[0][0][0], lane, plive, pp, pfull, nmax,
                                   (reinterpret_cast<uintptr_t>(pp) & 15) == 0);
         return;
     }
     const uint32_t role = PAIR ? lane & 1 : lane & 3;
-    const uint32_t ml = PAIR ? (wave - 1) * 32 + (lane >> 1) : (wave - 1) * 16 + (lane >> 2);
+    const uint32_t ml = PAIR ? (wave - PW) * 32 + (lane >> 1) : (wave - 1) * 16 + (lane >> 2);
     const uint32_t i = base + ml;
     const bool live = i < n;
     const uint8_t* p = live ? ptrs[i] : nullptr;
@@ -953,9 +1042,16 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
 #else
     if (form == 4 || form == 5) return hipErrorInvalidValue;
 #endif
-    if (form == 6) {  // the lag quad, two messages per quad (the auto form)
-        hipLaunchKernelGGL((sha256_quad_kernel<true, true>), dim3((a.n + 63) / 64), dim3(192), 0, s, a.ptrs, a.lens,
-                           a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
+    if (form == 6) {  // the lag quad, two messages per quad, two producer waves (the auto form)
+#ifdef MXEC_LAB
+        if (const char* e = getenv("MXEC_SHA_PRODUCERS"); e && atoi(e) == 1) {  // lab A/B: one producer wave
+            hipLaunchKernelGGL((sha256_quad_kernel<true, true, false>), dim3((a.n + 63) / 64), dim3(192), 0, s, a.ptrs,
+                               a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
+            return hipGetLastError();
+        }
+#endif
+        hipLaunchKernelGGL((sha256_quad_kernel<true, true, true>), dim3((a.n + 63) / 64), dim3(256), 0, s, a.ptrs,
+                           a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
         return hipGetLastError();
     }
     if (form == 3) {
