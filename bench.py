@@ -69,11 +69,13 @@ GIB = float(1 << 30)
 # one-wave form 1410 (64 x 14 rounds + 48 x 10 schedule + 16 byte swaps + 18);
 # stream form 1415 (the one-wave rounds plus the clamped prefetch).
 # Quad form (the lag variant with two messages per quad, 64 messages per
-# workgroup): producer 566 + 2 consumers x 607 wave-instructions per block
-# over 64 messages = 1780 lane-ops per message-block; it spends more lane-ops per hash to cut
-# the serial wave's count, so config 3 keeps the one-lane split form's 1470
-# as its chip-wide denominator (comparable across rounds).
-SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415, "quad": 1780}
+# workgroup): since round 5 two producer waves (two lanes per message, 367
+# wave-instructions per block each) + 2 consumers x 607 over 64 messages =
+# 1948 lane-ops per message-block (round 4's one producer wave: 566, 1780);
+# it spends more lane-ops per hash to cut the serial wave's count, so config 3
+# keeps the one-lane split form's 1470 as its chip-wide denominator
+# (comparable across rounds).
+SHA_VALU_PER_BLOCK = {"split": 1470, "one": 1410, "stream": 1415, "quad": 1948}
 # The serial wave (the consumer) of each latency form issues this many VALU
 # per block (split: 64 rounds x 14 + 9; quad, lag variant: 66 steps x 9 + 13); a wave issues at
 # most one VALU every 4 cycles, so a lone message's chain cannot beat that

@@ -1,6 +1,6 @@
 // combiner.cpp — cross-request coalescing of SHA-256 verification.
 //
-// SHA-256 of one message is a serial chain (1.27 us per 64-byte block in the
+// SHA-256 of one message is a serial chain (1.17 us per 64-byte block in the
 // lag pair form, ~1.8 in the split form: kernels.hpp kShaLagUsPerBlock /
 // kShaSplitUsPerBlock, sha256_kernel.hip), so a launch over 8 chunks of one GET takes as
 // long as a launch over thousands: per-request launches leave the GPU nearly
@@ -264,7 +264,7 @@ int sha256_combined(Device& d, Slot& slot, hipStream_t s, const std::vector<cons
         // are pending as the previous launch carried, so a steady stream of
         // concurrent callers keeps landing in few launches instead of a lone
         // first request and the rest; a lone leader waits a short window.  A
-        // launch lasts >= kShaLagUsPerBlock (1.27 us) per 64-byte block of its
+        // launch lasts >= kShaLagUsPerBlock (1.17 us) per 64-byte block of its
         // longest message (~21 ms per 1 MiB chunk), so the wait costs a few percent at most, and
         // the previous size is forgotten as soon as fewer come.
         const size_t want = c->last_batch;

@@ -127,9 +127,10 @@ constexpr uint32_t kShaQuadMsgs = 48;
 constexpr uint32_t kShaLagMsgs = 64;
 // A chain's pace per 64-byte block on the MI355X (us), for host-side
 // estimates of a launch's length (combiner.cpp): the lag pair form the auto
-// choice takes up to kShaLagMsgs per CU (config 3: 20.7 ms for 16 384
-// blocks), the split / one-wave forms beyond (29 ms per 1 MiB chunk).
-constexpr double kShaLagUsPerBlock = 1.27;
+// choice takes up to kShaLagMsgs per CU (config 3: 19.1 ms for 16 384
+// blocks, two producer waves since round 5), the split / one-wave forms
+// beyond (29 ms per 1 MiB chunk).
+constexpr double kShaLagUsPerBlock = 1.17;
 constexpr double kShaSplitUsPerBlock = 1.8;
 // Blocks per stream-form segment (32 KiB of each message).
 constexpr uint32_t kShaSegBlocks = 512;
