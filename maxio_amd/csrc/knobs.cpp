@@ -13,7 +13,7 @@ const char* const kKnobNames[] = {
     "MXEC_DEBUG_AFFINITY",
     "MXEC_HOST_NUMA",            "MXEC_SPIN_WAIT",    "MXEC_RS_TUNE",            "MXEC_RS_MULTI",
     "MXEC_SHA_FORM",             "MXEC_DESC_UPLOAD",  "MXEC_PIPE_PIECE_MB",      "MXEC_GET_WINDOW",
-    "MXEC_PIPE_COPY",            "MXEC_PIPE_SDMA_FLOOR",
+    "MXEC_PIPE_COPY",            "MXEC_PIPE_SDMA_FLOOR",   "MXEC_GET_VGROUPS",
     "MXEC_GATHER_US",            "MXEC_GATHER_MAX_US", "MXEC_GATHER_IDLE_US",    "MXEC_COMBINE_BELOW",
     "MXEC_COMBINE_STREAMS",      "MXEC_COMBINE_PRIORITY", "MXEC_COMBINE_LOG",    nullptr};
 
@@ -92,6 +92,7 @@ Knobs read_knobs() {
         if (c >= 0) k.pipe_copy = c;
     }
     k.pipe_sdma_floor = std::max(0L, env_long("MXEC_PIPE_SDMA_FLOOR", k.pipe_sdma_floor));
+    k.get_vgroups = int(std::max(1L, std::min(8L, env_long("MXEC_GET_VGROUPS", 1))));
     long window = 0;
     if (parse_long("MXEC_GET_WINDOW", &window)) k.get_window = uint64_t(std::max(1L, window));
     k.gather_us = env_long("MXEC_GATHER_US", k.gather_us);

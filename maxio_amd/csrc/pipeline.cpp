@@ -556,38 +556,20 @@ private:
     }
 
     // Verification groups of a piece-major reconstruct wave: cut points
-    // (first o0, last o1) by upload bytes.  With G groups the last group's
-    // chains start (G-1)/G of the way through the upload, and only the last
-    // group's rebuilt shards go down after the upload has ended, so the wave
-    // lasts about
-    //   max((G-1)/G * T_up + chain, T_up + one piece's hash) + D / G
-    // against max(chain, T_up + piece) + D for one group (T_up: the upload
-    // at the piece copies' rate, chain: the longest message's SHA-256, D:
-    // the rebuilt shards' download).  The smallest G (1..4) within 2 % of
-    // the best is taken.  A wave whose upload is shorter than its chain
-    // stays one group (128 x 4+2 x 10 MiB: 0.26 s either way).
+    // (first o0, last o1) by upload bytes, MXEC_GET_VGROUPS of them (default
+    // 1).  A model -- the last group's chains start (G-1)/G of the way
+    // through the upload and only its rebuilt shards go down after it, so
+    // max((G-1)/G * T_up + chain, T_up + piece) + D / G against one group's
+    // max(chain, T_up + piece) + D -- predicted 7-15 % from grouping at 512
+    // x 4+2 x 10 MiB, but the box does not overlap the two directions for
+    // free: the early groups' downloads run at the ~25 GB/s a D2H stream gets
+    // beside a full H2D stream (pcie duplex 2:1) and the last group's
+    // download waits behind them.  Measured (profiles/r5/get_groups/,
+    // MXEC_PIPE_TRACE marks): one group 0.655 s, two 0.818, four 0.631-0.640.
+    // So one group unless a caller's box says otherwise.
     std::vector<size_t> verify_cuts(const std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t up_bytes,
-                                    uint64_t longest, uint64_t P) const {
-        uint64_t down_bytes = 0;
-        for (size_t o = o0; o < o1; ++o)
-            for (int i = 0; i < objs[o].k + objs[o].m; ++i) down_bytes += objs[o].present[i] ? 0 : objs[o].len[i];
-        const double up_rate = (P >= (uint64_t(4) << 20) ? 43.0 : P >= (uint64_t(2) << 20) ? 38.0 : 33.0) * 1e9;
-        const double T = double(up_bytes) / up_rate, D = double(down_bytes) / 50e9;
-        const double chain = double(longest / 64) * kShaLagUsPerBlock * 1e-6;
-        const double piece = double(std::min(P, longest) / 64) * kShaLagUsPerBlock * 1e-6;
-        int G = 1;
-#ifdef MXEC_LAB
-        if (const char* e = getenv("MXEC_GET_VGROUPS")) G = std::max(1, std::min(8, atoi(e)));  // lab: force
-        else
-#endif
-        {
-            double est[5] = {0, 0, 0, 0, 0}, best = 1e30;
-            for (int g = 1; g <= 4; ++g) {
-                est[g] = std::max(double(g - 1) / g * T + chain, T + piece) + D / g;
-                best = std::min(best, est[g]);
-            }
-            while (G < 4 && est[G] > best * 1.02) ++G;
-        }
+                                    uint64_t /*longest*/, uint64_t /*P*/) const {
+        const int G = d_.kn ? int(d_.kn->get_vgroups) : 1;
         std::vector<size_t> cut{o0};
         const size_t n = o1 - o0;
         if (G > 1 && n >= size_t(G)) {

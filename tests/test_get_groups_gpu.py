@@ -1,7 +1,7 @@
-"""GPU: the verified host GET of a large batch runs as pipelined verification
-groups (pipeline.cpp verify_cuts / verify_enqueue / verify_collect): group
-j + 1's pieces go up and hash while the host collects group j's verdicts,
-rebuilds it and sends its shards down.  Reference: try_reconstruct_data_chunk,
+"""GPU: the verified host GET, as one verification group (the default) and as
+pipelined groups (MXEC_GET_VGROUPS; pipeline.cpp verify_cuts / verify_enqueue
+/ verify_collect): group j + 1's pieces go up and hash while the host
+collects group j's verdicts, rebuilds it and sends its shards down.  Reference: try_reconstruct_data_chunk,
 chunk_reader.rs:157-226, per object.
 
 160 objects of 8+4 x 1 MiB (some shards shorter) from page-locked memory, two
@@ -9,7 +9,7 @@ erasures each, silent corruption in objects on both sides of every group
 boundary, and two objects (one early, one late) with more bad shards than
 parity: every rebuilt shard equals the original, every failing object's
 buffers are untouched and its status is MXEC_E_TOO_FEW_SHARDS_PRESENT, and
-mxec_ctx_pipe_stats shows the wave ran as more than one group.
+mxec_ctx_pipe_stats shows the wave ran as that many groups.
 """
 from __future__ import annotations
 
@@ -24,7 +24,9 @@ M = 1 << 20
 TOO_FEW_SHARDS_PRESENT = -10  # include/maxio_ec.h MXEC_E_TOO_FEW_SHARDS_PRESENT
 
 
-def test_verified_get_in_groups_matches_originals(ctx):
+@pytest.mark.parametrize("groups", [1, 3])
+def test_verified_get_in_groups_matches_originals(ctx_with, groups):
+    ctx = ctx_with(MXEC_GET_VGROUPS=groups)
     k, m, n = 8, 4, 160
     S = M
     rng = np.random.default_rng(4242)
@@ -70,7 +72,7 @@ def test_verified_get_in_groups_matches_originals(ctx):
     s1 = ctx.pipe_stats()
     assert rc == TOO_FEW_SHARDS_PRESENT, rc  # the batch's first failing object
     assert s1["verify_waves"] > s0["verify_waves"]
-    assert s1["verify_groups"] - s0["verify_groups"] > s1["verify_waves"] - s0["verify_waves"], (s0, s1)
+    assert s1["verify_groups"] - s0["verify_groups"] == groups * (s1["verify_waves"] - s0["verify_waves"]), (s0, s1)
     for o in range(n):
         if o in failing:
             assert status[o] == TOO_FEW_SHARDS_PRESENT, (o, status[o])
