@@ -587,6 +587,31 @@ private:
         return cut;
     }
 
+    // The expected digests of objects [o0, o1) (message order from message
+    // mb) up in one copy: one per object went through the four-buffer
+    // staging ring, so every fourth object waited for the upload stream to
+    // reach the copy three objects back (the host enqueue crawled beside the
+    // GPU, and so did the watch's bracket around it).
+    int upload_expected(const std::vector<RecObj>& objs, size_t o0, size_t o1, uint8_t* exp, uint64_t mb) {
+        uint64_t gm = 0;
+        bool any = false;
+        for (size_t o = o0; o < o1; ++o) {
+            gm += uint64_t(objs[o].k + objs[o].m);
+            any = any || objs[o].expected;
+        }
+        if (!any || !gm) return MXEC_OK;
+        exp_host_.assign(gm * 32, 0);
+        uint64_t g = 0;
+        for (size_t o = o0; o < o1; ++o) {
+            const RecObj& h = objs[o];
+            if (h.expected) std::memcpy(&exp_host_[g * 32], &h.expected[0][0], uint64_t(h.k + h.m) * 32);
+            g += uint64_t(h.k + h.m);
+        }
+        MXEC_TRY(flush_up());
+        return upload(exp + mb * 32, exp_host_.data(), gm * 32);
+    }
+    std::vector<uint8_t> exp_host_;  // staging source of upload_expected (consumed by upload's ring copy)
+
     // Objects [q0, q1) of a wave, their present shards up (or verified):
     // rebuild each object's missing shards from its decode plan (one grouped
     // launch, run_rs_mixed, on cs after `up` if given), then send them down
@@ -688,6 +713,7 @@ private:
                 if (objs[o].present[i]) longest = std::max(longest, objs[o].len[i]);
         }
         const PieceGrid grid(P);
+        MXEC_TRY(upload_expected(objs, o0, o1, exp, mb));
         struct TwoD {
             bool& f;
             TwoD(bool& flag, bool on) : f(flag) { f = on; }
@@ -703,7 +729,6 @@ private:
             std::vector<uint32_t> ss;
             for (size_t o = o0; o < o1; ++o) {
                 const RecObj& h = objs[o];
-                if (pc == 0 && h.expected) MXEC_TRY(queue_up(exp + g * 32, &h.expected[0][0], uint64_t(h.k + h.m) * 32));
                 for (int i = 0; i < h.k + h.m; ++i, ++g) {
                     if (!h.present[i]) continue;
                     const uint64_t L = h.len[i];
@@ -759,6 +784,7 @@ private:
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         std::vector<hipEvent_t>& up = *up_out;
         up.assign(groups.size(), nullptr);
+        if (verify) MXEC_TRY(upload_expected(objs, o0, o1, exp, 0));
         uint64_t g = 0;
         for (size_t q = 0; q < groups.size(); ++q) {
             MXEC_TRY(watch_open());
@@ -770,7 +796,6 @@ private:
                     if (h.len[i] != h.slot()) MXEC_TRY(flush_up());
                 }
                 MXEC_TRY(flush_up());
-                if (h.expected) MXEC_TRY(queue_up(exp + g * 32, &h.expected[0][0], uint64_t(h.k + h.m) * 32));
                 g += uint64_t(h.k + h.m);
             }
             MXEC_TRY(flush_up());
