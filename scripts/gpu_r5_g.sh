@@ -16,3 +16,10 @@ for f in ('engine_fresh','engine_churn'):
     for l in open('$out/'+f+'.jsonl'):
         r=json.loads(l); print(f, r['objects'], r['kind'], r['mode'], r['median_s'], [c['s'] for c in r['calls']], sum(c['sdma_slow'] for c in r['calls']))
 "
+# Last (it may fault at exit): does torch's own async copy arm the
+# profiler's exit-time fault?
+R=$PWD
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/ex_t -o run --output-format csv \
+  -- python3 $R/tools/exit_probe.py torch_copy > $R/$out/exit_torch_copy.out 2> $R/$out/exit_torch_copy.err
+echo "{\"what\": \"torch_copy (no mxec call but open)\", \"rc\": $?}" | tee -a $R/$out/exit_probe4.jsonl

@@ -15,6 +15,8 @@ profiler narrows the trigger:
           host_pinned   + one mxec_encode_batch_host from mxec_host_alloc memory
           host_pageable + one mxec_encode_batch_host from pageable memory
           hash          + one mxec_sha256_batch (host pointers)
+          torch_copy    no mxec call after open: torch's own pinned H2D / D2H
+                        copies on a side stream (does any async copy arm it?)
   --no-close leaves the context open at exit (no stream / event teardown).
 """
 from __future__ import annotations
@@ -29,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["open", "device", "host_pinned", "host_pageable", "hash"])
+    ap.add_argument("what", choices=["open", "device", "host_pinned", "host_pageable", "hash", "torch_copy"])
     ap.add_argument("--no-close", action="store_true")
     a = ap.parse_args()
     import numpy as np
@@ -58,6 +60,16 @@ def main() -> int:
         if a.what == "host_pinned":
             ctx.host_free(data)
             ctx.host_free(par)
+    elif a.what == "torch_copy":
+        h = torch.empty(64 << 20, dtype=torch.uint8).pin_memory()
+        h.fill_(7)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            d = h.to("cuda", non_blocking=True)
+            back = torch.empty_like(h).pin_memory()
+            back.copy_(d, non_blocking=True)
+        s.synchronize()
+        assert int(back[12345]) == 7
     elif a.what == "hash":
         ctx.sha256([bytes(range(256)) * 4096] * 8)
     if not a.no_close:
