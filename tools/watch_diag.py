@@ -53,7 +53,7 @@ def main() -> int:
         blk = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
         flat = buf.reshape(-1)
         for o in range(0, flat.size, blk.size):
-            flat[o:o + min(blk.size, flat.size - o)] = blk[:min(blk.size, flat.size - o)] ^ np.uint8(o >> 26)
+            flat[o:o + min(blk.size, flat.size - o)] = blk[:min(blk.size, flat.size - o)] ^ np.uint8((o >> 26) & 255)
         objs = [(k, m, S)] * n
         dig = np.zeros(n * (k + m) * 32, np.uint8)
         base.encode_batch_host(objs, [buf[o, j].ctypes.data for o in range(n) for j in range(k)],
