@@ -17,6 +17,9 @@ profiler narrows the trigger:
           hash          + one mxec_sha256_batch (host pointers)
           torch_copy    no mxec call after open: torch's own pinned H2D / D2H
                         copies on a side stream (does any async copy arm it?)
+          torch_streams torch alone on eight streams (more than the four
+                        hardware queues HIP gives a process), each with a
+                        pinned H2D copy, a kernel and a D2H copy
   --no-close leaves the context open at exit (no stream / event teardown).
 """
 from __future__ import annotations
@@ -31,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["open", "device", "host_pinned", "host_pageable", "hash", "torch_copy"])
+    ap.add_argument("what", choices=["open", "device", "host_pinned", "host_pageable", "hash", "torch_copy", "torch_streams"])
     ap.add_argument("--no-close", action="store_true")
     a = ap.parse_args()
     import numpy as np
@@ -70,6 +73,20 @@ def main() -> int:
             back.copy_(d, non_blocking=True)
         s.synchronize()
         assert int(back[12345]) == 7
+    elif a.what == "torch_streams":
+        ss = [torch.cuda.Stream() for _ in range(8)]
+        hs = [torch.full((8 << 20,), j, dtype=torch.uint8).pin_memory() for j in range(8)]
+        outs = []
+        for j, s in enumerate(ss):
+            with torch.cuda.stream(s):
+                d = hs[j].to("cuda", non_blocking=True)
+                d.add_(1)
+                back = torch.empty_like(hs[j]).pin_memory()
+                back.copy_(d, non_blocking=True)
+                outs.append(back)
+        for s in ss:
+            s.synchronize()
+        assert all(int(o[777]) == j + 1 for j, o in enumerate(outs))
     elif a.what == "hash":
         ctx.sha256([bytes(range(256)) * 4096] * 8)
     if not a.no_close:
