@@ -9,7 +9,8 @@ expected digests; rs: none) and copy mode (auto, sdma, waves; a context
 each) a warm call and `--reps` timed calls, each with its pipeline-counter
 deltas (checks, slow verdicts, the last bracket's rate, wave blocks).
 `--churn GB` first allocates and frees that much HBM through torch, as
-bench.py's headline does before its host legs.  One JSON line per
+bench.py's headline does before its host legs; `--churn-each GB` does it
+between every warm call and its timed calls (no pause after the free).  One JSON line per
 (objects, kind, mode).
 
   python tools/watch_diag.py [--objects 128,512] [--kinds verified,rs] [--reps 3] [--churn 0]
@@ -33,18 +34,24 @@ def main() -> int:
     ap.add_argument("--modes", default="auto,sdma,waves")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--churn", type=float, default=0.0)
+    ap.add_argument("--churn-each", type=float, default=0.0)
     a = ap.parse_args()
     import numpy as np
     import torch
 
     import maxio_amd
 
-    if a.churn > 0:
-        t = torch.empty(int(a.churn * 1e9), dtype=torch.uint8, device="cuda")
+    def churn(gb: float) -> float:
+        t = torch.empty(int(gb * 1e9), dtype=torch.uint8, device="cuda")
         t.fill_(1)
         torch.cuda.synchronize()
         del t
+        t0 = time.perf_counter()
         torch.cuda.empty_cache()
+        return time.perf_counter() - t0
+
+    if a.churn > 0:
+        churn(a.churn)
     k, m, S = 4, 2, 10 << 20
     rng = np.random.default_rng(5)
     base = maxio_amd.Context(streams_per_device=2)
@@ -73,6 +80,9 @@ def main() -> int:
                 os.environ.pop("MXEC_PIPE_COPY")
                 row = {"objects": n, "kind": kind, "mode": mode, "churn_GB": a.churn, "calls": []}
                 for rep in range(a.reps + 1):
+                    if rep == 1 and a.churn_each > 0:  # after the warm call, right before the timed ones
+                        row["free_s"] = round(churn(a.churn_each), 4)
+                        row["churn_each_GB"] = a.churn_each
                     s0 = ctx.pipe_stats()
                     pr = present0.copy()
                     t0 = time.perf_counter()
