@@ -383,6 +383,10 @@ private:
     void start_copy_mode() {
         const int mode = d_.kn ? d_.kn->pipe_copy : 0;
         waves_now_ = mode == 1 || (mode == 2 && std::chrono::steady_clock::now() < res_.waves_until);
+#ifdef MXEC_LAB
+        const char* dw = getenv("MXEC_PIPE_DOWN_WAVES");
+        down_waves_ = dw && *dw == '1';
+#endif
     }
     bool watching() const { return d_.kn && d_.kn->pipe_copy == 2 && d_.kn->pipe_sdma_floor > 0 && !waves_now_; }
     int new_timed_event(hipEvent_t* e) {
@@ -868,10 +872,11 @@ private:
     // instead of SDMA DMAs; they are collected here and issued as one launch
     // at the next point the stream is waited on or marked (issue_up /
     // issue_down).
-    bool wave_copy(const void* host, const void* dev, uint64_t len) const {
-        return waves_now_ && copy_phase_ok(host, dev) && pinned_mapped(host, len);
+    bool wave_copy(const void* host, const void* dev, uint64_t len, bool down = false) const {
+        return (waves_now_ || (down && down_waves_)) && copy_phase_ok(host, dev) && pinned_mapped(host, len);
     }
     bool waves_now_ = false;  // this call's copies of mxec_host_alloc memory go by waves
+    bool down_waves_ = false;  // and its downloads (lab: MXEC_PIPE_DOWN_WAVES=1)
     static void add_blocks(std::vector<CopyBlk>& v, uint8_t* dst, const uint8_t* src, uint64_t len) {
         for (uint64_t o = 0; o < len; o += kCopyBlock)
             v.push_back(CopyBlk{reinterpret_cast<uint64_t>(dst + o), reinterpret_cast<uint64_t>(src + o),
@@ -1021,7 +1026,7 @@ private:
         down_run_ = Run{};
         if (!r.len) return MXEC_OK;
         if (r.rows == 1) return download(r.dst, r.src, r.len);
-        if (!waves_now_ && is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
+        if (!waves_now_ && !down_waves_ && is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
             if (affinity_on(d_)) {
                 const void* p = r.src;
                 MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download 2d", &arena_, &p, 1));
@@ -1054,7 +1059,7 @@ private:
             const void* p = src;
             MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download", &arena_, &p, 1));
         }
-        if (wave_copy(dst, src, len)) {
+        if (wave_copy(dst, src, len, true)) {
             add_blocks(down_blks_, dst, src, len);
             return MXEC_OK;
         }

@@ -75,9 +75,14 @@ def main() -> int:
         dig2 = np.zeros_like(dig)
         for kind in a.kinds.split(","):
             for mode in a.modes.split(","):
-                os.environ["MXEC_PIPE_COPY"] = mode
+                # sdma_down_waves (lab build): uploads by SDMA, downloads by waves
+                os.environ["MXEC_PIPE_COPY"] = "sdma" if mode == "sdma_down_waves" else mode
                 ctx = maxio_amd.Context(streams_per_device=2)
                 os.environ.pop("MXEC_PIPE_COPY")
+                if mode == "sdma_down_waves":
+                    os.environ["MXEC_PIPE_DOWN_WAVES"] = "1"
+                else:
+                    os.environ.pop("MXEC_PIPE_DOWN_WAVES", None)
                 row = {"objects": n, "kind": kind, "mode": mode, "churn_GB": a.churn, "calls": []}
                 for rep in range(a.reps + 1):
                     if rep == 1 and a.churn_each > 0:  # after the warm call, right before the timed ones
