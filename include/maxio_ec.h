@@ -119,10 +119,11 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
  * device `dev` since the context opened, into out[0 .. n): the copies it
  * issued (1D SDMA DMAs, 2D SDMA DMAs -- the PUT's piece copies -- and their
  * rows, CU-wave copy blocks), the upload brackets MXEC_PIPE_COPY=auto timed
- * and how many ran below its SDMA floor (the rest of those calls, and the
- * device's calls for 2 s, copied by waves), the piece-major verified
- * reconstruct waves and the verification groups they ran as, and the last
- * timed bracket's SDMA rate in MB/s.  Returns how many counters were
+ * and how many ran below its SDMA floor (the rest of those calls' uploads,
+ * and the device's for 2 s, copied by waves), the piece-major verified
+ * reconstruct waves and the verification groups they ran as, the last timed
+ * upload bracket's SDMA rate in MB/s, and the same three for downloads
+ * (brackets timed, below the floor, last rate).  Returns how many counters were
  * written (min(n, MXEC_PIPE_STAT_COUNT)), or an error.  Diagnostics (tests). */
 #define MXEC_PIPE_STAT_COPIES_1D 0
 #define MXEC_PIPE_STAT_COPIES_2D 1
@@ -133,7 +134,10 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
 #define MXEC_PIPE_STAT_VERIFY_WAVES 6
 #define MXEC_PIPE_STAT_VERIFY_GROUPS 7
 #define MXEC_PIPE_STAT_SDMA_LAST_MBPS 8
-#define MXEC_PIPE_STAT_COUNT 9
+#define MXEC_PIPE_STAT_SDMA_DOWN_CHECKS 9
+#define MXEC_PIPE_STAT_SDMA_DOWN_SLOW 10
+#define MXEC_PIPE_STAT_SDMA_DOWN_LAST_MBPS 11
+#define MXEC_PIPE_STAT_COUNT 12
 int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n);
 /* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
  * (k inputs, m outputs, shard_size) at: the grid tuner times the first

@@ -268,7 +268,8 @@ int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n) {
                                               d.copies_2d_rows.load(),   d.copy_wave_blocks.load(),
                                               d.sdma_probes.load(),      d.sdma_slow_verdicts.load(),
                                               d.verify_waves.load(),     d.verify_groups.load(),
-                                              d.sdma_last_mbps.load()};
+                                              d.sdma_last_mbps.load(),   d.sdma_down_probes.load(),
+                                              d.sdma_down_slow_verdicts.load(), d.sdma_down_last_mbps.load()};
     const int k = std::min(n, int(MXEC_PIPE_STAT_COUNT));
     for (int i = 0; i < k; ++i) out[i] = v[i];
     return k;

@@ -163,9 +163,10 @@ struct PipeRes {
     DevBuf chain_state;  // SHA-256 chain states between pieces (host reconstruct)
     PinnedBuf flags;  // verification verdicts read back (host reconstruct)
     Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
-    // MXEC_PIPE_COPY=auto: calls that start before this instant copy
-    // mxec_host_alloc memory by waves (a recent call measured SDMA slow).
-    std::chrono::steady_clock::time_point waves_until{};
+    // MXEC_PIPE_COPY=auto: calls that start before these instants copy
+    // mxec_host_alloc memory by waves, uploads / downloads (a recent call
+    // measured SDMA slow in that direction).
+    std::chrono::steady_clock::time_point waves_until{}, down_waves_until{};
     bool ready = false;
     int init(const Device& dev) {
         if (ready) return MXEC_OK;
@@ -375,20 +376,25 @@ private:
         hipEvent_t a, b;
         uint64_t bytes;
         bool staged;
+        bool down;
     };
     std::vector<Bracket> watch_;
-    hipEvent_t watch_a_ = nullptr;
-    bool watch_staged_ = false;
-    uint64_t watch_bytes_ = 0;  // SDMA bytes issued in the open bracket
+    hipEvent_t watch_a_ = nullptr, dwatch_a_ = nullptr;
+    bool watch_staged_ = false, dwatch_staged_ = false;
+    uint64_t watch_bytes_ = 0, dwatch_bytes_ = 0;  // SDMA bytes issued in the open brackets
     void start_copy_mode() {
         const int mode = d_.kn ? d_.kn->pipe_copy : 0;
-        waves_now_ = mode == 1 || (mode == 2 && std::chrono::steady_clock::now() < res_.waves_until);
+        const auto now = std::chrono::steady_clock::now();
+        waves_now_ = mode == 1 || (mode == 2 && now < res_.waves_until);
+        down_waves_ = mode == 1 || (mode == 2 && now < res_.down_waves_until);
 #ifdef MXEC_LAB
         const char* dw = getenv("MXEC_PIPE_DOWN_WAVES");
-        down_waves_ = dw && *dw == '1';
+        down_waves_ = down_waves_ || (dw && *dw == '1');
 #endif
     }
-    bool watching() const { return d_.kn && d_.kn->pipe_copy == 2 && d_.kn->pipe_sdma_floor > 0 && !waves_now_; }
+    bool watching(bool down = false) const {
+        return d_.kn && d_.kn->pipe_copy == 2 && d_.kn->pipe_sdma_floor > 0 && !(down ? down_waves_ : waves_now_);
+    }
     int new_timed_event(hipEvent_t* e) {
         MXEC_HIP(hipEventCreate(e));
         events_.push_back(*e);
@@ -408,9 +414,33 @@ private:
         hipEvent_t b = nullptr;
         MXEC_TRY(new_timed_event(&b));
         MXEC_HIP(hipEventRecord(b, h2d_));
-        watch_.push_back(Bracket{watch_a_, b, watch_bytes_, watch_staged_});
+        watch_.push_back(Bracket{watch_a_, b, watch_bytes_, watch_staged_, false});
         watch_bytes_ = 0;
         watch_a_ = nullptr;
+        return watch_poll();
+    }
+    // Downloads: the bracket opens after the d2h stream's wait for the
+    // compute it downloads (its first event marks when that wait let go),
+    // so it times the copies alone.
+    int dwatch_open() {
+        if (!watching(true) || dwatch_a_) return MXEC_OK;
+        MXEC_TRY(new_timed_event(&dwatch_a_));
+        MXEC_HIP(hipEventRecord(dwatch_a_, d2h_));
+        dwatch_staged_ = false;
+        dwatch_bytes_ = 0;
+        return MXEC_OK;
+    }
+    int dwatch_close() {
+        if (!dwatch_a_) return MXEC_OK;
+        hipEvent_t b = nullptr;
+        MXEC_TRY(new_timed_event(&b));
+        MXEC_HIP(hipEventRecord(b, d2h_));
+        watch_.push_back(Bracket{dwatch_a_, b, dwatch_bytes_, dwatch_staged_, true});
+        dwatch_bytes_ = 0;
+        dwatch_a_ = nullptr;
+        return watch_poll();
+    }
+    int watch_poll() {
         while (!watch_.empty()) {  // the finished ones, oldest first, without waiting
             if (hipEventQuery(watch_.front().b) != hipSuccess) {
                 (void)hipGetLastError();
@@ -427,21 +457,34 @@ private:
         float ms = 0;
         MXEC_HIP(hipEventElapsedTime(&ms, k.a, k.b));
         if (k.staged || k.bytes < kWatchMinBytes || ms <= 0) return MXEC_OK;
-        ++d_.sdma_probes;
         const double gbps = double(k.bytes) / (double(ms) * 1e6);
-        d_.sdma_last_mbps = uint64_t(gbps * 1e3);
-        if (!waves_now_ && gbps < double(d_.kn ? d_.kn->pipe_sdma_floor : 20)) {
-            ++d_.sdma_slow_verdicts;
-            waves_now_ = true;  // the rest of this call
-            res_.waves_until = std::chrono::steady_clock::now() + std::chrono::milliseconds(kWavesHoldMs);
+        const bool slow = gbps < double(d_.kn ? d_.kn->pipe_sdma_floor : 20);
+        const auto hold = std::chrono::steady_clock::now() + std::chrono::milliseconds(kWavesHoldMs);
+        if (k.down) {
+            ++d_.sdma_down_probes;
+            d_.sdma_down_last_mbps = uint64_t(gbps * 1e3);
+            if (!down_waves_ && slow) {
+                ++d_.sdma_down_slow_verdicts;
+                down_waves_ = true;  // the rest of this call's downloads
+                res_.down_waves_until = hold;
+            }
+        } else {
+            ++d_.sdma_probes;
+            d_.sdma_last_mbps = uint64_t(gbps * 1e3);
+            if (!waves_now_ && slow) {
+                ++d_.sdma_slow_verdicts;
+                waves_now_ = true;  // the rest of this call's uploads
+                res_.waves_until = hold;
+            }
         }
-        d_.sdma_slow = waves_now_;
+        d_.sdma_slow = waves_now_ || down_waves_;
         return MXEC_OK;
     }
     // End of a call: judge what is left (its copies are done), for the
     // device's next calls.
     int watch_drain() {
         watch_a_ = nullptr;
+        dwatch_a_ = nullptr;
         while (!watch_.empty()) MXEC_TRY(watch_judge());
         return MXEC_OK;
     }
@@ -680,6 +723,7 @@ private:
             PTRACE(now("rs_queued"));
             MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
+            MXEC_TRY(dwatch_open());
             for (size_t o = q0; o < q1; ++o) {
                 RecObj& h = objs[o];
                 const auto& p = plans[o - q0];
@@ -692,6 +736,7 @@ private:
                 }
             }
             MXEC_TRY(flush_down());
+            MXEC_TRY(dwatch_close());
         }
         return MXEC_OK;
     }
@@ -873,10 +918,10 @@ private:
     // at the next point the stream is waited on or marked (issue_up /
     // issue_down).
     bool wave_copy(const void* host, const void* dev, uint64_t len, bool down = false) const {
-        return (waves_now_ || (down && down_waves_)) && copy_phase_ok(host, dev) && pinned_mapped(host, len);
+        return (down ? down_waves_ : waves_now_) && copy_phase_ok(host, dev) && pinned_mapped(host, len);
     }
     bool waves_now_ = false;  // this call's copies of mxec_host_alloc memory go by waves
-    bool down_waves_ = false;  // and its downloads (lab: MXEC_PIPE_DOWN_WAVES=1)
+    bool down_waves_ = false;  // its downloads (lab: MXEC_PIPE_DOWN_WAVES=1 forces them)
     static void add_blocks(std::vector<CopyBlk>& v, uint8_t* dst, const uint8_t* src, uint64_t len) {
         for (uint64_t o = 0; o < len; o += kCopyBlock)
             v.push_back(CopyBlk{reinterpret_cast<uint64_t>(dst + o), reinterpret_cast<uint64_t>(src + o),
@@ -1026,13 +1071,14 @@ private:
         down_run_ = Run{};
         if (!r.len) return MXEC_OK;
         if (r.rows == 1) return download(r.dst, r.src, r.len);
-        if (!waves_now_ && !down_waves_ && is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
+        if (!down_waves_ && is_pinned(r.dst, (r.rows - 1) * r.dpitch + r.len)) {
             if (affinity_on(d_)) {
                 const void* p = r.src;
                 MXEC_TRY(affinity_check(d_, &slot_, d2h_, "pipeline download 2d", &arena_, &p, 1));
             }
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyDeviceToHost, d2h_));
             ++d_.copies_2d;
+            dwatch_bytes_ += r.len * r.rows;
             d_.copies_2d_rows += r.rows;
             return MXEC_OK;
         }
@@ -1066,8 +1112,10 @@ private:
         if (is_pinned(dst, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, d2h_));
             ++d_.copies_1d;
+            dwatch_bytes_ += len;
             return MXEC_OK;
         }
+        dwatch_staged_ = true;
         for (uint64_t off = 0; off < len; off += kRingBuf) {
             const uint64_t n = std::min(kRingBuf, len - off);
             MXEC_TRY(drain_next());
@@ -1232,6 +1280,7 @@ private:
             // This piece of every parity chunk goes down.
             MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
+            MXEC_TRY(dwatch_open());
             for (size_t o = o0; o < o1; ++o) {
                 const HostObj& h = objs[o];
                 if (h.S <= off) continue;
@@ -1240,6 +1289,7 @@ private:
                     MXEC_TRY(queue_down(h.parity[i] + off, ob + uint64_t(h.k + i) * h.slot(), std::min(pw, h.S - off)));
             }
             MXEC_TRY(flush_down());
+            MXEC_TRY(dwatch_close());
             PTRACE(mark("down", d2h_));
             PTRACE(now("piece_queued"));
         }
@@ -1373,6 +1423,7 @@ private:
         for (size_t g = 0; g < groups.size(); ++g) {
             MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, done[g], 0));
+            MXEC_TRY(dwatch_open());
             for (size_t o = groups[g].first; o < groups[g].second; ++o) {
                 const HostObj& h = objs[o];
                 uint8_t* ob = base + h.pool_off;
@@ -1382,6 +1433,7 @@ private:
                 }
             }
             MXEC_TRY(flush_down());  // before the next group's wait
+            MXEC_TRY(dwatch_close());
         }
         if (sha_done) {
             MXEC_TRY(issue_down());

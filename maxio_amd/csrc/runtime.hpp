@@ -278,6 +278,7 @@ struct Device {
     // current verdict also steers the single-request calls' copies of
     // mxec_host_alloc memory.
     std::atomic<uint64_t> sdma_probes{0}, sdma_slow_verdicts{0}, sdma_last_mbps{0};
+    std::atomic<uint64_t> sdma_down_probes{0}, sdma_down_slow_verdicts{0}, sdma_down_last_mbps{0};
     // Piece-major verified reconstruct waves and the verification groups
     // they ran as (pipeline.cpp verify_cuts).
     std::atomic<uint64_t> verify_waves{0}, verify_groups{0};

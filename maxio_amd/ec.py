@@ -199,7 +199,7 @@ class Context:
         return {"recycles": r.value, "relaunches": q.value, "fence_waits": w.value}
 
     PIPE_STATS = ("copies_1d", "copies_2d", "rows_2d", "wave_blocks", "sdma_checks", "sdma_slow", "verify_waves",
-                  "verify_groups", "sdma_last_mbps")
+                  "verify_groups", "sdma_last_mbps", "sdma_down_checks", "sdma_down_slow", "sdma_down_last_mbps")
 
     def pipe_stats(self, dev: int = 0) -> dict:
         """Host-batch pipeline counters of device `dev` since the context

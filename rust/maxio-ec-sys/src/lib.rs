@@ -101,7 +101,10 @@ pub const MXEC_PIPE_STAT_SDMA_SLOW: c_int = 5;
 pub const MXEC_PIPE_STAT_VERIFY_WAVES: c_int = 6;
 pub const MXEC_PIPE_STAT_VERIFY_GROUPS: c_int = 7;
 pub const MXEC_PIPE_STAT_SDMA_LAST_MBPS: c_int = 8;
-pub const MXEC_PIPE_STAT_COUNT: c_int = 9;
+pub const MXEC_PIPE_STAT_SDMA_DOWN_CHECKS: c_int = 9;
+pub const MXEC_PIPE_STAT_SDMA_DOWN_SLOW: c_int = 10;
+pub const MXEC_PIPE_STAT_SDMA_DOWN_LAST_MBPS: c_int = 11;
+pub const MXEC_PIPE_STAT_COUNT: c_int = 12;
 
 // ---- return codes (reed_solomon_erasure::Error one for one, then MaxIO's) --
 pub const MXEC_OK: c_int = 0;

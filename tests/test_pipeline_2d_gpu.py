@@ -172,3 +172,48 @@ def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
     assert (s2["wave_blocks"] > s1["wave_blocks"]) == waves, (s1, s2)
     if floor == "":
         assert s1["sdma_last_mbps"] > 20000, s1  # a healthy box's 1 MiB piece copies
+
+
+@pytest.mark.parametrize("floor", ["", "100000"])
+def test_get_download_watch(floor):
+    """MXEC_PIPE_COPY=auto times the GET's downloads too (a bracket per
+    rebuilt group, opened after the d2h stream's wait for the rebuild): with
+    the default floor the brackets are timed; with a floor no SDMA reaches
+    they are judged slow, the rest of the call's downloads and the device's
+    next call go by waves.  16 x 4+2 objects of 4 MiB + 4 KiB shards, two data
+    shards erased in each, RS-only GET twice: every rebuilt shard equals the
+    original both times."""
+    from conftest import open_ctx
+
+    ctx = open_ctx(2, 0, MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
+    k, m, n = 4, 2, 16
+    S = 4 * M + 4096
+    try:
+        buf = _random(ctx, (n, k + m, S), 4242 + len(floor))
+        objs = [(k, m, S)] * n
+        st = ctx.encode_batch_host(objs, [buf[o, j].ctypes.data for o in range(n) for j in range(k)],
+                                   [buf[o, k + i].ctypes.data for o in range(n) for i in range(m)])
+        assert (st == 0).all()
+        ref = buf.copy()
+        deltas = []
+        for call in range(2):
+            present = np.ones((n, k + m), np.uint8)
+            present[:, [1, 3]] = 0
+            buf[:, [1, 3]] = 0x77
+            before = ctx.pipe_stats()
+            pr = present.reshape(-1).copy()
+            rc, st = ctx.reconstruct_batch_host(objs, [buf[o, i].ctypes.data for o in range(n) for i in range(k + m)],
+                                                pr)
+            after = ctx.pipe_stats()
+            assert rc == 0 and not st.any() and pr.all()
+            assert np.array_equal(buf, ref), call
+            deltas.append({key: after[key] - before[key] for key in after} | {"down_mbps": after["sdma_down_last_mbps"]})
+        ctx.host_free(buf)
+    finally:
+        ctx.close()
+    d1, d2 = deltas
+    assert d1["sdma_down_checks"] > 0, deltas
+    assert d1["down_mbps"] > 0, deltas
+    if floor:
+        assert d1["sdma_down_slow"] > 0, deltas
+        assert d2["wave_blocks"] > 0 and d2["sdma_down_checks"] == 0, deltas  # within the 2 s hold

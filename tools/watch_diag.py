@@ -102,9 +102,11 @@ def main() -> int:
                     assert rc == 0 and not st.any()
                     row["calls"].append({"s": round(el, 4), "warm": rep == 0,
                                          **{key: s1[key] - s0[key] for key in ("sdma_checks", "sdma_slow",
+                                                                              "sdma_down_checks", "sdma_down_slow",
                                                                               "wave_blocks", "copies_1d",
                                                                               "copies_2d")},
-                                         "sdma_last_mbps": s1["sdma_last_mbps"]})
+                                         "sdma_last_mbps": s1["sdma_last_mbps"],
+                                         "sdma_down_last_mbps": s1["sdma_down_last_mbps"]})
                 timed = sorted(c["s"] for c in row["calls"][1:])
                 row["median_s"] = timed[len(timed) // 2]
                 ctx.close()
