@@ -5,9 +5,11 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/${1:-r5l}
 mkdir -p $out
+if [ -n "$AFTER_FREE" ]; then
 timeout -k 10 120 python -u tools/sdma_after_free.py --free-gb 60 --seconds 8 > $out/after_free_60.jsonl 2> $out/after_free_60.err \
   || { tail -5 $out/after_free_60.err; exit 1; }
 tail -1 $out/after_free_60.jsonl
+fi
 timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_pipeline_2d_gpu.py \
   > $out/pytest_2d.log 2>&1 || { tail -30 $out/pytest_2d.log; exit 1; }
 tail -1 $out/pytest_2d.log

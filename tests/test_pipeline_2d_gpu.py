@@ -178,9 +178,9 @@ def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
 def test_get_download_watch(floor):
     """MXEC_PIPE_COPY=auto times the GET's downloads too (a bracket per
     rebuilt group, opened after the d2h stream's wait for the rebuild): with
-    the default floor the brackets are timed; with a floor no SDMA reaches
-    they are judged slow, the rest of the call's downloads and the device's
-    next call go by waves.  16 x 4+2 objects of 4 MiB + 4 KiB shards, two data
+    the default floor the GET's bracket is timed and passes; with a floor no
+    SDMA reaches the PUT's first parity-download bracket is judged slow and
+    the device's downloads go by waves for the next 2 s (both GETs).  16 x 4+2 objects of 4 MiB + 4 KiB shards, two data
     shards erased in each, RS-only GET twice: every rebuilt shard equals the
     original both times."""
     from conftest import open_ctx
@@ -191,6 +191,7 @@ def test_get_download_watch(floor):
     try:
         buf = _random(ctx, (n, k + m, S), 4242 + len(floor))
         objs = [(k, m, S)] * n
+        s0 = ctx.pipe_stats()
         st = ctx.encode_batch_host(objs, [buf[o, j].ctypes.data for o in range(n) for j in range(k)],
                                    [buf[o, k + i].ctypes.data for o in range(n) for i in range(m)])
         assert (st == 0).all()
@@ -208,12 +209,18 @@ def test_get_download_watch(floor):
             assert rc == 0 and not st.any() and pr.all()
             assert np.array_equal(buf, ref), call
             deltas.append({key: after[key] - before[key] for key in after} | {"down_mbps": after["sdma_down_last_mbps"]})
+        ctx_down_slow = ctx.pipe_stats()["sdma_down_slow"]
         ctx.host_free(buf)
     finally:
         ctx.close()
     d1, d2 = deltas
-    assert d1["sdma_down_checks"] > 0, deltas
-    assert d1["down_mbps"] > 0, deltas
     if floor:
-        assert d1["sdma_down_slow"] > 0, deltas
-        assert d2["wave_blocks"] > 0 and d2["sdma_down_checks"] == 0, deltas  # within the 2 s hold
+        # the PUT's parity downloads are bracketed too: its first slow one
+        # already moved the device's downloads (and uploads) to waves
+        assert s0["sdma_down_slow"] == 0, s0
+        assert ctx_down_slow > 0, deltas
+        assert d1["sdma_down_checks"] == 0 and d2["sdma_down_checks"] == 0, deltas  # within the 2 s hold
+        assert d1["wave_blocks"] > 0 and d2["wave_blocks"] > 0, deltas
+    else:
+        assert d1["sdma_down_checks"] > 0 and d1["sdma_down_slow"] == 0, deltas
+        assert d1["down_mbps"] > 0, deltas
