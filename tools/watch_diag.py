@@ -75,10 +75,15 @@ def main() -> int:
         dig2 = np.zeros_like(dig)
         for kind in a.kinds.split(","):
             for mode in a.modes.split(","):
-                # sdma_down_waves (lab build): uploads by SDMA, downloads by waves
-                os.environ["MXEC_PIPE_COPY"] = "sdma" if mode == "sdma_down_waves" else mode
+                # sdma_down_waves (lab build): uploads by SDMA, downloads by
+                # waves; auto_nowatch: auto with the watch off (floor 0)
+                env = {"sdma_down_waves": {"MXEC_PIPE_COPY": "sdma"},
+                       "auto_nowatch": {"MXEC_PIPE_COPY": "auto", "MXEC_PIPE_SDMA_FLOOR": "0"}}.get(
+                           mode, {"MXEC_PIPE_COPY": mode})
+                os.environ.update(env)
                 ctx = maxio_amd.Context(streams_per_device=2)
-                os.environ.pop("MXEC_PIPE_COPY")
+                for key in env:
+                    os.environ.pop(key)
                 if mode == "sdma_down_waves":
                     os.environ["MXEC_PIPE_DOWN_WAVES"] = "1"
                 else:
