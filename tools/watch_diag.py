@@ -77,14 +77,18 @@ def main() -> int:
             for mode in a.modes.split(","):
                 # sdma_down_waves (lab build): uploads by SDMA, downloads by
                 # waves; auto_nowatch: auto with the watch off (floor 0)
+                # *_cus16 (lab): copy streams on 16 CUs, compute streams on the rest
                 env = {"sdma_down_waves": {"MXEC_PIPE_COPY": "sdma"},
+                       "sdma_down_waves_cus16": {"MXEC_PIPE_COPY": "auto", "MXEC_PIPE_SDMA_FLOOR": "0",
+                                                 "MXEC_PIPE_COPY_CUS": "16"},
+                       "waves_cus16": {"MXEC_PIPE_COPY": "waves", "MXEC_PIPE_COPY_CUS": "16"},
                        "auto_nowatch": {"MXEC_PIPE_COPY": "auto", "MXEC_PIPE_SDMA_FLOOR": "0"}}.get(
                            mode, {"MXEC_PIPE_COPY": mode})
                 os.environ.update(env)
                 ctx = maxio_amd.Context(streams_per_device=2)
                 for key in env:
                     os.environ.pop(key)
-                if mode == "sdma_down_waves":
+                if mode.startswith("sdma_down_waves"):
                     os.environ["MXEC_PIPE_DOWN_WAVES"] = "1"
                 else:
                     os.environ.pop("MXEC_PIPE_DOWN_WAVES", None)
