@@ -367,9 +367,11 @@ private:
     // kWatchMinBytes (16 MiB) of direct DMAs (no staging ring) that ran
     // below MXEC_PIPE_SDMA_FLOOR GB/s (default 20; healthy 1-4 MiB copies run
     // 33-43, the collapse seen after heavy HBM churn ran ~7) switches the
-    // rest of the call's copies of mxec_host_alloc memory (if any are still
-    // to be issued) and the device's calls for the next kWavesHoldMs to the
-    // wave kernels.
+    // rest of the call's uploads of mxec_host_alloc memory (if any are still
+    // to be issued) and the device's for the next kWavesHoldMs to the wave
+    // kernels; a download bracket (RS-only GET, below) does the same for
+    // downloads.  A slow-down lasts ~3.5 s after 60 GB of HBM is freed
+    // (profiles/r5/copy_engine/slow_duration_after_60GB_free_r5m.jsonl).
     static constexpr uint64_t kWatchMinBytes = uint64_t(16) << 20;
     static constexpr int kWavesHoldMs = 2000;
     struct Bracket {
@@ -419,9 +421,14 @@ private:
         watch_a_ = nullptr;
         return watch_poll();
     }
-    // Downloads: the bracket opens after the d2h stream's wait for the
-    // compute it downloads (its first event marks when that wait let go),
-    // so it times the copies alone.
+    // Downloads (an RS-only GET's rebuilt shards, rebuild_down): the bracket
+    // opens after the d2h stream's wait for the rebuild (its first event
+    // marks when that wait let go), so it times the copies alone.  The PUT's
+    // parity downloads are not bracketed: in the seconds after a large HBM
+    // free, timing events among the PUT-with-digests pieces' downloads
+    // slowed that call by 63 % (0.336 s against 0.206 at 128 objects,
+    // profiles/r5/copy_engine/auto_dwatch_churn60_r5l2.jsonl), and its SDMA
+    // downloads otherwise beat waves (0.204 s against 0.238 fresh).
     int dwatch_open() {
         if (!watching(true) || dwatch_a_) return MXEC_OK;
         MXEC_TRY(new_timed_event(&dwatch_a_));
@@ -458,7 +465,11 @@ private:
         MXEC_HIP(hipEventElapsedTime(&ms, k.a, k.b));
         if (k.staged || k.bytes < kWatchMinBytes || ms <= 0) return MXEC_OK;
         const double gbps = double(k.bytes) / (double(ms) * 1e6);
-        const bool slow = gbps < double(d_.kn ? d_.kn->pipe_sdma_floor : 20);
+        // A GET's download brackets run at 54-55 GB/s on a healthy box and
+        // ~24 in the seconds after a large HBM free (uploads: 33-55 healthy,
+        // unaffected by the free), so they are judged against twice the floor.
+        const double floor = double(d_.kn ? d_.kn->pipe_sdma_floor : 20) * (k.down ? 2.0 : 1.0);
+        const bool slow = gbps < floor;
         const auto hold = std::chrono::steady_clock::now() + std::chrono::milliseconds(kWavesHoldMs);
         if (k.down) {
             ++d_.sdma_down_probes;
@@ -518,6 +529,13 @@ private:
             ok = static_cast<uint8_t*>(scratch_.p);
             exp = ok + fo;
         }
+        // Under MXEC_PIPE_COPY=auto a verified wave's rebuilt shards go down
+        // by waves (they leave after the last verdict, alone on the link:
+        // waves move them as fast as a healthy SDMA and keep that rate when
+        // SDMA downloads run slow after a large HBM free); an
+        // RS-only wave's go by SDMA, each group's bracketed (dwatch_open).
+        const bool down_before = down_waves_;
+        if (verify && d_.kn && d_.kn->pipe_copy == 2) down_waves_ = true;
         uint64_t vmsgs = 0;  // present shards to verify
         for (size_t o = o0; o < o1; ++o)
             if (objs[o].expected)
@@ -579,6 +597,7 @@ private:
         PTRACE(now("down_queued"));
         const int frc = flush();
         PTRACE(report("rec_wave"));
+        if (verify) down_waves_ = down_before;
         return frc;
     }
 
@@ -1280,7 +1299,6 @@ private:
             // This piece of every parity chunk goes down.
             MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
-            MXEC_TRY(dwatch_open());
             for (size_t o = o0; o < o1; ++o) {
                 const HostObj& h = objs[o];
                 if (h.S <= off) continue;
@@ -1289,7 +1307,6 @@ private:
                     MXEC_TRY(queue_down(h.parity[i] + off, ob + uint64_t(h.k + i) * h.slot(), std::min(pw, h.S - off)));
             }
             MXEC_TRY(flush_down());
-            MXEC_TRY(dwatch_close());
             PTRACE(mark("down", d2h_));
             PTRACE(now("piece_queued"));
         }
@@ -1423,7 +1440,6 @@ private:
         for (size_t g = 0; g < groups.size(); ++g) {
             MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, done[g], 0));
-            MXEC_TRY(dwatch_open());
             for (size_t o = groups[g].first; o < groups[g].second; ++o) {
                 const HostObj& h = objs[o];
                 uint8_t* ob = base + h.pool_off;
@@ -1433,7 +1449,6 @@ private:
                 }
             }
             MXEC_TRY(flush_down());  // before the next group's wait
-            MXEC_TRY(dwatch_close());
         }
         if (sha_done) {
             MXEC_TRY(issue_down());

@@ -176,13 +176,14 @@ def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
 
 @pytest.mark.parametrize("floor", ["", "100000"])
 def test_get_download_watch(floor):
-    """MXEC_PIPE_COPY=auto times the GET's downloads too (a bracket per
-    rebuilt group, opened after the d2h stream's wait for the rebuild): with
-    the default floor the GET's bracket is timed and passes; with a floor no
-    SDMA reaches the PUT's first parity-download bracket is judged slow and
-    the device's downloads go by waves for the next 2 s (both GETs).  16 x 4+2 objects of 4 MiB + 4 KiB shards, two data
-    shards erased in each, RS-only GET twice: every rebuilt shard equals the
-    original both times."""
+    """MXEC_PIPE_COPY=auto times an RS-only GET's downloads (a bracket per
+    rebuilt group, opened after the d2h stream's wait for the rebuild) and
+    judges them against twice MXEC_PIPE_SDMA_FLOOR: with the default floor
+    the bracket is timed; with a floor no SDMA reaches it is judged slow and
+    the device's downloads go by waves for the next 2 s (the second GET).  A
+    verified GET's downloads go by waves under auto.  16 x 4+2 objects of
+    4 MiB + 4 KiB shards, two data shards erased in each: every rebuilt shard
+    equals the original every time."""
     from conftest import open_ctx
 
     ctx = open_ctx(2, 0, MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
@@ -191,36 +192,32 @@ def test_get_download_watch(floor):
     try:
         buf = _random(ctx, (n, k + m, S), 4242 + len(floor))
         objs = [(k, m, S)] * n
-        s0 = ctx.pipe_stats()
+        dig = np.zeros(n * (k + m) * 32, np.uint8)
         st = ctx.encode_batch_host(objs, [buf[o, j].ctypes.data for o in range(n) for j in range(k)],
-                                   [buf[o, k + i].ctypes.data for o in range(n) for i in range(m)])
+                                   [buf[o, k + i].ctypes.data for o in range(n) for i in range(m)], digests=dig)
         assert (st == 0).all()
+        s0 = ctx.pipe_stats()
+        assert s0["sdma_down_checks"] == 0, s0  # the PUT's downloads are not bracketed
         ref = buf.copy()
         deltas = []
-        for call in range(2):
+        for call in range(3):  # RS-only, RS-only, verified
             present = np.ones((n, k + m), np.uint8)
             present[:, [1, 3]] = 0
             buf[:, [1, 3]] = 0x77
             before = ctx.pipe_stats()
             pr = present.reshape(-1).copy()
             rc, st = ctx.reconstruct_batch_host(objs, [buf[o, i].ctypes.data for o in range(n) for i in range(k + m)],
-                                                pr)
+                                                pr, expected=dig if call == 2 else None)
             after = ctx.pipe_stats()
             assert rc == 0 and not st.any() and pr.all()
             assert np.array_equal(buf, ref), call
             deltas.append({key: after[key] - before[key] for key in after} | {"down_mbps": after["sdma_down_last_mbps"]})
-        ctx_down_slow = ctx.pipe_stats()["sdma_down_slow"]
         ctx.host_free(buf)
     finally:
         ctx.close()
-    d1, d2 = deltas
+    d1, d2, d3 = deltas
+    assert d1["sdma_down_checks"] > 0 and d1["down_mbps"] > 0, deltas
+    assert d3["sdma_down_checks"] == 0 and d3["wave_blocks"] > 0, deltas  # verified: downloads by waves
     if floor:
-        # the PUT's parity downloads are bracketed too: its first slow one
-        # already moved the device's downloads (and uploads) to waves
-        assert s0["sdma_down_slow"] == 0, s0
-        assert ctx_down_slow > 0, deltas
-        assert d1["sdma_down_checks"] == 0 and d2["sdma_down_checks"] == 0, deltas  # within the 2 s hold
-        assert d1["wave_blocks"] > 0 and d2["wave_blocks"] > 0, deltas
-    else:
-        assert d1["sdma_down_checks"] > 0 and d1["sdma_down_slow"] == 0, deltas
-        assert d1["down_mbps"] > 0, deltas
+        assert d1["sdma_down_slow"] > 0, deltas
+        assert d2["sdma_down_checks"] == 0 and d2["wave_blocks"] > 0, deltas  # within the 2 s hold
