@@ -1458,10 +1458,13 @@ def gpu_numa_node(torch, d: int):
 
 def _copy_delta(c0: list, c1: list) -> dict:
     """Host-pipeline counters (Context.pipe_stats, one dict per device)
-    accumulated over a leg; sdma_last_mbps is a gauge (the last timed upload
-    bracket's SDMA rate), reported as the lowest over the devices."""
-    out = {key: sum(b[key] - a[key] for a, b in zip(c0, c1)) for key in c1[0] if key != "sdma_last_mbps"}
-    out["sdma_last_mbps"] = min(b.get("sdma_last_mbps", 0) for b in c1)
+    accumulated over a leg; sdma_last_mbps / sdma_down_last_mbps are gauges
+    (the last timed upload / download bracket's SDMA rate), reported as the
+    lowest over the devices."""
+    gauges = ("sdma_last_mbps", "sdma_down_last_mbps")
+    out = {key: sum(b[key] - a[key] for a, b in zip(c0, c1)) for key in c1[0] if key not in gauges}
+    for g in gauges:
+        out[g] = min(b.get(g, 0) for b in c1)
     return out
 
 
