@@ -92,7 +92,7 @@ Knobs read_knobs() {
         if (c >= 0) k.pipe_copy = c;
     }
     k.pipe_sdma_floor = std::max(0L, env_long("MXEC_PIPE_SDMA_FLOOR", k.pipe_sdma_floor));
-    k.get_vgroups = int(std::max(1L, std::min(8L, env_long("MXEC_GET_VGROUPS", 1))));
+    k.get_vgroups = int(std::max(0L, std::min(8L, env_long("MXEC_GET_VGROUPS", 0))));
     long window = 0;
     if (parse_long("MXEC_GET_WINDOW", &window)) k.get_window = uint64_t(std::max(1L, window));
     k.gather_us = env_long("MXEC_GATHER_US", k.gather_us);

@@ -429,8 +429,9 @@ private:
     // slowed that call by 63 % (0.336 s against 0.206 at 128 objects,
     // profiles/r5/copy_engine/auto_dwatch_churn60_r5l2.jsonl), and its SDMA
     // downloads otherwise beat waves (0.204 s against 0.238 fresh).
+    bool dwatch_off_ = false;
     int dwatch_open() {
-        if (!watching(true) || dwatch_a_) return MXEC_OK;
+        if (!watching(true) || dwatch_off_ || dwatch_a_) return MXEC_OK;
         MXEC_TRY(new_timed_event(&dwatch_a_));
         MXEC_HIP(hipEventRecord(dwatch_a_, d2h_));
         dwatch_staged_ = false;
@@ -529,13 +530,16 @@ private:
             ok = static_cast<uint8_t*>(scratch_.p);
             exp = ok + fo;
         }
-        // Under MXEC_PIPE_COPY=auto a verified wave's rebuilt shards go down
-        // by waves (they leave after the last verdict, alone on the link:
-        // waves move them as fast as a healthy SDMA and keep that rate when
-        // SDMA downloads run slow after a large HBM free); an
-        // RS-only wave's go by SDMA, each group's bracketed (dwatch_open).
+        // Under MXEC_PIPE_COPY=auto a verified wave's last verification
+        // group's rebuilt shards go down by waves (they leave after the last
+        // verdict, alone on the link: waves move them as fast as a healthy
+        // SDMA and keep that rate when SDMA downloads run slow after a large
+        // HBM free), earlier groups' by SDMA, unbracketed; an
+        // RS-only wave's by SDMA, each group's bracketed (dwatch_open).
         const bool down_before = down_waves_;
-        if (verify && d_.kn && d_.kn->pipe_copy == 2) down_waves_ = true;
+        const bool auto_copy = d_.kn && d_.kn->pipe_copy == 2;
+        if (verify && auto_copy) down_waves_ = true;
+        dwatch_off_ = verify;  // a verified wave's downloads are not bracketed
         uint64_t vmsgs = 0;  // present shards to verify
         for (size_t o = o0; o < o1; ++o)
             if (objs[o].expected)
@@ -559,7 +563,10 @@ private:
             // j + 1's pieces go up and hash (on the other compute stream)
             // while the host waits for group j's verdicts, rebuilds it and
             // sends its shards down.
-            const std::vector<size_t> cut = verify_cuts(objs, o0, o1, up_bytes, longest_msg, P);
+            uint64_t down_bytes = 0;
+            for (size_t o = o0; o < o1; ++o)
+                for (int i = 0; i < objs[o].k + objs[o].m; ++i) down_bytes += objs[o].present[i] ? 0 : objs[o].len[i];
+            const std::vector<size_t> cut = verify_cuts(objs, o0, o1, up_bytes, longest_msg, down_bytes);
             MXEC_TRY(state_.ensure(msgs * 32));
             MXEC_TRY(flags_.ensure(msgs));
             std::vector<uint64_t> mbase(cut.size(), 0);
@@ -577,6 +584,11 @@ private:
                 if (j + 1 < G) MXEC_TRY(enqueue(j + 1));
                 MXEC_TRY(verify_collect(objs, cut[j], cut[j + 1], mbase[j], verdict[j]));
                 PTRACE(now("verified"));
+                // auto: the last group's shards (on the critical path, alone
+                // on the link) by waves; earlier groups' by SDMA beside the
+                // later groups' uploads and chains (wave copies there slow
+                // the chains: 0.64 s against 0.59 at 512 objects, G = 2).
+                if (auto_copy) down_waves_ = down_before || j + 1 == G;
                 for (const auto& q : object_groups(objs, cut[j], cut[j + 1]))
                     MXEC_TRY(rebuild_down(objs, q.first, q.second, cs_[j & 1], nullptr, data_only));
             }
@@ -598,6 +610,7 @@ private:
         const int frc = flush();
         PTRACE(report("rec_wave"));
         if (verify) down_waves_ = down_before;
+        dwatch_off_ = false;
         return frc;
     }
 
@@ -622,20 +635,37 @@ private:
     }
 
     // Verification groups of a piece-major reconstruct wave: cut points
-    // (first o0, last o1) by upload bytes, MXEC_GET_VGROUPS of them (default
-    // 1).  A model -- the last group's chains start (G-1)/G of the way
-    // through the upload and only its rebuilt shards go down after it, so
-    // max((G-1)/G * T_up + chain, T_up + piece) + D / G against one group's
-    // max(chain, T_up + piece) + D -- predicted 7-15 % from grouping at 512
-    // x 4+2 x 10 MiB, but the box does not overlap the two directions for
-    // free: the early groups' downloads run at the ~25 GB/s a D2H stream gets
-    // beside a full H2D stream (pcie duplex 2:1) and the last group's
-    // download waits behind them.  Measured (profiles/r5/get_groups/,
-    // MXEC_PIPE_TRACE marks): one group 0.655 s, two 0.818, four 0.631-0.640.
-    // So one group unless a caller's box says otherwise.
+    // (first o0, last o1) by upload bytes; MXEC_GET_VGROUPS of them, or (0,
+    // the default) the count the model below picks per wave.  Group j + 1's
+    // pieces go up and hash while group j's verdicts come back and its
+    // rebuilt shards go down, so only the last group's download follows the
+    // last verdict.  Measured at 512 x 4+2 x 10 MiB with SDMA downloads
+    // (profiles/r5/get_groups/vgroups_*_r5q.jsonl): one group 0.634 s, two
+    // 0.588, three 0.584, four 0.618; with every group's download by waves
+    // no count gained (0.637-0.690: wave copies beside the later groups'
+    // SHA-256 chains slow the chains).  Round 5's first measurement (one
+    // 0.655, two 0.818) predates the one-copy expected-digest upload.
     std::vector<size_t> verify_cuts(const std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t up_bytes,
-                                    uint64_t /*longest*/, uint64_t /*P*/) const {
-        const int G = d_.kn ? int(d_.kn->get_vgroups) : 1;
+                                    uint64_t longest, uint64_t down_bytes) const {
+        int G = d_.kn ? int(d_.kn->get_vgroups) : 1;
+        if (G == 0) {
+            // Per wave: the G that minimises max(T, (G-1)/G T + C) + D/G --
+            // the upload T (~50 GB/s), the chain C of the longest message,
+            // the rebuilt shards' download D (~55 GB/s), of which only the
+            // last group's is on the critical path.  512 x 4+2 x 10 MiB: 2
+            // (0.588 s against 0.634 for one group, with SDMA downloads);
+            // 128: 1 (the chain outlasts the upload).
+            const double T = double(up_bytes) / 50e9, D = double(down_bytes) / 55e9;
+            const double C = double(longest / 64) * kShaLagUsPerBlock * 1e-6;
+            double best = 0;
+            for (int g = 1; g <= 4; ++g) {
+                const double t = std::max(T, (g - 1) * T / g + C) + D / g + 0.005 * (g - 1);
+                if (g == 1 || t < best) {
+                    best = t;
+                    G = g;
+                }
+            }
+        }
         std::vector<size_t> cut{o0};
         const size_t n = o1 - o0;
         if (G > 1 && n >= size_t(G)) {

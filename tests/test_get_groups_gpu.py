@@ -1,5 +1,5 @@
-"""GPU: the verified host GET, as one verification group (the default) and as
-pipelined groups (MXEC_GET_VGROUPS; pipeline.cpp verify_cuts / verify_enqueue
+"""GPU: the verified host GET, as one verification group, as the count the
+library picks per wave (the default) and as pipelined groups (MXEC_GET_VGROUPS; pipeline.cpp verify_cuts / verify_enqueue
 / verify_collect): group j + 1's pieces go up and hash while the host
 collects group j's verdicts, rebuilds it and sends its shards down.  Reference: try_reconstruct_data_chunk,
 chunk_reader.rs:157-226, per object.
@@ -24,9 +24,11 @@ M = 1 << 20
 TOO_FEW_SHARDS_PRESENT = -10  # include/maxio_ec.h MXEC_E_TOO_FEW_SHARDS_PRESENT
 
 
-@pytest.mark.parametrize("groups", [1, 3])
+@pytest.mark.parametrize("groups", [0, 1, 3])
 def test_verified_get_in_groups_matches_originals(ctx_with, groups):
-    ctx = ctx_with(MXEC_GET_VGROUPS=groups)
+    """groups 0: the per-wave choice (pipeline.cpp verify_cuts), which keeps
+    this batch -- a 34 ms upload against a 19 ms chain -- as one group."""
+    ctx = ctx_with(MXEC_GET_VGROUPS=str(groups))
     k, m, n = 8, 4, 160
     S = M
     rng = np.random.default_rng(4242)
@@ -72,7 +74,8 @@ def test_verified_get_in_groups_matches_originals(ctx_with, groups):
     s1 = ctx.pipe_stats()
     assert rc == TOO_FEW_SHARDS_PRESENT, rc  # the batch's first failing object
     assert s1["verify_waves"] > s0["verify_waves"]
-    assert s1["verify_groups"] - s0["verify_groups"] == groups * (s1["verify_waves"] - s0["verify_waves"]), (s0, s1)
+    want = groups or 1
+    assert s1["verify_groups"] - s0["verify_groups"] == want * (s1["verify_waves"] - s0["verify_waves"]), (s0, s1)
     for o in range(n):
         if o in failing:
             assert status[o] == TOO_FEW_SHARDS_PRESENT, (o, status[o])

@@ -112,6 +112,7 @@ def main() -> int:
                     row["calls"].append({"s": round(el, 4), "warm": rep == 0,
                                          **{key: s1[key] - s0[key] for key in ("sdma_checks", "sdma_slow",
                                                                               "sdma_down_checks", "sdma_down_slow",
+                                                                              "verify_groups",
                                                                               "wave_blocks", "copies_1d",
                                                                               "copies_2d")},
                                          "sdma_last_mbps": s1["sdma_last_mbps"],
