@@ -373,7 +373,11 @@ private:
     // downloads.  A slow-down lasts ~3.5 s after 60 GB of HBM is freed
     // (profiles/r5/copy_engine/slow_duration_after_60GB_free_r5m.jsonl).
     static constexpr uint64_t kWatchMinBytes = uint64_t(16) << 20;
-    static constexpr int kWavesHoldMs = 2000;
+    // Downloads hold for 1 s: their slow spells follow HBM frees and last
+    // about freed bytes / 17 GB/s, so a 2 s hold after a pool-sized free
+    // kept an RS-only GET on waves (0.111 s) after SDMA had recovered
+    // (0.101; profiles/r5/copy_engine/vg_churn0_r5s.jsonl).
+    static constexpr int kWavesHoldMs = 2000, kDownWavesHoldMs = 1000;
     struct Bracket {
         hipEvent_t a, b;
         uint64_t bytes;
@@ -471,7 +475,8 @@ private:
         // unaffected by the free), so they are judged against twice the floor.
         const double floor = double(d_.kn ? d_.kn->pipe_sdma_floor : 20) * (k.down ? 2.0 : 1.0);
         const bool slow = gbps < floor;
-        const auto hold = std::chrono::steady_clock::now() + std::chrono::milliseconds(kWavesHoldMs);
+        const auto hold = std::chrono::steady_clock::now() +
+                          std::chrono::milliseconds(k.down ? kDownWavesHoldMs : kWavesHoldMs);
         if (k.down) {
             ++d_.sdma_down_probes;
             d_.sdma_down_last_mbps = uint64_t(gbps * 1e3);

@@ -163,7 +163,7 @@ def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
         s0 = ctx.pipe_stats()
         _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333})
         s1 = ctx.pipe_stats()
-        _put_and_check(ctx, 8, S, 1400 + len(floor))  # within the 2 s hold of a slow verdict
+        _put_and_check(ctx, 8, S, 1400 + len(floor))  # within the 2 s upload hold of a slow verdict
         s2 = ctx.pipe_stats()
     finally:
         ctx.close()
@@ -180,7 +180,7 @@ def test_get_download_watch(floor):
     rebuilt group, opened after the d2h stream's wait for the rebuild) and
     judges them against twice MXEC_PIPE_SDMA_FLOOR: with the default floor
     the bracket is timed; with a floor no SDMA reaches it is judged slow and
-    the device's downloads go by waves for the next 2 s (the second GET).  A
+    the device's downloads go by waves for the next 1 s (the second GET).  A
     verified GET's downloads go by waves under auto.  16 x 4+2 objects of
     4 MiB + 4 KiB shards, two data shards erased in each: every rebuilt shard
     equals the original every time."""
@@ -220,4 +220,4 @@ def test_get_download_watch(floor):
     assert d3["sdma_down_checks"] == 0 and d3["wave_blocks"] > 0, deltas  # verified: downloads by waves
     if floor:
         assert d1["sdma_down_slow"] > 0, deltas
-        assert d2["sdma_down_checks"] == 0 and d2["wave_blocks"] > 0, deltas  # within the 2 s hold
+        assert d2["sdma_down_checks"] == 0 and d2["wave_blocks"] > 0, deltas  # within the 1 s download hold
