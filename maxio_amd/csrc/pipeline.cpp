@@ -58,15 +58,15 @@ uint64_t rup(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // fixed cost.  With 2D copies (MXEC_PIPE_COPY2D=1) a 256 KiB ramp won 2 %
 // in one process (0.216 -> 0.211 s), but the 2D copies are off by default
 // (see queue_up), so the ramp is too (profiles/r3/pieces/).
+// Pieces of a piece-major wave: a ramp of pieces doubling from `ramp` bytes
+// up to P, then every P.
 struct PieceGrid {
     std::vector<uint64_t> starts;  // the ramp's pieces, then every P
     uint64_t P, ramp_end = 0;
-    explicit PieceGrid(uint64_t p) : P(p) {
+    PieceGrid(uint64_t p, uint64_t ramp) : P(p) {
+        uint64_t w = ramp;
 #ifdef MXEC_LAB
-        const char* e = getenv("MXEC_PIPE_RAMP_KB");  // lab builds only
-        uint64_t w = uint64_t(e ? atol(e) : 0) << 10;
-#else
-        uint64_t w = 0;
+        if (const char* e = getenv("MXEC_PIPE_RAMP_KB")) w = uint64_t(atol(e)) << 10;  // lab override
 #endif
         w = w / 64 * 64;
         for (; w && w < p; w *= 2) {
@@ -815,7 +815,7 @@ private:
             for (int i = 0; i < objs[o].k + objs[o].m; ++i)
                 if (objs[o].present[i]) longest = std::max(longest, objs[o].len[i]);
         }
-        const PieceGrid grid(P);
+        const PieceGrid grid(P, piece_ramp_);
         MXEC_TRY(upload_expected(objs, o0, o1, exp, mb));
         struct TwoD {
             bool& f;
@@ -1210,7 +1210,16 @@ private:
     // objects: 0.218 / 0.227 / 0.246 s, profiles/r4/e2e_pieces/).  So a wave
     // takes the smallest piece whose upload, at that piece's copy rate, still
     // fits inside the longest chain (the wave's floor either way), else 4 MiB.
-    uint64_t piece_bytes(uint64_t upload_bytes, uint64_t longest) const {
+    //
+    // A chain-bound wave (its upload fits inside its longest chain) also
+    // ramps its first pieces up from 256 KiB (piece_ramp_, PieceGrid): the
+    // wave ends about one chain after its first piece is up, so a smaller
+    // first piece ends it sooner -- verified GET of 128 x 4+2 x 10 MiB
+    // 0.241 s against 0.253, PUT with digests 0.2015 against 0.2033; an
+    // upload-bound wave loses to the extra copies (512 objects: 0.606 / 0.472
+    // against 0.588 / 0.457; profiles/r5/get_groups/ramp_*_r5u.jsonl).
+    uint64_t piece_bytes(uint64_t upload_bytes, uint64_t longest) {
+        piece_ramp_ = 0;
         if (!d_.kn) return uint64_t(1) << 20;
         if (!d_.kn->pipe_piece_auto) return d_.kn->pipe_piece;
         const double chain_s = double(longest / 64) * kShaLagUsPerBlock * 1e-6;
@@ -1219,9 +1228,13 @@ private:
             double gbps;  // sustained H2D rate of copies this size, measured (above)
         } kSteps[] = {{uint64_t(1) << 20, 33.0}, {uint64_t(2) << 20, 38.0}};
         for (const auto& s : kSteps)
-            if (double(upload_bytes) / (s.gbps * 1e9) <= chain_s) return s.bytes;
+            if (double(upload_bytes) / (s.gbps * 1e9) <= chain_s) {
+                piece_ramp_ = uint64_t(256) << 10;
+                return s.bytes;
+            }
         return uint64_t(4) << 20;
     }
+    uint64_t piece_ramp_ = 0;  // first piece of the current wave's ramp (0: none)
 
     int wave_pieces(std::vector<HostObj>& objs, size_t o0, size_t o1, uint64_t P) {
         Slot& slot = slot_;
@@ -1245,7 +1258,7 @@ private:
         MXEC_TRY(scratch_.ensure(nm * 64));  // digests [nm][32], then chain states [nm][8] words
         uint8_t* digests = static_cast<uint8_t*>(scratch_.p);
         uint32_t* state = reinterpret_cast<uint32_t*>(digests + nm * 32);
-        const PieceGrid grid(P);
+        const PieceGrid grid(P, piece_ramp_);
         const uint64_t npieces = grid.count(longest);
         hipStream_t rs_s = cs_[0], sha_s = cs_[1];
         hipEvent_t sha_done = nullptr;
