@@ -203,6 +203,16 @@ __device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], u32x4* dst) {
 // the step before: a v_cndmask picks which), and both store what arrives in
 // B[s - 1].  Each lane writes K + W of its own words into the message's LDS
 // column (rows of four words: components L and L + 2).  kown[k] = K[2k + L].
+// The K + W ring's barriers (producer and consumer sides).  Diagnostic
+// build `make nosync` (MXEC_LAB_SHA_NOSYNC): none at all -- every wave runs
+// its loop unsynchronised (wrong digests, same work), so the form's block
+// time without the barriers and the waits behind them.
+#ifdef MXEC_LAB_SHA_NOSYNC
+#define KW_SYNC() ((void)0)
+#else
+#define KW_SYNC() __syncthreads()
+#endif
+
 #define QDPP_SWAP(x) uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0xB1, 0xF, 0xF, true))  // quad_perm [1,0,3,2]
 
 template <int ROW>
@@ -322,7 +332,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
                 schedule(uint32_t(j));
             }
         }
-        __syncthreads();
+        KW_SYNC();
         // Whole groups of kShaPrefetch steps, then the rest: an exit in the
         // middle of a group would join the loop's back edge with fewer loads
         // issued, and the waits at the top would drain the ring again.
@@ -338,7 +348,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
                 load_block(ps + 64 * min_u64(b + AHEAD + kShaPrefetch, last), ring[j]);
                 schedule(wb);
                 wb = wb + 1 == NB ? 0 : wb + 1;
-                __syncthreads();
+                KW_SYNC();
             }
         }
 #pragma unroll
@@ -347,7 +357,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
                 block_words(ring[j], w);
                 schedule(wb);
                 wb = wb + 1 == NB ? 0 : wb + 1;
-                __syncthreads();
+                KW_SYNC();
             }
         }
     } else {
@@ -358,7 +368,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
                 message_words(p + 64 * j, aligned, w);
                 schedule(uint32_t(j));
             }
-        __syncthreads();
+        KW_SYNC();
         uint32_t wb = AHEAD % NB;
         for (uint64_t b = 0; b < nmax; ++b) {
             if (b + AHEAD < nfull) {
@@ -366,7 +376,7 @@ __device__ __forceinline__ void kw_producer(u32x4* kw, uint32_t lane, bool live,
                 schedule(wb);
             }
             wb = wb + 1 == NB ? 0 : wb + 1;
-            __syncthreads();
+            KW_SYNC();
         }
     }
 }
@@ -412,12 +422,12 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
     // The two roles run separate loops with one barrier per block each plus
     // one before the first (the trip counts match, so the barriers pair up).
     if (wave == 0) {
-        __syncthreads();
+        KW_SYNC();
         if constexpr (NB == 2) {
 #ifdef MXEC_LAB
             for (uint64_t b = 0; b < nmax; ++b) {
                 if (b < nfull) compress_kw(st, &kw[b & 1][0][lane]);
-                __syncthreads();
+                KW_SYNC();
             }
 #endif
         } else {
@@ -435,12 +445,12 @@ __global__ __launch_bounds__(128) void sha256_split_kernel(const uint8_t* const*
             for (uint64_t b = 0; b < nmax; b += 2) {
                 load_kw(&kw[rb][0][lane], nxt);
                 if (b < nfull) compress_regs(st, cur);
-                __syncthreads();
+                KW_SYNC();
                 rb = rb == 2 ? 0 : rb + 1;
                 if (b + 1 >= nmax) break;
                 load_kw(&kw[rb][0][lane], cur);
                 if (b + 1 < nfull) compress_regs(st, nxt);
-                __syncthreads();
+                KW_SYNC();
                 rb = rb == 2 ? 0 : rb + 1;
             }
         }
@@ -714,7 +724,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     const u32x4* kcol = &kw[0][0][role == 0 ? ml : role == 1 ? 65 : 64];
     // As the split form's NB = 3 consumer: block b + 1's reads go out right
     // after the barrier that opens block b, block b runs from registers.
-    __syncthreads();
+    KW_SYNC();
     u32x4 cur[16], nxt[16];
     load_kw<kQuadRow>(kcol, cur);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -728,7 +738,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
 #endif
             compress_lag(s, cur, q);
         }
-        __syncthreads();
+        KW_SYNC();
         rb = rb == 2 ? 0 : rb + 1;
         if (b + 1 >= nmax) break;
         load_kw<kQuadRow>(kcol + rb * BUF, cur);
@@ -739,7 +749,7 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
 #endif
             compress_lag(s, nxt, q);
         }
-        __syncthreads();
+        KW_SYNC();
         rb = rb == 2 ? 0 : rb + 1;
     }
     // Lane E takes (a, b, c, d) from lane A and finishes alone: padded tail,
