@@ -380,14 +380,19 @@ private:
     static constexpr int kWavesHoldMs = 2000, kDownWavesHoldMs = 1000;
     struct Bracket {
         hipEvent_t a, b;
-        uint64_t bytes;
+        uint64_t bytes, copies;
         bool staged;
         bool down;
     };
+    // Only brackets whose DMAs average at least this much are judged: many
+    // small copies run near the floor on a healthy SDMA (a 10 MiB chunk's
+    // 256 KiB tail piece, 512 copies, read 9 GB/s in a fresh process).
+    static constexpr uint64_t kWatchMinCopy = uint64_t(1) << 20;
     std::vector<Bracket> watch_;
     hipEvent_t watch_a_ = nullptr, dwatch_a_ = nullptr;
     bool watch_staged_ = false, dwatch_staged_ = false;
-    uint64_t watch_bytes_ = 0, dwatch_bytes_ = 0;  // SDMA bytes issued in the open brackets
+    uint64_t watch_bytes_ = 0, dwatch_bytes_ = 0;    // SDMA bytes issued in the open brackets
+    uint64_t watch_copies_ = 0, dwatch_copies_ = 0;  // and the DMAs (2D: rows) that moved them
     void start_copy_mode() {
         const int mode = d_.kn ? d_.kn->pipe_copy : 0;
         const auto now = std::chrono::steady_clock::now();
@@ -412,6 +417,7 @@ private:
         MXEC_HIP(hipEventRecord(watch_a_, h2d_));
         watch_staged_ = false;
         watch_bytes_ = 0;
+        watch_copies_ = 0;
         return MXEC_OK;
     }
     // After the bracket's copies are issued (issue_up done).
@@ -420,8 +426,9 @@ private:
         hipEvent_t b = nullptr;
         MXEC_TRY(new_timed_event(&b));
         MXEC_HIP(hipEventRecord(b, h2d_));
-        watch_.push_back(Bracket{watch_a_, b, watch_bytes_, watch_staged_, false});
+        watch_.push_back(Bracket{watch_a_, b, watch_bytes_, watch_copies_, watch_staged_, false});
         watch_bytes_ = 0;
+        watch_copies_ = 0;
         watch_a_ = nullptr;
         return watch_poll();
     }
@@ -440,6 +447,7 @@ private:
         MXEC_HIP(hipEventRecord(dwatch_a_, d2h_));
         dwatch_staged_ = false;
         dwatch_bytes_ = 0;
+        dwatch_copies_ = 0;
         return MXEC_OK;
     }
     int dwatch_close() {
@@ -447,8 +455,9 @@ private:
         hipEvent_t b = nullptr;
         MXEC_TRY(new_timed_event(&b));
         MXEC_HIP(hipEventRecord(b, d2h_));
-        watch_.push_back(Bracket{dwatch_a_, b, dwatch_bytes_, dwatch_staged_, true});
+        watch_.push_back(Bracket{dwatch_a_, b, dwatch_bytes_, dwatch_copies_, dwatch_staged_, true});
         dwatch_bytes_ = 0;
+        dwatch_copies_ = 0;
         dwatch_a_ = nullptr;
         return watch_poll();
     }
@@ -468,7 +477,7 @@ private:
         MXEC_HIP(hipEventSynchronize(k.b));
         float ms = 0;
         MXEC_HIP(hipEventElapsedTime(&ms, k.a, k.b));
-        if (k.staged || k.bytes < kWatchMinBytes || ms <= 0) return MXEC_OK;
+        if (k.staged || k.bytes < kWatchMinBytes || k.bytes < k.copies * kWatchMinCopy || ms <= 0) return MXEC_OK;
         const double gbps = double(k.bytes) / (double(ms) * 1e6);
         // A GET's download brackets run at 54-55 GB/s on a healthy box and
         // ~24 in the seconds after a large HBM free (uploads: 33-55 healthy,
@@ -1024,6 +1033,7 @@ private:
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, h2d_));
             ++d_.copies_1d;
             watch_bytes_ += len;
+            ++watch_copies_;
             return MXEC_OK;
         }
         watch_staged_ = true;  // host memcpy through the ring: not an SDMA rate
@@ -1110,6 +1120,7 @@ private:
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyHostToDevice, h2d_));
             ++d_.copies_2d;
             watch_bytes_ += r.len * r.rows;
+            watch_copies_ += r.rows;
             d_.copies_2d_rows += r.rows;
             return MXEC_OK;
         }
@@ -1136,6 +1147,7 @@ private:
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyDeviceToHost, d2h_));
             ++d_.copies_2d;
             dwatch_bytes_ += r.len * r.rows;
+            dwatch_copies_ += r.rows;
             d_.copies_2d_rows += r.rows;
             return MXEC_OK;
         }
@@ -1170,6 +1182,7 @@ private:
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, d2h_));
             ++d_.copies_1d;
             dwatch_bytes_ += len;
+            ++dwatch_copies_;
             return MXEC_OK;
         }
         dwatch_staged_ = true;
