@@ -589,6 +589,15 @@ private:
                 for (size_t o = cut[j - 1]; o < cut[j]; ++o) mbase[j] += uint64_t(objs[o].k + objs[o].m);
             }
             const size_t G = cut.size() - 1;
+            // auto: a wave verified as one group uploads by waves too (one
+            // copy launch per piece instead of a DMA per piece of every
+            // shard: 128 x 4+2 x 10 MiB 0.240 s against 0.256 by SDMA, 256
+            // objects 0.363 against 0.371); grouped waves keep SDMA uploads
+            // (512: 0.590 against 0.679 by waves, whose copies beside the
+            // earlier groups' downloads and chains slow both;
+            // profiles/r5/copy_engine/verified_uploads_r5z.jsonl).
+            const bool up_before = waves_now_;
+            if (auto_copy && G == 1) waves_now_ = true;
             std::vector<hipEvent_t> verdict(G, nullptr);
             auto enqueue = [&](size_t j) {
                 return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], P, cs_[j & 1], &verdict[j]);
@@ -608,6 +617,7 @@ private:
             }
             d_.verify_groups += G;
             d_.verify_waves += 1;
+            waves_now_ = up_before;
         } else {
             const auto groups = object_groups(objs, o0, o1);
             std::vector<hipEvent_t> up;  // per group: its upload is done
