@@ -1237,13 +1237,15 @@ private:
     // takes the smallest piece whose upload, at that piece's copy rate, still
     // fits inside the longest chain (the wave's floor either way), else 4 MiB.
     //
-    // A chain-bound wave (its upload fits inside its longest chain) also
-    // ramps its first pieces up from 256 KiB (piece_ramp_, PieceGrid): the
-    // wave ends about one chain after its first piece is up, so a smaller
-    // first piece ends it sooner -- verified GET of 128 x 4+2 x 10 MiB
-    // 0.241 s against 0.253, PUT with digests 0.2015 against 0.2033; an
-    // upload-bound wave loses to the extra copies (512 objects: 0.606 / 0.472
-    // against 0.588 / 0.457; profiles/r5/get_groups/ramp_*_r5u.jsonl).
+    // A chain-bound verified GET wave (its upload fits inside its longest
+    // chain) also ramps its first pieces up from 256 KiB (piece_ramp_,
+    // PieceGrid): it ends about one chain after its first piece is up, so a
+    // smaller first piece ends it sooner -- 128 x 4+2 x 10 MiB 0.2406 s
+    // against 0.2475 with its uploads by waves (rec_wave).  The PUT with
+    // digests lost to the same ramp (0.214-0.223 against 0.2033 by SDMA;
+    // profiles/r5/get_groups/ramp_ab_final_r5ab.jsonl), and an upload-bound
+    // wave loses to the extra copies (512 objects: 0.606 against 0.588,
+    // ramp_*_r5u.jsonl), so wave() clears it and only chain-bound waves set it.
     uint64_t piece_bytes(uint64_t upload_bytes, uint64_t longest) {
         piece_ramp_ = 0;
         if (!d_.kn) return uint64_t(1) << 20;
@@ -1413,6 +1415,7 @@ private:
                 longest_msg = std::max(longest_msg, objs[o].S);
             }
             const uint64_t P = piece_bytes(up_bytes, longest_msg);
+            piece_ramp_ = 0;  // the PUT keeps uniform pieces (the ramp cost it 5-9 %, below)
             if (P && msgs && msgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256))
                 return wave_pieces(objs, o0, o1, P);
         }
