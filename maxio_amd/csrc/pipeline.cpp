@@ -1297,7 +1297,12 @@ private:
         } twod(pieces2d_, !waves_now_ && P > (uint64_t(1) << 20));
         PTRACE(start(h2d_));
         for (uint64_t pc = 0; pc < npieces; ++pc) {
-            if (grid.width(pc) == P) MXEC_TRY(watch_open());  // not the ramp's pieces (verify_enqueue)
+            // No SDMA watch here: in the seconds after a large HBM free the
+            // bracket events among the pieces cost the PUT with digests 63 %
+            // (0.335 s against 0.206 unwatched at 128 objects,
+            // profiles/r5/copy_engine/final_churn60_r5ag.jsonl) while its
+            // uploads ran at full rate; its downloads, the direction that
+            // slows, stay on SDMA either way (waves cost it 14-18 %).
             const uint64_t off = grid.start(pc), pw = grid.width(pc);
             for (size_t o = o0; o < o1; ++o) {
                 const HostObj& h = objs[o];
