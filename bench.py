@@ -1662,6 +1662,198 @@ def e2e_host_leg(ctx, torch, plan: Plan, per_dev: int, reps: int = 5, get_only: 
     return res
 
 
+def _encoded_set(ctx, shapes, seed: int):
+    """Objects of `shapes` in page-locked memory, parity and digests filled
+    by one PUT: (rows per object, digests, data bytes)."""
+    import numpy as np
+
+    blk = np.random.default_rng(seed).integers(0, 256, (64 << 20) + 4096, dtype=np.uint8)
+    rows, dptr, pptr = [], [], []
+    for o, (k, m, S) in enumerate(shapes):
+        a = ctx.host_array((k + m) * S).reshape(k + m, S)
+        flat = a[:k].reshape(-1)
+        sh = (o * 4099) % 4096  # a different phase of the block per object
+        for x in range(0, flat.size, 64 << 20):
+            w = min(64 << 20, flat.size - x)
+            flat[x:x + w] = blk[sh:sh + w]
+        rows.append(a)
+        dptr += [a[j].ctypes.data for j in range(k)]
+        pptr += [a[k + i].ctypes.data for i in range(m)]
+    dig = np.zeros(sum(k + m for k, m, _ in shapes) * 32, np.uint8)
+    st = ctx.encode_batch_host(shapes, dptr, pptr, digests=dig)
+    assert (st == 0).all()
+    return rows, dig, dptr, pptr, sum(k * S for k, _, S in shapes)
+
+
+class _GetBatch:
+    """A verified host GET over an encoded set: two seeded erasures per
+    object (scribbled), every shard pointer, the expected digests."""
+
+    def __init__(self, ctx, shapes, rows, dig, seed: int):
+        import numpy as np
+
+        self.ctx, self.shapes, self.rows, self.dig = ctx, shapes, rows, dig
+        rng = np.random.default_rng(seed)
+        self.ptrs, pres = [], []
+        for (k, m, S), a in zip(shapes, rows):
+            self.ptrs += [a[i].ctypes.data for i in range(k + m)]
+            p = np.ones(k + m, np.uint8)
+            p[rng.choice(k + m, 2, replace=False)] = 0
+            pres.append(p)
+        self.present0 = np.concatenate(pres)
+        n = len(rows)
+        self.ref = {o: rows[o].copy() for o in sorted({0, n // 3, n // 2, n - 1})}  # a sample
+
+    def run(self):
+        g = 0
+        for (k, m, S), a in zip(self.shapes, self.rows):  # the lost shards' buffers scribbled
+            for i in range(k + m):
+                if not self.present0[g + i]:
+                    a[i, :4096] = 0x5A
+            g += k + m
+        pr = self.present0.copy()
+        rc, _ = self.ctx.reconstruct_batch_host(self.shapes, self.ptrs, pr, expected=self.dig)
+        assert rc == 0 and pr.all(), rc
+
+    def exact(self) -> bool:
+        import numpy as np
+
+        return all(np.array_equal(self.rows[o], r) for o, r in self.ref.items())
+
+
+def e2e_concurrent(ctx, n: int = 128, reps: int = 3, stream_s: float = 5.0) -> dict:
+    """Concurrent host-batch calls on one device (MaxIO
+    serves PUTs and GETs at once, filesystem.rs:686-828, chunk_reader.rs:87-226,
+    main.rs:81):
+
+    * pair: a PUT with digests and a verified GET (two erasures per object),
+      n x 4+2 x 10 MiB each from page-locked memory, each alone (median of
+      `reps` after a warm one) and both started together from two threads
+      (wall clock until both return) -- `pair_over_solo_sum` is the pair's
+      time over the two solo times added;
+    * mixed_stream: configs[4]'s shapes (4+2 / 8+4 / 10+4 at 64 KiB - 10 MiB
+      chunks, 60 objects per batch) from page-locked memory, one thread
+      issuing PUT-with-digests batches and one verified-GET batches back to
+      back for `stream_s` seconds: payload GiB/s (k x chunk bytes per
+      object) of each and together, per-call p50 / p99.
+    Spot checks: the pair's GET objects equal their originals, a PUT object's
+    parity against the oracle, the stream's GET objects after the stream."""
+    import threading
+
+    import numpy as np
+
+    res = {"workload": f"concurrent host batches on one device: pair = PUT with digests + verified GET, "
+                       f"{n} x 4+2 x 10 MiB each; mixed_stream = configs[4] shapes, two threads for {stream_s} s"}
+    k, m, S = 4, 2, 10 << 20
+    shapes = [(k, m, S)] * n
+    put_rows, _, put_d, put_p, put_bytes = _encoded_set(ctx, shapes, 31)
+    get_rows, get_dig, _, _, get_bytes = _encoded_set(ctx, shapes, 32)
+    put_dig = np.zeros(n * (k + m) * 32, np.uint8)
+    get = _GetBatch(ctx, shapes, get_rows, get_dig, SEED + 33)
+
+    def put():
+        st = ctx.encode_batch_host(shapes, put_d, put_p, digests=put_dig)
+        assert (st == 0).all()
+
+    def timed(fn):
+        t0 = time.perf_counter()
+        fn()
+        return time.perf_counter() - t0
+
+    put(), get.run()  # warm
+    s0 = ctx.pipe_stats()
+    solo_put = statistics.median([timed(put) for _ in range(reps)])
+    solo_get = statistics.median([timed(get.run) for _ in range(reps)])
+    pair, each = [], []
+    for _ in range(reps):
+        go = threading.Barrier(3)
+        t_end = {}
+
+        def run(name, fn):
+            go.wait()
+            fn()
+            t_end[name] = time.perf_counter()
+
+        th = [threading.Thread(target=run, args=("put", put)), threading.Thread(target=run, args=("get", get.run))]
+        for t in th:
+            t.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for t in th:
+            t.join()
+        pair.append(max(t_end.values()) - t0)
+        each.append({kname: round(v - t0, 4) for kname, v in t_end.items()})
+    s1 = ctx.pipe_stats()
+    el = statistics.median(pair)
+    o = n // 2
+    want = _oracle().encode(list(put_rows[o][:k]), m, S)
+    res["pair"] = {"solo_put_s": round(solo_put, 4), "solo_get_s": round(solo_get, 4),
+                   "pair_s": round(el, 4), "pair_each_s": pair and [round(p, 4) for p in pair],
+                   "finish_times_s": each,
+                   "pair_over_solo_sum": round(el / (solo_put + solo_get), 4),
+                   "payload_GiBps": round((put_bytes + get_bytes) / GIB / el, 2),
+                   "counters": {key: s1[key] - s0[key] for key in ("calls", "calls_shared", "spec_pieces",
+                                                                   "spec_redos", "pace_waits")},
+                   "spot_check": bool(get.exact() and all(np.array_equal(put_rows[o][k + i], want[i])
+                                                          for i in range(m)))}
+    for a in put_rows + get_rows:
+        ctx.host_free(a.reshape(-1))
+    del put_rows, get_rows, get
+
+    # configs[4]: mixed k+m at mixed chunk sizes, a continuous stream.
+    kinds = [(4, 2), (8, 4), (10, 4)]
+    sizes = [64 << 10, 256 << 10, 1 << 20, 4 << 20, 10 << 20]
+    mshapes = [(*kinds[i % 3], sizes[(i // 3) % 5]) for i in range(60)]
+    p_rows, _, p_d, p_p, p_bytes = _encoded_set(ctx, mshapes, 41)
+    g_rows, g_dig, _, _, g_bytes = _encoded_set(ctx, mshapes, 42)
+    p_dig = np.zeros(sum(kk + mm for kk, mm, _ in mshapes) * 32, np.uint8)
+    gb = _GetBatch(ctx, mshapes, g_rows, g_dig, SEED + 43)
+
+    def mput():
+        st = ctx.encode_batch_host(mshapes, p_d, p_p, digests=p_dig)
+        assert (st == 0).all()
+
+    mput(), gb.run()  # warm
+    times = {"put": [], "get": []}
+    stop = time.perf_counter() + stream_s
+    go = threading.Barrier(2)
+
+    def loop(name, fn):
+        go.wait()
+        while time.perf_counter() < stop:
+            times[name].append(timed(fn))
+
+    s0 = ctx.pipe_stats()
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=loop, args=("put", mput)), threading.Thread(target=loop, args=("get", gb.run))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    s1 = ctx.pipe_stats()
+
+    def pct(v, q):
+        v = sorted(v)
+        return round(v[min(len(v) - 1, int(q * len(v)))], 4)
+
+    res["mixed_stream"] = {
+        "batch": "60 objects: (4+2, 8+4, 10+4) x (64 KiB, 256 KiB, 1 MiB, 4 MiB, 10 MiB) chunks, 4 of each",
+        "seconds": round(wall, 3),
+        "put": {"calls": len(times["put"]), "GiBps_payload": round(len(times["put"]) * p_bytes / GIB / wall, 2),
+                "p50_s": pct(times["put"], 0.5), "p99_s": pct(times["put"], 0.99)},
+        "get": {"calls": len(times["get"]), "GiBps_payload": round(len(times["get"]) * g_bytes / GIB / wall, 2),
+                "p50_s": pct(times["get"], 0.5), "p99_s": pct(times["get"], 0.99)},
+        "GiBps_payload": round((len(times["put"]) * p_bytes + len(times["get"]) * g_bytes) / GIB / wall, 2),
+        "counters": {key: s1[key] - s0[key] for key in ("calls", "calls_shared", "spec_pieces", "spec_redos",
+                                                        "pace_waits")},
+        "spot_check": gb.exact(),
+    }
+    for a in p_rows + g_rows:
+        ctx.host_free(a.reshape(-1))
+    return res
+
+
 # ---- main ------------------------------------------------------------------------
 
 
@@ -1818,6 +2010,7 @@ def main() -> int:
         extra["e2e_host"] = e2e_host_leg(ctx, torch, plan, 128 if D == 1 and world == 1 else 64)
         if D == 1 and world == 1 and with_extra:
             extra["e2e_put_512"] = e2e_put_large(ctx)
+            extra["e2e_concurrent"] = e2e_concurrent(ctx)
     if rank == 0 and with_extra:
         extra.update(extras(ctx, torch, dev, stream, args.steps, cal))
         if not args.no_e2e:

@@ -122,8 +122,12 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
  * and how many ran below its SDMA floor (the rest of those calls' uploads,
  * and the device's for 2 s, copied by waves), the piece-major verified
  * reconstruct waves and the verification groups they ran as, the last timed
- * upload bracket's SDMA rate in MB/s, and the same three for downloads
- * (brackets timed, below the floor, last rate).  Returns how many counters were
+ * upload bracket's SDMA rate in MB/s, the same three for downloads
+ * (brackets timed, below the floor, last rate), the host-batch calls run on
+ * the device and how many of them started while another was in flight, the
+ * verified GET's speculative piece rebuilds and the objects it rebuilt
+ * again after a verdict, and the host waits that paced a shared call's
+ * enqueue.  Returns how many counters were
  * written (min(n, MXEC_PIPE_STAT_COUNT)), or an error.  Diagnostics (tests). */
 #define MXEC_PIPE_STAT_COPIES_1D 0
 #define MXEC_PIPE_STAT_COPIES_2D 1
@@ -137,7 +141,12 @@ int mxec_ctx_combiner_stats(mxec_ctx* ctx, int i, uint64_t* launches, uint64_t* 
 #define MXEC_PIPE_STAT_SDMA_DOWN_CHECKS 9
 #define MXEC_PIPE_STAT_SDMA_DOWN_SLOW 10
 #define MXEC_PIPE_STAT_SDMA_DOWN_LAST_MBPS 11
-#define MXEC_PIPE_STAT_COUNT 12
+#define MXEC_PIPE_STAT_CALLS 12
+#define MXEC_PIPE_STAT_CALLS_SHARED 13
+#define MXEC_PIPE_STAT_SPEC_PIECES 14
+#define MXEC_PIPE_STAT_SPEC_REDOS 15
+#define MXEC_PIPE_STAT_PACE_WAITS 16
+#define MXEC_PIPE_STAT_COUNT 17
 int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n);
 /* Workgroups per CU the ctx's device `dev` runs large uniform RS launches of
  * (k inputs, m outputs, shard_size) at: the grid tuner times the first
@@ -162,6 +171,13 @@ int mxec_ctx_coef_stats(mxec_ctx* ctx, int dev, uint64_t* recycles, uint64_t* re
  * library's pinned staging copy.  NULL on failure; free with
  * mxec_host_free. */
 void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes);
+/* The same, on the NUMA node of the ctx's device `dev` (MXEC_HOST_NUMA or
+ * not): on a host whose GPUs sit on two sockets, a request body meant for a
+ * GPU goes on that GPU's socket, and the host batch calls deal an object to
+ * a GPU on the node of its pages (pipeline.cpp deal_batch) -- the DMAs then
+ * stay off the socket link.  Replaces nothing in the reference (MaxIO's
+ * bodies are plain heap memory; filesystem.rs:686-828). */
+void* mxec_host_alloc_device(mxec_ctx* ctx, int dev, size_t bytes);
 void mxec_host_free(mxec_ctx* ctx, void* p);
 
 /* ---- ReedSolomon::new ----------------------------------------------------- */
@@ -290,7 +306,10 @@ int mxec_encode_batch_device(mxec_ctx* ctx, int dev, void* stream,
  * (direct from pinned memory, else via a pinned ring), RS + SHA-256 kernels
  * and downloads are pipelined on separate streams with the whole batch
  * resident in HBM.  Blocks until every
- * parity chunk and digest is in host memory. */
+ * parity chunk and digest is in host memory.  Thread-safe: concurrent
+ * calls (this one and mxec_reconstruct_batch_host, from any threads) share
+ * each device -- up to MXEC_PIPE_LANES at once, their waves interleaved on
+ * the device's four pipeline streams. */
 int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs,
                            uint64_t n_obj, const uint8_t* const* data,
                            const uint64_t* data_len, uint8_t* const* parity,
@@ -306,10 +325,17 @@ int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs,
  * verification; status_out (host, n_obj) may be NULL.  Objects are dealt
  * over the ctx's devices as mxec_encode_batch_host deals them; per device the
  * present shards go up (direct from pinned memory, else via a pinned ring),
- * are verified and rebuilt there, and only the rebuilt shards come back.  An
- * object short of k verified shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT and
- * none of its buffers is written; the call returns the first such status.
- * Blocks until every rebuilt shard is in host memory. */
+ * are verified and rebuilt there, and only the rebuilt shards come back.  With
+ * verification the missing shards are rebuilt piece by piece as the present
+ * ones arrive, before the verdict (MXEC_GET_SPECULATE, default on), and an
+ * object whose verdict drops a shard is rebuilt again from the verified
+ * ones.  An object short of k verified shards gets
+ * MXEC_E_TOO_FEW_SHARDS_PRESENT: its present shards' buffers are not written
+ * and its missing shards' buffers are undefined (not written with
+ * MXEC_GET_SPECULATE=0; the reference returns an error and no data,
+ * chunk_reader.rs:203-206); the call returns the first such status.
+ * Blocks until every rebuilt shard is in host memory.  Thread-safe, as
+ * mxec_encode_batch_host. */
 int mxec_reconstruct_batch_host(mxec_ctx* ctx, const mxec_object* objs,
                                 uint64_t n_obj, uint8_t* const* shards,
                                 const uint64_t* shard_len, uint8_t* present,

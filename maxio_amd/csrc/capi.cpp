@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <array>
 #include <cctype>
+#include <chrono>
 #include <fstream>
 #include <cstdio>
 #include <cstdlib>
@@ -27,7 +28,12 @@ namespace {
 // hash (GET) paths under auto and waves, the encode (PUT) path under waves
 // only (pipeline.cpp has the measurements behind the split).
 bool copy_waves_get(const Device& d) {
-    return d.kn && (d.kn->pipe_copy == 1 || (d.kn->pipe_copy == 2 && d.sdma_slow.load()));
+    if (!d.kn) return false;
+    if (d.kn->pipe_copy == 1) return true;
+    if (d.kn->pipe_copy != 2) return false;
+    const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+    return now < d.waves_up_until_ns.load() || now < d.waves_down_until_ns.load();
 }
 bool copy_waves_put(const Device& d) { return d.kn && d.kn->pipe_copy == 1; }
 
@@ -153,6 +159,34 @@ int mxec_device_count(void) {
 }
 
 namespace {
+
+// NUMA node of HIP device `dev` (sysfs, through its PCI bus id), or -1.
+int device_numa_node(int dev) {
+    char bus[64] = {};
+    if (hipDeviceGetPCIBusId(bus, int(sizeof bus), dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char& c : bus) c = char(std::tolower(static_cast<unsigned char>(c)));
+    std::ifstream f(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
+    int node = -1;
+    return f >> node ? node : -1;
+}
+
+// The node all of the context's devices sit on, or -1 (unknown or several).
+int ctx_numa_node(const mxec_ctx* ctx) {
+    int node = -1;
+    for (const auto& d : ctx->c.devs) {
+        const int n = d->numa_node;
+        if (n < 0 || (node >= 0 && n != node)) return -1;
+        node = n;
+    }
+    return node;
+}
+
+}  // namespace
+
+namespace {
 // The one open path.  `logical` > 1 (mxec_open_test only) opens every
 // selected device that many times, each copy with its own slots, streams,
 // arenas, combiner and pipeline, so the multi-device paths (per-device
@@ -178,6 +212,9 @@ mxec_ctx* open_ctx(uint32_t device_mask, int streams_per_device, const Knobs& kn
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && cus > 0)
                 dev->n_cus = cus;
+            // test-only logical copies pretend to sit on two nodes, so the
+            // host pipeline's NUMA dealing runs on a one-card box
+            dev->numa_node = logical > 1 ? (dl % logical) % 2 : device_numa_node(d);
             bool ok = true;
             for (int s = 0; s < streams_per_device; ++s) {
                 auto slot = std::make_unique<Slot>();
@@ -208,6 +245,10 @@ mxec_ctx* open_ctx(uint32_t device_mask, int streams_per_device, const Knobs& kn
             set_error(MXEC_E_NO_DEVICE, "no selected HIP device could be opened");
             return nullptr;
         }
+        bool multi = false;
+        for (const auto& d : ctx->c.devs)
+            multi = multi || (d->numa_node >= 0 && d->numa_node != ctx->c.devs[0]->numa_node);
+        for (auto& d : ctx->c.devs) d->ctx_multi_node = multi && d->numa_node >= 0;
         return ctx;
     } catch (...) {
         set_error(MXEC_E_OOM, "context allocation failed");
@@ -246,6 +287,17 @@ void mxec_close(mxec_ctx* ctx) {
     for (auto& d : ctx->c.devs) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
+        // The host pipeline's lanes (pinned rings, pools, descriptor arenas,
+        // events) and its four streams, and the combiner's streams, go first
+        // and explicitly, while the device is idle.
+        {
+            std::lock_guard<std::mutex> g(d->pipe_mu);
+            d->pipe.reset();
+        }
+        {
+            std::lock_guard<std::mutex> g(d->comb_mu);
+            d->comb.reset();
+        }
         rs_grid_release(*d);
         coef_release(*d);
         for (auto& s : d->slots) slot_destroy(*s);
@@ -269,7 +321,10 @@ int mxec_ctx_pipe_stats(mxec_ctx* ctx, int dev, uint64_t* out, int n) {
                                               d.sdma_probes.load(),      d.sdma_slow_verdicts.load(),
                                               d.verify_waves.load(),     d.verify_groups.load(),
                                               d.sdma_last_mbps.load(),   d.sdma_down_probes.load(),
-                                              d.sdma_down_slow_verdicts.load(), d.sdma_down_last_mbps.load()};
+                                              d.sdma_down_slow_verdicts.load(), d.sdma_down_last_mbps.load(),
+                                              d.pipe_calls.load(),       d.pipe_calls_shared.load(),
+                                              d.spec_pieces.load(),      d.spec_redos.load(),
+                                              d.pace_waits.load()};
     const int k = std::min(n, int(MXEC_PIPE_STAT_COUNT));
     for (int i = 0; i < k; ++i) out[i] = v[i];
     return k;
@@ -299,33 +354,6 @@ int mxec_ctx_rs_grid(mxec_ctx* ctx, int dev, int k, int m, uint64_t shard_size) 
     return guarded([&] { return rs_grid_in_use(*ctx->c.devs[size_t(dev)], k, m, shard_size); });
 }
 
-namespace {
-
-// NUMA node of HIP device `dev` (sysfs, through its PCI bus id), or -1.
-int device_numa_node(int dev) {
-    char bus[64] = {};
-    if (hipDeviceGetPCIBusId(bus, int(sizeof bus), dev) != hipSuccess) {
-        (void)hipGetLastError();
-        return -1;
-    }
-    for (char& c : bus) c = char(std::tolower(static_cast<unsigned char>(c)));
-    std::ifstream f(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
-    int node = -1;
-    return f >> node ? node : -1;
-}
-
-// The node all of the context's devices sit on, or -1 (unknown or several).
-int ctx_numa_node(const mxec_ctx* ctx) {
-    int node = -1;
-    for (const auto& d : ctx->c.devs) {
-        const int n = device_numa_node(d->id);
-        if (n < 0 || (node >= 0 && n != node)) return -1;
-        node = n;
-    }
-    return node;
-}
-
-}  // namespace
 
 // Page-locked memory on the NUMA node of the context's GPUs with
 // MXEC_HOST_NUMA=1 (default: wherever the calling thread's policy puts it).  The pages are placed when
@@ -334,28 +362,35 @@ int ctx_numa_node(const mxec_ctx* ctx) {
 // or the policy calls are refused, the allocation is the plain one.  A
 // process may run on every core of a two-socket host, and a DMA from the far
 // socket's memory crosses the socket link.
-void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes) {
-    if (!ctx || bytes == 0) return nullptr;
+namespace {
+void* host_alloc_on(size_t bytes, int node) {
     void* p = nullptr;
-    constexpr unsigned long kMaxNode = 1024;
-    const int node = ctx->c.knobs.host_numa ? ctx_numa_node(ctx) : -1;  // opt-in until measured
-    int old_mode = 0;
-    unsigned long old_mask[kMaxNode / 64] = {}, mask[kMaxNode / 64] = {};
-    bool bound = false;
-    if (node >= 0 && unsigned(node) < kMaxNode &&
-        syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNode + 1, nullptr, 0) == 0) {
-        mask[node / 64] = 1ul << (node % 64);
-        bound = syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, kMaxNode + 1) == 0;
-    }
-    const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocPortable | (bound ? hipHostMallocNumaUser : 0));
-    if (bound) (void)syscall(SYS_set_mempolicy, old_mode, old_mode ? old_mask : nullptr, old_mode ? kMaxNode + 1 : 0);
-    if (e != hipSuccess) {
+    if (host_malloc_on_node(&p, bytes, node, hipHostMallocPortable) != hipSuccess) {
         (void)hipGetLastError();
         set_error(MXEC_E_OOM, "pinned host allocation failed");
         return nullptr;
     }
     pinned_register(p, bytes);
     return p;
+}
+}  // namespace
+
+void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes) {
+    if (!ctx || bytes == 0) return nullptr;
+    return host_alloc_on(bytes, ctx->c.knobs.host_numa ? ctx_numa_node(ctx) : -1);  // opt-in until measured
+}
+
+// On a two-socket host a context spans both nodes and mxec_host_alloc has no
+// one node to pick (ctx_numa_node gives up): a request body meant for device
+// `dev` goes on that device's node, whatever MXEC_HOST_NUMA says, and the
+// host batch calls then deal the object to a device on that node
+// (deal.hpp deal_objects_numa).
+void* mxec_host_alloc_device(mxec_ctx* ctx, int dev, size_t bytes) {
+    if (!ctx || bytes == 0 || dev < 0 || dev >= int(ctx->c.devs.size())) {
+        set_error(MXEC_E_INVALID_ARG, "mxec_host_alloc_device: no such device or zero bytes");
+        return nullptr;
+    }
+    return host_alloc_on(bytes, ctx->c.devs[size_t(dev)]->numa_node);
 }
 
 void mxec_host_free(mxec_ctx* ctx, void* p) {

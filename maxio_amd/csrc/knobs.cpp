@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <strings.h>
 
 namespace mxec {
 
@@ -13,7 +14,8 @@ const char* const kKnobNames[] = {
     "MXEC_DEBUG_AFFINITY",
     "MXEC_HOST_NUMA",            "MXEC_SPIN_WAIT",    "MXEC_RS_TUNE",            "MXEC_RS_MULTI",
     "MXEC_SHA_FORM",             "MXEC_DESC_UPLOAD",  "MXEC_PIPE_PIECE_MB",      "MXEC_GET_WINDOW",
-    "MXEC_PIPE_COPY",            "MXEC_PIPE_SDMA_FLOOR",   "MXEC_GET_VGROUPS",
+    "MXEC_PIPE_COPY",            "MXEC_PIPE_SDMA_FLOOR",   "MXEC_GET_VGROUPS",   "MXEC_GET_SPECULATE",
+    "MXEC_PIPE_LANES",
     "MXEC_GATHER_US",            "MXEC_GATHER_MAX_US", "MXEC_GATHER_IDLE_US",    "MXEC_COMBINE_BELOW",
     "MXEC_COMBINE_STREAMS",      "MXEC_COMBINE_PRIORITY", "MXEC_COMBINE_LOG",    nullptr};
 
@@ -44,11 +46,17 @@ long env_long(const char* name, long dflt) {
     long v = dflt;
     return parse_long(name, &v) ? v : dflt;
 }
+// 0 / 1, and the usual spellings of false / true in any case (a
+// deployment that sets MXEC_HOST_NUMA=true must not get the default).
 bool env_flag(const char* name, bool dflt) {
     const char* e = env(name);
     if (!e) return dflt;
-    if (!std::strcmp(e, "0")) return false;
-    if (!std::strcmp(e, "1")) return true;
+    static const char* const no[] = {"0", "false", "no", "off", nullptr};
+    static const char* const yes[] = {"1", "true", "yes", "on", nullptr};
+    for (int i = 0; no[i]; ++i)
+        if (!strcasecmp(e, no[i])) return false;
+    for (int i = 0; yes[i]; ++i)
+        if (!strcasecmp(e, yes[i])) return true;
     bad_value(name, e, dflt ? "1" : "0");
     return dflt;
 }
@@ -93,6 +101,8 @@ Knobs read_knobs() {
     }
     k.pipe_sdma_floor = std::max(0L, env_long("MXEC_PIPE_SDMA_FLOOR", k.pipe_sdma_floor));
     k.get_vgroups = int(std::max(0L, std::min(8L, env_long("MXEC_GET_VGROUPS", 0))));
+    k.get_speculate = env_flag("MXEC_GET_SPECULATE", true);
+    k.pipe_lanes = int(std::max(1L, std::min(8L, env_long("MXEC_PIPE_LANES", k.pipe_lanes))));
     long window = 0;
     if (parse_long("MXEC_GET_WINDOW", &window)) k.get_window = uint64_t(std::max(1L, window));
     k.gather_us = env_long("MXEC_GATHER_US", k.gather_us);

@@ -34,6 +34,9 @@ struct Knobs {
     long pipe_sdma_floor = 20;     // MXEC_PIPE_SDMA_FLOOR: GB/s (auto's switch point; 0: never waves)
     uint64_t get_window = uint64_t(1) << 30;  // MXEC_GET_WINDOW: bytes of chunks per GET window
     int get_vgroups = 0;           // MXEC_GET_VGROUPS: verification groups of a verified host GET wave (1..8; 0 = per wave)
+    bool get_speculate = true;     // MXEC_GET_SPECULATE: the verified host GET rebuilds each piece as it
+                                   //   arrives, before the verdict (pipeline.cpp spec_piece)
+    int pipe_lanes = 4;            // MXEC_PIPE_LANES: host-batch calls admitted at once per device (1..8)
     long gather_us = 100;          // MXEC_GATHER_US
     long gather_max_us = 2000;     // MXEC_GATHER_MAX_US
     long gather_idle_us = 300;     // MXEC_GATHER_IDLE_US

@@ -20,17 +20,25 @@
 //     after the SHA launch, direct to pinned destinations or via a pinned ring.
 // Results are bit-identical to mxec_encode (same kernels, same planner).
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <system_error>
 #include <thread>
 #include <tuple>
 #include <vector>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "../../include/maxio_ec.h"
 #ifdef MXEC_LAB
-#include <chrono>
 #include <cstdio>
 #include <string>
 #endif
@@ -42,7 +50,7 @@ namespace mxec {
 namespace {
 
 constexpr uint64_t kAlign = 256;
-constexpr uint64_t kPoolCap = uint64_t(96) << 30;     // HBM per wave per device
+constexpr uint64_t kPoolCap = uint64_t(96) << 30;     // pool HBM per device, over the calls in flight
 constexpr uint64_t kGroupBytes = uint64_t(256) << 20;  // input bytes per group
 constexpr uint64_t kRingBuf = uint64_t(64) << 20;      // pinned ring buffer size
 constexpr int kRing = 4;
@@ -115,8 +123,9 @@ struct RecObj {
 
 class PinRing {
 public:
-    int init() {
+    int init(int node = -1) {
         for (int i = 0; i < kRing; ++i) {
+            buf_[i].node = node;
             MXEC_TRY(buf_[i].ensure(kRingBuf));
             MXEC_HIP(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming));
         }
@@ -153,33 +162,157 @@ private:
     int next_ = 0;
 };
 
-// Long-lived per-device resources of the pipeline.
-struct PipeRes {
-    hipStream_t h2d = nullptr, d2h = nullptr;
-    hipStream_t cs[kComputeStreams] = {};
+// Per-call resources of the pipeline (a lane): one host-batch call holds a
+// lane from admission to return, so concurrent calls on one device never
+// share a pool, staging ring, descriptor arena or verdict buffer.  Lanes
+// are kept for later calls (their pools stay allocated: a re-size frees,
+// and hipFree waits for the whole device).
+struct PipeLane {
     PinRing in, out;
     DescArena arena;
     DevBuf pool, digests;
     DevBuf chain_state;  // SHA-256 chain states between pieces (host reconstruct)
     PinnedBuf flags;  // verification verdicts read back (host reconstruct)
     Slot desc_slot;  // unused ring owner for DescWriter (tables come from the arena)
-    // MXEC_PIPE_COPY=auto: calls that start before these instants copy
-    // mxec_host_alloc memory by waves, uploads / downloads (a recent call
-    // measured SDMA slow in that direction).
-    std::chrono::steady_clock::time_point waves_until{}, down_waves_until{};
+    uint64_t admitted = 0;  // pool bytes this call was admitted with
     bool ready = false;
+    // On a context over several NUMA nodes the staging rings and the
+    // verdict buffer live on the device's node.
     int init(const Device& dev) {
         if (ready) return MXEC_OK;
         desc_slot.owner = &dev;
         arena.owner = &dev;
+        const int node = dev.ctx_multi_node ? dev.numa_node : -1;
+        flags.node = node;
+        MXEC_TRY(in.init(node));
+        MXEC_TRY(out.init(node));
+        ready = true;
+        return MXEC_OK;
+    }
+};
+
+// NUMA node of the page at p (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR), or -1.
+int page_node(const void* p) {
+    if (!p) return -1;
+    int node = -1;
+    return syscall(SYS_get_mempolicy, &node, nullptr, 0, const_cast<void*>(p), 3 /* MPOL_F_NODE | MPOL_F_ADDR */) == 0
+               ? node
+               : -1;
+}
+
+// Device of each object of a host batch: o mod D / by bytes (deal_objects);
+// on a context over several NUMA nodes, by the node of each object's first
+// host page (`first[o]`), balanced (deal_objects_numa).
+std::vector<uint32_t> deal_batch(const Ctx& c, const std::vector<uint64_t>& bytes, const std::vector<const void*>& first) {
+    const uint32_t D = uint32_t(c.devs.size());
+    if (D <= 1 || !c.devs[0]->ctx_multi_node) return deal_objects(bytes, D);
+    std::vector<int> dev_node(D), node(bytes.size(), -1);
+    for (uint32_t d = 0; d < D; ++d) dev_node[d] = c.devs[d]->numa_node;
+    for (size_t o = 0; o < bytes.size(); ++o) node[o] = page_node(first[o]);
+    return deal_objects_numa(bytes, node, dev_node);
+}
+
+// The device's pipeline: four streams shared by every call -- H2D, D2H and
+// two compute streams (the process gets 4 hardware queues; more streams
+// would share them and serialise behind each other) -- and the lanes.
+//
+// Concurrent calls (MaxIO serves PUTs and GETs at once
+// on its tokio runtime, main.rs:81): up to MXEC_PIPE_LANES calls hold lanes
+// at once, admitted while the pool bytes of the calls in flight stay within
+// kPoolCap (a lone call is always admitted).  Their waves interleave on the
+// same streams:
+//   * each call that runs SHA-256 chains takes the compute stream fewer
+//     chains use (chain_users), so a PUT's chains and a GET's run side by
+//     side instead of one queueing behind the other on one stream;
+//   * a call that finds another in flight paces its enqueue (pace()): it
+//     queues a piece (or group) only after its own piece kPaceDepth back
+//     is up, so the streams, which run in submission order, carry the calls'
+//     work in the order it can run instead of all of one call's uploads and
+//     then the other's;
+//   * the SDMA watch is off while calls share the copy streams (a bracket
+//     would time the other call's copies too).
+struct PipeHub {
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    hipStream_t cs[kComputeStreams] = {};
+    std::mutex mu;
+    std::condition_variable cv;  // a lane came back
+    std::vector<std::unique_ptr<PipeLane>> lanes;
+    std::vector<PipeLane*> idle;
+    int in_flight = 0;            // calls holding a lane
+    uint64_t admitted_bytes = 0;  // their pool bytes
+    int chain_users[kComputeStreams] = {0, 0};
+    std::atomic<int> calls{0};    // in_flight, readable without the lock
+    bool ready = false;
+    int init(const Device& dev) {
+        if (ready) return MXEC_OK;
         MXEC_TRY(create_streams(dev));
         affinity_tag(h2d, &dev);
         affinity_tag(d2h, &dev);
         for (auto s : cs) affinity_tag(s, &dev);
-        MXEC_TRY(in.init());
-        MXEC_TRY(out.init());
         ready = true;
         return MXEC_OK;
+    }
+    // A lane for a call whose waves need up to `bytes` of pool (capped at
+    // kPoolCap): waits while MXEC_PIPE_LANES calls are in flight, or while
+    // the calls in flight hold pool bytes that would push the total past
+    // kPoolCap.  Returns the lane and the bytes the call may use per wave.
+    int acquire(const Device& dev, uint64_t bytes, PipeLane** out, bool* shared) {
+        const int max_lanes = dev.kn ? dev.kn->pipe_lanes : 4;
+        bytes = std::min(bytes, kPoolCap);
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] {
+            return in_flight == 0 || (in_flight < max_lanes && admitted_bytes + bytes <= kPoolCap);
+        });
+        PipeLane* l = nullptr;
+        if (!idle.empty()) {
+            // the idle lane with the largest pool (fewest re-sizes)
+            size_t best = 0;
+            for (size_t i = 1; i < idle.size(); ++i)
+                if (idle[i]->pool.cap > idle[best]->pool.cap) best = i;
+            l = idle[best];
+            idle.erase(idle.begin() + long(best));
+        } else {
+            lanes.emplace_back(new PipeLane());
+            l = lanes.back().get();
+        }
+        *shared = in_flight > 0;
+        ++in_flight;
+        calls.store(in_flight);
+        admitted_bytes += bytes;
+        l->admitted = bytes;
+        lk.unlock();
+        const int rc = l->init(dev);
+        if (rc != MXEC_OK) release(l);
+        *out = rc == MXEC_OK ? l : nullptr;
+        return rc;
+    }
+    void release(PipeLane* l) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            --in_flight;
+            calls.store(in_flight);
+            admitted_bytes -= l->admitted;
+            l->admitted = 0;
+            idle.push_back(l);
+        }
+        cv.notify_all();
+    }
+    // The compute stream fewer chain-running calls use (ties: `prefer`),
+    // counted until unchain().
+    int chain(int prefer) {
+        std::lock_guard<std::mutex> g(mu);
+        const int c = chain_users[1 - prefer] < chain_users[prefer] ? 1 - prefer : prefer;
+        ++chain_users[c];
+        return c;
+    }
+    void unchain(int c) {
+        std::lock_guard<std::mutex> g(mu);
+        --chain_users[c];
+    }
+    // The compute stream with fewer chain users (ties: `prefer`), not counted.
+    int lighter(int prefer) {
+        std::lock_guard<std::mutex> g(mu);
+        return chain_users[1 - prefer] < chain_users[prefer] ? 1 - prefer : prefer;
     }
     // Plain non-blocking streams.  Lab builds can put the copy streams on a
     // few masked CUs and the compute streams on the rest
@@ -221,7 +354,10 @@ struct PipeRes {
         for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         return MXEC_OK;
     }
-    ~PipeRes() {
+    // Context close (mxec_close, after the device is idle): the lanes'
+    // rings, pools and events, then the streams.
+    ~PipeHub() {
+        lanes.clear();
         for (auto s : cs)
             if (s) {
                 affinity_untag(s);
@@ -232,6 +368,41 @@ struct PipeRes {
         if (h2d) (void)hipStreamDestroy(h2d);
         if (d2h) (void)hipStreamDestroy(d2h);
     }
+};
+
+// A lane of the device's pipeline for the duration of one call.
+class LaneScope {
+public:
+    LaneScope() = default;
+    LaneScope(const LaneScope&) = delete;
+    LaneScope& operator=(const LaneScope&) = delete;
+    ~LaneScope() {
+        if (lane_) hub_->release(lane_);
+    }
+    int open(Device& dev, uint64_t bytes) {
+        {
+            std::lock_guard<std::mutex> g(dev.pipe_mu);
+            if (!dev.pipe) dev.pipe = std::make_shared<PipeHub>();
+            keep_ = dev.pipe;
+        }
+        hub_ = static_cast<PipeHub*>(keep_.get());
+        {
+            std::lock_guard<std::mutex> g(dev.pipe_mu);  // stream creation, once
+            MXEC_TRY(hub_->init(dev));
+        }
+        bool shared = false;
+        MXEC_TRY(hub_->acquire(dev, bytes, &lane_, &shared));
+        ++dev.pipe_calls;
+        if (shared) ++dev.pipe_calls_shared;
+        return MXEC_OK;
+    }
+    PipeHub& hub() { return *hub_; }
+    PipeLane& lane() { return *lane_; }
+
+private:
+    std::shared_ptr<void> keep_;
+    PipeHub* hub_ = nullptr;
+    PipeLane* lane_ = nullptr;
 };
 
 #ifdef MXEC_LAB
@@ -296,11 +467,12 @@ struct PipeTrace {
 
 class DevicePipeline {
 public:
-    DevicePipeline(Device& d, PipeRes& r)
-        : d_(d), h2d_(r.h2d), d2h_(r.d2h), cs_(r.cs), in_(r.in), out_(r.out), arena_(r.arena),
-          pool_(r.pool), scratch_(r.digests), state_(r.chain_state), flags_(r.flags), slot_(r.desc_slot),
-          res_(r) {}
+    DevicePipeline(Device& d, PipeHub& h, PipeLane& l)
+        : d_(d), h2d_(h.h2d), d2h_(h.d2h), cs_(h.cs), in_(l.in), out_(l.out), arena_(l.arena),
+          pool_(l.pool), scratch_(l.digests), state_(l.chain_state), flags_(l.flags), slot_(l.desc_slot),
+          hub_(h), cap_(std::max<uint64_t>(l.admitted, 1)) {}
     ~DevicePipeline() {
+        if (chain_ >= 0) hub_.unchain(chain_);
         for (auto e : events_) (void)hipEventDestroy(e);
     }
 
@@ -319,7 +491,7 @@ public:
         while (o < objs.size()) {  // waves that fit the pool
             uint64_t need = 0, desc = 1 << 20;
             size_t e = o;
-            while (e < objs.size() && (e == o || need + objs[e].bytes() <= kPoolCap)) {
+            while (e < objs.size() && (e == o || need + objs[e].bytes() <= cap_)) {
                 objs[e].pool_off = need;
                 need += objs[e].bytes();
                 desc += uint64_t(objs[e].k + objs[e].m) * 48 + 256;
@@ -340,7 +512,7 @@ public:
         while (o < objs.size()) {
             uint64_t need = 0, desc = 1 << 20;
             size_t e = o;
-            while (e < objs.size() && (e == o || need + objs[e].bytes() <= kPoolCap)) {
+            while (e < objs.size() && (e == o || need + objs[e].bytes() <= cap_)) {
                 objs[e].pool_off = need;
                 need += objs[e].bytes();
                 // pointer / length / digest-index tables, the SHA tables and one
@@ -393,19 +565,27 @@ private:
     bool watch_staged_ = false, dwatch_staged_ = false;
     uint64_t watch_bytes_ = 0, dwatch_bytes_ = 0;    // SDMA bytes issued in the open brackets
     uint64_t watch_copies_ = 0, dwatch_copies_ = 0;  // and the DMAs (2D: rows) that moved them
+    static int64_t now_ns() {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
     void start_copy_mode() {
         const int mode = d_.kn ? d_.kn->pipe_copy : 0;
-        const auto now = std::chrono::steady_clock::now();
-        waves_now_ = mode == 1 || (mode == 2 && now < res_.waves_until);
-        down_waves_ = mode == 1 || (mode == 2 && now < res_.down_waves_until);
+        const int64_t now = now_ns();
+        waves_now_ = mode == 1 || (mode == 2 && now < d_.waves_up_until_ns.load());
+        down_waves_ = mode == 1 || (mode == 2 && now < d_.waves_down_until_ns.load());
 #ifdef MXEC_LAB
         const char* dw = getenv("MXEC_PIPE_DOWN_WAVES");
         down_waves_ = down_waves_ || (dw && *dw == '1');
 #endif
     }
+    // Not while another call shares the copy streams: its copies would land
+    // inside this call's brackets.
     bool watching(bool down = false) const {
-        return d_.kn && d_.kn->pipe_copy == 2 && d_.kn->pipe_sdma_floor > 0 && !(down ? down_waves_ : waves_now_);
+        return d_.kn && d_.kn->pipe_copy == 2 && d_.kn->pipe_sdma_floor > 0 && !(down ? down_waves_ : waves_now_) &&
+               !shared_now();
     }
+    bool shared_now() const { return hub_.calls.load() > 1; }
     int new_timed_event(hipEvent_t* e) {
         MXEC_HIP(hipEventCreate(e));
         events_.push_back(*e);
@@ -484,15 +664,14 @@ private:
         // unaffected by the free), so they are judged against twice the floor.
         const double floor = double(d_.kn ? d_.kn->pipe_sdma_floor : 20) * (k.down ? 2.0 : 1.0);
         const bool slow = gbps < floor;
-        const auto hold = std::chrono::steady_clock::now() +
-                          std::chrono::milliseconds(k.down ? kDownWavesHoldMs : kWavesHoldMs);
+        const int64_t hold = now_ns() + int64_t(k.down ? kDownWavesHoldMs : kWavesHoldMs) * 1000000;
         if (k.down) {
             ++d_.sdma_down_probes;
             d_.sdma_down_last_mbps = uint64_t(gbps * 1e3);
             if (!down_waves_ && slow) {
                 ++d_.sdma_down_slow_verdicts;
                 down_waves_ = true;  // the rest of this call's downloads
-                res_.down_waves_until = hold;
+                d_.waves_down_until_ns = hold;
             }
         } else {
             ++d_.sdma_probes;
@@ -500,10 +679,9 @@ private:
             if (!waves_now_ && slow) {
                 ++d_.sdma_slow_verdicts;
                 waves_now_ = true;  // the rest of this call's uploads
-                res_.waves_until = hold;
+                d_.waves_up_until_ns = hold;
             }
         }
-        d_.sdma_slow = waves_now_ || down_waves_;
         return MXEC_OK;
     }
     // End of a call: judge what is left (its copies are done), for the
@@ -516,16 +694,32 @@ private:
     }
 
     // One wave of a host reconstruct batch (try_reconstruct_data_chunk,
-    // chunk_reader.rs:157-226, per object): the present shards go up group
-    // by group (coalesced, direct from pinned memory), their digests are
-    // checked on the device against the expected ones when given (one
-    // SHA-256 launch for the whole wave once every group is up: a chain's
-    // latency does not depend on how many share the launch; a mismatch is an
-    // erasure, :176-196), each group is rebuilt (one grouped launch,
-    // run_rs_mixed) as soon as it is up (and verified), and its rebuilt
-    // shards go down while later groups still upload.  An object short of k
-    // shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT and none of its buffers is
-    // written.
+    // chunk_reader.rs:157-226, per object).
+    //
+    // Verified waves (expected digests given) run piece-major when their
+    // messages fit the lag quad form: piece p of every present shard goes up
+    // and is hashed with the chains carried in device state slots, so every
+    // chain starts after the first piece (verify_enqueue), and -- with
+    // MXEC_GET_SPECULATE (default) -- piece p of every missing shard is
+    // decoded from the first k present shards as soon as piece p is up, on
+    // the assumption that they verify, and goes down at once (spec_piece).
+    // The verdict then only confirms: an object whose shards all verified is
+    // done; one with a mismatch is decoded again with the corrected mask and
+    // its shards overwritten (a mismatch is an erasure, :176-196); one left
+    // short of k shards fails with MXEC_E_TOO_FEW_SHARDS_PRESENT -- its
+    // present shards untouched, its missing shards' buffers undefined (the
+    // reference returns Err and no data, :203-206).  Without speculation the
+    // rebuild waits for the verdict (nothing is written to a failing
+    // object's buffers), and a large wave runs as a few verification groups
+    // (verify_cuts) so that group j's rebuild and download overlap group
+    // j + 1's upload and chains; with it the downloads already overlap
+    // everything and the wave is one group.
+    //
+    // Other waves: the present shards go up group by group (coalesced,
+    // direct from pinned memory), are verified by one SHA-256 launch once
+    // all are up when digests are given, each group is rebuilt (one grouped
+    // launch, run_rs_mixed) as soon as it is up (and verified), and its
+    // rebuilt shards go down while later groups still upload.
     int rec_wave(std::vector<RecObj>& objs, size_t o0, size_t o1, bool data_only) {
         PTRACE(start(h2d_));
         uint64_t msgs = 0;
@@ -544,15 +738,8 @@ private:
             ok = static_cast<uint8_t*>(scratch_.p);
             exp = ok + fo;
         }
-        // Under MXEC_PIPE_COPY=auto a verified wave's last verification
-        // group's rebuilt shards go down by waves (they leave after the last
-        // verdict, alone on the link: waves move them as fast as a healthy
-        // SDMA and keep that rate when SDMA downloads run slow after a large
-        // HBM free), earlier groups' by SDMA, unbracketed; an
-        // RS-only wave's by SDMA, each group's bracketed (dwatch_open).
         const bool down_before = down_waves_;
         const bool auto_copy = d_.kn && d_.kn->pipe_copy == 2;
-        if (verify && auto_copy) down_waves_ = true;
         dwatch_off_ = verify;  // a verified wave's downloads are not bracketed
         uint64_t vmsgs = 0;  // present shards to verify
         for (size_t o = o0; o < o1; ++o)
@@ -567,20 +754,16 @@ private:
                 }
         const uint64_t P = piece_bytes(up_bytes, longest_msg);
         if (verify && P && vmsgs && vmsgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256)) {
-            // Piece-major upload + verification (the PUT wave's scheme, see
-            // wave_pieces): piece p of every present shard goes up and is
-            // hashed, chains carried in state slots, so every chain starts
-            // after the first piece instead of after the whole upload; the
-            // verdicts come back after the last piece, then the rebuild
-            // (nothing is written to the caller's buffers before).  A large
-            // wave runs as a few verification groups (verify_cuts): group
-            // j + 1's pieces go up and hash (on the other compute stream)
-            // while the host waits for group j's verdicts, rebuilds it and
-            // sends its shards down.
+            const bool shared = shared_now();
+            const bool spec = !d_.kn || d_.kn->get_speculate;
             uint64_t down_bytes = 0;
             for (size_t o = o0; o < o1; ++o)
                 for (int i = 0; i < objs[o].k + objs[o].m; ++i) down_bytes += objs[o].present[i] ? 0 : objs[o].len[i];
-            const std::vector<size_t> cut = verify_cuts(objs, o0, o1, up_bytes, longest_msg, down_bytes);
+            // One group when speculating (the downloads overlap the chains
+            // already) or when another call shares the device (one compute
+            // stream each: a second group's chains would queue behind the
+            // first's on it).
+            const std::vector<size_t> cut = verify_cuts(objs, o0, o1, up_bytes, longest_msg, down_bytes, spec || shared);
             MXEC_TRY(state_.ensure(msgs * 32));
             MXEC_TRY(flags_.ensure(msgs));
             std::vector<uint64_t> mbase(cut.size(), 0);
@@ -589,53 +772,96 @@ private:
                 for (size_t o = cut[j - 1]; o < cut[j]; ++o) mbase[j] += uint64_t(objs[o].k + objs[o].m);
             }
             const size_t G = cut.size() - 1;
-            // auto: a wave verified as one group uploads by waves too (one
-            // copy launch per piece instead of a DMA per piece of every
+            if (chain_ < 0) chain_ = hub_.chain(0);
+            // auto: a chain-bound wave verified as one group uploads by waves
+            // (one copy launch per piece instead of a DMA per piece of every
             // shard: 128 x 4+2 x 10 MiB 0.240 s against 0.256 by SDMA, 256
-            // objects 0.363 against 0.371); grouped waves keep SDMA uploads
-            // (512: 0.590 against 0.679 by waves, whose copies beside the
-            // earlier groups' downloads and chains slow both;
-            // profiles/r5/copy_engine/verified_uploads_r5z.jsonl).
+            // objects 0.363 against 0.371); an upload-bound wave keeps SDMA
+            // uploads (512: 0.590 against 0.679 by waves, whose copies beside
+            // the downloads and chains slow both;
+            // profiles/r5/copy_engine/verified_uploads_r5z.jsonl), and so does
+            // a call that shares the device.
             const bool up_before = waves_now_;
-            if (auto_copy && G == 1) waves_now_ = true;
+            const bool up_override = auto_copy && G == 1 && piece_ramp_ && !shared;
+            if (up_override) waves_now_ = true;
+            // Without speculation the last group's rebuilt shards (on the
+            // critical path, alone on the link) go down by waves, earlier
+            // groups' by SDMA beside the later groups' uploads and chains
+            // (wave copies there slow the chains: 0.64 s against 0.59 at 512
+            // objects, G = 2).  Speculative downloads run beside the chains,
+            // so they keep SDMA.
             std::vector<hipEvent_t> verdict(G, nullptr);
             auto enqueue = [&](size_t j) {
-                return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], P, cs_[j & 1], &verdict[j]);
+                return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], P, cs_[(chain_ + int(j)) & 1],
+                                      &verdict[j], spec, data_only);
             };
             MXEC_TRY(enqueue(0));
             for (size_t j = 0; j < G; ++j) {
                 if (j + 1 < G) MXEC_TRY(enqueue(j + 1));
-                MXEC_TRY(verify_collect(objs, cut[j], cut[j + 1], mbase[j], verdict[j]));
+                std::vector<size_t> changed;
+                MXEC_TRY(verify_collect(objs, cut[j], cut[j + 1], mbase[j], verdict[j], &changed));
                 PTRACE(now("verified"));
-                // auto: the last group's shards (on the critical path, alone
-                // on the link) by waves; earlier groups' by SDMA beside the
-                // later groups' uploads and chains (wave copies there slow
-                // the chains: 0.64 s against 0.59 at 512 objects, G = 2).
-                if (auto_copy) down_waves_ = down_before || j + 1 == G;
-                for (const auto& q : object_groups(objs, cut[j], cut[j + 1]))
-                    MXEC_TRY(rebuild_down(objs, q.first, q.second, cs_[j & 1], nullptr, data_only));
+                if (spec) {
+                    MXEC_TRY(confirm(objs, cut[j], cut[j + 1], changed, data_only));
+                    // The objects with a mismatch, decoded again with their
+                    // verified masks on the D2H stream: behind the
+                    // speculative downloads, which read the slots this
+                    // decode rewrites.
+                    if (!changed.empty()) {
+                        d_.spec_redos += changed.size();
+                        MXEC_TRY(rebuild_list(objs, changed, d2h_, nullptr, data_only));
+                    }
+                } else {
+                    if (auto_copy && !shared) down_waves_ = down_before || j + 1 == G;
+                    for (const auto& q : object_groups(objs, cut[j], cut[j + 1]))
+                        MXEC_TRY(rebuild_range(objs, q.first, q.second, cs_[(chain_ + int(j)) & 1], nullptr, data_only));
+                }
             }
             d_.verify_groups += G;
             d_.verify_waves += 1;
-            waves_now_ = up_before;
+            if (up_override) waves_now_ = up_before;  // only the override is undone
         } else {
             const auto groups = object_groups(objs, o0, o1);
+            if (verify && chain_ < 0) chain_ = hub_.chain(0);
+            hipStream_t cs = cs_[verify ? chain_ : hub_.lighter(0)];
             std::vector<hipEvent_t> up;  // per group: its upload is done
-            MXEC_TRY(upload_and_verify(objs, o0, o1, groups, ok, exp, verify, cs_[0], &up));
+            MXEC_TRY(upload_and_verify(objs, o0, o1, groups, ok, exp, verify, cs, &up));
             // Per group, rebuild once it is up (without verification, as soon
             // as it is up), then its shards down.
             for (size_t q = 0; q < groups.size(); ++q)
-                MXEC_TRY(rebuild_down(objs, groups[q].first, groups[q].second, cs_[0], verify ? nullptr : up[q],
-                                      data_only));
+                MXEC_TRY(rebuild_range(objs, groups[q].first, groups[q].second, cs, verify ? nullptr : up[q], data_only));
         }
         MXEC_TRY(issue_down());
         PTRACE(mark("d2h", d2h_));
         PTRACE(now("down_queued"));
         const int frc = flush();
         PTRACE(report("rec_wave"));
-        if (verify) down_waves_ = down_before;
+        down_waves_ = down_before;
         dwatch_off_ = false;
         return frc;
+    }
+
+    // Objects [o0, o1) of a speculatively rebuilt group whose present masks
+    // the verdict left as they were (all but `changed`): their rebuilt
+    // shards are already on their way down; status and present flags.
+    int confirm(std::vector<RecObj>& objs, size_t o0, size_t o1, const std::vector<size_t>& changed, bool data_only) {
+        size_t c = 0;
+        for (size_t o = o0; o < o1; ++o) {
+            if (c < changed.size() && changed[c] == o) {
+                ++c;
+                continue;
+            }
+            // decode_plan's rule (gf256.cpp): k present shards make a plan,
+            // and its missing shards are every absent one (data_only: every
+            // absent data shard)
+            RecObj& h = objs[o];
+            int np = 0;
+            for (int i = 0; i < h.k + h.m; ++i) np += h.present[i] ? 1 : 0;
+            *h.status = np >= h.k ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
+            if (np >= h.k)
+                for (int i = 0; i < h.k + (data_only ? 0 : h.m); ++i) h.present[i] = 1;
+        }
+        return MXEC_OK;
     }
 
     // Consecutive objects up to kGroupBytes of present input.
@@ -669,9 +895,11 @@ private:
     // no count gained (0.637-0.690: wave copies beside the later groups'
     // SHA-256 chains slow the chains).  Round 5's first measurement (one
     // 0.655, two 0.818) predates the one-copy expected-digest upload.
+    // `one`: one group unless MXEC_GET_VGROUPS forces a count (rec_wave).
     std::vector<size_t> verify_cuts(const std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t up_bytes,
-                                    uint64_t longest, uint64_t down_bytes) const {
+                                    uint64_t longest, uint64_t down_bytes, bool one) const {
         int G = d_.kn ? int(d_.kn->get_vgroups) : 1;
+        if (G == 0 && one) G = 1;
         if (G == 0) {
             // Per wave: the G that minimises max(T, (G-1)/G T + C) + D/G --
             // the upload T (~50 GB/s), the chain C of the longest message,
@@ -732,33 +960,42 @@ private:
     }
     std::vector<uint8_t> exp_host_;  // staging source of upload_expected (consumed by upload's ring copy)
 
-    // Objects [q0, q1) of a wave, their present shards up (or verified):
+    // Objects `which` of a wave, their present shards up (or verified):
     // rebuild each object's missing shards from its decode plan (one grouped
     // launch, run_rs_mixed, on cs after `up` if given), then send them down
     // to the caller's buffers and mark them present.  An object short of k
     // shards gets MXEC_E_TOO_FEW_SHARDS_PRESENT and none of its buffers is
-    // written.
-    int rebuild_down(std::vector<RecObj>& objs, size_t q0, size_t q1, hipStream_t cs, hipEvent_t up, bool data_only) {
+    // written here.
+    int rebuild_range(std::vector<RecObj>& objs, size_t q0, size_t q1, hipStream_t cs, hipEvent_t up, bool data_only) {
+        std::vector<size_t> which(q1 - q0);
+        for (size_t o = q0; o < q1; ++o) which[o - q0] = o;
+        return rebuild_list(objs, which, cs, up, data_only);
+    }
+    int rebuild_list(std::vector<RecObj>& objs, const std::vector<size_t>& which, hipStream_t cs, hipEvent_t up,
+                     bool data_only) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        if (cs == d2h_) MXEC_TRY(issue_down());  // wave copy blocks queued for d2h go before this launch
         if (up) MXEC_HIP(hipStreamWaitEvent(cs, up, 0));
         {
-            std::vector<std::shared_ptr<const DecodePlan>> plans(q1 - q0);
-            std::vector<uint32_t> offs(q1 - q0);
+            const size_t n = which.size();
+            std::vector<std::shared_ptr<const DecodePlan>> plans(n);
+            std::vector<uint32_t> offs(n);
             std::vector<const uint8_t*> in;
             std::vector<uint8_t*> out;
             std::vector<uint64_t> il, ol;
             std::map<int, std::vector<RsMixedObject>> rs_groups;
             auto collect = [&]() -> int {
-                for (size_t o = q0; o < q1; ++o)
-                    MXEC_TRY(decode_plan(d_, objs[o].k, objs[o].m, objs[o].present, data_only, &plans[o - q0],
-                                         &offs[o - q0]));
+                for (size_t t = 0; t < n; ++t) {
+                    const RecObj& h = objs[which[t]];
+                    MXEC_TRY(decode_plan(d_, h.k, h.m, h.present, data_only, &plans[t], &offs[t]));
+                }
                 return MXEC_OK;
             };
             auto launch = [&]() -> int {
                 size_t n_in = 0, n_out = 0;
-                for (size_t t = 0; t < plans.size(); ++t)
+                for (size_t t = 0; t < n; ++t)
                     if (plans[t] && !plans[t]->missing.empty()) {
-                        n_in += size_t(objs[q0 + t].k);
+                        n_in += size_t(objs[which[t]].k);
                         n_out += plans[t]->missing.size();
                     }
                 in.assign(n_in, nullptr);
@@ -767,9 +1004,9 @@ private:
                 ol.assign(n_out, 0);
                 rs_groups.clear();
                 size_t pi = 0, po = 0;
-                for (size_t t = 0; t < plans.size(); ++t) {
+                for (size_t t = 0; t < n; ++t) {
                     if (!plans[t] || plans[t]->missing.empty()) continue;
-                    const RecObj& h = objs[q0 + t];
+                    const RecObj& h = objs[which[t]];
                     const DecodePlan& p = *plans[t];
                     const int r = int(p.missing.size());
                     uint8_t* ob = base + h.pool_off;
@@ -789,17 +1026,19 @@ private:
                 return run_rs_mixed(d_, slot_, cs, rs_groups, &arena_);
             };
             MXEC_TRY(with_stable_coef(d_, cs, collect, launch));
-            hipEvent_t rs_done;
-            MXEC_TRY(new_event(&rs_done));
-            MXEC_HIP(hipEventRecord(rs_done, cs));
             PTRACE(mark("rs", cs));
             PTRACE(now("rs_queued"));
             MXEC_TRY(issue_down());
-            MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
+            if (cs != d2h_) {
+                hipEvent_t rs_done;
+                MXEC_TRY(new_event(&rs_done));
+                MXEC_HIP(hipEventRecord(rs_done, cs));
+                MXEC_HIP(hipStreamWaitEvent(d2h_, rs_done, 0));
+            }
             MXEC_TRY(dwatch_open());
-            for (size_t o = q0; o < q1; ++o) {
-                RecObj& h = objs[o];
-                const auto& p = plans[o - q0];
+            for (size_t t = 0; t < n; ++t) {
+                RecObj& h = objs[which[t]];
+                const auto& p = plans[t];
                 *h.status = p ? MXEC_OK : MXEC_E_TOO_FEW_SHARDS_PRESENT;
                 if (!p) continue;
                 for (int e : p->missing) {
@@ -814,6 +1053,89 @@ private:
         return MXEC_OK;
     }
 
+    // Speculative rebuild of piece [off, off + pw) of objects [o0, o1)
+    // (MXEC_GET_SPECULATE): once the piece of every present shard is up
+    // (`up`), the same piece of each object's missing shards is decoded from
+    // its first k present shards -- RS is bytewise, so a piece of the output
+    // comes from the same piece of the inputs, as in the PUT's piece-major
+    // encode -- and goes down to the caller's buffers.  Launch and downloads
+    // both on the D2H stream, so the downloads follow the decode in order.
+    // An object short of k present shards is skipped (it fails anyway).
+    int spec_piece(std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t off, uint64_t pw, hipEvent_t up,
+                   bool data_only) {
+        uint8_t* base = static_cast<uint8_t*>(pool_.p);
+        const size_t n = o1 - o0;
+        std::vector<std::shared_ptr<const DecodePlan>> plans(n);
+        std::vector<uint32_t> offs(n);
+        std::vector<const uint8_t*> in;
+        std::vector<uint8_t*> out;
+        std::vector<uint64_t> il, ol;
+        std::map<int, std::vector<RsMixedObject>> rs_groups;
+        auto collect = [&]() -> int {
+            for (size_t t = 0; t < n; ++t) {
+                const RecObj& h = objs[o0 + t];
+                plans[t].reset();
+                if (h.S > off) MXEC_TRY(decode_plan(d_, h.k, h.m, h.present, data_only, &plans[t], &offs[t]));
+            }
+            return MXEC_OK;
+        };
+        auto launch = [&]() -> int {
+            size_t n_in = 0, n_out = 0;
+            for (size_t t = 0; t < n; ++t)
+                if (plans[t] && !plans[t]->missing.empty()) {
+                    n_in += size_t(objs[o0 + t].k);
+                    n_out += plans[t]->missing.size();
+                }
+            in.assign(n_in, nullptr);
+            out.assign(n_out, nullptr);
+            il.assign(n_in, 0);
+            ol.assign(n_out, 0);
+            rs_groups.clear();
+            size_t pi = 0, po = 0;
+            for (size_t t = 0; t < n; ++t) {
+                if (!plans[t] || plans[t]->missing.empty()) continue;
+                const RecObj& h = objs[o0 + t];
+                const DecodePlan& p = *plans[t];
+                const int r = int(p.missing.size());
+                uint8_t* ob = base + h.pool_off + off;
+                for (int v = 0; v < h.k; ++v) {
+                    const uint64_t L = h.len[p.valid[size_t(v)]];
+                    in[pi + v] = ob + uint64_t(p.valid[size_t(v)]) * h.slot();
+                    il[pi + v] = L > off ? std::min(pw, L - off) : 0;
+                }
+                for (int e = 0; e < r; ++e) {
+                    const uint64_t L = h.len[p.missing[size_t(e)]];
+                    out[po + e] = ob + uint64_t(p.missing[size_t(e)]) * h.slot();
+                    ol[po + e] = L > off ? std::min(pw, L - off) : 0;
+                }
+                rs_groups[r].push_back(RsMixedObject{h.k, std::min(pw, h.S - off),
+                                                     RsObject{&in[pi], &il[pi], &out[po], &ol[po], offs[t]}});
+                pi += size_t(h.k);
+                po += size_t(r);
+            }
+            return rs_groups.empty() ? MXEC_OK : run_rs_mixed(d_, slot_, d2h_, rs_groups, &arena_);
+        };
+        MXEC_TRY(flush_down());
+        MXEC_TRY(issue_down());  // wave copy blocks queued earlier go before the wait
+        MXEC_HIP(hipStreamWaitEvent(d2h_, up, 0));
+        MXEC_TRY(with_stable_coef(d_, d2h_, collect, launch));
+        bool any = false;
+        for (size_t t = 0; t < n; ++t) {
+            if (!plans[t]) continue;
+            const RecObj& h = objs[o0 + t];
+            for (int e : plans[t]->missing) {
+                const uint64_t L = h.len[e];
+                if (off >= L) continue;
+                MXEC_TRY(queue_down(h.shards[e] + off, base + h.pool_off + uint64_t(e) * h.slot() + off,
+                                    std::min(pw, L - off)));
+                any = true;
+            }
+        }
+        MXEC_TRY(flush_down());
+        if (any) ++d_.spec_pieces;
+        return MXEC_OK;
+    }
+
     // Piece-major upload of every present shard of objects [o0, o1) (and the
     // expected digests), each piece of the shards to verify hashed on cs as
     // soon as it is up with the chains carried in device state slots
@@ -824,8 +1146,10 @@ private:
     // copies are as large as the wave's, whatever its share of the upload).
     // Above 1 MiB the same piece of an object's adjacent present shards goes
     // up as one 2D copy, as in the PUT's upload-bound waves.
+    // spec: each piece's missing shards are also decoded and sent down as
+    // soon as the piece is up (spec_piece).
     int verify_enqueue(std::vector<RecObj>& objs, size_t o0, size_t o1, uint8_t* ok, uint8_t* exp, uint64_t mb,
-                       uint64_t P, hipStream_t cs, hipEvent_t* verdict) {
+                       uint64_t P, hipStream_t cs, hipEvent_t* verdict, bool spec, bool data_only) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         uint32_t* state = static_cast<uint32_t*>(state_.p);
         uint64_t longest = 0, gm = 0;
@@ -878,7 +1202,10 @@ private:
             if (!sp.empty())
                 MXEC_TRY(run_sha_pieces(d_, slot_, cs, sp, sl, ss, st, state, pc > 0, nullptr, &arena_, exp, ok));
             PTRACE(mark("sha", cs));
+            if (spec) MXEC_TRY(spec_piece(objs, o0, o1, off, pw, up, data_only));
+            MXEC_TRY(pace(up));
         }
+        paced_.clear();
         PTRACE(now("pieces_queued"));
         MXEC_HIP(hipMemcpyAsync(static_cast<uint8_t*>(flags_.p) + mb, ok + mb, gm, hipMemcpyDeviceToHost, cs));
         MXEC_TRY(new_event(verdict));
@@ -888,14 +1215,21 @@ private:
 
     // Waits for objects [o0, o1)'s verdicts (verify_enqueue): a mismatch
     // becomes an erasure (chunk_reader.rs:176-196).
-    int verify_collect(std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t mb, hipEvent_t verdict) {
+    // The objects whose masks changed go to *changed (ascending).
+    int verify_collect(std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t mb, hipEvent_t verdict,
+                       std::vector<size_t>* changed) {
         MXEC_HIP(hipEventSynchronize(verdict));
         const auto* okh = static_cast<const uint8_t*>(flags_.p);
         uint64_t g = mb;
         for (size_t o = o0; o < o1; ++o) {
             RecObj& h = objs[o];
+            bool c = false;
             for (int i = 0; i < h.k + h.m; ++i, ++g)
-                if (h.expected && h.present[i] && !okh[g]) h.present[i] = 0;
+                if (h.expected && h.present[i] && !okh[g]) {
+                    h.present[i] = 0;
+                    c = true;
+                }
+            if (c) changed->push_back(o);
         }
         return MXEC_OK;
     }
@@ -928,7 +1262,9 @@ private:
             MXEC_TRY(issue_up());
             MXEC_HIP(hipEventRecord(up[q], h2d_));
             MXEC_TRY(watch_close());
+            MXEC_TRY(pace(up[q]));
         }
+        paced_.clear();
         if (verify) {
             std::vector<const uint8_t*> sp;
             std::vector<uint64_t> sl, idx;
@@ -949,7 +1285,7 @@ private:
                 MXEC_TRY(run_sha(d_, slot_, cs, sp, sl, nullptr, exp, ok, &idx, &arena_));
                 MXEC_TRY(flags_.ensure(sp.size()));
                 MXEC_HIP(hipMemcpyAsync(flags_.p, ok, sp.size(), hipMemcpyDeviceToHost, cs));
-                MXEC_HIP(hipStreamSynchronize(cs));
+                MXEC_TRY(sync_point(cs));  // not the stream: another call's work may follow on it
                 const auto* okh = static_cast<const uint8_t*>(flags_.p);
                 for (size_t t = 0; t < who.size(); ++t)
                     if (!okh[t]) objs[who[t].first].present[who[t].second] = 0;
@@ -978,13 +1314,46 @@ private:
     DevBuf& state_;    // chain states of a piece-major verification
     PinnedBuf& flags_;
     Slot& slot_;
-    PipeRes& res_;
+    PipeHub& hub_;
+    const uint64_t cap_;  // pool bytes per wave (the lane's admission)
+    int chain_ = -1;      // the compute stream this call's SHA-256 chains run on (PipeHub::chain)
     std::vector<Pending> pend_;
     std::vector<hipEvent_t> events_;
 
     int new_event(hipEvent_t* e) {
         MXEC_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
         events_.push_back(*e);
+        return MXEC_OK;
+    }
+    // Wait for this call's work queued on `s` so far (an event, not the
+    // stream: calls share the streams, and a stream sync would wait for the
+    // other calls' later work too).
+    int sync_point(hipStream_t s) {
+        hipEvent_t e;
+        MXEC_TRY(new_event(&e));
+        MXEC_HIP(hipEventRecord(e, s));
+        MXEC_HIP(hipEventSynchronize(e));
+        return MXEC_OK;
+    }
+    // While another call shares the device, queue a piece (or group) only
+    // once this call's piece kPaceDepth back is up: the shared streams run
+    // in submission order, and a call that queued all its pieces at once
+    // would put the other call's uploads (and what waits on them) behind
+    // all of its own.  A lone call never waits here.
+    static constexpr size_t kPaceDepth = 2;
+    std::deque<hipEvent_t> paced_;
+    int pace(hipEvent_t up) {
+        paced_.push_back(up);
+        while (paced_.size() > kPaceDepth) {
+            hipEvent_t e = paced_.front();
+            paced_.pop_front();
+            if (!shared_now()) continue;
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipSuccess) continue;
+            (void)hipGetLastError();
+            ++d_.pace_waits;
+            MXEC_HIP(hipEventSynchronize(e));
+        }
         return MXEC_OK;
     }
 
@@ -1211,7 +1580,7 @@ private:
 
     int flush() {
         MXEC_TRY(issue_down());
-        MXEC_HIP(hipStreamSynchronize(d2h_));
+        MXEC_TRY(sync_point(d2h_));
         for (auto& p : pend_) std::memcpy(p.dst, out_.ptr(p.ring), p.len);
         pend_.clear();
         out_.release_all();
@@ -1288,7 +1657,13 @@ private:
         uint32_t* state = reinterpret_cast<uint32_t*>(digests + nm * 32);
         const PieceGrid grid(P, piece_ramp_);
         const uint64_t npieces = grid.count(longest);
-        hipStream_t rs_s = cs_[0], sha_s = cs_[1];
+        // The chains on the compute stream fewer other calls' chains use, RS
+        // on the other one -- or, when another call shares the device, on
+        // the chains' own stream (ahead of each piece's hash), so that no
+        // piece of this call waits behind the other call's chains.
+        if (nm && chain_ < 0) chain_ = hub_.chain(1);
+        const int sc = nm ? chain_ : hub_.lighter(1);
+        hipStream_t sha_s = cs_[sc], rs_s = shared_now() && nm ? sha_s : cs_[1 - sc];
         hipEvent_t sha_done = nullptr;
         struct TwoD {  // 2D piece copies for this wave's SDMA copies (queue_up)
             bool& f;
@@ -1390,7 +1765,9 @@ private:
             MXEC_TRY(flush_down());
             PTRACE(mark("down", d2h_));
             PTRACE(now("piece_queued"));
+            MXEC_TRY(pace(up));
         }
+        paced_.clear();
         if (nm) {
             MXEC_TRY(new_event(&sha_done));
             MXEC_HIP(hipEventRecord(sha_done, sha_s));
@@ -1446,7 +1823,32 @@ private:
         // host only waits on the input ring (an H2D copy), so uploads stream
         // at PCIe rate while RS runs behind them.
         std::vector<hipEvent_t> done(groups.size());
-        hipStream_t rs_s = cs_[0], sha_s = cs_[1];
+        bool any_dig = false;
+        for (size_t o = o0; o < o1; ++o) any_dig = any_dig || objs[o].dig;
+        if (any_dig && chain_ < 0) chain_ = hub_.chain(1);
+        const int sc = any_dig ? chain_ : hub_.lighter(1);
+        hipStream_t rs_s = cs_[1 - sc], sha_s = cs_[sc];
+        // Each group's parity down: group by group after phase 1 (a lone
+        // call queues all of phase 1 at once); while another call shares the
+        // device, right behind the group's RS, since the paced phase 1 would
+        // hold phase 3 back until the last uploads were queued.
+        const bool down_early = shared_now();
+        size_t downed = 0;
+        auto down_group = [&](size_t g) -> int {
+            MXEC_TRY(issue_down());
+            MXEC_HIP(hipStreamWaitEvent(d2h_, done[g], 0));
+            for (size_t o = groups[g].first; o < groups[g].second; ++o) {
+                const HostObj& h = objs[o];
+                uint8_t* ob = base + h.pool_off;
+                for (int i = 0; i < h.m; ++i) {
+                    MXEC_TRY(queue_down(h.parity[i], ob + uint64_t(h.k + i) * h.slot(), h.S));
+                    if (h.S != h.slot()) MXEC_TRY(flush_down());
+                }
+            }
+            MXEC_TRY(flush_down());  // before the next group's wait
+            downed = g + 1;
+            return MXEC_OK;
+        };
         for (size_t g = 0; g < groups.size(); ++g) {
             MXEC_TRY(watch_open());
             const size_t g0 = groups[g].first, g1 = groups[g].second;
@@ -1495,7 +1897,10 @@ private:
                     }));
             }
             MXEC_HIP(hipEventRecord(done[g], rs_s));
+            if (down_early) MXEC_TRY(down_group(g));
+            MXEC_TRY(pace(up));
         }
+        paced_.clear();
         // Phase 2: ONE SHA-256 launch over every chunk of the wave once all
         // parity exists.  A message's hash time does not depend on how many
         // messages share the launch (up to the split-form limit), so one
@@ -1519,19 +1924,7 @@ private:
             MXEC_HIP(hipEventRecord(sha_done, sha_s));
         }
         // Phase 3: parity back group by group as RS finishes, digests last.
-        for (size_t g = 0; g < groups.size(); ++g) {
-            MXEC_TRY(issue_down());
-            MXEC_HIP(hipStreamWaitEvent(d2h_, done[g], 0));
-            for (size_t o = groups[g].first; o < groups[g].second; ++o) {
-                const HostObj& h = objs[o];
-                uint8_t* ob = base + h.pool_off;
-                for (int i = 0; i < h.m; ++i) {
-                    MXEC_TRY(queue_down(h.parity[i], ob + uint64_t(h.k + i) * h.slot(), h.S));
-                    if (h.S != h.slot()) MXEC_TRY(flush_down());
-                }
-            }
-            MXEC_TRY(flush_down());  // before the next group's wait
-        }
+        for (size_t g = downed; g < groups.size(); ++g) MXEC_TRY(down_group(g));
         if (sha_done) {
             MXEC_TRY(issue_down());
             MXEC_HIP(hipStreamWaitEvent(d2h_, sha_done, 0));
@@ -1572,7 +1965,10 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
         std::vector<uint64_t> obj_bytes(size_t(n_obj), 0);
         for (uint64_t o = 0; o < n_obj; ++o)
             obj_bytes[o] = uint64_t(std::max(objs[o].k, 0) + std::max(objs[o].m, 0)) * rup(objs[o].shard_size, kAlign);
-        const std::vector<uint32_t> owner = deal_objects(obj_bytes, uint32_t(D));
+        std::vector<const void*> first(size_t(n_obj), nullptr);
+        for (uint64_t o = 0, j = 0; o < n_obj; j += uint64_t(std::max(objs[o].k, 0)), ++o)
+            if (objs[o].k > 0) first[o] = data[j];
+        const std::vector<uint32_t> owner = deal_batch(ctx->c, obj_bytes, first);
         uint64_t doff = 0, poff = 0, goff = 0;
         int first_err = MXEC_OK;
         std::string first_msg;
@@ -1617,11 +2013,11 @@ extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, ui
                 Device& dev = *ctx->c.devs[d];
                 rcs[d] = [&]() -> int {
                     MXEC_HIP(hipSetDevice(dev.id));
-                    std::lock_guard<std::mutex> g(dev.pipe_mu);
-                    if (!dev.pipe) dev.pipe = std::make_shared<PipeRes>();
-                    PipeRes& r = *static_cast<PipeRes*>(dev.pipe.get());
-                    MXEC_TRY(r.init(dev));
-                    DevicePipeline p(dev, r);
+                    uint64_t bytes = 0;
+                    for (const auto& h : per[d]) bytes += h.bytes();
+                    LaneScope lane;
+                    MXEC_TRY(lane.open(dev, bytes));
+                    DevicePipeline p(dev, lane.hub(), lane.lane());
                     return p.run(per[d]);
                 }();
                 if (rcs[d] != MXEC_OK) errs[d] = last_error();
@@ -1688,7 +2084,11 @@ extern "C" int mxec_reconstruct_batch_host(mxec_ctx* ctx, const mxec_object* obj
             obj_bytes[o] = all.back().bytes();
             g0 += uint64_t(k + m);
         }
-        const std::vector<uint32_t> owner = deal_objects(obj_bytes, uint32_t(D));
+        std::vector<const void*> first(size_t(n_obj), nullptr);
+        for (uint64_t o = 0; o < n_obj; ++o)
+            for (int i = 0; i < all[o].k + all[o].m && !first[o]; ++i)
+                if (all[o].present[i]) first[o] = all[o].shards[i];
+        const std::vector<uint32_t> owner = deal_batch(ctx->c, obj_bytes, first);
         std::vector<std::vector<RecObj>> per(D);
         for (uint64_t o = 0; o < n_obj; ++o) per[owner[o]].push_back(all[o]);
         const bool data_only = (flags & MXEC_F_DATA_ONLY) != 0;
@@ -1706,11 +2106,11 @@ extern "C" int mxec_reconstruct_batch_host(mxec_ctx* ctx, const mxec_object* obj
                 Device& dev = *ctx->c.devs[d];
                 rcs[d] = [&]() -> int {
                     MXEC_HIP(hipSetDevice(dev.id));
-                    std::lock_guard<std::mutex> g(dev.pipe_mu);
-                    if (!dev.pipe) dev.pipe = std::make_shared<PipeRes>();
-                    PipeRes& r = *static_cast<PipeRes*>(dev.pipe.get());
-                    MXEC_TRY(r.init(dev));
-                    DevicePipeline p(dev, r);
+                    uint64_t bytes = 0;
+                    for (const auto& h : per[d]) bytes += h.bytes();
+                    LaneScope lane;
+                    MXEC_TRY(lane.open(dev, bytes));
+                    DevicePipeline p(dev, lane.hub(), lane.lane());
                     return p.run_rec(per[d], data_only);
                 }();
                 if (rcs[d] != MXEC_OK) errs[d] = last_error();

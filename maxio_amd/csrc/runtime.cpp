@@ -9,6 +9,9 @@
 #include <cstring>
 #include <map>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 namespace mxec {
 
 namespace {
@@ -50,11 +53,26 @@ void DevBuf::release() {
     cap = 0;
 }
 
+hipError_t host_malloc_on_node(void** p, size_t n, int node, unsigned flags) {
+    constexpr unsigned long kMaxNode = 1024;
+    int old_mode = 0;
+    unsigned long old_mask[kMaxNode / 64] = {}, mask[kMaxNode / 64] = {};
+    bool bound = false;
+    if (node >= 0 && unsigned(node) < kMaxNode &&
+        syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNode + 1, nullptr, 0) == 0) {
+        mask[node / 64] = 1ul << (node % 64);
+        bound = syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, kMaxNode + 1) == 0;
+    }
+    const hipError_t e = hipHostMalloc(p, n, flags | (bound ? hipHostMallocNumaUser : 0));
+    if (bound) (void)syscall(SYS_set_mempolicy, old_mode, old_mode ? old_mask : nullptr, old_mode ? kMaxNode + 1 : 0);
+    return e;
+}
+
 int PinnedBuf::ensure(size_t n) {
     if (n <= cap && p) return MXEC_OK;
     release();
     size_t want = n < 4096 ? 4096 : n;
-    MXEC_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+    MXEC_HIP(host_malloc_on_node(&p, want, node, hipHostMallocDefault));
     cap = want;
     return MXEC_OK;
 }
@@ -162,6 +180,7 @@ int wave_copy_segments(Slot& slot, hipStream_t s, const std::vector<CopyBlk>& bl
     char* hb = nullptr;
     MXEC_TRY(w.commit_host(&hb));
     MXEC_HIP(launch_copy_blocks(reinterpret_cast<const CopyBlk*>(hb + o), blks.size(), to_host, 16, s));
+    if (slot.owner) slot.owner->copy_wave_blocks += blks.size();
     return w.finish(s);
 }
 void add_blocks(std::vector<CopyBlk>& v, uint64_t dst, uint64_t src, uint64_t len) {
@@ -319,7 +338,7 @@ int PinnedBuf::grow(size_t n) {
     if (n <= cap && p) return MXEC_OK;
     const size_t want = std::max(std::max(n, cap * 2), DevBuf::kGrowFloor);
     void* q = nullptr;
-    MXEC_HIP(hipHostMalloc(&q, want, hipHostMallocDefault));
+    MXEC_HIP(host_malloc_on_node(&q, want, node, hipHostMallocDefault));
     if (p) retired.push_back(p);
     p = q;
     cap = want;

@@ -57,9 +57,16 @@ struct DevBuf {
     static constexpr size_t kGrowFloor = size_t(1) << 20;
 };
 
+// Page-locked host memory (hipHostMalloc) on NUMA node `node` (-1: where
+// the calling thread's policy puts it): the thread prefers that node around
+// the call (hipHostMallocNumaUser) and gets its policy back after; if the
+// node does not exist or the policy calls are refused, the plain allocation.
+hipError_t host_malloc_on_node(void** p, size_t n, int node, unsigned flags);
+
 struct PinnedBuf {
     void* p = nullptr;
     size_t cap = 0;
+    int node = -1;  // NUMA node its pages go on (host_malloc_on_node; -1: anywhere)
     std::vector<void*> retired;
     int ensure(size_t n);
     int grow(size_t n);
@@ -195,6 +202,13 @@ struct GridTuner {
 struct Device {
     int id = 0;
     int n_cus = 256;
+    // NUMA node of the GPU (sysfs; -1 unknown; mxec_open_test logical copies
+    // alternate between pretend nodes 0 and 1), and whether the context's
+    // devices sit on more than one node: only then does the host pipeline
+    // deal objects by where their pages are and keep its page-locked rings
+    // on the device's node (pipeline.cpp).
+    int numa_node = -1;
+    bool ctx_multi_node = false;
     const Knobs* kn = nullptr;  // the context's settings (read at mxec_open)
     GridTuner tuner;
     std::vector<std::unique_ptr<Slot>> slots;
@@ -266,23 +280,35 @@ struct Device {
         uint64_t seq;  // the table's upload (Device::CoefEntry)
     };
     std::unordered_map<PatternKey, PatternVal, PatternHash> patterns;
-    // Host-batch pipeline state (pipeline.cpp): streams, pinned rings, pools;
-    // created on first use and kept, one batch at a time per device.
-    std::mutex pipe_mu;
+    // Host-batch pipeline state (pipeline.cpp PipeHub): the four shared
+    // streams and the per-call lanes (pinned rings, pools, descriptor
+    // arenas); created on first use and kept.  Up to MXEC_PIPE_LANES calls
+    // run at once per device, their waves interleaving on the same streams.
+    std::mutex pipe_mu;  // guards creation of `pipe`
     std::shared_ptr<void> pipe;
     // Copies the host pipeline issued (mxec_ctx_copy_stats): 1D SDMA DMAs,
-    // 2D SDMA DMAs and their rows, CU-wave copy blocks (copy_kernel.hip).
-    std::atomic<uint64_t> copies_1d{0}, copies_2d{0}, copies_2d_rows{0}, copy_wave_blocks{0};
+    // 2D SDMA DMAs and their rows, CU-wave copy blocks (copy_kernel.hip; the
+    // single-request calls' wave copies count too).
+    std::atomic<uint64_t> copies_1d{0}, copies_2d{0}, copies_2d_rows{0};
+    mutable std::atomic<uint64_t> copy_wave_blocks{0};
     // SDMA watch of the host pipeline (MXEC_PIPE_COPY=auto): upload brackets
-    // judged, how many ran below the floor, the last one's rate (MB/s); the
-    // current verdict also steers the single-request calls' copies of
-    // mxec_host_alloc memory.
+    // judged, how many ran below the floor, the last one's rate (MB/s).
     std::atomic<uint64_t> sdma_probes{0}, sdma_slow_verdicts{0}, sdma_last_mbps{0};
     std::atomic<uint64_t> sdma_down_probes{0}, sdma_down_slow_verdicts{0}, sdma_down_last_mbps{0};
     // Piece-major verified reconstruct waves and the verification groups
     // they ran as (pipeline.cpp verify_cuts).
     std::atomic<uint64_t> verify_waves{0}, verify_groups{0};
-    std::atomic<bool> sdma_slow{false};
+    // The watch's verdicts as holds (steady_clock ns): calls that start
+    // before these instants copy mxec_host_alloc memory by waves, uploads /
+    // downloads.  Only a measured slow bracket sets one, and it lapses on its
+    // own: the single-request calls read the same instants
+    // (capi.cpp copy_waves_get).
+    std::atomic<int64_t> waves_up_until_ns{0}, waves_down_until_ns{0};
+    // Host-batch calls (per device share), those admitted while another ran
+    // on the device, speculative piece rebuilds of verified GETs and the
+    // objects re-decoded after a verdict, and host waits that paced a shared
+    // call's enqueue (pipeline.cpp).
+    std::atomic<uint64_t> pipe_calls{0}, pipe_calls_shared{0}, spec_pieces{0}, spec_redos{0}, pace_waits{0};
     // SHA-256 combiner (combiner.cpp): one launch for the verification work
     // of every concurrent caller on this device.
     std::mutex comb_mu;

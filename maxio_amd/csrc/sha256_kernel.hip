@@ -589,7 +589,15 @@ __device__ __forceinline__ uint32_t lag_xc(uint32_t x3, uint32_t ma, uint32_t c)
 // floor; a hand order spacing every on-chain pair two slots apart, held
 // with sched_barriers, measured 1.48 us per block against 1.265
 // (profiles/r3/sha_lag/ab_order.jsonl).
-__device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[16], const QuadLane& q) {
+//
+// `at(t)` runs at the top of step t (the caller's K + W reads for the next
+// block, spread over the block: sha256_quad_kernel LDG).
+struct NoStep {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <class AT = NoStep>
+__device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[16], const QuadLane& q,
+                                             const AT& at = AT()) {
     const bool is_a = q.ma != 0;
     const uint32_t one = q.ma & 1;  // c after lane E's rounds: 1 in lane A (-X3 = ~X3 + 1), 0 elsewhere
     uint32_t x[8];
@@ -604,6 +612,7 @@ __device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[
     uint32_t xc = lag_xc(x[6], q.ma, v[0][1]);
 #pragma unroll
     for (int t = 0; t < 66; ++t) {
+        at(t);
         const uint32_t X0 = x[t & 7], X1 = x[(t + 7) & 7], X2 = x[(t + 6) & 7];
         const uint32_t S = xor3(rotr(X0, q.sh1), rotr(X0, q.sh2), rotr(X0, q.sh3));
         const uint32_t sel = __builtin_amdgcn_bitop3_b32(X0, X1, q.ma, 0xD2);  // X0 ^ (~X1 & ma)
@@ -633,7 +642,14 @@ __device__ __forceinline__ void compress_lag(uint32_t (&s)[4], const u32x4 (&v)[
 // P2 (PAIR only; the auto form): two producer waves of 32 messages, two
 // lanes per message (schedule_kw_pair), waves 0-1; consumers waves 2-3: a
 // workgroup of four waves, one per SIMD.
-template <bool LAG, bool PAIR = false, bool P2 = false>
+// LDG (lag forms): the next block's 16 ds_read_b128 of K + W go out in LDG
+// groups spread over the current block -- group g at the top of step
+// 64 g / LDG -- instead of all 16 right after the barrier.  A wave may hold
+// at most 15 LDS instructions in flight (lgkmcnt is 4 bits), so the 16th
+// read of a burst waited for the first to come back, and the in-order wave
+// issued no VALU meanwhile (round 5: ~260 cycles per block above the step
+// lab's 66 x 37.4).
+template <bool LAG, bool PAIR = false, bool P2 = false, int LDG = 1>
 __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* __restrict__ ptrs,
                                                          const uint64_t* __restrict__ lens,
                                                          uint8_t* __restrict__ digests,
@@ -728,27 +744,42 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     u32x4 cur[16], nxt[16];
     load_kw<kQuadRow>(kcol, cur);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    static_assert(LDG == 1 || LDG == 2 || LDG == 4, "K + W read groups: 1, 2 or 4");
+    constexpr int RPG = 16 / LDG;  // rows per read group
+    // Rows [g RPG, (g + 1) RPG) of the block in ring buffer `buf` into `dst`.
+    auto rows = [&](u32x4 (&dst)[16], uint32_t buf, int g) {
+#pragma unroll
+        for (int r = g * RPG; r < (g + 1) * RPG; ++r) dst[r] = kcol[buf * BUF + r * kQuadRow];
+    };
     uint32_t rb = 1;
     for (uint64_t b = 0; b < nmax; b += 2) {
-        load_kw<kQuadRow>(kcol + rb * BUF, nxt);
+        rows(nxt, rb, 0);
         if (b < nfull) {
 #ifdef MXEC_LAB
-            if constexpr (!LAG) compress_quad(s, cur, q);
-            else
+            if constexpr (!LAG) {
+                for (int g = 1; g < LDG; ++g) rows(nxt, rb, g);
+                compress_quad(s, cur, q);
+            } else
 #endif
-            compress_lag(s, cur, q);
-        }
+            compress_lag(s, cur, q, [&](int t) {
+                if (LDG > 1 && t > 0 && t < 64 && t % (64 / LDG) == 0) rows(nxt, rb, t / (64 / LDG));
+            });
+        }  // a lane past its message's blocks never reads K + W again: no reads here
         KW_SYNC();
         rb = rb == 2 ? 0 : rb + 1;
         if (b + 1 >= nmax) break;
-        load_kw<kQuadRow>(kcol + rb * BUF, cur);
+        rows(cur, rb, 0);
         if (b + 1 < nfull) {
 #ifdef MXEC_LAB
-            if constexpr (!LAG) compress_quad(s, nxt, q);
-            else
+            if constexpr (!LAG) {
+                for (int g = 1; g < LDG; ++g) rows(cur, rb, g);
+                compress_quad(s, nxt, q);
+            } else
 #endif
-            compress_lag(s, nxt, q);
-        }
+            compress_lag(s, nxt, q, [&](int t) {
+                if (LDG > 1 && t > 0 && t < 64 && t % (64 / LDG) == 0) rows(cur, rb, t / (64 / LDG));
+            });
+        }  // a lane past its message's blocks never reads K + W again: no reads here
         KW_SYNC();
         rb = rb == 2 ? 0 : rb + 1;
     }
@@ -1004,6 +1035,9 @@ constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 // Forms 4 and 5 and the split form's two-buffer ring exist in lab builds
 // only (`make lab`, -DMXEC_LAB).
 constexpr int kShaQuadAuto = 6;
+// K + W read groups of the auto form's consumers (sha256_quad_kernel LDG;
+// lab builds A/B it with MXEC_SHA_LDG=1|2|4).
+constexpr int kShaLdg = 4;
 
 #ifdef MXEC_LAB
 // MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read
@@ -1060,8 +1094,18 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
             return hipGetLastError();
         }
 #endif
-        hipLaunchKernelGGL((sha256_quad_kernel<true, true, true>), dim3((a.n + 63) / 64), dim3(256), 0, s, a.ptrs,
-                           a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
+#ifdef MXEC_LAB
+        if (const char* e = getenv("MXEC_SHA_LDG"); e && atoi(e) != kShaLdg) {  // lab A/B: K + W read groups
+            const int g = atoi(e);
+            auto* kern = g == 1 ? &sha256_quad_kernel<true, true, true, 1>
+                                : g == 2 ? &sha256_quad_kernel<true, true, true, 2> : &sha256_quad_kernel<true, true, true, 4>;
+            hipLaunchKernelGGL(kern, dim3((a.n + 63) / 64), dim3(256), 0, s, a.ptrs, a.lens, a.digests, a.expected,
+                               a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
+            return hipGetLastError();
+        }
+#endif
+        hipLaunchKernelGGL((sha256_quad_kernel<true, true, true, kShaLdg>), dim3((a.n + 63) / 64), dim3(256), 0, s,
+                           a.ptrs, a.lens, a.digests, a.expected, a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
         return hipGetLastError();
     }
     if (form == 3) {

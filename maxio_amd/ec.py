@@ -199,7 +199,8 @@ class Context:
         return {"recycles": r.value, "relaunches": q.value, "fence_waits": w.value}
 
     PIPE_STATS = ("copies_1d", "copies_2d", "rows_2d", "wave_blocks", "sdma_checks", "sdma_slow", "verify_waves",
-                  "verify_groups", "sdma_last_mbps", "sdma_down_checks", "sdma_down_slow", "sdma_down_last_mbps")
+                  "verify_groups", "sdma_last_mbps", "sdma_down_checks", "sdma_down_slow", "sdma_down_last_mbps",
+                  "calls", "calls_shared", "spec_pieces", "spec_redos", "pace_waits")
 
     def pipe_stats(self, dev: int = 0) -> dict:
         """Host-batch pipeline counters of device `dev` since the context
@@ -219,14 +220,16 @@ class Context:
             _check(rc)
         return rc
 
-    def host_array(self, n: int) -> np.ndarray:
-        """A uint8 array of n bytes in page-locked memory (mxec_host_alloc):
-        uploads from it and downloads into it skip the staging copy.  Free it
-        with host_free(); otherwise it is freed when the array is garbage
-        collected -- but never from an interpreter-exit callback (the HIP
-        runtime may be tearing down by then): memory still held at exit goes
-        back with the process."""
-        p = self._lib.mxec_host_alloc(self._h, max(1, n))
+    def host_array(self, n: int, dev: Optional[int] = None) -> np.ndarray:
+        """A uint8 array of n bytes in page-locked memory (mxec_host_alloc;
+        with `dev`, mxec_host_alloc_device: on that context device's NUMA
+        node): uploads from it and downloads into it skip the staging copy.
+        Free it with host_free(); otherwise it is freed when the array is
+        garbage collected -- but never from an interpreter-exit callback (the
+        HIP runtime may be tearing down by then): memory still held at exit
+        goes back with the process."""
+        p = (self._lib.mxec_host_alloc(self._h, max(1, n)) if dev is None
+             else self._lib.mxec_host_alloc_device(self._h, dev, max(1, n)))
         if not p:
             raise MemoryError("mxec_host_alloc failed")
         buf = (ctypes.c_uint8 * max(1, n)).from_address(p)

@@ -104,7 +104,12 @@ pub const MXEC_PIPE_STAT_SDMA_LAST_MBPS: c_int = 8;
 pub const MXEC_PIPE_STAT_SDMA_DOWN_CHECKS: c_int = 9;
 pub const MXEC_PIPE_STAT_SDMA_DOWN_SLOW: c_int = 10;
 pub const MXEC_PIPE_STAT_SDMA_DOWN_LAST_MBPS: c_int = 11;
-pub const MXEC_PIPE_STAT_COUNT: c_int = 12;
+pub const MXEC_PIPE_STAT_CALLS: c_int = 12;
+pub const MXEC_PIPE_STAT_CALLS_SHARED: c_int = 13;
+pub const MXEC_PIPE_STAT_SPEC_PIECES: c_int = 14;
+pub const MXEC_PIPE_STAT_SPEC_REDOS: c_int = 15;
+pub const MXEC_PIPE_STAT_PACE_WAITS: c_int = 16;
+pub const MXEC_PIPE_STAT_COUNT: c_int = 17;
 
 // ---- return codes (reed_solomon_erasure::Error one for one, then MaxIO's) --
 pub const MXEC_OK: c_int = 0;
@@ -158,6 +163,7 @@ extern "C" {
     pub fn mxec_ctx_coef_stats(ctx: *mut MxecCtx, dev: c_int, recycles: *mut u64, relaunches: *mut u64,
                                fence_waits: *mut u64) -> c_int;
     pub fn mxec_host_alloc(ctx: *mut MxecCtx, bytes: usize) -> *mut c_void;
+    pub fn mxec_host_alloc_device(ctx: *mut MxecCtx, dev: c_int, bytes: usize) -> *mut c_void;
     pub fn mxec_host_free(ctx: *mut MxecCtx, p: *mut c_void);
     pub fn mxec_rs_check(k: c_int, m: c_int) -> c_int;
     pub fn mxec_rs_parity_matrix(k: c_int, m: c_int, out: *mut u8) -> c_int;

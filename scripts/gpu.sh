@@ -28,7 +28,14 @@
 #             effective clock per kernel (tools/clock_summary.py)
 #   rust      probe for rustc / cargo
 #   cfg:<c>   python bench.py --config <c> --no-extra -> cfg_<c>.json
-# Env: BENCH_ARGS (extra bench.py args for bench/prof).
+#   pyt:<f+f> the named test files only (tests/<f>.py, `+`-separated), -m gpu
+#             -> pytest_<first>.log
+#   tool:<t>  python tools/<t>.py $TOOL_ARGS_<t> (else $TOOL_ARGS) -> <t>.jsonl
+#             (stderr <t>.err);
+#             the round-4/5 study scripts' one-off runs (watch_diag,
+#             sha_alone, exit_probe, concurrent_e2e, ...) go through this
+# Env: BENCH_ARGS (extra bench.py args for bench/prof), TOOL_ARGS, TOOL_TIMEOUT
+# (seconds, default 600).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -123,6 +130,17 @@ for st in "${STEPS[@]}"; do
     rust)
       { command -v rustc; command -v cargo; rustc --version; cargo --version; } > "$O/rust_probe.txt" 2>&1 || true
       cat "$O/rust_probe.txt" ;;
+    pyt:*)
+      IFS=+ read -ra F <<< "${st#pyt:}"
+      files=(); for f in "${F[@]}"; do files+=("tests/$f.py"); done
+      timeout -k 10 900 python -u -m pytest "${files[@]}" -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$O/pytest_${F[0]}.log" 2>&1 || { tail -40 "$O/pytest_${F[0]}.log"; exit 1; }
+      tail -2 "$O/pytest_${F[0]}.log" ;;
+    tool:*)
+      t="${st#tool:}"; v="TOOL_ARGS_$t"; targs="${!v:-$TOOL_ARGS}"
+      timeout -k 10 "${TOOL_TIMEOUT:-600}" python -u "tools/$t.py" $targs > "$O/$t.jsonl" 2> "$O/$t.err" \
+        || { tail -20 "$O/$t.err"; exit 1; }
+      cat "$O/$t.jsonl" ;;
     cfg:*)
       c="${st#cfg:}"
       timeout -k 10 900 python bench.py --config "$c" --no-extra $BENCH_ARGS > "$O/cfg_$c.json" 2> "$O/cfg_$c.err" || { tail -20 "$O/cfg_$c.err"; exit 1; }

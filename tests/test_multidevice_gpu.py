@@ -123,3 +123,48 @@ def test_device_entry_points_by_index(ctx2):
         assert all(np.array_equal(outs[0][o][i], want[i]) for i in range(m))
     with pytest.raises(maxio_amd.RSError):
         ctx2.encode_strided_device(k, m, S, n, data.data_ptr(), k * S, S, data.data_ptr(), m * S, S, dev=2)
+
+
+def test_numa_deal_on_pretend_nodes(ctx2):
+    """on a context whose devices sit on two NUMA nodes,
+    the host batch calls deal each object to a device on the node of its
+    pages, balanced by bytes (deal.hpp deal_objects_numa; the rule itself is
+    unit-tested with a fake node map in tests/c_manifest/deal_check.cpp).
+    mxec_open_test's two logical copies of the card pretend to sit on nodes
+    0 and 1; the objects' pages come from mxec_host_alloc_device(dev = o % 2)
+    (on that node where the host has it).  A PUT with digests and a verified
+    GET (two erasures, one corrupted present shard) over 12 x 4+2 x 2 MiB:
+    every parity chunk, digest and rebuilt shard exact, both devices used."""
+    k, m, n, S = 4, 2, 12, (2 << 20) + 48
+    rng = np.random.default_rng(606)
+    rows = [ctx2.host_array((k + m) * S, dev=o % 2).reshape(k + m, S) for o in range(n)]
+    for r in rows:
+        r[:k] = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    objs = [(k, m, S)] * n
+    dig = np.zeros(n * (k + m) * 32, np.uint8)
+    c0 = [ctx2.pipe_stats(d) for d in range(2)]
+    st = ctx2.encode_batch_host(objs, [r[j].ctypes.data for r in rows for j in range(k)],
+                                [r[k + i].ctypes.data for r in rows for i in range(m)], digests=dig)
+    assert (st == 0).all()
+    for o, r in enumerate(rows):
+        want, want_dig, rc = oracle.compute_parity([r[j] for j in range(k)], m, S)
+        assert rc == 0 and all(np.array_equal(r[k + i], want[i]) for i in range(m)), o
+        assert [dig[(o * (k + m) + t) * 32:][:32].tobytes() for t in range(k + m)] == want_dig, o
+    ref = [r.copy() for r in rows]
+    present = np.ones((n, k + m), np.uint8)
+    for o, r in enumerate(rows):
+        lost = rng.choice(k + m, 1 if o == 3 else 2, replace=False)
+        present[o, lost] = 0
+        r[lost] = 0x5A
+    r3 = rows[3]
+    r3[int(np.flatnonzero(present[3])[0]), 1234] ^= 0x40  # silently corrupt: caught, rebuilt
+    pr = present.reshape(-1).copy()
+    rc, st = ctx2.reconstruct_batch_host(objs, [r[i].ctypes.data for r in rows for i in range(k + m)], pr,
+                                         expected=dig)
+    assert rc == 0 and not st.any() and pr.all()
+    for o in range(n):
+        assert np.array_equal(rows[o], ref[o]), o
+    c1 = [ctx2.pipe_stats(d) for d in range(2)]
+    assert all(c1[d]["calls"] - c0[d]["calls"] == 2 for d in range(2)), (c0, c1)
+    for r in rows:
+        ctx2.host_free(r.reshape(-1))

@@ -40,10 +40,11 @@ def _random(ctx, shape, seed):
     return a
 
 
-def _put_and_check(ctx, n, S, seed, short=None, digests=True):
+def _put_and_check(ctx, n, S, seed, short=None, digests=True, check=True):
     """n x 4+2 objects of shard size S from host_array memory, PUT with
     digests (or without: the group form); `short` maps object -> length of
-    its last data chunk.  Returns the copy-statistics delta."""
+    its last data chunk.  Returns the copy-statistics delta (check=False:
+    (delta, a function that checks the objects and frees the buffers))."""
     k, m = 4, 2
     short = short or {}
     data = _random(ctx, (n, k, S), seed)
@@ -73,13 +74,19 @@ def _put_and_check(ctx, n, S, seed, short=None, digests=True):
             got = [dig[(o * (k + m) + t) * 32:(o * (k + m) + t + 1) * 32].tobytes() for t in range(k + m)]
             assert got == want_dig, o
 
-    from concurrent.futures import ThreadPoolExecutor
+    def check_all():
+        from concurrent.futures import ThreadPoolExecutor
 
-    with ThreadPoolExecutor(8) as ex:
-        list(ex.map(check, range(n)))
-    ctx.host_free(data)
-    ctx.host_free(par)
-    return {key: after[key] - before[key] for key in after}
+        with ThreadPoolExecutor(8) as ex:
+            list(ex.map(check, range(n)))
+        ctx.host_free(data)
+        ctx.host_free(par)
+
+    delta = {key: after[key] - before[key] for key in after}
+    if not check:
+        return delta, check_all
+    check_all()
+    return delta
 
 
 @pytest.mark.parametrize("piece_mb", ["2", "4"])
@@ -152,9 +159,11 @@ def test_get_wave_copies_ragged_and_odd_offsets(ctx_with, copy, offset, floor):
 @pytest.mark.parametrize("floor,waves", [("0", False), ("", False), ("100000", True)])
 def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
     """MXEC_PIPE_COPY=auto: an RS-only PUT's group uploads are timed (floor
-    0: not watched; the default floor: a healthy SDMA passes; an unreachable
-    floor: the call's brackets are judged slow, and the device's next calls
-    copy by waves); parity against the oracle either way."""
+    0: not watched; the default floor: timed, the rate recorded; an
+    unreachable floor: the call's brackets are judged slow, and the device's
+    next call, issued right after it -- well inside the 2 s hold -- copies
+    by waves); parity against the oracle either way.  No assertion on the
+    box's own SDMA rate."""
     from conftest import open_ctx
 
     # a context of its own: a cached one may still hold an earlier call's
@@ -163,17 +172,19 @@ def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
     S = 3 * M + 4096 + 48
     try:
         s0 = ctx.pipe_stats()
-        _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333}, digests=False)
+        _, check1 = _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333}, digests=False, check=False)
         s1 = ctx.pipe_stats()
-        _put_and_check(ctx, 8, S, 1400 + len(floor), digests=False)  # within the 2 s upload hold of a slow verdict
+        _, check2 = _put_and_check(ctx, 8, S, 1400 + len(floor), digests=False, check=False)
         s2 = ctx.pipe_stats()
+        check1()
+        check2()
     finally:
         ctx.close()
     assert (s1["sdma_checks"] > s0["sdma_checks"]) == (floor != "0"), (s0, s1)
     assert (s1["sdma_slow"] > s0["sdma_slow"]) == waves, (s0, s1)
     assert (s2["wave_blocks"] > s1["wave_blocks"]) == waves, (s1, s2)
     if floor == "":
-        assert s1["sdma_last_mbps"] > 20000, s1  # a healthy box's 1 MiB piece copies
+        assert s1["sdma_last_mbps"] > 0, s1  # a bracket was timed and its rate recorded
 
 
 @pytest.mark.parametrize("floor", ["", "100000"])

@@ -247,7 +247,8 @@ def test_reconstruct_batch_host_verify_in_pieces(ctx_with, piece_mb):
     piece (MXEC_PIPE_PIECE_MB; 0 = one launch after the whole upload):
     shards over several pieces and off the piece grid, short and empty last
     chunks, a corrupt present shard caught as an erasure, an object that
-    fails (buffers untouched), the rest bit-exact."""
+    fails (its present shards untouched; with whole-chunk hashing, piece 0,
+    nothing of it written), the rest bit-exact."""
     ctx = ctx_with(MXEC_PIPE_PIECE_MB=piece_mb)
     rng = np.random.default_rng(50 + int(piece_mb or 9))
     M = 1 << 20
@@ -265,7 +266,8 @@ def test_reconstruct_batch_host_verify_in_pieces(ctx_with, piece_mb):
     for o, (k, m, s) in enumerate(objs):
         for i in range(k + m):
             if o == 4:
-                assert np.array_equal(bufs[g + i], before[g + i])  # failing object untouched
+                if present[g + i] or piece_mb == "0":  # the speculative rebuild may have written the missing ones
+                    assert np.array_equal(bufs[g + i], before[g + i])
             else:
                 assert np.array_equal(bufs[g + i][:lens[g + i]], originals[o][i]), (o, i)
         g += k + m
@@ -273,8 +275,10 @@ def test_reconstruct_batch_host_verify_in_pieces(ctx_with, piece_mb):
 
 def test_reconstruct_batch_host_failing_object(ctx):
     """An object with more than m shards lost or corrupt: -10 for it and the
-    call, its buffers untouched, the present mask minus the mismatches; the
-    other objects bit-exact (chunk_reader.rs:199-208)."""
+    call, its present shards untouched (its missing shards' buffers are
+    undefined: rebuilt speculatively before the verdict), the present mask
+    minus the mismatches; the other objects bit-exact
+    (chunk_reader.rs:199-208)."""
     rng = np.random.default_rng(42)
     specs = [(4, 2, 8192, None, {0}, set()), (4, 2, 8192, None, {1, 5}, {0}), (8, 4, 4096, 100, {2}, set())]
     objs, ptrs, lens, present, expected, originals, bufs = _rec_batch(rng, specs)
@@ -283,8 +287,8 @@ def test_reconstruct_batch_host_failing_object(ctx):
     rc, status = ctx.reconstruct_batch_host(objs, ptrs, p, shard_len=lens, expected=expected)
     assert rc == -10 and list(status) == [0, -10, 0]
     assert "too many missing/corrupt shards" in ctx._lib.mxec_last_error().decode()
-    for i in range(6):
-        assert np.array_equal(bufs[6 + i], before[6 + i])  # failing object untouched
+    for i in (0, 2, 3, 4):  # the present shards (0 corrupt) of the failing object
+        assert np.array_equal(bufs[6 + i], before[6 + i])
     assert list(p[6:12]) == [0, 0, 1, 1, 1, 0]
     for o, g in ((0, 0), (2, 12)):
         k, m, s = objs[o]
@@ -467,3 +471,47 @@ def test_single_request_calls_on_host_alloc_buffers(ctx_with, copy):
                                    ctypes.byref(npres))
     assert rc == 0 and present.all() and npres.value == k + m - 3
     assert np.array_equal(sh, ref)
+
+
+@pytest.mark.parametrize("floor,waves", [("0", False), ("100000", True)])
+def test_single_request_calls_follow_the_verdict(floor, waves):
+    """under MXEC_PIPE_COPY=auto the single-request hash call
+    copies mxec_host_alloc buffers by waves exactly while a measured slow
+    bracket's hold lasts (capi.cpp copy_waves_get reads the holds).  An
+    RS-only host GET with an unreachable floor is judged slow (its upload
+    and download brackets); a mxec_sha256_batch issued right after it --
+    well inside the 1-2 s holds -- moves its buffers by waves (wave_blocks
+    rises); with floor 0 (no brackets, no verdict) it stays on SDMA.
+    Digests against hashlib either way."""
+    import hashlib
+
+    from conftest import open_ctx
+
+    ctx = open_ctx(2, 0, MXEC_PIPE_COPY="auto", MXEC_PIPE_SDMA_FLOOR=floor)
+    try:
+        k, m, n, S = 4, 2, 16, 4 * (1 << 20)
+        rng = np.random.default_rng(4343)
+        buf = ctx.host_array(n * (k + m) * S).reshape(n, k + m, S)
+        buf[:, :k] = rng.integers(0, 256, (n, k, S), dtype=np.uint8)
+        objs = [(k, m, S)] * n
+        st = ctx.encode_batch_host(objs, [buf[o, j].ctypes.data for o in range(n) for j in range(k)],
+                                   [buf[o, k + i].ctypes.data for o in range(n) for i in range(m)])
+        assert (st == 0).all()
+        ref = buf.copy()
+        buf[:, [0, 5]] = 0x11
+        present = np.ones((n, k + m), np.uint8)
+        present[:, [0, 5]] = 0
+        pr = present.reshape(-1).copy()
+        rc, st = ctx.reconstruct_batch_host(objs, [buf[o, i].ctypes.data for o in range(n) for i in range(k + m)], pr)
+        assert rc == 0 and pr.all() and np.array_equal(buf, ref)
+        s0 = ctx.pipe_stats()
+        cuts = [(0, 1 << 20), (3 << 20, 5 << 20), (4096, 1000)]  # 16-byte phase kept (copy_phase_ok)
+        flat = buf.reshape(-1)
+        got = ctx.sha256([flat[o:o + ln] for o, ln in cuts])
+        s1 = ctx.pipe_stats()
+        assert got == [hashlib.sha256(flat[o:o + ln].tobytes()).digest() for o, ln in cuts]
+        assert (s0["sdma_slow"] + s0["sdma_down_slow"] > 0) == waves, s0
+        assert (s1["wave_blocks"] > s0["wave_blocks"]) == waves, (s0, s1)
+        ctx.host_free(buf.reshape(-1))
+    finally:
+        ctx.close()
