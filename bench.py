@@ -155,6 +155,15 @@ def cpu_leg(work, payload_per_call: int, seconds: float, threads: int):
 # ---- workloads ------------------------------------------------------------------
 
 
+class _DevMem:
+    """Device memory the library allocated, viewed by torch without a copy
+    (__cuda_array_interface__; torch.as_tensor wraps it)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
 class Encode:
     """RS encode of n uniform objects (data [n][k][S] -> parity [n][m][S])."""
 
@@ -184,6 +193,14 @@ class Encode:
         # (profiles/r2_shard_pad_spread.txt).
         self.pad = (2 << 20) + (64 << 10) if S >= (4 << 20) and not separate else 0
         self.sstride = S + self.pad
+        # The batch's HBM from the library's batch allocator (mxec_batch_alloc,
+        # placement.cpp): of two allocations x two shard strides, the one its
+        # own encode ran fastest on (where a batch lies moves the encode by up
+        # to ~8 %).  BENCH_TORCH_ALLOC=1: torch's allocator at the
+        # round-2 pad instead (the A/B).
+        self.batch_ptr = None
+        self.placement = None
+        lib_alloc = not separate and os.environ.get("BENCH_TORCH_ALLOC") != "1"
         if separate:
             # What a caller with its own buffers hands the *_device API: data
             # [n][k][S] and parity [n][m][S] as two allocations, no pad
@@ -195,7 +212,15 @@ class Encode:
             self.data, self.parity = self.obj, self.par_buf
             self.stride, self.pstride = k * S, m * S
         else:
-            self.obj = torch.empty((n, k + m, self.sstride), dtype=torch.uint8, device=dev)
+            if lib_alloc:
+                ptr, stride, probe = ctx.batch_alloc(k, m, S, n)
+                self.batch_ptr, self.sstride, self.pad = ptr, stride, stride - S
+                self.placement = {"allocator": "mxec_batch_alloc", "shard_stride": stride, "pad": stride - S,
+                                  "probe_ms": probe}
+                self.obj = torch.as_tensor(_DevMem(ptr, n * (k + m) * stride), device=dev).view(n, k + m, stride)
+            else:
+                self.obj = torch.empty((n, k + m, self.sstride), dtype=torch.uint8, device=dev)
+                self.placement = {"allocator": "torch", "shard_stride": self.sstride, "pad": self.pad}
             for o in range(n):  # per object keeps the randint temporary small
                 self.obj[o, :k, :S].copy_(torch.randint(0, 256, (k, S), dtype=torch.uint8, device=dev, generator=g))
             self.obj[:, k:].zero_()
@@ -256,6 +281,10 @@ class Encode:
         del self.data, self.parity, self.obj
         if self.separate:
             del self.par_buf
+        if self.batch_ptr:
+            self.torch.cuda.synchronize()
+            self.ctx.batch_free(self.batch_ptr)
+            self.batch_ptr = None
 
 
 class Reconstruct:
@@ -1264,7 +1293,7 @@ class DevView:
     _DEV_CALLS = frozenset((
         "rs_grid", "encode_strided_device", "encode_batch_device", "reconstruct_strided_device",
         "reconstruct_strided_device_async", "reconstruct_batch_device", "reconstruct_batch_device_async",
-        "sha256_batch_device", "body_sums_device", "frames_device", "combiner_stats"))
+        "sha256_batch_device", "body_sums_device", "frames_device", "combiner_stats", "batch_alloc"))
 
     def __init__(self, ctx, di: int):
         self._ctx, self.di = ctx, di
@@ -1799,6 +1828,8 @@ def e2e_concurrent(ctx, n: int = 128, reps: int = 3, stream_s: float = 5.0) -> d
     for a in put_rows + get_rows:
         ctx.host_free(a.reshape(-1))
     del put_rows, get_rows, get
+    if stream_s <= 0:
+        return res
 
     # configs[4]: mixed k+m at mixed chunk sizes, a continuous stream.
     kinds = [(4, 2), (8, 4), (10, 4)]
@@ -1996,6 +2027,7 @@ def main() -> int:
     cpu_spec = w.cpu_work() if (rank == 0 and one_gpu and args.cpu_seconds > 0) else None
     cpu_sha_ni = getattr(w, "cpu_sha_ni", None)  # set by cpu_work when the baseline hashes
     alg_bytes, w_name, w_kernel, w_bound, w_payload = w.alg_bytes, w.name, w.kernel, w.bound, w.payload
+    w_placement = getattr(w, "placement", None)
     is_stream = isinstance(w, ReconstructStream)
     stream_dims = (len(w.parts), w.parts[0].n) if is_stream else None
     mixed_batch = args.config == "5" and getattr(w, "mode", "") == "batch"
@@ -2080,6 +2112,7 @@ def main() -> int:
                 "workload": w_name,
                 "bench_config": args.config,
                 "payload_bytes_per_step_per_gpu": int(w_payload),
+                "placement": w_placement,
                 "parallelism": par,
             },
             "roofline": {

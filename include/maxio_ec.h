@@ -180,6 +180,22 @@ void* mxec_host_alloc(mxec_ctx* ctx, size_t bytes);
 void* mxec_host_alloc_device(mxec_ctx* ctx, int dev, size_t bytes);
 void mxec_host_free(mxec_ctx* ctx, void* p);
 
+/* HBM for a device-resident batch of n_obj objects of (k, m, shard_size),
+ * laid out object-major: shard j of object o at
+ * base + (o * (k + m) + j) * (*shard_stride), each object's parity after its
+ * data -- the layout mxec_encode_strided_device / _reconstruct_strided_device
+ * take with obj_stride = (k + m) * shard_stride.  The placement is measured:
+ * up to two allocations (the second while the first is held) times two shard
+ * strides, each timed by one encode over the whole candidate; the fastest is
+ * kept (where a batch lies in HBM moves the encode by up to ~8 %, DESIGN.md
+ * §7).  Transiently up to twice the batch's bytes.  probe_ms: NULL, or 4
+ * floats receiving the candidates' times (allocation-major; -1 for a
+ * candidate not tried).  NULL on failure (mxec_last_error).  Replaces nothing
+ * in the reference: a long-lived process allocates its batch buffers once. */
+void* mxec_batch_alloc(mxec_ctx* ctx, int dev, int k, int m, uint64_t shard_size,
+                       uint64_t n_obj, uint64_t* shard_stride, float* probe_ms);
+int mxec_batch_free(mxec_ctx* ctx, void* p);
+
 /* ---- ReedSolomon::new ----------------------------------------------------- */
 /* 0 if new(k, m) would succeed; otherwise the crate's error
  * (TooFewDataShards / TooFewParityShards / TooManyShards). */

@@ -105,6 +105,8 @@ _SIGS = {
     "mxec_ctx_coef_stats": (INT, [P, INT, U64P, U64P, U64P]),
     "mxec_host_alloc": (P, [P, ctypes.c_size_t]),
     "mxec_host_alloc_device": (P, [P, INT, ctypes.c_size_t]),
+    "mxec_batch_alloc": (P, [P, INT, INT, INT, U64, U64, U64P, ctypes.POINTER(ctypes.c_float)]),
+    "mxec_batch_free": (INT, [P, P]),
     "mxec_host_free": (None, [P, P]),
     "mxec_rs_check": (INT, [INT, INT]),
     "mxec_rs_parity_matrix": (INT, [INT, INT, U8P]),

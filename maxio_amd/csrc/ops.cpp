@@ -101,7 +101,7 @@ int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_onl
 }
 
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
-           const std::vector<RsObject>& objs, DescArena* arena) {
+           const std::vector<RsObject>& objs, DescArena* arena, bool tune) {
     if (objs.empty() || r == 0) return MXEC_OK;
     const size_t n = objs.size();
     if (affinity_on(dev)) {
@@ -172,7 +172,7 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     // Large aligned single-launch batches take the grid tuner's pick.
     GridTuner::Trial trial;
     const double gb = double(n) * double(k + r) * double(shard_size) / 1e9;
-    if (aligned && r <= 4) MXEC_TRY(rs_grid_pick(dev, k, r, shard_size, gb, &a.blocks_per_cu, &trial));
+    if (aligned && r <= 4 && tune) MXEC_TRY(rs_grid_pick(dev, k, r, shard_size, gb, &a.blocks_per_cu, &trial));
     hipError_t e = trial.a ? hipEventRecord(trial.a, s) : hipSuccess;
     for (int row0 = 0; row0 < r && e == hipSuccess; row0 += 8) {
         a.row0 = uint32_t(row0);

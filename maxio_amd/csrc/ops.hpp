@@ -28,8 +28,10 @@ struct RsObject {
 // Applies each object's matrix; all objects share (k, r, shard_size).
 // arena: take the descriptor tables from it instead of the slot's ring (many
 // launches in flight, see pipeline.cpp).
+// tune = false: the default grid, and the grid tuner neither picks nor
+// records (the batch allocator's placement probes, placement.cpp).
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
-           const std::vector<RsObject>& objs, DescArena* arena = nullptr);
+           const std::vector<RsObject>& objs, DescArena* arena = nullptr, bool tune = true);
 
 // Grid tuner of large uniform RS launches (runtime.hpp GridTuner):
 // rs_grid_pick sets *bpc (0 = the default grid) and, while a shape is still

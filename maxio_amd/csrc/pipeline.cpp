@@ -263,6 +263,8 @@ struct PipeHub {
         cv.wait(lk, [&] {
             return in_flight == 0 || (in_flight < max_lanes && admitted_bytes + bytes <= kPoolCap);
         });
+        if (in_flight == 0)  // nothing of ours runs: buffers retired by re-sizes can go now
+            for (auto& ln : lanes) ln->pool.free_retired();
         PipeLane* l = nullptr;
         if (!idle.empty()) {
             // the idle lane with the largest pool (fewest re-sizes)
@@ -346,6 +348,16 @@ struct PipeHub {
             for (auto& s : cs) MXEC_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(rm.size()), rm.data()));
             return MXEC_OK;
         }
+        if (const char* e = getenv("MXEC_PIPE_OWN_QUEUES"); e && *e == '1') {  // lab A/B
+            // Every CU in the mask: the stream gets a hardware queue of its own
+            // (a CU mask is a queue property), not one of the process's
+            // GPU_MAX_HW_QUEUES shared ones.
+            std::vector<uint32_t> all(size_t((n + 31) / 32), 0xFFFFFFFFu);
+            MXEC_HIP(hipExtStreamCreateWithCUMask(&h2d, uint32_t(all.size()), all.data()));
+            MXEC_HIP(hipExtStreamCreateWithCUMask(&d2h, uint32_t(all.size()), all.data()));
+            for (auto& s : cs) MXEC_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(all.size()), all.data()));
+            return MXEC_OK;
+        }
 #else
         (void)dev;
 #endif
@@ -409,19 +421,44 @@ private:
 // MXEC_PIPE_TRACE=1 (lab builds): where a host reconstruct wave's time goes
 // -- timing events on the copy and compute streams and host clocks around
 // every wait, one stderr JSON line per wave (tools: the GET-stall study).
+// The marks of every traced wave are reported against one process-wide
+// reference event (recorded and completed by the first traced wave) and the
+// host clock against one reference instant, so concurrent calls' traces line
+// up.
 struct PipeTrace {
     bool on = false;
     std::chrono::steady_clock::time_point h0;
     hipEvent_t e0 = nullptr;
     std::vector<std::pair<std::string, hipEvent_t>> ev;
     std::vector<std::pair<std::string, double>> host;
+    static hipEvent_t& ref() {
+        static hipEvent_t r = nullptr;
+        return r;
+    }
+    static std::chrono::steady_clock::time_point& href() {
+        static std::chrono::steady_clock::time_point t{};
+        return t;
+    }
     void start(hipStream_t s) {
         const char* e = getenv("MXEC_PIPE_TRACE");
         on = e && *e == '1';
         if (!on) return;
-        h0 = std::chrono::steady_clock::now();
-        (void)hipEventCreate(&e0);
-        (void)hipEventRecord(e0, s);
+        static std::mutex mu;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!ref()) {
+                hipStream_t rs = nullptr;
+                (void)hipStreamCreateWithFlags(&rs, hipStreamNonBlocking);
+                (void)hipEventCreate(&ref());
+                (void)hipEventRecord(ref(), rs);
+                (void)hipEventSynchronize(ref());
+                href() = std::chrono::steady_clock::now();
+            }
+        }
+        h0 = href();
+        e0 = ref();
+        mark("start", s);
+        now("start");
     }
     void mark(const char* what, hipStream_t s) {
         if (!on) return;
@@ -455,7 +492,6 @@ struct PipeTrace {
         }
         out += "]}";
         fprintf(stderr, "%s\n", out.c_str());
-        (void)hipEventDestroy(e0);
         ev.clear();
         host.clear();
     }
@@ -497,7 +533,7 @@ public:
                 desc += uint64_t(objs[e].k + objs[e].m) * 48 + 256;
                 ++e;
             }
-            MXEC_TRY(pool_.ensure(need));
+            MXEC_TRY(pool_.replace(need));  // no free while other calls run (retired until idle)
             MXEC_TRY(arena_.reserve(desc * 2));
             MXEC_TRY(wave(objs, o, e));
             o = e;
@@ -520,7 +556,7 @@ public:
                 desc += uint64_t(objs[e].k + objs[e].m) * 96 + 512 + (objs[e].S / 8192 + 2) * 32;
                 ++e;
             }
-            MXEC_TRY(pool_.ensure(need));
+            MXEC_TRY(pool_.replace(need));  // no free while other calls run (retired until idle)
             MXEC_TRY(arena_.reserve(desc * 2));
             MXEC_TRY(rec_wave(objs, o, e, data_only));
             o = e;
@@ -591,18 +627,39 @@ private:
         events_.push_back(*e);
         return MXEC_OK;
     }
+    // A bracket opens (watch_open) before its copies are queued, but its
+    // start event is recorded only after its first SDMA copy (watch_count),
+    // which it does not time: an event recorded on an idle copy stream
+    // completes at once, and the bracket would then time the host queueing
+    // the first copy too.
+    bool watch_on_ = false, dwatch_on_ = false;
     int watch_open() {
-        if (!watching() || watch_a_) return MXEC_OK;
-        MXEC_TRY(new_timed_event(&watch_a_));
-        MXEC_HIP(hipEventRecord(watch_a_, h2d_));
+        if (!watching() || watch_on_) return MXEC_OK;
+        watch_on_ = true;
+        watch_a_ = nullptr;
         watch_staged_ = false;
         watch_bytes_ = 0;
         watch_copies_ = 0;
         return MXEC_OK;
     }
+    // After an SDMA copy of `bytes` in `copies` DMAs (2D: rows) was queued.
+    int watch_count(bool down, uint64_t bytes, uint64_t copies) {
+        if (!(down ? dwatch_on_ : watch_on_)) return MXEC_OK;
+        hipEvent_t& a = down ? dwatch_a_ : watch_a_;
+        if (!a) {
+            MXEC_TRY(new_timed_event(&a));
+            MXEC_HIP(hipEventRecord(a, down ? d2h_ : h2d_));
+            return MXEC_OK;
+        }
+        (down ? dwatch_bytes_ : watch_bytes_) += bytes;
+        (down ? dwatch_copies_ : watch_copies_) += copies;
+        return MXEC_OK;
+    }
     // After the bracket's copies are issued (issue_up done).
     int watch_close() {
-        if (!watch_a_) return MXEC_OK;
+        if (!watch_on_) return MXEC_OK;
+        watch_on_ = false;
+        if (!watch_a_) return MXEC_OK;  // no SDMA copy to time
         hipEvent_t b = nullptr;
         MXEC_TRY(new_timed_event(&b));
         MXEC_HIP(hipEventRecord(b, h2d_));
@@ -612,25 +669,27 @@ private:
         watch_a_ = nullptr;
         return watch_poll();
     }
-    // Downloads (an RS-only GET's rebuilt shards, rebuild_down): the bracket
-    // opens after the d2h stream's wait for the rebuild (its first event
-    // marks when that wait let go), so it times the copies alone.  The PUT's
-    // parity downloads are not bracketed: in the seconds after a large HBM
-    // free, timing events among the PUT-with-digests pieces' downloads
-    // slowed that call by 63 % (0.336 s against 0.206 at 128 objects,
+    // Downloads (an RS-only GET's rebuilt shards, rebuild_list): the bracket
+    // opens after the d2h stream's wait for the rebuild, so it times the
+    // copies alone.  The PUT's parity downloads are not bracketed: in the
+    // seconds after a large HBM free, timing events among the
+    // PUT-with-digests pieces' downloads slowed that call by 63 % (0.336 s
+    // against 0.206 at 128 objects,
     // profiles/r5/copy_engine/auto_dwatch_churn60_r5l2.jsonl), and its SDMA
     // downloads otherwise beat waves (0.204 s against 0.238 fresh).
     bool dwatch_off_ = false;
     int dwatch_open() {
-        if (!watching(true) || dwatch_off_ || dwatch_a_) return MXEC_OK;
-        MXEC_TRY(new_timed_event(&dwatch_a_));
-        MXEC_HIP(hipEventRecord(dwatch_a_, d2h_));
+        if (!watching(true) || dwatch_off_ || dwatch_on_) return MXEC_OK;
+        dwatch_on_ = true;
+        dwatch_a_ = nullptr;
         dwatch_staged_ = false;
         dwatch_bytes_ = 0;
         dwatch_copies_ = 0;
         return MXEC_OK;
     }
     int dwatch_close() {
+        if (!dwatch_on_) return MXEC_OK;
+        dwatch_on_ = false;
         if (!dwatch_a_) return MXEC_OK;
         hipEvent_t b = nullptr;
         MXEC_TRY(new_timed_event(&b));
@@ -689,6 +748,7 @@ private:
     int watch_drain() {
         watch_a_ = nullptr;
         dwatch_a_ = nullptr;
+        watch_on_ = dwatch_on_ = false;
         while (!watch_.empty()) MXEC_TRY(watch_judge());
         return MXEC_OK;
     }
@@ -734,7 +794,7 @@ private:
         uint8_t* ok = nullptr;
         uint8_t* exp = nullptr;
         if (verify) {
-            MXEC_TRY(scratch_.ensure(fo + msgs * 32));
+            MXEC_TRY(scratch_.grow(fo + msgs * 32));
             ok = static_cast<uint8_t*>(scratch_.p);
             exp = ok + fo;
         }
@@ -764,8 +824,8 @@ private:
             // stream each: a second group's chains would queue behind the
             // first's on it).
             const std::vector<size_t> cut = verify_cuts(objs, o0, o1, up_bytes, longest_msg, down_bytes, spec || shared);
-            MXEC_TRY(state_.ensure(msgs * 32));
-            MXEC_TRY(flags_.ensure(msgs));
+            MXEC_TRY(state_.grow(msgs * 32));
+            MXEC_TRY(flags_.grow(msgs));
             std::vector<uint64_t> mbase(cut.size(), 0);
             for (size_t j = 1; j < cut.size(); ++j) {
                 mbase[j] = mbase[j - 1];
@@ -844,6 +904,15 @@ private:
     // Objects [o0, o1) of a speculatively rebuilt group whose present masks
     // the verdict left as they were (all but `changed`): their rebuilt
     // shards are already on their way down; status and present flags.
+    static bool spec_on_chain() {
+#ifdef MXEC_LAB
+        const char* e = getenv("MXEC_SPEC_ON_CHAIN");
+        return e && *e == '1';
+#else
+        return false;
+#endif
+    }
+
     int confirm(std::vector<RecObj>& objs, size_t o0, size_t o1, const std::vector<size_t>& changed, bool data_only) {
         size_t c = 0;
         for (size_t o = o0; o < o1; ++o) {
@@ -1061,8 +1130,11 @@ private:
     // encode -- and goes down to the caller's buffers.  Launch and downloads
     // both on the D2H stream, so the downloads follow the decode in order.
     // An object short of k present shards is skipped (it fails anyway).
+    // ds: the stream the decode runs on -- the D2H stream itself, or (lab
+    // MXEC_SPEC_ON_CHAIN=1) the group's chain stream behind the piece's hash,
+    // the downloads then waiting for it.
     int spec_piece(std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t off, uint64_t pw, hipEvent_t up,
-                   bool data_only) {
+                   bool data_only, hipStream_t ds) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         const size_t n = o1 - o0;
         std::vector<std::shared_ptr<const DecodePlan>> plans(n);
@@ -1113,12 +1185,20 @@ private:
                 pi += size_t(h.k);
                 po += size_t(r);
             }
-            return rs_groups.empty() ? MXEC_OK : run_rs_mixed(d_, slot_, d2h_, rs_groups, &arena_);
+            return rs_groups.empty() ? MXEC_OK : run_rs_mixed(d_, slot_, ds, rs_groups, &arena_);
         };
         MXEC_TRY(flush_down());
         MXEC_TRY(issue_down());  // wave copy blocks queued earlier go before the wait
-        MXEC_HIP(hipStreamWaitEvent(d2h_, up, 0));
-        MXEC_TRY(with_stable_coef(d_, d2h_, collect, launch));
+        if (ds == d2h_) {
+            MXEC_HIP(hipStreamWaitEvent(d2h_, up, 0));
+            MXEC_TRY(with_stable_coef(d_, d2h_, collect, launch));
+        } else {  // ds already waits for `up` (the piece's hash did)
+            MXEC_TRY(with_stable_coef(d_, ds, collect, launch));
+            hipEvent_t done;
+            MXEC_TRY(new_event(&done));
+            MXEC_HIP(hipEventRecord(done, ds));
+            MXEC_HIP(hipStreamWaitEvent(d2h_, done, 0));
+        }
         bool any = false;
         for (size_t t = 0; t < n; ++t) {
             if (!plans[t]) continue;
@@ -1132,6 +1212,7 @@ private:
             }
         }
         MXEC_TRY(flush_down());
+        PTRACE(mark("sdown", d2h_));
         if (any) ++d_.spec_pieces;
         return MXEC_OK;
     }
@@ -1202,7 +1283,7 @@ private:
             if (!sp.empty())
                 MXEC_TRY(run_sha_pieces(d_, slot_, cs, sp, sl, ss, st, state, pc > 0, nullptr, &arena_, exp, ok));
             PTRACE(mark("sha", cs));
-            if (spec) MXEC_TRY(spec_piece(objs, o0, o1, off, pw, up, data_only));
+            if (spec) MXEC_TRY(spec_piece(objs, o0, o1, off, pw, up, data_only, spec_on_chain() ? cs : d2h_));
             MXEC_TRY(pace(up));
         }
         paced_.clear();
@@ -1283,7 +1364,7 @@ private:
             MXEC_HIP(hipStreamWaitEvent(cs, up.back(), 0));
             if (!sp.empty()) {
                 MXEC_TRY(run_sha(d_, slot_, cs, sp, sl, nullptr, exp, ok, &idx, &arena_));
-                MXEC_TRY(flags_.ensure(sp.size()));
+                MXEC_TRY(flags_.grow(sp.size()));
                 MXEC_HIP(hipMemcpyAsync(flags_.p, ok, sp.size(), hipMemcpyDeviceToHost, cs));
                 MXEC_TRY(sync_point(cs));  // not the stream: another call's work may follow on it
                 const auto* okh = static_cast<const uint8_t*>(flags_.p);
@@ -1352,7 +1433,9 @@ private:
             if (q == hipSuccess) continue;
             (void)hipGetLastError();
             ++d_.pace_waits;
+            PTRACE(now("pace"));
             MXEC_HIP(hipEventSynchronize(e));
+            PTRACE(now("paced"));
         }
         return MXEC_OK;
     }
@@ -1411,9 +1494,7 @@ private:
         if (is_pinned(src, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, h2d_));
             ++d_.copies_1d;
-            watch_bytes_ += len;
-            ++watch_copies_;
-            return MXEC_OK;
+            return watch_count(false, len, 1);
         }
         watch_staged_ = true;  // host memcpy through the ring: not an SDMA rate
         for (uint64_t off = 0; off < len; off += kRingBuf) {
@@ -1498,10 +1579,8 @@ private:
             }
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyHostToDevice, h2d_));
             ++d_.copies_2d;
-            watch_bytes_ += r.len * r.rows;
-            watch_copies_ += r.rows;
             d_.copies_2d_rows += r.rows;
-            return MXEC_OK;
+            return watch_count(false, r.len * r.rows, r.rows);
         }
         for (uint64_t i = 0; i < r.rows; ++i) MXEC_TRY(upload(r.dst + i * r.dpitch, r.src + i * r.spitch, r.len));
         return MXEC_OK;
@@ -1525,10 +1604,8 @@ private:
             }
             MXEC_HIP(hipMemcpy2DAsync(r.dst, r.dpitch, r.src, r.spitch, r.len, r.rows, hipMemcpyDeviceToHost, d2h_));
             ++d_.copies_2d;
-            dwatch_bytes_ += r.len * r.rows;
-            dwatch_copies_ += r.rows;
             d_.copies_2d_rows += r.rows;
-            return MXEC_OK;
+            return watch_count(true, r.len * r.rows, r.rows);
         }
         for (uint64_t i = 0; i < r.rows; ++i) MXEC_TRY(download(r.dst + i * r.dpitch, r.src + i * r.spitch, r.len));
         return MXEC_OK;
@@ -1560,9 +1637,7 @@ private:
         if (is_pinned(dst, len)) {
             MXEC_HIP(hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToHost, d2h_));
             ++d_.copies_1d;
-            dwatch_bytes_ += len;
-            ++dwatch_copies_;
-            return MXEC_OK;
+            return watch_count(true, len, 1);
         }
         dwatch_staged_ = true;
         for (uint64_t off = 0; off < len; off += kRingBuf) {
@@ -1615,10 +1690,21 @@ private:
     // profiles/r5/get_groups/ramp_ab_final_r5ab.jsonl), and an upload-bound
     // wave loses to the extra copies (512 objects: 0.606 against 0.588,
     // ramp_*_r5u.jsonl), so wave() clears it and only chain-bound waves set it.
+    //
+    // While other calls share the device, they share its upload link too: the
+    // wave's upload is weighed as if it were the calls-in-flight times larger
+    // (a PUT with digests beside a verified GET, 128 x 4+2 x 10 MiB each:
+    // 10.7 GB over the link against a 191 ms chain, upload-bound, so 4 MiB
+    // pieces and 2D copies instead of 1 MiB ones at ~33 GB/s).
     uint64_t piece_bytes(uint64_t upload_bytes, uint64_t longest) {
         piece_ramp_ = 0;
         if (!d_.kn) return uint64_t(1) << 20;
         if (!d_.kn->pipe_piece_auto) return d_.kn->pipe_piece;
+        bool share = true;
+#ifdef MXEC_LAB
+        if (const char* e = getenv("MXEC_PIPE_SHARE_PIECES")) share = *e != '0';  // lab A/B
+#endif
+        if (share) upload_bytes *= uint64_t(std::max(1, hub_.calls.load()));
         const double chain_s = double(longest / 64) * kShaLagUsPerBlock * 1e-6;
         static constexpr struct {
             uint64_t bytes;
@@ -1652,7 +1738,7 @@ private:
                                    j < h.k ? std::min<uint64_t>(h.dlen[j], h.S) : h.S});
         }
         const uint64_t nm = ch.size();
-        MXEC_TRY(scratch_.ensure(nm * 64));  // digests [nm][32], then chain states [nm][8] words
+        MXEC_TRY(scratch_.grow(nm * 64));  // digests [nm][32], then chain states [nm][8] words
         uint8_t* digests = static_cast<uint8_t*>(scratch_.p);
         uint32_t* state = reinterpret_cast<uint32_t*>(digests + nm * 32);
         const PieceGrid grid(P, piece_ramp_);
@@ -1805,7 +1891,7 @@ private:
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
         uint64_t msgs = 0;
         for (size_t o = o0; o < o1; ++o) msgs += uint64_t(objs[o].k + objs[o].m);
-        MXEC_TRY(scratch_.ensure(msgs * 32));
+        MXEC_TRY(scratch_.grow(msgs * 32));
         uint8_t* digests = static_cast<uint8_t*>(scratch_.p);
         // Groups: consecutive objects up to kGroupBytes of input.
         std::vector<std::pair<size_t, size_t>> groups;

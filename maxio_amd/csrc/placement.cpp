@@ -1,0 +1,172 @@
+// placement.cpp — mxec_batch_alloc: HBM for a device-resident batch, placed
+// by measurement.
+//
+// The RS encode's rate over a configs[1] batch (4+2 x 10 MiB x 1024, 74 GB)
+// is a property of where the batch lies in HBM and of the shard stride
+// against that placement, not of the kernel (DESIGN_HISTORY R4
+// "RS against the float4 copy"; profiles/r4/placement_full/): on "fast"
+// allocations the kernel runs at 1.00 of the guide's float4 copy over its
+// own buffers, on "slow" ones at 0.93-0.96 at every grid; successive
+// allocations alternate between the two kinds, and which shard stride wins
+// flips with the kind (box 6: one kind 5.40-5.58 TB/s at pads <= 1 MiB and
+// 6.26 at 8 MiB, the other 6.24-6.29 up to 4 MiB).  The driver's round-5
+// box drew a slow one: 3 586 GiB/s = 0.72 of spec where fast boxes ran
+// 3 880-3 900.
+//
+// A caller that lets the library lay out its batch -- a long-lived process
+// allocating its device-resident batch buffers once -- gets the best of a few
+// measured candidates: up to two allocations (the second taken while the
+// first is held, so it lands elsewhere) times two shard strides, each timed
+// by the shipping encode itself over the whole candidate layout (default
+// grid, the grid tuner left alone; one warm launch and the faster of two
+// timed ones, ~11 ms each for configs[1]); the fastest is kept and the rest
+// freed.  Transiently up to twice the batch's bytes at the larger stride;
+// when the second allocation does not fit, one allocation's strides decide.
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "../../include/maxio_ec.h"
+#include "ops.hpp"
+
+using namespace mxec;
+
+namespace {
+
+// Shard pads tried: multi-MiB shards at the bench's round-2 pad (2 MiB +
+// 64 KiB: the shards of an object at different offsets modulo 2 MiB) and at
+// a 6 MiB pad (R4: a 16 MiB stride held 6.16-6.17 TB/s on both kinds of one
+// box); smaller shards at no pad and a 256 KiB pad.
+std::vector<uint64_t> candidate_pads(uint64_t S) {
+    if (S >= (uint64_t(4) << 20)) return {(uint64_t(2) << 20) + (uint64_t(64) << 10), uint64_t(6) << 20};
+    return {0, uint64_t(256) << 10};
+}
+
+struct Held {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+// Time one encode over [n][k+m][stride] at `base` (contents are whatever the
+// memory holds: the rate does not depend on the bytes).
+int probe(Device& d, Slot& slot, hipStream_t s, uint8_t* base, int k, int m, uint64_t S, uint64_t n,
+          uint64_t stride, float* ms_out) {
+    std::vector<const uint8_t*> in(size_t(n * k));
+    std::vector<uint8_t*> out(size_t(n * m));
+    std::vector<uint64_t> lens(size_t(n * (k + m)), S);
+    std::vector<RsObject> ro(static_cast<size_t>(n));
+    for (uint64_t o = 0; o < n; ++o) {
+        uint8_t* ob = base + o * uint64_t(k + m) * stride;
+        for (int j = 0; j < k; ++j) in[size_t(o * k + j)] = ob + uint64_t(j) * stride;
+        for (int i = 0; i < m; ++i) out[size_t(o * m + i)] = ob + uint64_t(k + i) * stride;
+        ro[size_t(o)] = RsObject{&in[size_t(o * k)], &lens[size_t(o * (k + m))], &out[size_t(o * m)],
+                                 &lens[size_t(o * (k + m) + k)], 0};
+    }
+    hipEvent_t a = nullptr, b = nullptr;
+    MXEC_HIP(hipEventCreate(&a));
+    if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        return set_error(MXEC_E_DEVICE, "hipEventCreate failed");
+    }
+    float best = 1e30f;
+    int rc = MXEC_OK;
+    for (int rep = 0; rep < 3 && rc == MXEC_OK; ++rep) {
+        uint32_t coff = 0;
+        if (hipEventRecord(a, s) != hipSuccess) rc = set_error(MXEC_E_DEVICE, "hipEventRecord failed");
+        if (rc == MXEC_OK)
+            rc = with_stable_coef(
+                d, s, [&] { return encode_coef(d, k, m, &coff); },
+                [&] {
+                    for (auto& r : ro) r.coef_off = coff;
+                    return run_rs(d, slot, s, S, k, m, ro, nullptr, /*tune=*/false);
+                });
+        if (rc == MXEC_OK && (hipEventRecord(b, s) != hipSuccess || hipEventSynchronize(b) != hipSuccess))
+            rc = set_error(MXEC_E_DEVICE, "probe launch failed");
+        float ms = 0;
+        if (rc == MXEC_OK && rep > 0 && hipEventElapsedTime(&ms, a, b) == hipSuccess) best = std::min(best, ms);
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms_out = best;
+    return rc;
+}
+
+std::mutex g_batches_mu;
+struct BatchRec {
+    void* p;
+    int dev;  // HIP device id
+};
+std::vector<BatchRec> g_batches;  // mxec_batch_alloc's live allocations
+
+}  // namespace
+
+extern "C" void* mxec_batch_alloc(mxec_ctx* ctx, int dev, int k, int m, uint64_t shard_size, uint64_t n_obj,
+                                  uint64_t* shard_stride, float* probe_ms) {
+    void* result = nullptr;
+    const int rc = guarded([&]() -> int {
+        if (!ctx || !shard_stride || n_obj == 0 || shard_size == 0)
+            return set_error(MXEC_E_INVALID_ARG, "mxec_batch_alloc: null context / output or empty batch");
+        MXEC_TRY(check_km(k, m));
+        DevScope ds;
+        MXEC_TRY(ds.open(ctx, dev));
+        Device& d = *ds.d;
+        hipStream_t s = ds.slot->stream;
+        const std::vector<uint64_t> pads = candidate_pads(shard_size);
+        const uint64_t max_pad = *std::max_element(pads.begin(), pads.end());
+        const size_t bytes = size_t(n_obj) * size_t(k + m) * size_t(shard_size + max_pad);
+        if (probe_ms)
+            for (int i = 0; i < 4; ++i) probe_ms[i] = -1.0f;
+        std::vector<Held> held;
+        int best_a = -1;
+        uint64_t best_stride = 0;
+        float best_ms = 1e30f;
+        int rc2 = MXEC_OK;
+        for (int attempt = 0; attempt < 2 && rc2 == MXEC_OK; ++attempt) {
+            Held h;
+            h.bytes = bytes;
+            if (hipMalloc(&h.p, bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                if (attempt == 0) rc2 = set_error(MXEC_E_OOM, "mxec_batch_alloc: hipMalloc failed");
+                break;  // no room for a second candidate: the first decides
+            }
+            held.push_back(h);
+            for (size_t c = 0; c < pads.size(); ++c) {
+                const uint64_t pad = pads[c];
+                float ms = 0;
+                rc2 = probe(d, *ds.slot, s, static_cast<uint8_t*>(h.p), k, m, shard_size, n_obj, shard_size + pad, &ms);
+                if (rc2 != MXEC_OK) break;
+                if (probe_ms) probe_ms[size_t(attempt) * pads.size() + c] = ms;
+                if (ms < best_ms) {
+                    best_ms = ms;
+                    best_a = int(held.size()) - 1;
+                    best_stride = shard_size + pad;
+                }
+            }
+        }
+        MXEC_HIP(hipStreamSynchronize(s));
+        for (int i = 0; i < int(held.size()); ++i)
+            if (i != best_a || rc2 != MXEC_OK) (void)hipFree(held[size_t(i)].p);
+        MXEC_TRY(rc2);
+        result = held[size_t(best_a)].p;
+        *shard_stride = best_stride;
+        std::lock_guard<std::mutex> g(g_batches_mu);
+        g_batches.push_back(BatchRec{result, d.id});
+        return MXEC_OK;
+    });
+    return rc == MXEC_OK ? result : nullptr;
+}
+
+extern "C" int mxec_batch_free(mxec_ctx* ctx, void* p) {
+    return guarded([&]() -> int {
+        if (!ctx || !p) return set_error(MXEC_E_INVALID_ARG, "mxec_batch_free: null argument");
+        {
+            std::lock_guard<std::mutex> g(g_batches_mu);
+            auto it = std::find_if(g_batches.begin(), g_batches.end(), [&](const BatchRec& b) { return b.p == p; });
+            if (it == g_batches.end()) return set_error(MXEC_E_INVALID_ARG, "mxec_batch_free: not a batch allocation");
+            MXEC_HIP(hipSetDevice(it->dev));
+            g_batches.erase(it);
+        }
+        MXEC_HIP(hipFree(p));
+        return MXEC_OK;
+    });
+}

@@ -45,6 +45,21 @@ int DevBuf::grow(size_t n) {
     return MXEC_OK;
 }
 
+int DevBuf::replace(size_t n) {
+    if (n <= cap && p) return MXEC_OK;
+    void* q = nullptr;
+    MXEC_HIP(hipMalloc(&q, n < 4096 ? 4096 : n));
+    if (p) retired.push_back(p);
+    p = q;
+    cap = n < 4096 ? 4096 : n;
+    return MXEC_OK;
+}
+
+void DevBuf::free_retired() {
+    for (void* q : retired) (void)hipFree(q);
+    retired.clear();
+}
+
 void DevBuf::release() {
     if (p) (void)hipFree(p);
     for (void* q : retired) (void)hipFree(q);

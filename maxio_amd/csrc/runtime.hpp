@@ -52,6 +52,11 @@ struct DevBuf {
     std::vector<void*> retired;
     int ensure(size_t n);
     int grow(size_t n);
+    // At least n bytes, exactly n when it re-sizes; the old buffer is retired
+    // (no free, so no device-wide wait while other work runs) until
+    // free_retired() or release().
+    int replace(size_t n);
+    void free_retired();
     void release();
     ~DevBuf() { release(); }
     static constexpr size_t kGrowFloor = size_t(1) << 20;
@@ -343,12 +348,17 @@ struct DescArena {
     size_t cur = 0;   // block being filled
     size_t used = 0;  // bytes used in it
     uint64_t grown = 0;  // blocks chained beyond the first, over the arena's life (stats)
-    // Start a wave: the first block holds at least `bytes`; everything is free.
+    // Start a wave: the first block holds at least `bytes`; everything is
+    // free.  A first block too small is not re-sized (a free waits for the
+    // whole device, and concurrent host-batch calls share it): a new one of
+    // `bytes` goes in front, the old ones stay chained behind it.
     int reserve(size_t bytes) {
-        if (blocks.empty()) blocks.emplace_back(new Block());
-        Block& b = *blocks[0];
-        MXEC_TRY(b.host.ensure(bytes));
-        MXEC_TRY(b.dev.ensure(bytes));
+        if (blocks.empty() || blocks[0]->host.cap < bytes || blocks[0]->dev.cap < bytes) {
+            std::unique_ptr<Block> b(new Block());
+            MXEC_TRY(b->host.ensure(bytes));
+            MXEC_TRY(b->dev.ensure(bytes));
+            blocks.insert(blocks.begin(), std::move(b));
+        }
         cur = 0;
         used = 0;
         return 0;

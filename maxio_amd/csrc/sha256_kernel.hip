@@ -1036,8 +1036,13 @@ constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 // only (`make lab`, -DMXEC_LAB).
 constexpr int kShaQuadAuto = 6;
 // K + W read groups of the auto form's consumers (sha256_quad_kernel LDG;
-// lab builds A/B it with MXEC_SHA_LDG=1|2|4).
-constexpr int kShaLdg = 4;
+// lab builds A/B it with MXEC_SHA_LDG=1|2|4).  Spreading the next block's
+// reads over the block lost: 10 240 x 1 MiB took
+// 22.0 ms with two groups and 22.4 with four against 19.6 with all 16 reads
+// after the barrier, on one box in interleaved fresh processes
+// (profiles/r6/sha_ldg_ab.jsonl; ~30 cycles of the wave's in-order issue
+// per ds_read_b128 placed among the chain's VALU, against ~20 in the burst).
+constexpr int kShaLdg = 1;
 
 #ifdef MXEC_LAB
 // MXEC_SHA_SPLIT_BUFS=2: the split form's one-ahead K+W ring (lab A/B; read

@@ -242,6 +242,21 @@ class Context:
         self._host[p] = fin
         return a
 
+    def batch_alloc(self, k: int, m: int, shard_size: int, n_obj: int, dev: int = 0):
+        """mxec_batch_alloc: HBM for a device-resident batch laid out
+        [n_obj][k+m][shard_stride], placed by measurement.  Returns (device
+        pointer, shard_stride, the candidates' probe times in ms).  Free with
+        batch_free()."""
+        stride = ctypes.c_uint64(0)
+        ms = (ctypes.c_float * 4)()
+        p = self._lib.mxec_batch_alloc(self._h, dev, k, m, shard_size, n_obj, ctypes.byref(stride), ms)
+        if not p:
+            raise RSError(-31, self._lib.mxec_last_error().decode(errors="replace"))
+        return p, stride.value, [round(x, 4) for x in ms]
+
+    def batch_free(self, p: int) -> None:
+        _check(self._lib.mxec_batch_free(self._h, p))
+
     def host_free(self, a: np.ndarray) -> None:
         """Free a host_array now (the array must not be used afterwards)."""
         fin = self._host.pop(a.ctypes.data, None)

@@ -164,6 +164,9 @@ extern "C" {
                                fence_waits: *mut u64) -> c_int;
     pub fn mxec_host_alloc(ctx: *mut MxecCtx, bytes: usize) -> *mut c_void;
     pub fn mxec_host_alloc_device(ctx: *mut MxecCtx, dev: c_int, bytes: usize) -> *mut c_void;
+    pub fn mxec_batch_alloc(ctx: *mut MxecCtx, dev: c_int, k: c_int, m: c_int, shard_size: u64, n_obj: u64,
+                            shard_stride: *mut u64, probe_ms: *mut f32) -> *mut c_void;
+    pub fn mxec_batch_free(ctx: *mut MxecCtx, p: *mut c_void) -> c_int;
     pub fn mxec_host_free(ctx: *mut MxecCtx, p: *mut c_void);
     pub fn mxec_rs_check(k: c_int, m: c_int) -> c_int;
     pub fn mxec_rs_parity_matrix(k: c_int, m: c_int, out: *mut u8) -> c_int;

@@ -28,6 +28,8 @@
 #             effective clock per kernel (tools/clock_summary.py)
 #   rust      probe for rustc / cargo
 #   cfg:<c>   python bench.py --config <c> --no-extra -> cfg_<c>.json
+#   exitprobe tools/exit_probe.py host_pageable under rocprofv3 --kernel-trace
+#             --memory-copy-trace (the round-5 exit fault); last in a call
 #   pyt:<f+f> the named test files only (tests/<f>.py, `+`-separated), -m gpu
 #             -> pytest_<first>.log
 #   tool:<t>  python tools/<t>.py $TOOL_ARGS_<t> (else $TOOL_ARGS) -> <t>.jsonl
@@ -141,6 +143,16 @@ for st in "${STEPS[@]}"; do
       timeout -k 10 "${TOOL_TIMEOUT:-600}" python -u "tools/$t.py" $targs > "$O/$t.jsonl" 2> "$O/$t.err" \
         || { tail -20 "$O/$t.err"; exit 1; }
       cat "$O/$t.jsonl" ;;
+    exitprobe)
+      # one pageable host batch under the profiler options
+      # whose teardown faulted in round 5 (tools/exit_probe.py).  Run it last:
+      # a non-zero exit (139) ends the call.
+      ( cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/exitprobe -o run \
+          --output-format csv -- python3 "$R/tools/exit_probe.py" host_pageable > "$O/exit_pageable.out" \
+          2> "$O/exit_pageable.err" ); rc=$?
+      echo "{\"what\": \"host_pageable under rocprofv3 --kernel-trace --memory-copy-trace\", \"rc\": $rc}" \
+        | tee -a "$O/exit_probe.jsonl"
+      [ "$rc" = 0 ] || exit 1 ;;
     cfg:*)
       c="${st#cfg:}"
       timeout -k 10 900 python bench.py --config "$c" --no-extra $BENCH_ARGS > "$O/cfg_$c.json" 2> "$O/cfg_$c.err" || { tail -20 "$O/cfg_$c.err"; exit 1; }

@@ -40,10 +40,10 @@ def _random(ctx, shape, seed):
     return a
 
 
-def _put_and_check(ctx, n, S, seed, short=None, digests=True, check=True):
+def _put_and_check(ctx, n, S, seed, short=None, digests=True, defer=False):
     """n x 4+2 objects of shard size S from host_array memory, PUT with
     digests (or without: the group form); `short` maps object -> length of
-    its last data chunk.  Returns the copy-statistics delta (check=False:
+    its last data chunk.  Returns the copy-statistics delta (defer=True:
     (delta, a function that checks the objects and frees the buffers))."""
     k, m = 4, 2
     short = short or {}
@@ -83,7 +83,7 @@ def _put_and_check(ctx, n, S, seed, short=None, digests=True, check=True):
         ctx.host_free(par)
 
     delta = {key: after[key] - before[key] for key in after}
-    if not check:
+    if defer:
         return delta, check_all
     check_all()
     return delta
@@ -172,9 +172,9 @@ def test_auto_copy_engine_follows_the_sdma_watch(floor, waves):
     S = 3 * M + 4096 + 48
     try:
         s0 = ctx.pipe_stats()
-        _, check1 = _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333}, digests=False, check=False)
+        _, check1 = _put_and_check(ctx, 8, S, 1300 + len(floor), short={3: S - 3333}, digests=False, defer=True)
         s1 = ctx.pipe_stats()
-        _, check2 = _put_and_check(ctx, 8, S, 1400 + len(floor), digests=False, check=False)
+        _, check2 = _put_and_check(ctx, 8, S, 1400 + len(floor), digests=False, defer=True)
         s2 = ctx.pipe_stats()
         check1()
         check2()

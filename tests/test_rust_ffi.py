@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "maxio_ec.h")
 RUST = os.path.join(ROOT, "rust", "maxio-ec-sys", "src", "lib.rs")
 
-C_SCALAR = {"int": "i32", "int32_t": "i32", "uint32_t": "u32", "uint64_t": "u64", "int64_t": "i64",
+C_SCALAR = {"int": "i32", "float": "f32", "int32_t": "i32", "uint32_t": "u32", "uint64_t": "u64", "int64_t": "i64",
             "size_t": "usize", "uint8_t": "u8", "char": "i8", "void": "void"}
 R_SCALAR = {"c_int": "i32", "i32": "i32", "u32": "u32", "u64": "u64", "i64": "i64", "usize": "usize",
             "u8": "u8", "c_char": "i8", "c_void": "void"}
