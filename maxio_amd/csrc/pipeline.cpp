@@ -221,9 +221,10 @@ std::vector<uint32_t> deal_batch(const Ctx& c, const std::vector<uint64_t>& byte
 // at once, admitted while the pool bytes of the calls in flight stay within
 // kPoolCap (a lone call is always admitted).  Their waves interleave on the
 // same streams:
-//   * each call that runs SHA-256 chains takes the compute stream fewer
-//     chains use (chain_users), so a PUT's chains and a GET's run side by
-//     side instead of one queueing behind the other on one stream;
+//   * each call takes the compute stream fewer calls in flight use (use())
+//     and queues all its kernels there, so a PUT's chains and a GET's run
+//     side by side instead of one queueing behind the other, and no call's
+//     RS piece waits behind another call's chain piece;
 //   * a call that finds another in flight paces its enqueue (pace()): it
 //     queues a piece (or group) only after its own piece kPaceDepth back
 //     is up, so the streams, which run in submission order, carry the calls'
@@ -240,7 +241,7 @@ struct PipeHub {
     std::vector<PipeLane*> idle;
     int in_flight = 0;            // calls holding a lane
     uint64_t admitted_bytes = 0;  // their pool bytes
-    int chain_users[kComputeStreams] = {0, 0};
+    int users[kComputeStreams] = {0, 0};  // calls in flight per compute stream (use())
     std::atomic<int> calls{0};    // in_flight, readable without the lock
     bool ready = false;
     int init(const Device& dev) {
@@ -299,38 +300,41 @@ struct PipeHub {
         }
         cv.notify_all();
     }
-    // The compute stream fewer chain-running calls use (ties: `prefer`),
-    // counted until unchain().
-    int chain(int prefer) {
+    // The compute stream fewer calls in flight use (ties: `prefer`), counted
+    // until unuse().  A call puts all its kernels there (its SHA-256 chains
+    // and its RS launches; a verified GET's speculative decodes go on the
+    // D2H stream): a kernel queued on a stream another call's chains use
+    // waits for that call's chain pieces (a PUT's RS pieces behind a GET's
+    // 4 MiB chain pieces held the PUT's chain to the GET's pace: the pair
+    // ran 0.45-0.48 s, no faster than the two calls one after the other).
+    int use(int prefer) {
         std::lock_guard<std::mutex> g(mu);
-        const int c = chain_users[1 - prefer] < chain_users[prefer] ? 1 - prefer : prefer;
-        ++chain_users[c];
+        const int c = users[1 - prefer] < users[prefer] ? 1 - prefer : prefer;
+        ++users[c];
         return c;
     }
-    void unchain(int c) {
+    void unuse(int c) {
         std::lock_guard<std::mutex> g(mu);
-        --chain_users[c];
-    }
-    // The compute stream with fewer chain users (ties: `prefer`), not counted.
-    int lighter(int prefer) {
-        std::lock_guard<std::mutex> g(mu);
-        return chain_users[1 - prefer] < chain_users[prefer] ? 1 - prefer : prefer;
+        --users[c];
     }
     // Plain non-blocking streams.  Lab builds can put the copy streams on a
     // few masked CUs and the compute streams on the rest
     // (MXEC_PIPE_COPY_CUS = n; measured no different from unmasked at the
     // wave copies' 16 workgroups, profiles/r4/get_stall/) or at different
-    // priorities (MXEC_PIPE_COPY_PRIO 1 = copies highest, 2 = compute).
+    // priorities (MXEC_PIPE_COPY_PRIO 1 = copies highest, 2 = compute, 3 =
+    // all four: the high-priority queue pool, apart from the process's
+    // GPU_MAX_HW_QUEUES normal ones).
     int create_streams(const Device& dev) {
 #ifdef MXEC_LAB
         const bool waves = dev.kn && dev.kn->pipe_copy != 0;
         const char* ce = getenv("MXEC_PIPE_COPY_CUS");
         const char* pe = getenv("MXEC_PIPE_COPY_PRIO");
-        const int prio_mode = waves && pe ? atoi(pe) : 0;
-        if (prio_mode == 1 || prio_mode == 2) {
+        const int prio_mode = pe ? atoi(pe) : 0;
+        (void)waves;
+        if (prio_mode >= 1 && prio_mode <= 3) {
             int least = 0, greatest = 0;
             MXEC_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            const int pc = prio_mode == 1 ? greatest : least, pk = prio_mode == 2 ? greatest : least;
+            const int pc = prio_mode != 2 ? greatest : least, pk = prio_mode >= 2 ? greatest : least;
             MXEC_HIP(hipStreamCreateWithPriority(&h2d, hipStreamNonBlocking, pc));
             MXEC_HIP(hipStreamCreateWithPriority(&d2h, hipStreamNonBlocking, pc));
             for (auto& s : cs) MXEC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, pk));
@@ -346,6 +350,18 @@ struct PipeHub {
             MXEC_HIP(hipExtStreamCreateWithCUMask(&h2d, uint32_t(cm.size()), cm.data()));
             MXEC_HIP(hipExtStreamCreateWithCUMask(&d2h, uint32_t(cm.size()), cm.data()));
             for (auto& s : cs) MXEC_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(rm.size()), rm.data()));
+            return MXEC_OK;
+        }
+        if (const char* e = getenv("MXEC_PIPE_SPLIT_CUS"); e && *e == '1') {  // lab A/B
+            // The two compute streams on complementary halves of the CUs (even
+            // / odd): two calls' SHA-256 chains, each a few workgroups, never
+            // share a CU (side by side on one CU each runs at half speed).
+            std::vector<uint32_t> ev(size_t((n + 31) / 32), 0u), od(ev.size(), 0u);
+            for (int i = 0; i < n; ++i) (i % 2 ? od : ev)[size_t(i / 32)] |= 1u << (i % 32);
+            MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+            MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+            MXEC_HIP(hipExtStreamCreateWithCUMask(&cs[0], uint32_t(ev.size()), ev.data()));
+            MXEC_HIP(hipExtStreamCreateWithCUMask(&cs[1], uint32_t(od.size()), od.data()));
             return MXEC_OK;
         }
         if (const char* e = getenv("MXEC_PIPE_OWN_QUEUES"); e && *e == '1') {  // lab A/B
@@ -508,7 +524,7 @@ public:
           pool_(l.pool), scratch_(l.digests), state_(l.chain_state), flags_(l.flags), slot_(l.desc_slot),
           hub_(h), cap_(std::max<uint64_t>(l.admitted, 1)) {}
     ~DevicePipeline() {
-        if (chain_ >= 0) hub_.unchain(chain_);
+        if (cs_idx_ >= 0) hub_.unuse(cs_idx_);
         for (auto e : events_) (void)hipEventDestroy(e);
     }
 
@@ -523,6 +539,7 @@ public:
     // against 0.263 by waves).
     int run(std::vector<HostObj>& objs) {
         start_copy_mode();
+        cs_idx_ = hub_.use(1);
         size_t o = 0;
         while (o < objs.size()) {  // waves that fit the pool
             uint64_t need = 0, desc = 1 << 20;
@@ -544,6 +561,7 @@ public:
     // Host reconstruct batch: waves that fit the pool, as run().
     int run_rec(std::vector<RecObj>& objs, bool data_only) {
         start_copy_mode();
+        cs_idx_ = hub_.use(0);
         size_t o = 0;
         while (o < objs.size()) {
             uint64_t need = 0, desc = 1 << 20;
@@ -832,7 +850,6 @@ private:
                 for (size_t o = cut[j - 1]; o < cut[j]; ++o) mbase[j] += uint64_t(objs[o].k + objs[o].m);
             }
             const size_t G = cut.size() - 1;
-            if (chain_ < 0) chain_ = hub_.chain(0);
             // auto: a chain-bound wave verified as one group uploads by waves
             // (one copy launch per piece instead of a DMA per piece of every
             // shard: 128 x 4+2 x 10 MiB 0.240 s against 0.256 by SDMA, 256
@@ -852,7 +869,7 @@ private:
             // so they keep SDMA.
             std::vector<hipEvent_t> verdict(G, nullptr);
             auto enqueue = [&](size_t j) {
-                return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], P, cs_[(chain_ + int(j)) & 1],
+                return verify_enqueue(objs, cut[j], cut[j + 1], ok, exp, mbase[j], P, cs_[(cs_idx_ + int(j)) & 1],
                                       &verdict[j], spec, data_only);
             };
             MXEC_TRY(enqueue(0));
@@ -874,7 +891,7 @@ private:
                 } else {
                     if (auto_copy && !shared) down_waves_ = down_before || j + 1 == G;
                     for (const auto& q : object_groups(objs, cut[j], cut[j + 1]))
-                        MXEC_TRY(rebuild_range(objs, q.first, q.second, cs_[(chain_ + int(j)) & 1], nullptr, data_only));
+                        MXEC_TRY(rebuild_range(objs, q.first, q.second, cs_[(cs_idx_ + int(j)) & 1], nullptr, data_only));
                 }
             }
             d_.verify_groups += G;
@@ -882,8 +899,7 @@ private:
             if (up_override) waves_now_ = up_before;  // only the override is undone
         } else {
             const auto groups = object_groups(objs, o0, o1);
-            if (verify && chain_ < 0) chain_ = hub_.chain(0);
-            hipStream_t cs = cs_[verify ? chain_ : hub_.lighter(0)];
+            hipStream_t cs = cs_[cs_idx_];
             std::vector<hipEvent_t> up;  // per group: its upload is done
             MXEC_TRY(upload_and_verify(objs, o0, o1, groups, ok, exp, verify, cs, &up));
             // Per group, rebuild once it is up (without verification, as soon
@@ -1397,7 +1413,7 @@ private:
     Slot& slot_;
     PipeHub& hub_;
     const uint64_t cap_;  // pool bytes per wave (the lane's admission)
-    int chain_ = -1;      // the compute stream this call's SHA-256 chains run on (PipeHub::chain)
+    int cs_idx_ = -1;     // the compute stream this call's kernels run on (PipeHub::use)
     std::vector<Pending> pend_;
     std::vector<hipEvent_t> events_;
 
@@ -1743,13 +1759,10 @@ private:
         uint32_t* state = reinterpret_cast<uint32_t*>(digests + nm * 32);
         const PieceGrid grid(P, piece_ramp_);
         const uint64_t npieces = grid.count(longest);
-        // The chains on the compute stream fewer other calls' chains use, RS
-        // on the other one -- or, when another call shares the device, on
-        // the chains' own stream (ahead of each piece's hash), so that no
-        // piece of this call waits behind the other call's chains.
-        if (nm && chain_ < 0) chain_ = hub_.chain(1);
-        const int sc = nm ? chain_ : hub_.lighter(1);
-        hipStream_t sha_s = cs_[sc], rs_s = shared_now() && nm ? sha_s : cs_[1 - sc];
+        // RS and the chains on the call's compute stream (PipeHub::use): each
+        // piece's RS ahead of its hash, so no piece of this call waits behind
+        // another call's chains.
+        hipStream_t sha_s = cs_[cs_idx_], rs_s = sha_s;
         hipEvent_t sha_done = nullptr;
         struct TwoD {  // 2D piece copies for this wave's SDMA copies (queue_up)
             bool& f;
@@ -1911,9 +1924,7 @@ private:
         std::vector<hipEvent_t> done(groups.size());
         bool any_dig = false;
         for (size_t o = o0; o < o1; ++o) any_dig = any_dig || objs[o].dig;
-        if (any_dig && chain_ < 0) chain_ = hub_.chain(1);
-        const int sc = any_dig ? chain_ : hub_.lighter(1);
-        hipStream_t rs_s = cs_[1 - sc], sha_s = cs_[sc];
+        hipStream_t rs_s = cs_[cs_idx_], sha_s = rs_s;
         // Each group's parity down: group by group after phase 1 (a lone
         // call queues all of phase 1 at once); while another call shares the
         // device, right behind the group's RS, since the paced phase 1 would

@@ -28,6 +28,8 @@
 #             effective clock per kernel (tools/clock_summary.py)
 #   rust      probe for rustc / cargo
 #   cfg:<c>   python bench.py --config <c> --no-extra -> cfg_<c>.json
+#   pmc5      FETCH_SIZE / WRITE_SIZE passes over config 5's step (grouped /
+#             multi-r RS launches) -> r6_pmc_cfg5_grouped_traffic.json
 #   exitprobe tools/exit_probe.py host_pageable under rocprofv3 --kernel-trace
 #             --memory-copy-trace (the round-5 exit fault); last in a call
 #   pyt:<f+f> the named test files only (tests/<f>.py, `+`-separated), -m gpu
@@ -143,6 +145,17 @@ for st in "${STEPS[@]}"; do
       timeout -k 10 "${TOOL_TIMEOUT:-600}" python -u "tools/$t.py" $targs > "$O/$t.jsonl" 2> "$O/$t.err" \
         || { tail -20 "$O/$t.err"; exit 1; }
       cat "$O/$t.jsonl" ;;
+    pmc5)
+      # config 5's step (grouped / multi-r launches) under FETCH_SIZE and
+      # WRITE_SIZE passes, one run each: 1 warmup + 3 timed steps
+      for c in FETCH_SIZE WRITE_SIZE; do
+        ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex rs_apply -d "/tmp/pmc5/$c" -o run \
+            --output-format csv -- python3 "$R/bench.py" --config 5 --steps 3 --warmup 1 --cpu-seconds 0 --no-extra \
+            --no-e2e > "$O/pmc5_$c.log" 2>&1 ) || { tail -5 "$O/pmc5_$c.log"; exit 1; }
+        find "/tmp/pmc5/$c" -name "*counter_collection.csv" -exec cp {} "$O/pmc5_$c.csv" \;
+      done
+      python tools/pmc_step_summary.py "$O/pmc5_FETCH_SIZE.csv" "$O/pmc5_WRITE_SIZE.csv" "$O/pmc5_FETCH_SIZE.log" \
+        --blocks-per-cu 512 --out "$O/r6_pmc_cfg5_grouped_traffic.json" || exit 1 ;;
     exitprobe)
       # one pageable host batch under the profiler options
       # whose teardown faulted in round 5 (tools/exit_probe.py).  Run it last:
