@@ -238,6 +238,10 @@ mxec_ctx* open_ctx(uint32_t device_mask, int streams_per_device, const Knobs& kn
                 }
                 dev->slots.push_back(std::move(slot));
             }
+            if (ok && pipe_open(*dev) != MXEC_OK) {
+                for (auto& sl : dev->slots) slot_destroy(*sl);
+                ok = false;
+            }
             if (ok) ctx->c.devs.push_back(std::move(dev));
         }
         if (ctx->c.devs.empty()) {

@@ -172,6 +172,10 @@ struct DevScope {
 int run_body_sums(Device& d, Slot& slot, hipStream_t s, const std::vector<const uint8_t*>& ptrs,
                   const std::vector<uint64_t>& lens, uint32_t which, uint8_t* out_dev, uint64_t stride);
 
+// Creates the device's host-pipeline hub and its streams (pipeline.cpp),
+// called by mxec_open for every device.
+int pipe_open(Device& dev);
+
 // filesystem.rs:1095 guard, then the crate's ReedSolomon::new checks.
 int check_km(int k, int m);
 

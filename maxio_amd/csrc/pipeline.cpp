@@ -374,12 +374,33 @@ struct PipeHub {
             for (auto& s : cs) MXEC_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(all.size()), all.data()));
             return MXEC_OK;
         }
+        if (const char* e = getenv("MXEC_PIPE_NORMAL_PRIO"); e && *e == '1') {  // lab A/B: round 5's streams
+            MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+            MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+            for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            return MXEC_OK;
+        }
 #else
         (void)dev;
 #endif
-        MXEC_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
-        MXEC_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
-        for (auto& s : cs) MXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        // The highest stream priority, created when the context opens
+        // (pipe_open): HIP serves a process's streams from GPU_MAX_HW_QUEUES
+        // (4) hardware queues per priority, and normal-priority streams --
+        // the context's slots, the table stream, torch's -- already share
+        // them.  Two of the pipeline's streams on one queue serialise
+        // across it: with a GET's chain stream and the D2H stream on one
+        // queue every hash piece waited for the previous piece's speculative
+        // decode and download (26 ms per 1 MiB piece against 19;
+        // profiles/r6/).  The high-priority pool is empty at mxec_open, so
+        // the four streams get four queues; the compute streams are created
+        // first, so the SHA-256 combiner's high-priority streams (created
+        // on its first use) share the compute streams' queues, never a copy
+        // stream's.
+        int least = 0, greatest = 0;
+        MXEC_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        for (auto& s : cs) MXEC_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest));
+        MXEC_HIP(hipStreamCreateWithPriority(&h2d, hipStreamNonBlocking, greatest));
+        MXEC_HIP(hipStreamCreateWithPriority(&d2h, hipStreamNonBlocking, greatest));
         return MXEC_OK;
     }
     // Context close (mxec_close, after the device is idle): the lanes'
@@ -859,7 +880,10 @@ private:
             // profiles/r5/copy_engine/verified_uploads_r5z.jsonl), and so does
             // a call that shares the device.
             const bool up_before = waves_now_;
-            const bool up_override = auto_copy && G == 1 && piece_ramp_ && !shared;
+            bool up_override = auto_copy && G == 1 && piece_ramp_ && !shared;
+#ifdef MXEC_LAB
+            if (const char* e = getenv("MXEC_GET_WAVE_UPLOADS"); e && *e == '0') up_override = false;  // lab A/B
+#endif
             if (up_override) waves_now_ = true;
             // Without speculation the last group's rebuilt shards (on the
             // critical path, alone on the link) go down by waves, earlier
@@ -1490,7 +1514,20 @@ private:
         return MXEC_OK;
     }
     int issue_up() { return issue_blocks(up_blks_, false, h2d_); }
-    int issue_down() { return issue_blocks(down_blks_, true, d2h_); }
+    int issue_down() {
+        MXEC_TRY(issue_blocks(down_blks_, true, d2h_));
+        return mark_d2h();
+    }
+    // This call's newest work on the D2H stream, re-recorded after each of
+    // its enqueues there: the call's end waits for it, not for a fresh event
+    // behind the other calls' downloads queued since (a verified GET beside a
+    // PUT ended with the PUT's parity downloads, ~100 ms after its own).
+    hipEvent_t d2h_mark_ = nullptr;
+    int mark_d2h() {
+        if (!d2h_mark_) MXEC_TRY(new_event(&d2h_mark_));
+        MXEC_HIP(hipEventRecord(d2h_mark_, d2h_));
+        return MXEC_OK;
+    }
     std::vector<CopyBlk> up_blks_, down_blks_;
     // Workgroups per copy launch: few, so the copy's host loads in flight do
     // not queue ahead of the SHA-256 chains' HBM loads (128 slowed the chains
@@ -1609,6 +1646,10 @@ private:
         return MXEC_OK;
     }
     int flush_down() {
+        MXEC_TRY(flush_down_run());
+        return mark_d2h();
+    }
+    int flush_down_run() {
         const Run r = down_run_;
         down_run_ = Run{};
         if (!r.len) return MXEC_OK;
@@ -1670,8 +1711,8 @@ private:
     }
 
     int flush() {
-        MXEC_TRY(issue_down());
-        MXEC_TRY(sync_point(d2h_));
+        MXEC_TRY(issue_down());  // marks
+        MXEC_HIP(hipEventSynchronize(d2h_mark_));
         for (auto& p : pend_) std::memcpy(p.dst, out_.ptr(p.ring), p.len);
         pend_.clear();
         out_.release_all();
@@ -1720,7 +1761,8 @@ private:
 #ifdef MXEC_LAB
         if (const char* e = getenv("MXEC_PIPE_SHARE_PIECES")) share = *e != '0';  // lab A/B
 #endif
-        if (share) upload_bytes *= uint64_t(std::max(1, hub_.calls.load()));
+        const int calls = std::max(1, hub_.calls.load());
+        if (share) upload_bytes *= uint64_t(calls);
         const double chain_s = double(longest / 64) * kShaLagUsPerBlock * 1e-6;
         static constexpr struct {
             uint64_t bytes;
@@ -1731,6 +1773,12 @@ private:
                 piece_ramp_ = uint64_t(256) << 10;
                 return s.bytes;
             }
+        // Upload-bound.  A wave that shares the link still ramps: its first
+        // pieces go up between the other call's, so both calls' chains start
+        // early (without, a GET's first 4 MiB piece -- 2 GB for 128 x 4+2 --
+        // held a PUT's first piece back 45 ms, and the PUT's chain set the
+        // pair's end).
+        if (share && calls > 1) piece_ramp_ = uint64_t(256) << 10;
         return uint64_t(4) << 20;
     }
     uint64_t piece_ramp_ = 0;  // first piece of the current wave's ramp (0: none)
@@ -1896,7 +1944,7 @@ private:
                 longest_msg = std::max(longest_msg, objs[o].S);
             }
             const uint64_t P = piece_bytes(up_bytes, longest_msg);
-            piece_ramp_ = 0;  // the PUT keeps uniform pieces (the ramp cost it 5-9 %, below)
+            if (!shared_now()) piece_ramp_ = 0;  // a lone PUT keeps uniform pieces (the ramp cost it 5-9 %, below)
             if (P && msgs && msgs <= uint64_t(kShaLagMsgs) * uint64_t(d_.n_cus ? d_.n_cus : 256))
                 return wave_pieces(objs, o0, o1, P);
         }
@@ -2043,6 +2091,16 @@ private:
 }  // namespace mxec
 
 using namespace mxec;
+
+namespace mxec {
+// The device's pipeline hub and its four streams, at context open (their
+// hardware queues depend on what the process created before them).
+int pipe_open(Device& dev) {
+    std::lock_guard<std::mutex> g(dev.pipe_mu);
+    if (!dev.pipe) dev.pipe = std::make_shared<PipeHub>();
+    return static_cast<PipeHub*>(dev.pipe.get())->init(dev);
+}
+}  // namespace mxec
 
 extern "C" int mxec_encode_batch_host(mxec_ctx* ctx, const mxec_object* objs, uint64_t n_obj,
                                       const uint8_t* const* data, const uint64_t* data_len,
