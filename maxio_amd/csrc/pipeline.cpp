@@ -1456,26 +1456,39 @@ private:
         MXEC_HIP(hipEventSynchronize(e));
         return MXEC_OK;
     }
-    // While another call shares the device, queue a piece (or group) only
-    // once this call's piece kPaceDepth back is up: the shared streams run
-    // in submission order, and a call that queued all its pieces at once
-    // would put the other call's uploads (and what waits on them) behind
-    // all of its own.  A lone call never waits here.
-    static constexpr size_t kPaceDepth = 2;
-    std::deque<hipEvent_t> paced_;
+    // While another call shares the device, a call keeps at most
+    // kPaceBytes of its own uploads queued ahead of the piece (or group) it
+    // has just queued: the shared streams run in submission order, and a
+    // call that queued all its pieces at once would put the other call's
+    // uploads (and what waits on them) behind all of its own.  Bytes, not
+    // pieces: with two pieces each, a GET's 1 GB pieces took twice the
+    // link a PUT's 512 MiB pieces got, and the starved PUT chain set the
+    // pair's end.  A lone call never waits here.
+    static constexpr uint64_t kPaceBytes = uint64_t(1) << 30;
+    std::deque<std::pair<hipEvent_t, uint64_t>> paced_;
+    uint64_t up_since_pace_ = 0;  // bytes queue_up took since the last pace()
     int pace(hipEvent_t up) {
-        paced_.push_back(up);
-        while (paced_.size() > kPaceDepth) {
-            hipEvent_t e = paced_.front();
-            paced_.pop_front();
-            if (!shared_now()) continue;
+        paced_.emplace_back(up, up_since_pace_);
+        up_since_pace_ = 0;
+        auto ahead = [&] {  // queued before the newest entry
+            uint64_t b = 0;
+            for (size_t i = 0; i + 1 < paced_.size(); ++i) b += paced_[i].second;
+            return b;
+        };
+        while (paced_.size() > 1) {
+            hipEvent_t e = paced_.front().first;
             const hipError_t q = hipEventQuery(e);
-            if (q == hipSuccess) continue;
+            if (q == hipSuccess) {
+                paced_.pop_front();
+                continue;
+            }
             (void)hipGetLastError();
+            if (!shared_now() || ahead() <= kPaceBytes) break;
             ++d_.pace_waits;
             PTRACE(now("pace"));
             MXEC_HIP(hipEventSynchronize(e));
             PTRACE(now("paced"));
+            paced_.pop_front();
         }
         return MXEC_OK;
     }
@@ -1515,6 +1528,7 @@ private:
     }
     int issue_up() { return issue_blocks(up_blks_, false, h2d_); }
     int issue_down() {
+        if (down_blks_.empty()) return MXEC_OK;
         MXEC_TRY(issue_blocks(down_blks_, true, d2h_));
         return mark_d2h();
     }
@@ -1615,6 +1629,7 @@ private:
     Run up_run_, down_run_;
     int queue_up(uint8_t* dst, const uint8_t* src, uint64_t len) {
         if (!len) return MXEC_OK;
+        up_since_pace_ += len;
         if (extend(up_run_, dst, src, len)) return MXEC_OK;
         MXEC_TRY(flush_up());
         up_run_ = Run{dst, src, len, 1, 0, 0};
@@ -1646,6 +1661,7 @@ private:
         return MXEC_OK;
     }
     int flush_down() {
+        if (!down_run_.len) return MXEC_OK;
         MXEC_TRY(flush_down_run());
         return mark_d2h();
     }
@@ -1711,8 +1727,8 @@ private:
     }
 
     int flush() {
-        MXEC_TRY(issue_down());  // marks
-        MXEC_HIP(hipEventSynchronize(d2h_mark_));
+        MXEC_TRY(issue_down());  // marks what it issues
+        if (d2h_mark_) MXEC_HIP(hipEventSynchronize(d2h_mark_));
         for (auto& p : pend_) std::memcpy(p.dst, out_.ptr(p.ring), p.len);
         pend_.clear();
         out_.release_all();
@@ -1778,7 +1794,10 @@ private:
         // early (without, a GET's first 4 MiB piece -- 2 GB for 128 x 4+2 --
         // held a PUT's first piece back 45 ms, and the PUT's chain set the
         // pair's end).
-        if (share && calls > 1) piece_ramp_ = uint64_t(256) << 10;
+        if (share && calls > 1) {
+            piece_ramp_ = uint64_t(256) << 10;
+            return uint64_t(2) << 20;  // pieces the other call's can interleave with (2D copies above 1 MiB)
+        }
         return uint64_t(4) << 20;
     }
     uint64_t piece_ramp_ = 0;  // first piece of the current wave's ramp (0: none)
