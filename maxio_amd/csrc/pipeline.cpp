@@ -71,6 +71,7 @@ uint64_t rup(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 struct PieceGrid {
     std::vector<uint64_t> starts;  // the ramp's pieces, then every P
     uint64_t P, ramp_end = 0;
+    uint64_t base_pc = 0, base_off = 0;  // first piece of the current P and its offset
     PieceGrid(uint64_t p, uint64_t ramp) : P(p) {
         uint64_t w = ramp;
 #ifdef MXEC_LAB
@@ -81,15 +82,24 @@ struct PieceGrid {
             starts.push_back(ramp_end);
             ramp_end += w;
         }
+        base_pc = starts.size();
+        base_off = ramp_end;
     }
-    uint64_t start(uint64_t pc) const { return pc < starts.size() ? starts[pc] : ramp_end + (pc - starts.size()) * P; }
+    uint64_t start(uint64_t pc) const { return pc < starts.size() ? starts[pc] : base_off + (pc - base_pc) * P; }
     uint64_t width(uint64_t pc) const {
         return pc < starts.size() ? (pc + 1 < starts.size() ? starts[pc + 1] : ramp_end) - starts[pc] : P;
     }
     uint64_t count(uint64_t longest) const {
         for (uint64_t pc = 0; pc < starts.size(); ++pc)
             if (longest <= start(pc) + width(pc)) return pc + 1;
-        return starts.size() + std::max<uint64_t>(1, (longest - ramp_end + P - 1) / P);
+        const uint64_t rest = longest > base_off ? (longest - base_off + P - 1) / P : 0;
+        return base_pc + std::max<uint64_t>(base_pc == starts.size() ? 1 : 0, rest);
+    }
+    // Pieces from pc on (pc past the ramp, not yet issued) are p wide.
+    void widen(uint64_t pc, uint64_t p) {
+        base_off = start(pc);
+        base_pc = pc;
+        P = p;
     }
 };
 
@@ -1279,19 +1289,19 @@ private:
             for (int i = 0; i < objs[o].k + objs[o].m; ++i)
                 if (objs[o].present[i]) longest = std::max(longest, objs[o].len[i]);
         }
-        const PieceGrid grid(P, piece_ramp_);
+        PieceGrid grid(P, piece_ramp_);
         MXEC_TRY(upload_expected(objs, o0, o1, exp, mb));
         struct TwoD {
             bool& f;
             TwoD(bool& flag, bool on) : f(flag) { f = on; }
             ~TwoD() { f = false; }
         } twod(pieces2d_, !waves_now_ && P > (uint64_t(1) << 20));
-        const uint64_t npieces = grid.count(longest);
-        for (uint64_t pc = 0; pc < npieces; ++pc) {
+        for (uint64_t pc = 0; pc < grid.count(longest); ++pc) {
+            widen_if_shared(grid, pc);
             // the ramp's small pieces are not timed: their many small copies
             // run near the floor on a healthy SDMA (a false verdict sent the
             // default line's PUT with digests to waves, 0.316 s)
-            if (grid.width(pc) == P) MXEC_TRY(watch_open());
+            if (grid.width(pc) == grid.P) MXEC_TRY(watch_open());
             const uint64_t off = grid.start(pc), pw = grid.width(pc);
             uint64_t g = mb;
             std::vector<const uint8_t*> sp;
@@ -1802,6 +1812,24 @@ private:
     }
     uint64_t piece_ramp_ = 0;  // first piece of the current wave's ramp (0: none)
 
+    // A wave sized while it had the device to itself (1 MiB pieces: its
+    // upload fit inside its chains) goes on in 2 MiB pieces, 2D copies, once
+    // another call shares the link -- piece_bytes' choice had it known (a
+    // PUT with digests admitted just before a verified GET otherwise kept
+    // its ~33 GB/s 1 MiB copies through the pair and ended ~90 ms after the
+    // GET).
+    void widen_if_shared(PieceGrid& grid, uint64_t pc) {
+        static constexpr uint64_t kShared = uint64_t(2) << 20;
+        if (!d_.kn || !d_.kn->pipe_piece_auto || pc < grid.starts.size() || grid.P >= kShared || !shared_now())
+            return;
+#ifdef MXEC_LAB
+        if (const char* e = getenv("MXEC_PIPE_WIDEN"))
+            if (*e == '0') return;  // lab A/B
+#endif
+        grid.widen(pc, kShared);
+        pieces2d_ = !waves_now_;
+    }
+
     int wave_pieces(std::vector<HostObj>& objs, size_t o0, size_t o1, uint64_t P) {
         Slot& slot = slot_;
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
@@ -1824,8 +1852,7 @@ private:
         MXEC_TRY(scratch_.grow(nm * 64));  // digests [nm][32], then chain states [nm][8] words
         uint8_t* digests = static_cast<uint8_t*>(scratch_.p);
         uint32_t* state = reinterpret_cast<uint32_t*>(digests + nm * 32);
-        const PieceGrid grid(P, piece_ramp_);
-        const uint64_t npieces = grid.count(longest);
+        PieceGrid grid(P, piece_ramp_);
         // RS and the chains on the call's compute stream (PipeHub::use): each
         // piece's RS ahead of its hash, so no piece of this call waits behind
         // another call's chains.
@@ -1837,7 +1864,8 @@ private:
             ~TwoD() { f = false; }
         } twod(pieces2d_, !waves_now_ && P > (uint64_t(1) << 20));
         PTRACE(start(h2d_));
-        for (uint64_t pc = 0; pc < npieces; ++pc) {
+        for (uint64_t pc = 0; pc < grid.count(longest); ++pc) {
+            widen_if_shared(grid, pc);
             // No SDMA watch here: in the seconds after a large HBM free the
             // bracket events among the pieces cost the PUT with digests 63 %
             // (0.335 s against 0.206 unwatched at 128 objects,
