@@ -101,7 +101,7 @@ int decode_plan(Device& dev, int k, int m, const uint8_t* present, bool data_onl
 }
 
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
-           const std::vector<RsObject>& objs, DescArena* arena, bool tune) {
+           const std::vector<RsObject>& objs, DescArena* arena, bool tune, uint32_t max_blocks) {
     if (objs.empty() || r == 0) return MXEC_OK;
     const size_t n = objs.size();
     if (affinity_on(dev)) {
@@ -168,7 +168,8 @@ int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, i
     a.k = uint32_t(k);
     a.r_total = uint32_t(r);
     a.aligned = aligned ? 1u : 0u;
-    a.max_blocks = dev.kn ? dev.kn->test_rs_grid : 0u;
+    a.max_blocks = max_blocks ? max_blocks : dev.kn ? dev.kn->test_rs_grid : 0u;
+    if (max_blocks) tune = false;
     // Large aligned single-launch batches take the grid tuner's pick.
     GridTuner::Trial trial;
     const double gb = double(n) * double(k + r) * double(shard_size) / 1e9;
@@ -313,7 +314,7 @@ void rs_grid_release(Device& dev) {
 }
 
 int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups,
-                 DescArena* arena) {
+                 DescArena* arena, uint32_t cap) {
     // Which groups take the grouped kernel: every pointer 16-byte aligned,
     // r <= 8, index ranges that fit its 32-bit fields.  A call that is one
     // uniform group keeps the uniform kernel (no tile table).
@@ -363,7 +364,8 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
             if (v.empty()) order.push_back(key);
             v.push_back(ob.o);
         }
-        for (const auto& key : order) MXEC_TRY(run_rs(dev, slot, s, key.second, key.first, g.first, by[key], arena));
+        for (const auto& key : order)
+            MXEC_TRY(run_rs(dev, slot, s, key.second, key.first, g.first, by[key], arena, true, cap));
     }
     if (grouped.empty()) return MXEC_OK;
     if (affinity_on(dev)) {
@@ -379,7 +381,7 @@ int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std
     // multi-r launch instead (rs_apply_multi; MXEC_RS_MULTI=0 keeps one
     // launch per r).
     const bool multi_on = !dev.kn || dev.kn->rs_multi;
-    const uint32_t max_blocks = dev.kn ? dev.kn->test_rs_grid : 0u;
+    const uint32_t max_blocks = cap ? cap : dev.kn ? dev.kn->test_rs_grid : 0u;
     bool multi = multi_on && grouped.size() >= 2;
     uint64_t m_obj = 0, m_k = 0, m_tiles = 0;
     const uint64_t m_tile = rs_tile_bytes(rs_group_variant(kMultiR));

@@ -31,7 +31,8 @@ struct RsObject {
 // tune = false: the default grid, and the grid tuner neither picks nor
 // records (the batch allocator's placement probes, placement.cpp).
 int run_rs(Device& dev, Slot& slot, hipStream_t s, uint64_t shard_size, int k, int r,
-           const std::vector<RsObject>& objs, DescArena* arena = nullptr, bool tune = true);
+           const std::vector<RsObject>& objs, DescArena* arena = nullptr, bool tune = true,
+           uint32_t max_blocks = 0);
 
 // Grid tuner of large uniform RS launches (runtime.hpp GridTuner):
 // rs_grid_pick sets *bpc (0 = the default grid) and, while a shape is still
@@ -58,8 +59,10 @@ struct RsMixedObject {
 // launch instead (rs_apply_multi; MXEC_RS_MULTI=0 disables).  The others run
 // one run_rs per (k, shard_size).  A lone uniform group runs the uniform
 // kernel.
+// max_blocks (here and in run_rs): a cap on each launch's workgroups, the
+// grid tuner left alone (0: the default grid, or mxec_open_test's cap).
 int run_rs_mixed(Device& dev, Slot& slot, hipStream_t s, const std::map<int, std::vector<RsMixedObject>>& groups,
-                 DescArena* arena = nullptr);
+                 DescArena* arena = nullptr, uint32_t max_blocks = 0);
 
 // SHA-256 of n device buffers.  digests_dev / expected_dev / ok_dev may be
 // null (see ShaArgs).

@@ -895,6 +895,16 @@ private:
             if (const char* e = getenv("MXEC_GET_WAVE_UPLOADS"); e && *e == '0') up_override = false;  // lab A/B
 #endif
             if (up_override) waves_now_ = true;
+            // A lone speculating wave's downloads run beside its chains and
+            // uploads: by SDMA, unless an earlier call found them slow there
+            // (spec_judge) less than kSpecWavesHoldMs ago.
+            const bool spec_sdma = spec && auto_copy && !shared && !down_waves_;
+            if (spec && auto_copy && !shared &&
+                (spec_down_waves() || now_ns() < d_.spec_waves_until_ns.load()))
+                down_waves_ = true;  // restored at the end
+            const bool judge = spec_sdma && !down_waves_;
+            int64_t t_verdict = 0;
+            bool redo = false;
             // Without speculation the last group's rebuilt shards (on the
             // critical path, alone on the link) go down by waves, earlier
             // groups' by SDMA beside the later groups' uploads and chains
@@ -912,6 +922,8 @@ private:
                 std::vector<size_t> changed;
                 MXEC_TRY(verify_collect(objs, cut[j], cut[j + 1], mbase[j], verdict[j], &changed));
                 PTRACE(now("verified"));
+                t_verdict = now_ns();
+                redo = redo || !changed.empty();
                 if (spec) {
                     MXEC_TRY(confirm(objs, cut[j], cut[j + 1], changed, data_only));
                     // The objects with a mismatch, decoded again with their
@@ -931,6 +943,8 @@ private:
             d_.verify_groups += G;
             d_.verify_waves += 1;
             if (up_override) waves_now_ = up_before;  // only the override is undone
+            judge_ = judge && !redo;
+            t_verdict_ = t_verdict;
         } else {
             const auto groups = object_groups(objs, o0, o1);
             hipStream_t cs = cs_[cs_idx_];
@@ -946,6 +960,8 @@ private:
         PTRACE(now("down_queued"));
         const int frc = flush();
         PTRACE(report("rec_wave"));
+        if (frc == MXEC_OK && judge_) spec_judge();
+        judge_ = false;
         down_waves_ = down_before;
         dwatch_off_ = false;
         return frc;
@@ -954,13 +970,73 @@ private:
     // Objects [o0, o1) of a speculatively rebuilt group whose present masks
     // the verdict left as they were (all but `changed`): their rebuilt
     // shards are already on their way down; status and present flags.
-    static bool spec_on_chain() {
+    // Workgroups of a speculative piece decode: four per CU.  It runs beside
+    // the wave's SHA-256 chains; at the RS kernel's default grid (512-1024
+    // per CU, 0.13-0.26 M workgroups for a 1 MiB piece of 128 x 4+2) it
+    // either slowed the chains (19 -> 35 ms a piece) or was starved by them
+    // (a piece's decode + download 42 ms instead of 9), which of the two
+    // changing from call to call: 0.19-0.46 s for the same 128-object GET
+    // (pipe traces, profiles/r6/spec_grid/).  A piece's decode moves ~0.8 GB
+    // in the ~9 ms the link takes to bring the next piece up; at one
+    // workgroup per CU the GET ended ~6 ms later than at four
+    // (profiles/r6/spec_grid/spec_grid_ab_r6q.jsonl).
+    uint32_t spec_blocks() const {
+        uint32_t b = 4u * (d_.n_cus ? uint32_t(d_.n_cus) : 256u);
 #ifdef MXEC_LAB
-        const char* e = getenv("MXEC_SPEC_ON_CHAIN");
+        if (const char* e = getenv("MXEC_SPEC_BLOCKS")) b = uint32_t(atol(e));  // lab A/B (0: default grid)
+#endif
+        return b;
+    }
+    // A lone speculating wave's speculative downloads go by SDMA: healthy,
+    // they keep pace with the chains and the wave ends ~1 ms after its last
+    // verdict (128 x 4+2 x 10 MiB: 0.193 s).  But in some processes, and in
+    // the seconds after a large HBM free, those SDMA downloads crawl at
+    // ~6 GB/s while the chains run and the same GET takes 0.42-0.47 s; by CU
+    // waves it takes 0.24 s in either state (and without speculation 0.242;
+    // profiles/r6/spec_grid/get_churn_ab_*.jsonl).  Nothing measured ahead of
+    // the wave tells the states apart: a 32 MiB D2H copy on the idle link ran
+    // at 54-55 GB/s in both, the same copy beside the first piece's upload
+    // at 13.4 GB/s in both (get_churn_ab_r6u/r6v), and the pieces' own
+    // download brackets during the upload phase run at ~6 GB/s in both.  So
+    // the wave is judged after the fact: downloads still running more than
+    // kSpecTailMs after the last verdict (healthy ~1 ms, slow ~140) send the
+    // device's next lone speculating waves' downloads to waves for
+    // kSpecWavesHoldMs, doubled for each slow verdict in a row up to 16 s;
+    // the first wave after the hold tries SDMA again (a healthy one ends the
+    // run of slow verdicts).
+    static constexpr int64_t kSpecTailMs = 25, kSpecWavesHoldMs = 2000;
+    bool judge_ = false;
+    int64_t t_verdict_ = 0;
+    void spec_judge() {
+        if (!t_verdict_) return;
+        const int64_t tail_ms = (now_ns() - t_verdict_) / 1000000;
+        ++d_.sdma_down_probes;
+        if (tail_ms <= kSpecTailMs) {
+            d_.spec_slow_run = 0;
+            return;
+        }
+        ++d_.sdma_down_slow_verdicts;
+        const int run = std::min(d_.spec_slow_run.fetch_add(1), 3);
+        d_.spec_waves_until_ns = now_ns() + (kSpecWavesHoldMs << run) * 1000000;
+    }
+    // Speculative downloads by CU waves instead of SDMA (lab A/B).
+    static bool spec_down_waves() {
+#ifdef MXEC_LAB
+        const char* e = getenv("MXEC_SPEC_DOWN_WAVES");
         return e && *e == '1';
 #else
         return false;
 #endif
+    }
+    // The stream of a speculative piece decode (cs: the wave's chain stream).
+    hipStream_t spec_stream(hipStream_t cs) const {
+#ifdef MXEC_LAB
+        if (const char* e = getenv("MXEC_SPEC_STREAM")) {
+            if (!strcmp(e, "chain")) return cs;
+            if (!strcmp(e, "other")) return shared_now() ? cs : cs_[(cs_idx_ + 1) & 1];
+        }
+#endif
+        return d2h_;
     }
 
     int confirm(std::vector<RecObj>& objs, size_t o0, size_t o1, const std::vector<size_t>& changed, bool data_only) {
@@ -1180,9 +1256,8 @@ private:
     // encode -- and goes down to the caller's buffers.  Launch and downloads
     // both on the D2H stream, so the downloads follow the decode in order.
     // An object short of k present shards is skipped (it fails anyway).
-    // ds: the stream the decode runs on -- the D2H stream itself, or (lab
-    // MXEC_SPEC_ON_CHAIN=1) the group's chain stream behind the piece's hash,
-    // the downloads then waiting for it.
+    // ds: the stream the decode runs on (spec_stream) -- the D2H stream
+    // itself, or another, the downloads then waiting for it.
     int spec_piece(std::vector<RecObj>& objs, size_t o0, size_t o1, uint64_t off, uint64_t pw, hipEvent_t up,
                    bool data_only, hipStream_t ds) {
         uint8_t* base = static_cast<uint8_t*>(pool_.p);
@@ -1235,14 +1310,15 @@ private:
                 pi += size_t(h.k);
                 po += size_t(r);
             }
-            return rs_groups.empty() ? MXEC_OK : run_rs_mixed(d_, slot_, ds, rs_groups, &arena_);
+            return rs_groups.empty() ? MXEC_OK : run_rs_mixed(d_, slot_, ds, rs_groups, &arena_, spec_blocks());
         };
         MXEC_TRY(flush_down());
         MXEC_TRY(issue_down());  // wave copy blocks queued earlier go before the wait
         if (ds == d2h_) {
             MXEC_HIP(hipStreamWaitEvent(d2h_, up, 0));
             MXEC_TRY(with_stable_coef(d_, d2h_, collect, launch));
-        } else {  // ds already waits for `up` (the piece's hash did)
+        } else {
+            MXEC_HIP(hipStreamWaitEvent(ds, up, 0));
             MXEC_TRY(with_stable_coef(d_, ds, collect, launch));
             hipEvent_t done;
             MXEC_TRY(new_event(&done));
@@ -1333,7 +1409,7 @@ private:
             if (!sp.empty())
                 MXEC_TRY(run_sha_pieces(d_, slot_, cs, sp, sl, ss, st, state, pc > 0, nullptr, &arena_, exp, ok));
             PTRACE(mark("sha", cs));
-            if (spec) MXEC_TRY(spec_piece(objs, o0, o1, off, pw, up, data_only, spec_on_chain() ? cs : d2h_));
+            if (spec) MXEC_TRY(spec_piece(objs, o0, o1, off, pw, up, data_only, spec_stream(cs)));
             MXEC_TRY(pace(up));
         }
         paced_.clear();

@@ -309,6 +309,10 @@ struct Device {
     // own: the single-request calls read the same instants
     // (capi.cpp copy_waves_get).
     std::atomic<int64_t> waves_up_until_ns{0}, waves_down_until_ns{0};
+    // Until this instant a lone speculating verified GET wave downloads by
+    // waves (pipeline.cpp spec_judge).
+    std::atomic<int64_t> spec_waves_until_ns{0};
+    std::atomic<int> spec_slow_run{0};  // slow verdicts in a row
     // Host-batch calls (per device share), those admitted while another ran
     // on the device, speculative piece rebuilds of verified GETs and the
     // objects re-decoded after a verdict, and host waits that paced a shared
