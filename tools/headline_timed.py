@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """The headline encode's launches in a rocprofv3 kernel trace of bench.py,
-split into the phases the bench line reports: the tuning launches
+split into the phases the bench line reports: mxec_batch_alloc's placement
+probes (three encodes per probed layout, `config.placement.probe_ms`), the
+tuning launches
 (`tuning.launches`, run before --warmup until the RS grid tuner decided),
 the --warmup launches and the timed --steps launches.  Prints one JSON
 object: the grids of each phase, whether every timed launch ran one grid,
@@ -32,11 +34,12 @@ def main() -> int:
     if line is None:
         raise SystemExit("no bench line in " + a.bench_json)
     tune = int(line.get("tuning", {}).get("launches", 0))
+    probes = 3 * sum(1 for x in (line.get("config", {}).get("placement") or {}).get("probe_ms", []) if x > 0)
     warm, steps = int(line["warmup"]), int(line["steps"])
     with open(a.trace) as f:
         rows = sorted((r for r in csv.DictReader(f) if a.match in r["Kernel_Name"]),
                       key=lambda r: int(r["Start_Timestamp"]))
-    rows = rows[: tune + warm + steps]
+    probe_rows, rows = rows[:probes], rows[probes: probes + tune + warm + steps]
 
     def grid(r):
         return int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
@@ -46,8 +49,10 @@ def main() -> int:
     out = {
         "source": f"{a.trace} (rocprofv3 --kernel-trace of bench.py) and {a.bench_json}",
         "command_steps_warmup": [steps, warm],
-        "what": (f"the headline kernel ({a.match}...) in trace order: {tune} tuning launches before the warmup "
-                 f"(the grid tuner's trials), {warm} warmup, then the {steps} timed steps"),
+        "what": (f"the headline kernel ({a.match}...) in trace order: {probes} placement probe launches, "
+                 f"{tune} tuning launches before the warmup (the grid tuner's trials), {warm} warmup, then the "
+                 f"{steps} timed steps"),
+        "placement_probe_grids": sorted({grid(r) for r in probe_rows}),
         "tuning_grids": [grid(r) for r in rows[:tune]],
         "warmup_grids": [grid(r) for r in rows[tune:tune + warm]],
         "timed_grids": timed_grids,
