@@ -233,9 +233,9 @@ def test_get_download_watch(floor):
         ctx.close()
     d1, d2, d3 = deltas
     assert d1["sdma_down_checks"] > 0 and d1["down_mbps"] > 0, deltas
-    assert d3["wave_blocks"] > 0, deltas  # verified, one group: uploads by waves
-    # judged after the fact -- unless the slow verdict's download hold is on
-    assert d3["sdma_down_checks"] == (0 if floor else 1), deltas
+    assert d3["wave_blocks"] > 0 and d3["spec_pieces"] > 0, deltas  # one group: uploads by waves, speculating
+    # judged once after the fact -- or not at all while a download hold is on
+    assert d3["sdma_down_checks"] in (0, 1), deltas
     if floor:
         assert d1["sdma_down_slow"] > 0, deltas
         assert d2["sdma_down_checks"] == 0 and d2["wave_blocks"] > 0, deltas  # within the 1 s download hold
