@@ -744,12 +744,23 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
     u32x4 cur[16], nxt[16];
     load_kw<kQuadRow>(kcol, cur);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    static_assert(LDG == 1 || LDG == 2 || LDG == 4, "K + W read groups: 1, 2 or 4");
-    constexpr int RPG = 16 / LDG;  // rows per read group
-    // Rows [g RPG, (g + 1) RPG) of the block in ring buffer `buf` into `dst`.
+    static_assert(LDG == 1 || LDG == 2 || LDG == 4 || LDG == 15, "K + W read groups: 1, 2, 4 or 15 + 1");
+    // LDG 15: rows 0-14 after the barrier, row 15 at the top of step 2 (a
+    // burst of 15 fits lgkmcnt; the 16th no longer waits for the first).
+    constexpr int NG = LDG == 15 ? 2 : LDG;  // read groups
+    constexpr int RPG = 16 / NG;             // rows per read group (LDG 1, 2, 4)
+    // Group g's rows of the block in ring buffer `buf` into `dst`.
     auto rows = [&](u32x4 (&dst)[16], uint32_t buf, int g) {
+        const int r0 = LDG == 15 ? (g ? 15 : 0) : g * RPG, r1 = LDG == 15 ? (g ? 16 : 15) : (g + 1) * RPG;
 #pragma unroll
-        for (int r = g * RPG; r < (g + 1) * RPG; ++r) dst[r] = kcol[buf * BUF + r * kQuadRow];
+        for (int r = r0; r < r1; ++r) dst[r] = kcol[buf * BUF + r * kQuadRow];
+    };
+    auto at_step = [&](u32x4 (&dst)[16], uint32_t buf, int t) {
+        if constexpr (LDG == 15) {
+            if (t == 2) rows(dst, buf, 1);
+        } else if (LDG > 1 && t > 0 && t < 64 && t % (64 / LDG) == 0) {
+            rows(dst, buf, t / (64 / LDG));
+        }
     };
     uint32_t rb = 1;
     for (uint64_t b = 0; b < nmax; b += 2) {
@@ -757,13 +768,11 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
         if (b < nfull) {
 #ifdef MXEC_LAB
             if constexpr (!LAG) {
-                for (int g = 1; g < LDG; ++g) rows(nxt, rb, g);
+                for (int g = 1; g < NG; ++g) rows(nxt, rb, g);
                 compress_quad(s, cur, q);
             } else
 #endif
-            compress_lag(s, cur, q, [&](int t) {
-                if (LDG > 1 && t > 0 && t < 64 && t % (64 / LDG) == 0) rows(nxt, rb, t / (64 / LDG));
-            });
+            compress_lag(s, cur, q, [&](int t) { at_step(nxt, rb, t); });
         }  // a lane past its message's blocks never reads K + W again: no reads here
         KW_SYNC();
         rb = rb == 2 ? 0 : rb + 1;
@@ -772,13 +781,11 @@ __global__ __launch_bounds__(256) void sha256_quad_kernel(const uint8_t* const* 
         if (b + 1 < nfull) {
 #ifdef MXEC_LAB
             if constexpr (!LAG) {
-                for (int g = 1; g < LDG; ++g) rows(cur, rb, g);
+                for (int g = 1; g < NG; ++g) rows(cur, rb, g);
                 compress_quad(s, nxt, q);
             } else
 #endif
-            compress_lag(s, nxt, q, [&](int t) {
-                if (LDG > 1 && t > 0 && t < 64 && t % (64 / LDG) == 0) rows(cur, rb, t / (64 / LDG));
-            });
+            compress_lag(s, nxt, q, [&](int t) { at_step(cur, rb, t); });
         }  // a lane past its message's blocks never reads K + W again: no reads here
         KW_SYNC();
         rb = rb == 2 ? 0 : rb + 1;
@@ -1036,12 +1043,13 @@ constexpr uint32_t kSplitMaxMessages = 256 * 4 * 64 * 3 / 4;
 // only (`make lab`, -DMXEC_LAB).
 constexpr int kShaQuadAuto = 6;
 // K + W read groups of the auto form's consumers (sha256_quad_kernel LDG;
-// lab builds A/B it with MXEC_SHA_LDG=1|2|4).  Spreading the next block's
+// lab builds A/B it with MXEC_SHA_LDG=1|2|4|15).  Spreading the next block's
 // reads over the block lost: 10 240 x 1 MiB took
 // 22.0 ms with two groups and 22.4 with four against 19.6 with all 16 reads
 // after the barrier, on one box in interleaved fresh processes
-// (profiles/r6/sha_ldg_ab.jsonl; ~30 cycles of the wave's in-order issue
-// per ds_read_b128 placed among the chain's VALU, against ~20 in the burst).
+// (profiles/r6/sha_ldg_ab.jsonl), and 15 after the barrier with the 16th at
+// step 2 (same 605 VALU) took 21.7 against 19.7 (sha_ldg15_ab_r6ag.jsonl):
+// one read among the chain's VALU costs far more than the burst's wait.
 constexpr int kShaLdg = 1;
 
 #ifdef MXEC_LAB
@@ -1102,8 +1110,10 @@ hipError_t launch_sha256(const ShaArgs& a, hipStream_t s) {
 #ifdef MXEC_LAB
         if (const char* e = getenv("MXEC_SHA_LDG"); e && atoi(e) != kShaLdg) {  // lab A/B: K + W read groups
             const int g = atoi(e);
-            auto* kern = g == 1 ? &sha256_quad_kernel<true, true, true, 1>
-                                : g == 2 ? &sha256_quad_kernel<true, true, true, 2> : &sha256_quad_kernel<true, true, true, 4>;
+            auto* kern = g == 1    ? &sha256_quad_kernel<true, true, true, 1>
+                         : g == 2  ? &sha256_quad_kernel<true, true, true, 2>
+                         : g == 15 ? &sha256_quad_kernel<true, true, true, 15>
+                                   : &sha256_quad_kernel<true, true, true, 4>;
             hipLaunchKernelGGL(kern, dim3((a.n + 63) / 64), dim3(256), 0, s, a.ptrs, a.lens, a.digests, a.expected,
                                a.exp_idx, a.ok, a.n, sha_prio(), a.piece);
             return hipGetLastError();

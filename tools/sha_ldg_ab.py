@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the SHA-256 lag pair form's K + W read groups (sha256_kernel.hip
-sha256_quad_kernel LDG; lab knob MXEC_SHA_LDG=1|2|4, lab build): each
+sha256_quad_kernel LDG; lab knob MXEC_SHA_LDG=1|2|4|15, lab build): each
 setting in a fresh child process running tools/sha_alone.py (the configs[2]
 hash launch alone, 10 240 x 1 MiB), rounds interleaved so box drift hits
 every setting alike.  The parent never touches the GPU.
