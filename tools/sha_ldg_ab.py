@@ -6,6 +6,7 @@ hash launch alone, 10 240 x 1 MiB), rounds interleaved so box drift hits
 every setting alike.  The parent never touches the GPU.
 
   python tools/sha_ldg_ab.py --rounds 3 --ldg 1,2,4
+  python tools/sha_ldg_ab.py --ldg "" --libs maxilp:maxio_amd/lib/libmaxio_ec_sched_max-ilp.so
 """
 from __future__ import annotations
 
@@ -24,9 +25,11 @@ def main() -> int:
     ap.add_argument("--ldg", default="1,2,4")
     ap.add_argument("--n", type=int, default=10240)
     ap.add_argument("--mib", type=int, default=1)
+    ap.add_argument("--libs", default="", help="name:path,... other builds of the library to time beside")
     a = ap.parse_args()
     lab = os.path.join(ROOT, "maxio_amd", "lib", "libmaxio_ec_lab.so")
-    runs = [("product", {})] + [(f"lab_ldg{g}", {"MXEC_LIB": lab, "MXEC_SHA_LDG": g}) for g in a.ldg.split(",")]
+    runs = [("product", {})] + [(f"lab_ldg{g}", {"MXEC_LIB": lab, "MXEC_SHA_LDG": g}) for g in a.ldg.split(",") if g]
+    runs += [(n, {"MXEC_LIB": os.path.join(ROOT, pth)}) for n, pth in (x.split(":", 1) for x in a.libs.split(",") if x)]
     for r in range(a.rounds):
         for name, env in runs:
             e = dict(os.environ, **env)
