@@ -24,6 +24,9 @@ def main() -> int:
     ap.add_argument("bench_json")
     ap.add_argument("--match", default="rs_apply_fast<2")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--min-frac", type=float, default=0.5,
+                    help="launches shorter than this fraction of the line's ms_per_launch are not the headline's "
+                         "(the host legs, which run before it, launch the same kernel over pieces of a batch)")
     a = ap.parse_args()
     line = None
     with open(a.bench_json) as f:
@@ -36,20 +39,26 @@ def main() -> int:
     tune = int(line.get("tuning", {}).get("launches", 0))
     probes = 3 * sum(1 for x in (line.get("config", {}).get("placement") or {}).get("probe_ms", []) if x > 0)
     warm, steps = int(line["warmup"]), int(line["steps"])
-    with open(a.trace) as f:
-        rows = sorted((r for r in csv.DictReader(f) if a.match in r["Kernel_Name"]),
-                      key=lambda r: int(r["Start_Timestamp"]))
-    probe_rows, rows = rows[:probes], rows[probes: probes + tune + warm + steps]
-
     def grid(r):
         return int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
+
+    def dur_ms(r):
+        return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+
+    floor_ms = a.min_frac * float(line["roofline"]["ms_per_launch"])
+    with open(a.trace) as f:
+        rows = sorted((r for r in csv.DictReader(f) if a.match in r["Kernel_Name"] and dur_ms(r) >= floor_ms),
+                      key=lambda r: int(r["Start_Timestamp"]))
+    probe_rows, rows = rows[:probes], rows[probes: probes + tune + warm + steps]
 
     ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows[tune + warm:]]
     timed_grids = sorted({grid(r) for r in rows[tune + warm:]})
     out = {
         "source": f"{a.trace} (rocprofv3 --kernel-trace of bench.py) and {a.bench_json}",
         "command_steps_warmup": [steps, warm],
-        "what": (f"the headline kernel ({a.match}...) in trace order: {probes} placement probe launches, "
+        "what": (f"the headline kernel ({a.match}..., launches of >= {floor_ms:.2f} ms: whole-batch encodes) in "
+                 f"trace order: "
+                 f"{probes} placement probe launches, "
                  f"{tune} tuning launches before the warmup (the grid tuner's trials), {warm} warmup, then the "
                  f"{steps} timed steps"),
         "placement_probe_grids": sorted({grid(r) for r in probe_rows}),
