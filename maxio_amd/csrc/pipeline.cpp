@@ -137,7 +137,11 @@ public:
         for (int i = 0; i < kRing; ++i) {
             buf_[i].node = node;
             MXEC_TRY(buf_[i].ensure(kRingBuf));
-            MXEC_HIP(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming));
+            unsigned flags = hipEventDisableTiming;
+#ifdef MXEC_LAB
+            if (const char* e = getenv("MXEC_RING_TIMED_EVENTS"); e && *e == '1') flags = hipEventDefault;  // lab: exit probe
+#endif
+            MXEC_HIP(hipEventCreateWithFlags(&ev_[i], flags));
         }
         return MXEC_OK;
     }

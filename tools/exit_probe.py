@@ -17,6 +17,11 @@ profiler narrows the trigger:
           hash          + one mxec_sha256_batch (host pointers)
           torch_copy    no mxec call after open: torch's own pinned H2D / D2H
                         copies on a side stream (does any async copy arm it?)
+          torch_pageable no mxec call after open: torch's H2D / D2H copies of
+                        pageable memory (HIP stages them itself)
+          attr_pageable no mxec work after open: hipPointerGetAttributes on a
+                        pageable buffer (what is_pinned() asks of every
+                        pageable shard), its error cleared
           torch_streams torch alone on eight streams (more than the four
                         hardware queues HIP gives a process), each with a
                         pinned H2D copy, a kernel and a D2H copy
@@ -34,7 +39,8 @@ sys.path.insert(0, ROOT)
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["open", "device", "host_pinned", "host_pageable", "hash", "torch_copy", "torch_streams"])
+    ap.add_argument("what", choices=["open", "device", "host_pinned", "host_pageable", "hash", "torch_copy",
+                                        "torch_pageable", "attr_pageable", "torch_streams"])
     ap.add_argument("--no-close", action="store_true")
     a = ap.parse_args()
     import numpy as np
@@ -73,6 +79,20 @@ def main() -> int:
             back.copy_(d, non_blocking=True)
         s.synchronize()
         assert int(back[12345]) == 7
+    elif a.what == "torch_pageable":
+        h = torch.full((64 << 20,), 7, dtype=torch.uint8)  # pageable
+        d = h.to("cuda")
+        back = d.cpu()
+        assert int(back[12345]) == 7
+    elif a.what == "attr_pageable":
+        import ctypes
+
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = np.zeros(1 << 20, np.uint8)  # pageable
+        attr = ctypes.create_string_buffer(512)  # hipPointerAttribute_t (smaller)
+        rc = hip.hipPointerGetAttributes(attr, ctypes.c_void_p(buf.ctypes.data))
+        hip.hipGetLastError()
+        print(f"hipPointerGetAttributes(pageable) = {rc}", flush=True)
     elif a.what == "torch_streams":
         ss = [torch.cuda.Stream() for _ in range(8)]
         hs = [torch.full((8 << 20,), j, dtype=torch.uint8).pin_memory() for j in range(8)]
