@@ -639,6 +639,7 @@ private:
     // kept an RS-only GET on waves (0.111 s) after SDMA had recovered
     // (0.101; profiles/r5/copy_engine/vg_churn0_r5s.jsonl).
     static constexpr int kWavesHoldMs = 2000, kDownWavesHoldMs = 1000;
+    static constexpr int kDownSlowRun = 2;  // slow download brackets in a row for a verdict
     struct Bracket {
         hipEvent_t a, b;
         uint64_t bytes, copies;
@@ -778,9 +779,17 @@ private:
         const bool slow = gbps < floor;
         const int64_t hold = now_ns() + int64_t(k.down ? kDownWavesHoldMs : kWavesHoldMs) * 1000000;
         if (k.down) {
+            // Two slow download brackets in a row make a verdict: an RS-only
+            // GET's downloads share the link with its uploads, and a lone
+            // bracket under the bar sent healthy calls to waves for a second
+            // (0.128 s against 0.101 by SDMA; profiles/r6/final_r6aq/), where
+            // a real slow state repeats bracket after bracket (~24 GB/s).
             ++d_.sdma_down_probes;
             d_.sdma_down_last_mbps = uint64_t(gbps * 1e3);
-            if (!down_waves_ && slow) {
+            if (!slow) {
+                d_.down_slow_run = 0;
+            } else if (!down_waves_ && d_.down_slow_run.fetch_add(1) + 1 >= kDownSlowRun) {
+                d_.down_slow_run = 0;
                 ++d_.sdma_down_slow_verdicts;
                 down_waves_ = true;  // the rest of this call's downloads
                 d_.waves_down_until_ns = hold;

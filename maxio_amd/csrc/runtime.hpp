@@ -313,6 +313,7 @@ struct Device {
     // waves (pipeline.cpp spec_judge).
     std::atomic<int64_t> spec_waves_until_ns{0};
     std::atomic<int> spec_slow_run{0};  // slow verdicts in a row
+    std::atomic<int> down_slow_run{0};  // slow SDMA download brackets in a row (pipeline watch_judge)
     // Host-batch calls (per device share), those admitted while another ran
     // on the device, speculative piece rebuilds of verified GETs and the
     // objects re-decoded after a verdict, and host waits that paced a shared
