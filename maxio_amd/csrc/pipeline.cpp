@@ -44,6 +44,7 @@
 #endif
 #include "deal.hpp"
 #include "kernels.hpp"
+#include "piece_grid.hpp"
 #include "ops.hpp"
 
 namespace mxec {
@@ -57,51 +58,6 @@ constexpr int kRing = 4;
 constexpr int kComputeStreams = 2;  // RS stream + SHA stream (4 HW queues per process)
 
 uint64_t rup(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
-
-// Piece grid of the piece-major host waves: pieces of P, after a ramp from
-// MXEC_PIPE_RAMP_KB doubling up to P when set (lab; every chain waits for
-// the first piece's upload).  With one copy per chunk a ramp measured slower
-// than uniform pieces (64 KiB ramp 0.245, a P/4 first piece 0.223, uniform
-// 0.220 s for 128 x 4+2 x 10 MiB with digests): small copies pay the DMA's
-// fixed cost.  With 2D copies (MXEC_PIPE_COPY2D=1) a 256 KiB ramp won 2 %
-// in one process (0.216 -> 0.211 s), but the 2D copies are off by default
-// (see queue_up), so the ramp is too (profiles/r3/pieces/).
-// Pieces of a piece-major wave: a ramp of pieces doubling from `ramp` bytes
-// up to P, then every P.
-struct PieceGrid {
-    std::vector<uint64_t> starts;  // the ramp's pieces, then every P
-    uint64_t P, ramp_end = 0;
-    uint64_t base_pc = 0, base_off = 0;  // first piece of the current P and its offset
-    PieceGrid(uint64_t p, uint64_t ramp) : P(p) {
-        uint64_t w = ramp;
-#ifdef MXEC_LAB
-        if (const char* e = getenv("MXEC_PIPE_RAMP_KB")) w = uint64_t(atol(e)) << 10;  // lab override
-#endif
-        w = w / 64 * 64;
-        for (; w && w < p; w *= 2) {
-            starts.push_back(ramp_end);
-            ramp_end += w;
-        }
-        base_pc = starts.size();
-        base_off = ramp_end;
-    }
-    uint64_t start(uint64_t pc) const { return pc < starts.size() ? starts[pc] : base_off + (pc - base_pc) * P; }
-    uint64_t width(uint64_t pc) const {
-        return pc < starts.size() ? (pc + 1 < starts.size() ? starts[pc + 1] : ramp_end) - starts[pc] : P;
-    }
-    uint64_t count(uint64_t longest) const {
-        for (uint64_t pc = 0; pc < starts.size(); ++pc)
-            if (longest <= start(pc) + width(pc)) return pc + 1;
-        const uint64_t rest = longest > base_off ? (longest - base_off + P - 1) / P : 0;
-        return base_pc + std::max<uint64_t>(base_pc == starts.size() ? 1 : 0, rest);
-    }
-    // Pieces from pc on (pc past the ramp, not yet issued) are p wide.
-    void widen(uint64_t pc, uint64_t p) {
-        base_off = start(pc);
-        base_pc = pc;
-        P = p;
-    }
-};
 
 bool is_pinned(const void* p, uint64_t len) { return pinned_range(p, len); }
 
