@@ -23,6 +23,8 @@
 // freed.  Transiently up to twice the batch's bytes at the larger stride;
 // when the second allocation does not fit, one allocation's strides decide.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -38,6 +40,19 @@ namespace {
 // a 6 MiB pad (R4: a 16 MiB stride held 6.16-6.17 TB/s on both kinds of one
 // box); smaller shards at no pad and a 256 KiB pad.
 std::vector<uint64_t> candidate_pads(uint64_t S) {
+#ifdef MXEC_LAB
+    if (const char* e = getenv("MXEC_BATCH_PADS_KB")) {  // lab A/B: comma-separated pads in KiB
+        std::vector<uint64_t> v;
+        for (const char* q = e; *q;) {
+            char* end = nullptr;
+            const unsigned long long kb = strtoull(q, &end, 10);
+            if (end == q) break;
+            v.push_back(uint64_t(kb) << 10);
+            q = *end == ',' ? end + 1 : end;
+        }
+        if (!v.empty()) return v;
+    }
+#endif
     if (S >= (uint64_t(4) << 20)) return {(uint64_t(2) << 20) + (uint64_t(64) << 10), uint64_t(6) << 20};
     return {0, uint64_t(256) << 10};
 }
@@ -135,7 +150,13 @@ extern "C" void* mxec_batch_alloc(mxec_ctx* ctx, int dev, int k, int m, uint64_t
                 float ms = 0;
                 rc2 = probe(d, *ds.slot, s, static_cast<uint8_t*>(h.p), k, m, shard_size, n_obj, shard_size + pad, &ms);
                 if (rc2 != MXEC_OK) break;
-                if (probe_ms) probe_ms[size_t(attempt) * pads.size() + c] = ms;
+                const size_t slot = size_t(attempt) * pads.size() + c;
+                if (probe_ms && slot < 4) probe_ms[slot] = ms;
+#ifdef MXEC_LAB
+                if (getenv("MXEC_BATCH_PADS_KB"))
+                    fprintf(stderr, "{\"batch_alloc_candidate\": %d, \"pad_KiB\": %llu, \"ms\": %.3f}\n", attempt,
+                            (unsigned long long)(pad >> 10), ms);
+#endif
                 if (ms < best_ms) {
                     best_ms = ms;
                     best_a = int(held.size()) - 1;
